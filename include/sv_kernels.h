@@ -1,0 +1,187 @@
+/*
+ * sv_kernels.h -- C ABI of the spine-vision MI355X (gfx950) training-path kernel library.
+ *
+ * This is the drop-in boundary for the north-star hot path of nghiant03/spine-vision: the per-step
+ * forward -> backward -> (RCCL all-reduce) -> clip -> AdamW of LocalizationTrainer /
+ * ClassificationTrainer.  The reference launches every one of these computations implicitly through
+ * timm modules on PyTorch/cuDNN/cuBLAS; the entry points below replace those implicit kernels one for
+ * one (or fused).  Reference interfaces replaced (paths relative to the reference repo root):
+ *
+ *   backbone constructor   timm.create_model(...) at spine_vision/training/models/backbone.py:166-170
+ *                          (timm 1.0.22 ConvNeXt / ResNet, not vendored; pinned at uv.lock:3994-3995)
+ *   model forward          CoordinateRegressor.forward  spine_vision/training/models/generic.py:380-391
+ *                          Classifier.forward           spine_vision/training/models/generic.py:134-145
+ *   backward + DDP         accelerator.backward(loss)   spine_vision/training/trainers/base.py:590
+ *   clip                   accelerator.clip_grad_norm_  spine_vision/training/trainers/base.py:592-595
+ *   optimizer              torch.optim.AdamW            spine_vision/training/trainers/base.py:384-390
+ *
+ * ABI rules
+ *   - plain C types only: raw device pointers, int / int64 sizes, an sv_dtype enum, hipStream_t.
+ *   - every entry point is asynchronous on `stream` and returns SV_OK (0) or an sv_status; the message
+ *     of the last failure on the calling thread is in sv_last_error_string().
+ *   - the library never allocates or frees device memory and never retains a pointer after the call:
+ *     activations, saved tensors, partial-sum workspaces and outputs are owned by the caller
+ *     (PyTorch's caching allocator in the Python host).
+ *   - activations are NHWC: a [rows = B*H*W][C] row-major matrix.  bf16 is passed as uint16 bits.
+ */
+#ifndef SV_KERNELS_H
+#define SV_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* sv_stream_t; /* == hipStream_t */
+
+typedef enum { SV_F32 = 0, SV_BF16 = 1 } sv_dtype;
+
+typedef enum {
+  SV_OK = 0,
+  SV_ERR_INVALID_ARG = 1,
+  SV_ERR_UNSUPPORTED = 2,
+  SV_ERR_LAUNCH = 3
+} sv_status;
+
+/* ---- library ------------------------------------------------------------------------------- */
+int sv_version(void);                        /* ABI version, bumped on any signature change      */
+const char* sv_last_error_string(void);      /* thread-local message of the last failing call    */
+const char* sv_build_target(void);           /* offload arch the device code was compiled for     */
+
+/* ---- GEMM on MFMA (bf16 in / f32 accumulate, or exact f32 in / f32 accumulate) --------------
+ * C[m,n] = epilogue( sum_k A(m,k) * B(k,n) ),  m < M, n < N, k < K.
+ *   A(m,k) = A[m*lda + k]  if a_kmajor  else  A[k*lda + m]
+ *   B(k,n) = B[n*ldb + k]  if b_kmajor  else  B[k*ldb + n]     (b_kmajor == torch Linear weight)
+ * Replaces: timm Mlp.fc1 / fc2 (+GELU, *gamma, +shortcut) and the downsample Conv2d(k2,s2) of
+ * ConvNeXt (timm convnext.py ConvNeXtBlock / ConvNeXtStage) and their autograd dgrad / wgrad.     */
+typedef enum {
+  SV_EPI_STORE = 0,          /* C = acc (+ bias[n])                                               */
+  SV_EPI_BIAS_GELU2 = 1,     /* C = acc + bias[n]  (pre-activation), C2 = GELU_erf(C)             */
+  SV_EPI_BIAS_GAMMA_RES = 2, /* C = aux[m,n] + gamma[n] * (acc + bias[n])   (layer-scale residual) */
+  SV_EPI_GELU_GRAD = 3,      /* C = acc * GELU_erf'(aux[m,n])                                      */
+  SV_EPI_SLAB = 4            /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32)       */
+} sv_epilogue;
+
+typedef struct {
+  int32_t M, N, K;
+  const void* A; int32_t a_dtype; int32_t a_kmajor; int64_t lda;
+  const void* B; int32_t b_dtype; int32_t b_kmajor; int64_t ldb;
+  const float* a_scale_k;    /* optional: A(m,k) *= a_scale_k[k]                                  */
+  int32_t epilogue;          /* sv_epilogue                                                       */
+  void* C; int32_t c_dtype; int64_t ldc;
+  void* C2; int32_t c2_dtype; /* second output for SV_EPI_BIAS_GELU2 (same ldc)                   */
+  const float* bias;         /* [N] or NULL                                                       */
+  const float* gamma;        /* [N]  (SV_EPI_BIAS_GAMMA_RES)                                      */
+  const void* aux; int32_t aux_dtype; int64_t ld_aux; /* residual / pre-activation input          */
+  int32_t split_k;           /* SV_EPI_SLAB: number of K slices (>= 1); slab stride = M*N floats  */
+  int32_t compute;           /* SV_BF16: bf16 MFMA (operands rounded to bf16); SV_F32: f32 MFMA    */
+} sv_gemm_desc;
+
+int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
+
+/* ---- LayerNorm over the channel (last) dim -------------------------------------------------
+ * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.
+ * fwd: y = (x-mean)*rstd*w + b; saves mean/rstd [rows] (f32).
+ * bwd: dx = rstd*(g - mean_c(g) - xhat*mean_c(g*xhat)), g = dy*w;  dx written (accumulate=0) or
+ *      added (accumulate=1);  per-block partial sums of dw = sum dy*xhat, db = sum dy are written to
+ *      dw_part/db_part [nparts][C]; nparts = sv_layernorm_bwd_nparts(rows, C).                       */
+int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
+                     int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C, float eps,
+                     sv_stream_t stream);
+int sv_layernorm_bwd_nparts(int64_t rows, int32_t C);
+int sv_layernorm_bwd(const float* dy, const void* x, int32_t x_dtype, const float* mean,
+                     const float* rstd, const float* w, float* dx, int32_t accumulate, float* dw_part,
+                     float* db_part, int64_t rows, int32_t C, sv_stream_t stream);
+
+/* ---- ConvNeXt block head: depthwise 7x7 (pad 3, bias) fused with the channels-last LayerNorm --
+ * Replaces ConvNeXtBlock.conv_dw + permute + ConvNeXtBlock.norm (timm convnext.py).
+ * x [B,H,W,C] (x_dtype), wdw [C][49] (timm weight [C,1,7,7]), bdw [C].
+ * outputs: z = dwconv(x) (saved for backward, z_dtype), y = LN(z) (y_dtype), mean/rstd [B*H*W].  */
+int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const float* bdw,
+                      const float* lnw, const float* lnb, float eps, void* z, int32_t z_dtype, void* y,
+                      int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
+                      int32_t C, sv_stream_t stream);
+/* backward-data of the depthwise conv: dx[p] = (accumulate ? dx[p] : 0) + sum_tap w*dz.           */
+int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, int32_t accumulate, int32_t B,
+                        int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+/* backward-weight: per-workgroup partials dw_part [nparts][C*49], db_part [nparts][C].             */
+int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
+int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float* dw_part,
+                          float* db_part, int32_t B, int32_t H, int32_t W, int32_t C,
+                          sv_stream_t stream);
+
+/* ---- ConvNeXt stem: Conv2d(3, C, k=4, s=4) + LayerNorm2d, fused --------------------------------
+ * img: NCHW f32 [B,3,H,W] (ImageNet-normalised, = the reference batch["image"]); w [C][3*16]
+ * (timm stem.0.weight), b [C]; y: NHWC [B,H/4,W/4,C] (y_dtype); mean/rstd [B*H/4*W/4].            */
+int sv_stem_patchify_ln_fwd(const float* img, const float* w, const float* b, const float* lnw,
+                            const float* lnb, float eps, void* y, int32_t y_dtype, float* mean,
+                            float* rstd, int32_t B, int32_t H, int32_t W, int32_t C,
+                            sv_stream_t stream);
+/* backward (weights only; the image needs no gradient): partials [nparts][C*48], [nparts][C] x3. */
+int sv_stem_patchify_ln_bwd_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
+int sv_stem_patchify_ln_bwd(const float* img, const float* w, const float* b, const float* lnw,
+                            const float* mean, const float* rstd, const float* dy, float* dw_part,
+                            float* db_part, float* dlnw_part, float* dlnb_part, int32_t B, int32_t H,
+                            int32_t W, int32_t C, sv_stream_t stream);
+
+/* ---- ConvNeXt stage downsample: LayerNorm2d + 2x2/s2 patch gather (GEMM A operand) ------------
+ * x [B,H,W,C] f32 -> patches [B*(H/2)*(W/2)][C*4] with k = c*4 + kh*2 + kw (= timm conv weight
+ * [2C,C,2,2] flattened), so the Conv2d(k2,s2) is one sv_gemm with b_kmajor=1 on the weight.        */
+int sv_downsample_ln_patch2_fwd(const float* x, const float* lnw, const float* lnb, float eps,
+                                void* patches, int32_t p_dtype, float* mean, float* rstd, int32_t B,
+                                int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+/* dpatches (f32, same layout) -> dx [B,H,W,C] (written), LN weight partials [nparts][C].           */
+int sv_downsample_ln_patch2_bwd_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
+int sv_downsample_ln_patch2_bwd(const float* dpatches, const float* x, const float* mean,
+                                const float* rstd, const float* lnw, float* dx, float* dlnw_part,
+                                float* dlnb_part, int32_t B, int32_t H, int32_t W, int32_t C,
+                                sv_stream_t stream);
+
+/* ---- backbone head: global average pool + LayerNorm (timm NormMlpClassifierHead, num_classes=0) -
+ * x [B,HW,C] f32 -> feat [B,C] f32; saves pooled [B,C], mean/rstd [B].                             */
+int sv_pool_ln_fwd(const float* x, const float* lnw, const float* lnb, float eps, float* pooled,
+                   float* feat, float* mean, float* rstd, int32_t B, int32_t HW, int32_t C,
+                   sv_stream_t stream);
+/* dfeat [B,C] -> dx [B,HW,C] (written); dlnw/dlnb partials [B][C].                                */
+int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, const float* rstd,
+                   const float* lnw, float* dx, float* dlnw_part, float* dlnb_part, int32_t B,
+                   int32_t HW, int32_t C, sv_stream_t stream);
+
+/* ---- reductions used by backward -------------------------------------------------------------
+ * out[i] = (accumulate ? out[i] : 0) + alpha * sum_{p<P} part[p*n + i]                             */
+int sv_reduce_partials(const float* part, int32_t P, int64_t n, float* out, float alpha,
+                       int32_t accumulate, sv_stream_t stream);
+/* column sums of a [rows][C] matrix into partials [nparts][C]; nparts = sv_colsum_nparts(rows,C). */
+int sv_colsum_nparts(int64_t rows, int32_t C);
+int sv_colsum(const void* x, int32_t x_dtype, int64_t rows, int32_t C, float* part,
+              sv_stream_t stream);
+/* layer-scale fc2 weight-gradient finish.  G[C][K4] = d_out^T * GELU(h) (reduced, f32),
+ * cs[C] = colsum(d_out).  Accumulates: dW2 += gamma (.) G (row scale), dgamma += rowdot(W2, G) +
+ * b2 (.) cs, db2 += gamma (.) cs.                                                                   */
+int sv_layerscale_wgrad_finish(const float* G, const float* cs, const float* W2, const float* gamma,
+                               const float* b2, float* dW2, float* dgamma, float* db2, int32_t C,
+                               int32_t K4, sv_stream_t stream);
+
+/* ---- optimizer step on flat buffers (all params of the model live in one f32 buffer) ----------
+ * Replaces accelerator.clip_grad_norm_ (torch.nn.utils.clip_grad_norm_) + torch.optim.AdamW.step.
+ * sqnorm: per-block partial sums of g^2 -> part[nparts]; clip_coef: coef = min(1, max_norm /
+ * (sqrt(sum)+1e-6)) written to out[1], total norm to out[0] (device scalars; no host sync).        */
+int sv_sqnorm_nparts(int64_t n);
+int sv_sqnorm_partial(const float* g, int64_t n, float* part, sv_stream_t stream);
+int sv_clip_coef(const float* part, int32_t nparts, float max_norm, float* out, sv_stream_t stream);
+/* AdamW (decoupled weight decay, torch semantics, amsgrad=False, maximize=False):
+ *   g' = g * (*grad_scale) (if grad_scale != NULL);  p *= 1 - lr*wd;
+ *   m = b1*m + (1-b1) g';  v = b2*v + (1-b2) g'^2;
+ *   p -= (lr / (1-b1^step)) * m / (sqrt(v)/sqrt(1-b2^step) + eps)
+ * and, if p_bf16 != NULL, p_bf16 = bf16(p) (the shadow the MFMA kernels read next step).          */
+int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n,
+                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                  const float* grad_scale, sv_stream_t stream);
+/* y = bf16(x) over n elements (weight shadows after load_state_dict / init).                       */
+int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SV_KERNELS_H */

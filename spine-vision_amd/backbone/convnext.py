@@ -1,0 +1,303 @@
+"""ConvNeXt backbone on the gfx950 kernel library -- drop-in for
+``timm.create_model("convnext_{base,large}...", num_classes=0)`` as called at
+spine_vision/training/models/backbone.py:166-170 (timm 1.0.22 ``timm/models/convnext.py``).
+
+* Same module tree and ``state_dict`` keys as timm (``stem.{0,1}``, ``stages.i.downsample.{0,1}``,
+  ``stages.i.blocks.j.{conv_dw,norm,mlp.fc1,mlp.fc2,gamma}``, ``head.norm``), ``num_features``,
+  ``forward([B,3,H,W] f32) -> [B,F]``.  The sub-modules are parameter containers only; their own
+  ``forward`` is never called.
+* Forward and backward are explicit sequences of HIP kernels over NHWC activations (see
+  DESIGN.md "ConvNeXt step"): stem conv+LN, per block {dwconv7 -> LN, fc1 GEMM (+bias, +GELU),
+  fc2 GEMM (+bias, *gamma, +residual)}, downsample LN+patch GEMM, pool+LN.  Backward writes the
+  parameter gradients straight into ``p.grad`` (views of the trainer's flat gradient buffer) and
+  calls ``grad_ready_hook`` after each block so the DDP bucketer can start its all-reduce while the
+  remaining blocks are still being differentiated.
+* ``precision="bf16"``: bf16 MFMA, bf16 saved activations, f32 residual/gradient streams, f32
+  master weights.  ``precision="fp32"``: every tensor f32 and f32 MFMA (parity mode, <=1e-3 vs the
+  reference CPU path).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable
+
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+from .. import native as nv
+
+CONVNEXT_CFGS = {
+    "convnext_tiny": ((3, 3, 9, 3), (96, 192, 384, 768)),
+    "convnext_small": ((3, 3, 27, 3), (96, 192, 384, 768)),
+    "convnext_base": ((3, 3, 27, 3), (128, 256, 512, 1024)),
+    "convnext_large": ((3, 3, 27, 3), (192, 384, 768, 1536)),
+}
+
+
+class _Mlp(nn.Module):
+    def __init__(self, dim: int, hidden: int) -> None:
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class ConvNeXtBlock(nn.Module):
+    """Parameter container for timm ConvNeXtBlock (conv_mlp=False, ls_init_value, no drop_path)."""
+
+    def __init__(self, dim: int, ls_init_value: float = 1e-6) -> None:
+        super().__init__()
+        self.conv_dw = nn.Conv2d(dim, dim, kernel_size=7, padding=3, groups=dim, bias=True)
+        self.norm = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = _Mlp(dim, 4 * dim)
+        self.gamma = nn.Parameter(ls_init_value * torch.ones(dim))
+
+
+class ConvNeXtStage(nn.Module):
+    def __init__(self, in_chs: int, out_chs: int, depth: int, downsample: bool) -> None:
+        super().__init__()
+        if downsample:
+            self.downsample = nn.Sequential(nn.LayerNorm(in_chs, eps=1e-6), nn.Conv2d(in_chs, out_chs, 2, stride=2))
+        else:
+            self.downsample = nn.Identity()
+        self.blocks = nn.Sequential(*[ConvNeXtBlock(out_chs) for _ in range(depth)])
+
+
+class _Head(nn.Module):
+    def __init__(self, dim: int) -> None:
+        super().__init__()
+        self.norm = nn.LayerNorm(dim, eps=1e-6)
+
+
+@dataclass
+class _Tape:
+    """Activations saved by the training forward for the explicit backward."""
+
+    img: torch.Tensor
+    stem: tuple = ()
+    stages: list = field(default_factory=list)  # per stage: (ds_saved or None, [block_saved...])
+    pool: tuple = ()
+    out_shape: tuple = ()
+    wcache: dict = field(default_factory=dict)  # bf16 weight casts shared by forward and backward
+
+
+class _ConvNeXtFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, model):  # noqa: D401 - autograd signature
+        feat, tape = model._forward_impl(x, save=True)
+        ctx.model = model
+        ctx.tape = tape
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        ctx.model._backward_impl(ctx.tape, dfeat)
+        ctx.tape = None
+        return None, None, None
+
+
+class ConvNeXtHip(nn.Module):
+    def __init__(self, depths=(3, 3, 27, 3), dims=(128, 256, 512, 1024), ls_init_value: float = 1e-6,
+                 precision: str = "bf16") -> None:
+        super().__init__()
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        self.depths, self.dims = tuple(depths), tuple(dims)
+        self.precision = precision
+        self.stem = nn.Sequential(nn.Conv2d(3, dims[0], kernel_size=4, stride=4), nn.LayerNorm(dims[0], eps=1e-6))
+        stages = []
+        prev = dims[0]
+        for i, (d, c) in enumerate(zip(depths, dims)):
+            stages.append(ConvNeXtStage(prev, c, d, downsample=i > 0))
+            prev = c
+        self.stages = nn.Sequential(*stages)
+        self.norm_pre = nn.Identity()
+        self.head = _Head(prev)
+        self.num_features = self.head_hidden_size = prev
+        self.grad_ready_hook: Callable[[list], None] | None = None
+        self._shadow: dict[int, torch.Tensor] | None = None  # id(param) -> bf16 shadow view
+        self._init_weights()
+
+    # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
+    def _init_weights(self) -> None:
+        for m in self.modules():
+            if isinstance(m, (nn.Conv2d, nn.Linear)):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+
+    # -- precision / weight shadows --------------------------------------------------------------
+    @property
+    def compute_bf16(self) -> bool:
+        return self.precision == "bf16"
+
+    @property
+    def act_dtype(self) -> torch.dtype:
+        return torch.bfloat16 if self.compute_bf16 else torch.float32
+
+    def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
+        """Install bf16 views kept fresh by the flat optimizer (id(param) -> bf16 tensor)."""
+        self._shadow = shadow
+
+    def gemm_weight_params(self) -> list[nn.Parameter]:
+        ps = [self.stem[0].weight]
+        for st in self.stages:
+            if not isinstance(st.downsample, nn.Identity):
+                ps.append(st.downsample[1].weight)
+            for blk in st.blocks:
+                ps += [blk.mlp.fc1.weight, blk.mlp.fc2.weight]
+        return ps
+
+    def _w(self, p: torch.Tensor, cache: dict) -> torch.Tensor:
+        """Weight as the GEMM reads it: f32 param (fp32 mode) or its bf16 shadow."""
+        if not self.compute_bf16:
+            return p.detach()
+        if self._shadow is not None and id(p) in self._shadow:
+            return self._shadow[id(p)]
+        k = id(p)
+        if k not in cache:
+            cache[k] = K.cast_bf16(p.detach().contiguous())
+        return cache[k]
+
+    # -- forward -----------------------------------------------------------------------------------
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("ConvNeXtHip runs on the MI355X kernel library only (got a CPU tensor)")
+        x = x.float().contiguous()
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if need_grad:
+            anchor = torch.zeros((), device=x.device, requires_grad=True)
+            return _ConvNeXtFn.apply(x, anchor, self)
+        feat, _ = self._forward_impl(x, save=False)
+        return feat
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward(x)
+
+    @torch.no_grad()
+    def _forward_impl(self, img: torch.Tensor, save: bool):
+        bf = self.compute_bf16
+        act = self.act_dtype
+        tape = _Tape(img=img) if save else None
+        cache: dict = tape.wcache if save else {}
+        stem_conv, stem_ln = self.stem[0], self.stem[1]
+        x, s_mean, s_rstd = K.stem_fwd(img, stem_conv.weight, stem_conv.bias, stem_ln.weight, stem_ln.bias)
+        if save:
+            tape.stem = (s_mean, s_rstd)
+        for st in self.stages:
+            ds_saved = None
+            if not isinstance(st.downsample, nn.Identity):
+                ln, conv = st.downsample[0], st.downsample[1]
+                B, H, W, C = x.shape
+                patches, d_mean, d_rstd = K.downsample_fwd(x, ln.weight, ln.bias, act_dtype=act)
+                Cout = conv.weight.shape[0]
+                wds = self._w(conv.weight, cache).reshape(Cout, 4 * C)
+                xn = torch.empty(B, H // 2, W // 2, Cout, device=x.device, dtype=torch.float32)
+                K.linear_fwd(patches, wds, out=xn.view(-1, Cout), bias=conv.bias, compute_bf16=bf)
+                if save:
+                    ds_saved = (x, patches, d_mean, d_rstd)
+                x = xn
+            blocks_saved = []
+            for blk in st.blocks:
+                B, H, W, C = x.shape
+                M = B * H * W
+                z, y, mean, rstd = K.dwconv7_ln_fwd(x, blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight,
+                                                    blk.norm.bias, act_dtype=act)
+                w1 = self._w(blk.mlp.fc1.weight, cache)
+                w2 = self._w(blk.mlp.fc2.weight, cache)
+                h = torch.empty(M, 4 * C, device=x.device, dtype=act)
+                a = torch.empty(M, 4 * C, device=x.device, dtype=act)
+                K.linear_fwd(y, w1, out=h, out2=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU2,
+                             compute_bf16=bf)
+                xo = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
+                K.linear_fwd(a, w2, out=xo.view(M, C), bias=blk.mlp.fc2.bias, gamma=blk.gamma,
+                             residual=x.view(M, C), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, compute_bf16=bf)
+                if save:
+                    blocks_saved.append((x, z, y, mean, rstd, h, a))
+                x = xo
+            if save:
+                tape.stages.append((ds_saved, blocks_saved))
+        feat, pooled, p_mean, p_rstd = K.pool_ln_fwd(x, self.head.norm.weight, self.head.norm.bias)
+        if save:
+            tape.pool = (pooled, p_mean, p_rstd)
+            tape.out_shape = tuple(x.shape)
+        return feat, tape
+
+    # -- backward ----------------------------------------------------------------------------------
+    @staticmethod
+    def _grad(p: torch.Tensor) -> torch.Tensor:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        return p.grad
+
+    def _ready(self, params: list) -> None:
+        if self.grad_ready_hook is not None:
+            self.grad_ready_hook(params)
+
+    @torch.no_grad()
+    def _backward_impl(self, tape: _Tape, dfeat: torch.Tensor) -> None:
+        bf = self.compute_bf16
+        act = self.act_dtype
+        cache: dict = tape.wcache
+        g = self._grad
+        hn = self.head.norm
+        d = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight), dlnb=g(hn.bias))
+        self._ready([hn.weight, hn.bias])
+        for st, (ds_saved, blocks_saved) in zip(reversed(list(self.stages)), reversed(tape.stages)):
+            for blk, saved in zip(reversed(list(st.blocks)), reversed(blocks_saved)):
+                x, z, y, mean, rstd, h, a = saved
+                B, H, W, C = x.shape
+                M = B * H * W
+                d2 = d.view(M, C)
+                w1 = self._w(blk.mlp.fc1.weight, cache)
+                w2 = self._w(blk.mlp.fc2.weight, cache)
+                # fc2: dh = ((d * gamma) @ W2) * GELU'(h)
+                dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
+                K.linear_dgrad(d2, w2, out=dh, epilogue=nv.SV_EPI_GELU_GRAD, a_scale_k=blk.gamma, aux=h,
+                               compute_bf16=bf)
+                G = K.linear_wgrad(d2, a, compute_bf16=bf)  # [C, 4C] = d^T a
+                cs = K.colsum(d2)
+                nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),
+                        nv.ptr(blk.gamma), nv.ptr(blk.mlp.fc2.bias), nv.ptr(g(blk.mlp.fc2.weight)),
+                        nv.ptr(g(blk.gamma)), nv.ptr(g(blk.mlp.fc2.bias)), C, 4 * C)
+                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh)
+                dy = torch.empty(M, C, device=d.device, dtype=torch.float32)
+                K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
+                K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, compute_bf16=bf)
+                K.colsum_into(dh, g(blk.mlp.fc1.bias))
+                # LayerNorm + depthwise conv
+                dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                     db=g(blk.norm.bias))
+                dz4 = dz.view(B, H, W, C)
+                K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+                K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True)
+                self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
+                             blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
+            if ds_saved is not None:
+                x_prev, patches, d_mean, d_rstd = ds_saved
+                ln, conv = st.downsample[0], st.downsample[1]
+                B, H, W, C = x_prev.shape
+                Cout = conv.weight.shape[0]
+                Mo = B * (H // 2) * (W // 2)
+                d2 = d.view(Mo, Cout)
+                wds = self._w(conv.weight, cache).reshape(Cout, 4 * C)
+                dpatch = torch.empty(Mo, 4 * C, device=d.device, dtype=torch.float32)
+                K.linear_dgrad(d2, wds, out=dpatch, compute_bf16=bf)
+                K.linear_wgrad(d2, patches, out=g(conv.weight), accumulate=True, compute_bf16=bf)
+                K.colsum_into(d2, g(conv.bias))
+                d = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight), dlnb=g(ln.bias))
+                self._ready([ln.weight, ln.bias, conv.weight, conv.bias])
+        s_mean, s_rstd = tape.stem
+        conv, ln = self.stem[0], self.stem[1]
+        K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
+                   db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
+        self._ready([conv.weight, conv.bias, ln.weight, ln.bias])
+
+
+def create_convnext(name: str, precision: str = "bf16") -> ConvNeXtHip:
+    key = name.split(".")[0]
+    if key not in CONVNEXT_CFGS:
+        raise ValueError(f"unsupported ConvNeXt variant {name!r}")
+    depths, dims = CONVNEXT_CFGS[key]
+    return ConvNeXtHip(depths, dims, precision=precision)

@@ -1,0 +1,411 @@
+// MFMA GEMM family for the ConvNeXt hot path (gfx950 / CDNA4, wave64).
+//
+// Replaces the cuBLAS GEMMs that timm's Mlp.fc1 / Mlp.fc2 / downsample Conv2d(k2,s2) launch under
+// the reference (spine_vision/training/models/backbone.py:166 -> timm convnext.py) and their
+// autograd dgrad/wgrad, with the elementwise neighbours fused into the epilogue:
+//   fc1 fwd   h = y_ln W1^T + b1, a = GELU(h)                 (SV_EPI_BIAS_GELU2, both stored bf16)
+//   fc2 fwd   out = x + gamma * (a W2^T + b2)                 (SV_EPI_BIAS_GAMMA_RES)
+//   fc2 dgrad dh = ((d_out * gamma) W2) * GELU'(h)            (a_scale_k = gamma, SV_EPI_GELU_GRAD)
+//   wgrads    split-K over the pixel dimension into f32 slabs (SV_EPI_SLAB)
+//
+// Structure: 128x128 output tile per 256-thread workgroup (4 waves in 2x2, 64x64 per wave = 4x4
+// v_mfma_f32_16x16x32_bf16 fragments, or 16x16x4_f32 for the exact-f32 parity mode), BK = 32,
+// register-staged double-buffered LDS (global loads for tile k+1 are issued before the MFMAs of
+// tile k; one barrier per k-step).  Operands may be K-contiguous ("k-major": torch Linear weights,
+// activations as the reduction operand) or M/N-contiguous (activations as the wgrad operand);
+// k-major tiles are read with ds_read_b128, M/N-contiguous tiles are kept in their natural
+// [k][m] image and turned into MFMA fragments by the gfx950 LDS transpose read
+// ds_read_b64_tr_b16 -- no transposed copies of activations ever go through HBM.
+// f32 operands (the f32 gradient stream) are rounded to bf16 while staging.
+// Epilogue: the 64x64 f32 accumulator of each wave is staged through LDS in 16-row slabs and
+// re-read row-contiguous, so every global load/store of the epilogue is a 16-B vector access.
+// The blockIdx -> tile map is XCD-aware (each XCD gets a contiguous run of tiles, which share
+// A row panels in its private L2).
+#include "common.h"
+
+namespace sv {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BKT = 32;
+constexpr int kGemmThreads = 256;
+constexpr int EPI_LD = 64 + 4;  // f32 epilogue slab row stride
+
+// ---------------------------------------------------------------------------------------------
+// LDS images.  bf16 compute: k-major [R][BKT+8] (80 B rows), m-major [BKT][R+16] (288 B rows).
+//               f32 compute:  k-major [R][BKT+4] (144 B rows), m-major [BKT][R+4] (528 B rows).
+template <bool BF16, bool KMAJ>
+struct Img {
+  static constexpr int LD = BF16 ? (KMAJ ? BKT + 8 : BM + 16) : (KMAJ ? BKT + 4 : BM + 4);
+  static constexpr int ROWS = KMAJ ? BM : BKT;
+  static constexpr int BYTES = ROWS * LD * (BF16 ? 2 : 4);
+};
+
+// Global -> register stage of one operand tile (rows = M or N extent of the tile, BKT deep).
+// Chunk = 16 B of the LDS image: 8 bf16 or 4 f32 compute elements.
+template <bool BF16, typename T, bool KMAJ>
+struct Stage {
+  static constexpr int EPC = BF16 ? 8 : 4;                       // elements per chunk
+  static constexpr int CHUNKS = BM * BKT / EPC;                  // per tile
+  static constexpr int PER_THREAD = CHUNKS / kGemmThreads;       // 2 (bf16) or 4 (f32)
+  uint4 r[PER_THREAD];
+
+  // p: operand base; ld: leading dim; row0: tile offset along M/N; k0: k offset;
+  // R: M/N bound; K: k bound; scale: optional per-k scale (A operand only)
+  __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int row0, int k0, int R, int K,
+                                       const float* __restrict__ scale) {
+#pragma unroll
+    for (int s = 0; s < PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      int row, kk;  // position of the chunk's first element: (row along M/N, k)
+      if (KMAJ) {
+        constexpr int CPR = BKT / EPC;  // chunks per row
+        row = q / CPR;
+        kk = (q % CPR) * EPC;
+      } else {
+        constexpr int CPR = BM / EPC;
+        kk = q / CPR;
+        row = (q % CPR) * EPC;
+      }
+      const int gr = row0 + row, gk = k0 + kk;
+      const bool ok = gr < R && gk < K;
+      const T* src = KMAJ ? p + (size_t)gr * ld + gk : p + (size_t)gk * ld + gr;
+      if (BF16) {
+        if constexpr (sizeof(T) == 2) {
+          uint4 v = make_uint4(0, 0, 0, 0);
+          if (ok) v = *reinterpret_cast<const uint4*>(src);
+          if (scale && ok) {
+            // rare path (only f32 operands carry a scale in practice) -- keep it exact anyway
+            const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+            float f[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = bf2f(e[j]) * scale[KMAJ ? gk + j : gk];
+            v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+          }
+          r[s] = v;
+        } else {
+          float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+          if (ok) {
+            a = *reinterpret_cast<const float4*>(src);
+            b = *reinterpret_cast<const float4*>(src + 4);
+            if (scale) {
+              if (KMAJ) {
+                const float4 sa = *reinterpret_cast<const float4*>(scale + gk);
+                const float4 sb = *reinterpret_cast<const float4*>(scale + gk + 4);
+                a.x *= sa.x; a.y *= sa.y; a.z *= sa.z; a.w *= sa.w;
+                b.x *= sb.x; b.y *= sb.y; b.z *= sb.z; b.w *= sb.w;
+              } else {
+                const float sc = scale[gk];
+                a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+                b.x *= sc; b.y *= sc; b.z *= sc; b.w *= sc;
+              }
+            }
+          }
+          r[s] = make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
+        }
+      } else {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) {
+          a = *reinterpret_cast<const float4*>(src);
+          if (scale) {
+            if (KMAJ) {
+              const float4 sa = *reinterpret_cast<const float4*>(scale + gk);
+              a.x *= sa.x; a.y *= sa.y; a.z *= sa.z; a.w *= sa.w;
+            } else {
+              const float sc = scale[gk];
+              a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+            }
+          }
+        }
+        r[s] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* __restrict__ img) const {
+    constexpr int ES = BF16 ? 2 : 4;
+    constexpr int LD = Img<BF16, KMAJ>::LD;
+#pragma unroll
+    for (int s = 0; s < PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      int row, kk;
+      if (KMAJ) {
+        constexpr int CPR = BKT / EPC;
+        row = q / CPR;
+        kk = (q % CPR) * EPC;
+        *reinterpret_cast<uint4*>(img + ((size_t)row * LD + kk) * ES) = r[s];
+      } else {
+        constexpr int CPR = BM / EPC;
+        kk = q / CPR;
+        row = (q % CPR) * EPC;
+        *reinterpret_cast<uint4*>(img + ((size_t)kk * LD + row) * ES) = r[s];
+      }
+    }
+  }
+};
+
+// bf16 fragment for v_mfma_f32_16x16x32_bf16: lane l holds X[row = base + (l&15)][k = 8(l>>4)+j].
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag_bf16(const char* __restrict__ img, int base) {
+  const int l = threadIdx.x & 63;
+  if (KMAJ) {
+    constexpr int LD = Img<true, true>::LD;
+    return *reinterpret_cast<const bf16x8*>(img + ((size_t)(base + (l & 15)) * LD + 8 * (l >> 4)) * 2);
+  } else {
+    // [k][row] image: two ds_read_b64_tr_b16, k rows 8g..8g+3 and 8g+4..8g+7 (g = l>>4);
+    // lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3 of the 4x16 block.
+    constexpr int LD = Img<true, false>::LD;
+    const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const char* a0 = img + ((size_t)(8 * g + q) * LD + base + 4 * p) * 2;
+    const char* a1 = a0 + (size_t)4 * LD * 2;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// f32 fragment for v_mfma_f32_16x16x4_f32: lane l holds X[row = base + (l&15)][k = kk + (l>>4)].
+template <bool KMAJ>
+__device__ __forceinline__ float frag_f32(const char* __restrict__ img, int base, int kk) {
+  const int l = threadIdx.x & 63;
+  constexpr int LD = Img<false, KMAJ>::LD;
+  const float* f = reinterpret_cast<const float*>(img);
+  return KMAJ ? f[(size_t)(base + (l & 15)) * LD + kk + (l >> 4)] : f[(size_t)(kk + (l >> 4)) * LD + base + (l & 15)];
+}
+
+struct EpiArgs {
+  int M, N;
+  int epi;
+  void* C; int c_dtype; int64_t ldc;
+  void* C2; int c2_dtype;
+  const float* bias;
+  const float* gamma;
+  const void* aux; int aux_dtype; int64_t ld_aux;
+};
+
+__device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
+  return dt == SV_F32 ? ld4(reinterpret_cast<const float*>(p), i) : ld4(reinterpret_cast<const uint16_t*>(p), i);
+}
+__device__ __forceinline__ void st4_any(void* p, int dt, size_t i, float4 v) {
+  if (dt == SV_F32) st4(reinterpret_cast<float*>(p), i, v);
+  else st4(reinterpret_cast<uint16_t*>(p), i, v);
+}
+
+// apply the epilogue to 4 consecutive columns n..n+3 of row m
+__device__ __forceinline__ void epi4(const EpiArgs& e, int m, int n, float4 v, int split) {
+  if (e.epi == SV_EPI_SLAB) {
+    float* C = reinterpret_cast<float*>(e.C) + (size_t)split * e.M * e.N;
+    *reinterpret_cast<float4*>(C + (size_t)m * e.N + n) = v;
+    return;
+  }
+  if (e.bias && e.epi != SV_EPI_GELU_GRAD) {
+    const float4 b = *reinterpret_cast<const float4*>(e.bias + n);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  }
+  const size_t ci = (size_t)m * e.ldc + n;
+  if (e.epi == SV_EPI_STORE) {
+    st4_any(e.C, e.c_dtype, ci, v);
+  } else if (e.epi == SV_EPI_BIAS_GELU2) {
+    st4_any(e.C, e.c_dtype, ci, v);
+    st4_any(e.C2, e.c2_dtype, ci, make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)));
+  } else if (e.epi == SV_EPI_BIAS_GAMMA_RES) {
+    const float4 g = *reinterpret_cast<const float4*>(e.gamma + n);
+    const float4 r = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
+    st4_any(e.C, e.c_dtype, ci, make_float4(r.x + g.x * v.x, r.y + g.y * v.y, r.z + g.z * v.z, r.w + g.w * v.w));
+  } else {  // SV_EPI_GELU_GRAD
+    const float4 h = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
+    st4_any(e.C, e.c_dtype, ci,
+            make_float4(v.x * gelu_grad_f(h.x), v.y * gelu_grad_f(h.y), v.z * gelu_grad_f(h.z), v.w * gelu_grad_f(h.w)));
+  }
+}
+
+template <bool BF16, typename TA, typename TB, bool AK, bool BKM>
+__global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict__ A, int64_t lda,
+                                                            const TB* __restrict__ B, int64_t ldb,
+                                                            const float* __restrict__ a_scale, int K,
+                                                            int kper, int tilesM, int tilesN, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ABYTES = Img<BF16, AK>::BYTES, BBYTES = Img<BF16, BKM>::BYTES;
+  constexpr int STAGE_BYTES = ABYTES + BBYTES;
+
+  // ---- XCD-aware tile map: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of
+  //      tiles (tn fastest) so the tiles co-resident in one L2 share their A row panel.
+  const int nwg = tilesM * tilesN;
+  const int pid = blockIdx.x;
+  const int xcd = pid & 7, loc = pid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = wg / tilesN, tn = wg % tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * kper;
+  int kend = kbeg + kper;
+  if (kend > K) kend = K;
+  const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
+
+  const int wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<BF16, TA, AK> sa;
+  Stage<BF16, TB, BKM> sb;
+  if (nk > 0) {
+    sa.load(A, lda, m0, kbeg, e.M, kend, a_scale);
+    sb.load(B, ldb, n0, kbeg, e.N, kend, nullptr);
+    sa.store(smem);
+    sb.store(smem + ABYTES);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BKT;
+      sa.load(A, lda, m0, k0, e.M, kend, a_scale);
+      sb.load(B, ldb, n0, k0, e.N, kend, nullptr);
+    }
+    const char* ai = cur;
+    const char* bi = cur + ABYTES;
+    if constexpr (BF16) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_bf16<AK>(ai, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag_bf16<BKM>(bi, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BKT; kk += 4) {
+        float af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = frag_f32<AK>(ai, wm * 64 + i * 16, kk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag_f32<BKM>(bi, wn * 64 + j * 16, kk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      sa.store(nxt);
+      sb.store(nxt + ABYTES);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: per wave, 4 slabs of 16 rows x 64 cols staged through its private LDS region
+  float* slab = reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD;
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int row = l >> 2, cb = (l & 3) * 16;
+    const int m = m0 + wm * 64 + i * 16 + row;
+    if (m < e.M) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 64 + cb + 4 * g;
+        if (n < e.N) {
+          const float* sp = slab + row * EPI_LD + cb + 4 * g;
+          epi4(e, m, n, make_float4(sp[0], sp[1], sp[2], sp[3]), split);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
+template <bool BF16, typename TA, typename TB, bool AK, bool BKM>
+static int launch(const sv_gemm_desc* d, hipStream_t s) {
+  const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
+  int split = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
+  int kper = ceil_div(ceil_div(d->K, split), BKT) * BKT;
+  EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
+            d->aux, d->aux_dtype, d->ld_aux};
+  constexpr size_t main_lds = 2 * (size_t)(Img<BF16, AK>::BYTES + Img<BF16, BKM>::BYTES);
+  constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
+  constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
+  dim3 grid(tilesM * tilesN, 1, split);
+  if (lds > 65536) {
+    static bool attr_set = false;  // per template instantiation
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BF16, TA, TB, AK, BKM>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+  }
+  gemm_kernel<BF16, TA, TB, AK, BKM><<<grid, kGemmThreads, lds, s>>>(
+      reinterpret_cast<const TA*>(d->A), d->lda, reinterpret_cast<const TB*>(d->B), d->ldb, d->a_scale_k, d->K,
+      kper, tilesM, tilesN, e);
+  return check_launch("sv_gemm");
+}
+
+template <bool BF16, typename TA, typename TB>
+static int launch_layout(const sv_gemm_desc* d, hipStream_t s) {
+  if (d->a_kmajor && d->b_kmajor) return launch<BF16, TA, TB, true, true>(d, s);
+  if (d->a_kmajor && !d->b_kmajor) return launch<BF16, TA, TB, true, false>(d, s);
+  if (!d->a_kmajor && d->b_kmajor) return launch<BF16, TA, TB, false, true>(d, s);
+  return launch<BF16, TA, TB, false, false>(d, s);
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace sv
+
+using namespace sv;
+
+extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
+  SV_REQUIRE(d, "sv_gemm: null descriptor");
+  SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
+  SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_SLAB, "sv_gemm: bad epilogue %d", d->epilogue);
+  if (d->M == 0 || d->N == 0) return SV_OK;
+  const bool bf = d->compute == SV_BF16;
+  SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
+  SV_REQUIRE(bf || (d->a_dtype == SV_F32 && d->b_dtype == SV_F32), "sv_gemm: f32 compute needs f32 operands");
+  const int vec = bf ? 8 : 4;
+  // contiguous dims must hold whole 16-B chunks; leading dims keep every chunk 16-B aligned
+  SV_REQUIRE((d->a_kmajor ? d->K : d->M) % vec == 0, "sv_gemm: A contiguous dim not a multiple of %d", vec);
+  SV_REQUIRE((d->b_kmajor ? d->K : d->N) % vec == 0, "sv_gemm: B contiguous dim not a multiple of %d", vec);
+  SV_REQUIRE(d->lda % vec == 0 && d->ldb % vec == 0, "sv_gemm: lda/ldb must be multiples of %d", vec);
+  SV_REQUIRE(al16(d->A) && al16(d->B) && al16(d->C), "sv_gemm: operands must be 16-byte aligned");
+  SV_REQUIRE(d->N % 4 == 0, "sv_gemm: N must be a multiple of 4");
+  if (d->epilogue == SV_EPI_SLAB) {
+    SV_REQUIRE(d->c_dtype == SV_F32, "sv_gemm: slab epilogue writes f32");
+  } else {
+    SV_REQUIRE(d->ldc % 4 == 0, "sv_gemm: ldc must be a multiple of 4");
+  }
+  if (d->epilogue == SV_EPI_BIAS_GELU2) SV_REQUIRE(d->C2 && al16(d->C2), "sv_gemm: GELU2 needs aligned C2");
+  if (d->epilogue == SV_EPI_BIAS_GAMMA_RES) SV_REQUIRE(d->gamma && d->aux, "sv_gemm: gamma/residual missing");
+  if (d->epilogue == SV_EPI_GELU_GRAD) SV_REQUIRE(d->aux, "sv_gemm: pre-activation missing");
+  if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
+  if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (!bf) return launch_layout<false, float, float>(d, s);
+  const bool a32 = d->a_dtype == SV_F32, b32 = d->b_dtype == SV_F32;
+  SV_REQUIRE((a32 || d->a_dtype == SV_BF16) && (b32 || d->b_dtype == SV_BF16), "sv_gemm: bad operand dtype");
+  if (!a32 && !b32) return launch_layout<true, uint16_t, uint16_t>(d, s);
+  if (a32 && !b32) return launch_layout<true, float, uint16_t>(d, s);
+  if (!a32 && b32) return launch_layout<true, uint16_t, float>(d, s);
+  return launch_layout<true, float, float>(d, s);
+}

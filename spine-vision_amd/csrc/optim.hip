@@ -1,0 +1,242 @@
+// Flat-buffer optimizer step and the small reductions used by backward (gfx950).
+//
+// The Python host lays every parameter of the model out in ONE f32 buffer (and the gradients,
+// AdamW moments and the bf16 weight shadow in buffers with identical offsets), so the reference's
+// foreach clip_grad_norm_ + foreach AdamW (spine_vision/training/trainers/base.py:592-597,
+// 384-390) become: one grid-stride sum-of-squares pass, one 1-block finisher producing the clip
+// coefficient ON DEVICE (no host sync), and one fused AdamW pass that also refreshes the bf16
+// shadow the MFMA GEMMs read.  All of them are HBM-bound streaming kernels: 16 B per lane.
+#include <math.h>
+
+#include "common.h"
+
+namespace sv {
+
+constexpr int kThreads = 256;
+
+__global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* __restrict__ part,
+                                                                    int P, int64_t n,
+                                                                    float* __restrict__ out,
+                                                                    float alpha, int accumulate) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int p = 0; p < P; ++p) s += part[(size_t)p * n + i];
+    s *= alpha;
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+// column sums: workgroup b sums rows [b*rpb, (b+1)*rpb) of all C columns -> part[b][C]
+template <typename T>
+__global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, int64_t rows, int C,
+                                                          int64_t rpb, float* __restrict__ part) {
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  int64_t r1 = r0 + rpb;
+  if (r1 > rows) r1 = rows;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += ld(x, (size_t)r * C + c);
+    part[(size_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// dW2 += gamma*G ; dgamma += rowdot(W2,G) + b2*cs ; db2 += gamma*cs.  One wave per row c.
+__global__ void __launch_bounds__(kThreads) layerscale_finish_kernel(
+    const float* __restrict__ G, const float* __restrict__ cs, const float* __restrict__ W2,
+    const float* __restrict__ gamma, const float* __restrict__ b2, float* __restrict__ dW2,
+    float* __restrict__ dgamma, float* __restrict__ db2, int C, int K4) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float gc = gamma[c];
+  float dot = 0.f;
+  for (int k = lane; k < K4; k += 64) {
+    const size_t i = (size_t)c * K4 + k;
+    const float g = G[i];
+    dot += W2[i] * g;
+    dW2[i] += gc * g;
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) {
+    dgamma[c] += dot + b2[c] * cs[c];
+    db2[c] += gc * cs[c];
+  }
+}
+
+constexpr int kSqBlocks = 1024;
+
+__global__ void __launch_bounds__(kThreads) sqnorm_kernel(const float* __restrict__ g, int64_t n,
+                                                          float* __restrict__ part) {
+  __shared__ float red[kThreads / 64];
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) s += g[i] * g[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(kThreads) clip_coef_kernel(const float* __restrict__ part, int P,
+                                                             float max_norm, float* __restrict__ out) {
+  __shared__ float red[kThreads / 64];
+  // fixed-order (deterministic) sum of the per-block partials
+  float s = 0.f;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) s += part[p];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(s);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef < 1.0f ? coef : 1.0f;
+    out[0] = norm;
+    out[1] = coef;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         uint16_t* __restrict__ pb, int64_t n, float lr,
+                                                         float b1, float b2, float eps, float wd,
+                                                         float bc1, float bc2_sqrt,
+                                                         const float* __restrict__ gscale) {
+  const float sc = gscale ? *gscale : 1.0f;
+  const float step_size = lr / bc1;
+  const float decay = 1.0f - lr * wd;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = ga[k] * sc;
+      float pk = pa[k] * decay;
+      ma[k] = b1 * ma[k] + (1.0f - b1) * gk;
+      va[k] = b2 * va[k] + (1.0f - b2) * gk * gk;
+      const float denom = sqrtf(va[k]) / bc2_sqrt + eps;
+      pa[k] = pk - step_size * (ma[k] / denom);
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (pb) reinterpret_cast<uint2*>(pb)[i] = make_uint2(pack2bf(pp.x, pp.y), pack2bf(pp.z, pp.w));
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gk = g[i] * sc;
+    const float pk = p[i] * decay;
+    m[i] = b1 * m[i] + (1.0f - b1) * gk;
+    v[i] = b2 * v[i] + (1.0f - b2) * gk * gk;
+    p[i] = pk - step_size * (m[i] / (sqrtf(v[i]) / bc2_sqrt + eps));
+    if (pb) pb[i] = f2bf(p[i]);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) cast_bf16_kernel(const float* __restrict__ x,
+                                                             uint16_t* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf(x[i]);
+}
+
+static int stream_grid(int64_t n, int per_thread) {
+  const int64_t g = (n / per_thread + kThreads - 1) / kThreads;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+}  // namespace sv
+
+using namespace sv;
+
+extern "C" {
+
+int sv_reduce_partials(const float* part, int32_t P, int64_t n, float* out, float alpha,
+                       int32_t accumulate, sv_stream_t stream) {
+  SV_REQUIRE(part && out && P >= 1, "sv_reduce_partials: bad args");
+  if (n <= 0) return SV_OK;
+  reduce_partials_kernel<<<stream_grid(n, 1), kThreads, 0, (hipStream_t)stream>>>(part, P, n, out, alpha, accumulate);
+  return check_launch("sv_reduce_partials");
+}
+
+static int64_t colsum_rpb(int64_t rows) {
+  int64_t rpb = (rows + 511) / 512;
+  return rpb < 1 ? 1 : rpb;
+}
+
+int sv_colsum_nparts(int64_t rows, int32_t C) {
+  (void)C;
+  const int64_t rpb = colsum_rpb(rows);
+  return (int)((rows + rpb - 1) / rpb);
+}
+
+int sv_colsum(const void* x, int32_t x_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream) {
+  SV_REQUIRE(x && part && C > 0, "sv_colsum: bad args");
+  if (rows <= 0) return SV_OK;
+  const int64_t rpb = colsum_rpb(rows);
+  const int grid = sv_colsum_nparts(rows, C);
+  if (x_dtype == SV_F32)
+    colsum_kernel<float><<<grid, kThreads, 0, (hipStream_t)stream>>>((const float*)x, rows, C, rpb, part);
+  else if (x_dtype == SV_BF16)
+    colsum_kernel<uint16_t><<<grid, kThreads, 0, (hipStream_t)stream>>>((const uint16_t*)x, rows, C, rpb, part);
+  else
+    return set_error(SV_ERR_INVALID_ARG, "sv_colsum: bad dtype");
+  return check_launch("sv_colsum");
+}
+
+int sv_layerscale_wgrad_finish(const float* G, const float* cs, const float* W2, const float* gamma,
+                               const float* b2, float* dW2, float* dgamma, float* db2, int32_t C,
+                               int32_t K4, sv_stream_t stream) {
+  SV_REQUIRE(G && cs && W2 && gamma && b2 && dW2 && dgamma && db2, "sv_layerscale_wgrad_finish: null");
+  if (C <= 0) return SV_OK;
+  layerscale_finish_kernel<<<ceil_div(C, kThreads / 64), kThreads, 0, (hipStream_t)stream>>>(
+      G, cs, W2, gamma, b2, dW2, dgamma, db2, C, K4);
+  return check_launch("sv_layerscale_wgrad_finish");
+}
+
+int sv_sqnorm_nparts(int64_t n) {
+  const int g = stream_grid(n, 4);
+  return g < kSqBlocks ? g : kSqBlocks;
+}
+
+int sv_sqnorm_partial(const float* g, int64_t n, float* part, sv_stream_t stream) {
+  SV_REQUIRE(g && part, "sv_sqnorm_partial: null");
+  SV_REQUIRE(((uintptr_t)g & 15) == 0, "sv_sqnorm_partial: buffer must be 16-byte aligned");
+  sqnorm_kernel<<<sv_sqnorm_nparts(n), kThreads, 0, (hipStream_t)stream>>>(g, n, part);
+  return check_launch("sv_sqnorm_partial");
+}
+
+int sv_clip_coef(const float* part, int32_t nparts, float max_norm, float* out, sv_stream_t stream) {
+  SV_REQUIRE(part && out && nparts >= 1, "sv_clip_coef: bad args");
+  clip_coef_kernel<<<1, kThreads, 0, (hipStream_t)stream>>>(part, nparts, max_norm, out);
+  return check_launch("sv_clip_coef");
+}
+
+int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n,
+                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                  const float* grad_scale, sv_stream_t stream) {
+  SV_REQUIRE(p && g && m && v && step >= 1, "sv_adamw_flat: bad args");
+  SV_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                 (((uintptr_t)p_bf16) & 7) == 0,
+             "sv_adamw_flat: buffers must be 16-byte aligned");
+  if (n <= 0) return SV_OK;
+  // bias corrections in double on the host, as torch computes them in Python floats
+  const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+  const float bc2 = (float)(1.0 - pow((double)beta2, (double)step));
+  adamw_kernel<<<stream_grid(n, 4), kThreads, 0, (hipStream_t)stream>>>(
+      p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale);
+  return check_launch("sv_adamw_flat");
+}
+
+int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream) {
+  SV_REQUIRE(x && y, "sv_cast_f32_bf16: null");
+  if (n <= 0) return SV_OK;
+  cast_bf16_kernel<<<stream_grid(n, 1), kThreads, 0, (hipStream_t)stream>>>(x, y, n);
+  return check_launch("sv_cast_f32_bf16");
+}
+
+}  // extern "C"

@@ -1,0 +1,308 @@
+"""Typed host-side launch helpers over the C ABI (``include/sv_kernels.h``).
+
+Every helper takes/returns torch device tensors, validates shapes on the host *before* launching
+(the kernels assume the grid/shape contract checked here), allocates outputs and workspaces from
+PyTorch's caching allocator and enqueues on the current stream.  There is no fallback path: a
+missing library or a CPU tensor raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import native as nv
+from .native import SV_BF16, SV_F32, call, dt, ptr, value
+
+EPS_LN = 1e-6
+
+
+def _check(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _cdt(compute_bf16: bool) -> int:
+    return SV_BF16 if compute_bf16 else SV_F32
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM
+def gemm(
+    A: torch.Tensor,
+    B: torch.Tensor,
+    *,
+    M: int,
+    N: int,
+    K: int,
+    a_kmajor: bool,
+    b_kmajor: bool,
+    lda: int,
+    ldb: int,
+    epilogue: int = nv.SV_EPI_STORE,
+    C: torch.Tensor | None = None,
+    C2: torch.Tensor | None = None,
+    ldc: int | None = None,
+    bias: torch.Tensor | None = None,
+    gamma: torch.Tensor | None = None,
+    aux: torch.Tensor | None = None,
+    ld_aux: int | None = None,
+    a_scale_k: torch.Tensor | None = None,
+    split_k: int = 1,
+    compute_bf16: bool = True,
+) -> torch.Tensor:
+    """C = epilogue(A(m,k) . B(k,n)); see sv_gemm in include/sv_kernels.h for the layouts."""
+    _check(C is not None, "gemm: output tensor C is required")
+    need_a = (M - 1) * lda + K if a_kmajor else (K - 1) * lda + M
+    need_b = (N - 1) * ldb + K if b_kmajor else (K - 1) * ldb + N
+    _check(A.numel() >= need_a, f"gemm: A too small ({A.numel()} < {need_a})")
+    _check(B.numel() >= need_b, f"gemm: B too small ({B.numel()} < {need_b})")
+    if epilogue == nv.SV_EPI_SLAB:
+        _check(C.dtype == torch.float32 and C.numel() >= split_k * M * N, "gemm: slab too small")
+    else:
+        ldc = N if ldc is None else ldc
+        _check(C.numel() >= (M - 1) * ldc + N, "gemm: C too small")
+    if bias is not None:
+        _check(bias.numel() >= N and bias.dtype == torch.float32, "gemm: bad bias")
+    d = nv.GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.a_dtype, d.a_kmajor, d.lda = ptr(A), dt(A), int(a_kmajor), lda
+    d.B, d.b_dtype, d.b_kmajor, d.ldb = ptr(B), dt(B), int(b_kmajor), ldb
+    d.a_scale_k = ptr(a_scale_k)
+    d.epilogue = epilogue
+    d.C, d.c_dtype, d.ldc = ptr(C), dt(C), ldc if ldc is not None else N
+    if C2 is not None:
+        d.C2, d.c2_dtype = ptr(C2), dt(C2)
+    d.bias = ptr(bias)
+    d.gamma = ptr(gamma)
+    if aux is not None:
+        d.aux, d.aux_dtype, d.ld_aux = ptr(aux), dt(aux), ld_aux if ld_aux is not None else N
+    d.split_k = split_k
+    d.compute = _cdt(compute_bf16)
+    call("sv_gemm", ctypes.byref(d))
+    return C
+
+
+def linear_fwd(x2d, w, *, out, bias=None, epilogue=nv.SV_EPI_STORE, out2=None, gamma=None, residual=None,
+               compute_bf16=True):
+    """out[M,N] = epilogue(x2d[M,K] @ w[N,K]^T)  (torch Linear weight layout)."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    return gemm(x2d, w, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=K, ldb=K, epilogue=epilogue, C=out,
+                C2=out2, bias=bias, gamma=gamma, aux=residual, compute_bf16=compute_bf16)
+
+
+def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=None, compute_bf16=True):
+    """out[M,K] = epilogue((dy2d[M,N] * a_scale_k[N]) @ w[N,K])."""
+    M, N = dy2d.shape
+    K = w.shape[1]
+    return gemm(dy2d, w, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=N, ldb=K, epilogue=epilogue, C=out,
+                a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16)
+
+
+def _wgrad_split(tiles: int, K: int) -> int:
+    split = max(1, -(-1024 // max(tiles, 1)))
+    return max(1, min(split, -(-K // 256)))
+
+
+def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, compute_bf16=True) -> torch.Tensor:
+    """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
+    writes -- or, with ``accumulate``, adds -- into ``out``)."""
+    M, N = dy2d.shape
+    K = x2d.shape[1]
+    tiles = -(-N // 128) * -(-K // 128)
+    split = _wgrad_split(tiles, M)
+    slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
+    gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, epilogue=nv.SV_EPI_SLAB,
+         C=slab, split_k=split, compute_bf16=compute_bf16)
+    if out is None:
+        if split == 1 and not accumulate:
+            return slab.view(N, K)
+        out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
+        accumulate = False
+    _check(out.numel() == N * K and out.is_contiguous(), "linear_wgrad: bad out")
+    call("sv_reduce_partials", ptr(slab), split, N * K, ptr(out), 1.0, int(accumulate))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# reductions
+def reduce_into(part: torch.Tensor, nparts: int, out: torch.Tensor, accumulate: bool = True, alpha: float = 1.0):
+    n = out.numel()
+    _check(part.numel() >= nparts * n, "reduce_into: partial buffer too small")
+    _check(out.dtype == torch.float32 and out.is_contiguous(), "reduce_into: out must be contiguous f32")
+    call("sv_reduce_partials", ptr(part), nparts, n, ptr(out), alpha, int(accumulate))
+
+
+def colsum_into(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = True):
+    rows, C = x2d.shape
+    P = value("sv_colsum_nparts", rows, C)
+    part = torch.empty(P * C, device=x2d.device, dtype=torch.float32)
+    call("sv_colsum", ptr(x2d), dt(x2d), rows, C, ptr(part))
+    reduce_into(part, P, out, accumulate)
+
+
+def colsum(x2d: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(x2d.shape[1], device=x2d.device, dtype=torch.float32)
+    colsum_into(x2d, out, accumulate=False)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# LayerNorm
+def layernorm_fwd(x2d, w, b, *, out_dtype, eps=EPS_LN):
+    rows, C = x2d.shape
+    y = torch.empty(rows, C, device=x2d.device, dtype=out_dtype)
+    mean = torch.empty(rows, device=x2d.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_layernorm_fwd", ptr(x2d), dt(x2d), ptr(w), ptr(b), ptr(y), dt(y), ptr(mean), ptr(rstd), rows, C, eps)
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=False):
+    rows, C = x2d.shape
+    _check(dy2d.dtype == torch.float32 and dy2d.shape == (rows, C), "layernorm_bwd: dy must be f32 [rows,C]")
+    if dx is None:
+        dx = torch.empty(rows, C, device=x2d.device, dtype=torch.float32)
+    P = value("sv_layernorm_bwd_nparts", rows, C)
+    pw = torch.empty(2, P * C, device=x2d.device, dtype=torch.float32)
+    call("sv_layernorm_bwd", ptr(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx),
+         int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
+    if dw is not None:
+        reduce_into(pw[0], P, dw)
+    if db is not None:
+        reduce_into(pw[1], P, db)
+    return dx
+
+
+# ----------------------------------------------------------------------------------------------
+# depthwise 7x7 + LN
+def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN):
+    B, H, W, C = x4d.shape
+    _check(C % 64 == 0, "dwconv7: C must be a multiple of 64")
+    z = torch.empty(B, H, W, C, device=x4d.device, dtype=act_dtype)
+    y = torch.empty(B * H * W, C, device=x4d.device, dtype=act_dtype)
+    mean = torch.empty(B * H * W, device=x4d.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_dwconv7_ln_fwd", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw), ptr(lnw), ptr(lnb), eps, ptr(z), dt(z),
+         ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C)
+    return z, y, mean, rstd
+
+
+def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True):
+    B, H, W, C = dz4d.shape
+    _check(dx4d.shape == dz4d.shape and dx4d.dtype == torch.float32, "dwconv7_bwd_data: shape")
+    call("sv_dwconv7_bwd_data", ptr(dz4d), ptr(wdw), ptr(dx4d), int(accumulate), B, H, W, C)
+
+
+def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
+    B, H, W, C = dz4d.shape
+    P = value("sv_dwconv7_bwd_weight_nparts", B, H, W, C)
+    pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
+    pb = torch.empty(P * C, device=dz4d.device, dtype=torch.float32)
+    call("sv_dwconv7_bwd_weight", ptr(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb), B, H, W, C)
+    reduce_into(pw, P, dw)
+    reduce_into(pb, P, db)
+
+
+# ----------------------------------------------------------------------------------------------
+# stem / downsample / pool
+def stem_fwd(img, w, b, lnw, lnb, *, eps=EPS_LN):
+    B, Cin, H, W = img.shape
+    _check(Cin == 3 and H % 4 == 0 and W % 4 == 0, "stem: expects [B,3,H,W] with H,W % 4 == 0")
+    _check(img.dtype == torch.float32 and img.is_contiguous(), "stem: image must be contiguous f32 NCHW")
+    C = w.shape[0]
+    y = torch.empty(B, H // 4, W // 4, C, device=img.device, dtype=torch.float32)
+    mean = torch.empty(B * (H // 4) * (W // 4), device=img.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_stem_patchify_ln_fwd", ptr(img), ptr(w), ptr(b), ptr(lnw), ptr(lnb), eps, ptr(y), dt(y), ptr(mean),
+         ptr(rstd), B, H, W, C)
+    return y, mean, rstd
+
+
+def stem_bwd(img, w, b, lnw, mean, rstd, dy, *, dw, db, dlnw, dlnb):
+    B, _, H, W = img.shape
+    C = w.shape[0]
+    P = value("sv_stem_patchify_ln_bwd_nparts", B, H, W, C)
+    pw = torch.empty(P * C * 48, device=img.device, dtype=torch.float32)
+    pv = torch.empty(3, P * C, device=img.device, dtype=torch.float32)
+    call("sv_stem_patchify_ln_bwd", ptr(img), ptr(w), ptr(b), ptr(lnw), ptr(mean), ptr(rstd), ptr(dy), ptr(pw),
+         ptr(pv[0]), ptr(pv[1]), ptr(pv[2]), B, H, W, C)
+    reduce_into(pw, P, dw)
+    reduce_into(pv[0], P, db)
+    reduce_into(pv[1], P, dlnw)
+    reduce_into(pv[2], P, dlnb)
+
+
+def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):
+    B, H, W, C = x4d.shape
+    _check(H % 2 == 0 and W % 2 == 0, "downsample: H, W must be even")
+    patches = torch.empty(B * (H // 2) * (W // 2), 4 * C, device=x4d.device, dtype=act_dtype)
+    mean = torch.empty(B * H * W, device=x4d.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_downsample_ln_patch2_fwd", ptr(x4d), ptr(lnw), ptr(lnb), eps, ptr(patches), dt(patches), ptr(mean),
+         ptr(rstd), B, H, W, C)
+    return patches, mean, rstd
+
+
+def downsample_bwd(dpatches, x4d, mean, rstd, lnw, *, dlnw, dlnb):
+    B, H, W, C = x4d.shape
+    dx = torch.empty(B, H, W, C, device=x4d.device, dtype=torch.float32)
+    P = value("sv_downsample_ln_patch2_bwd_nparts", B, H, W, C)
+    pv = torch.empty(2, P * C, device=x4d.device, dtype=torch.float32)
+    call("sv_downsample_ln_patch2_bwd", ptr(dpatches), ptr(x4d), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(pv[0]),
+         ptr(pv[1]), B, H, W, C)
+    reduce_into(pv[0], P, dlnw)
+    reduce_into(pv[1], P, dlnb)
+    return dx
+
+
+def pool_ln_fwd(x4d, lnw, lnb, *, eps=EPS_LN):
+    B, H, W, C = x4d.shape
+    pooled = torch.empty(B, C, device=x4d.device, dtype=torch.float32)
+    feat = torch.empty_like(pooled)
+    mean = torch.empty(B, device=x4d.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_pool_ln_fwd", ptr(x4d), ptr(lnw), ptr(lnb), eps, ptr(pooled), ptr(feat), ptr(mean), ptr(rstd), B,
+         H * W, C)
+    return feat, pooled, mean, rstd
+
+
+def pool_ln_bwd(dfeat, pooled, mean, rstd, lnw, shape, *, dlnw, dlnb):
+    B, H, W, C = shape
+    dx = torch.empty(B, H, W, C, device=dfeat.device, dtype=torch.float32)
+    pv = torch.empty(2, B * C, device=dfeat.device, dtype=torch.float32)
+    call("sv_pool_ln_bwd", ptr(dfeat.contiguous()), ptr(pooled), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(pv[0]),
+         ptr(pv[1]), B, H * W, C)
+    reduce_into(pv[0], B, dlnw)
+    reduce_into(pv[1], B, dlnb)
+    return dx
+
+
+# ----------------------------------------------------------------------------------------------
+# optimizer pieces
+def cast_bf16(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _check(x.dtype == torch.float32 and x.is_contiguous(), "cast_bf16: need contiguous f32")
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    call("sv_cast_f32_bf16", ptr(x), ptr(out), x.numel())
+    return out
+
+
+def grad_clip_coef(g_flat: torch.Tensor, max_norm: float) -> torch.Tensor:
+    """Device tensor [norm, coef] with coef = min(1, max_norm/(norm+1e-6)) -- no host sync."""
+    n = g_flat.numel()
+    P = value("sv_sqnorm_nparts", n)
+    part = torch.empty(P, device=g_flat.device, dtype=torch.float32)
+    call("sv_sqnorm_partial", ptr(g_flat), n, ptr(part))
+    out = torch.empty(2, device=g_flat.device, dtype=torch.float32)
+    call("sv_clip_coef", ptr(part), P, float(max_norm), ptr(out))
+    return out
+
+
+def adamw_flat(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=None):
+    n = p.numel()
+    _check(g.numel() == n and m.numel() == n and v.numel() == n, "adamw_flat: size mismatch")
+    call("sv_adamw_flat", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(lr), float(beta1), float(beta2),
+         float(eps), float(weight_decay), int(step), ptr(grad_scale))

@@ -1,0 +1,153 @@
+"""ctypes binding of ``libsv_kernels.so`` -- the C ABI declared in ``include/sv_kernels.h``.
+
+The product path has no CPU or PyTorch fallback: if the library is missing, fails to load, or a
+declared symbol is absent, every call raises.  Tensors cross the boundary as raw device pointers
+(``tensor.data_ptr()``) and the work is enqueued on ``torch.cuda.current_stream()``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsv_kernels.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
+
+SV_F32, SV_BF16 = 0, 1
+SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB = range(5)
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", _i32), ("N", _i32), ("K", _i32),
+        ("A", _p), ("a_dtype", _i32), ("a_kmajor", _i32), ("lda", _i64),
+        ("B", _p), ("b_dtype", _i32), ("b_kmajor", _i32), ("ldb", _i64),
+        ("a_scale_k", _p),
+        ("epilogue", _i32),
+        ("C", _p), ("c_dtype", _i32), ("ldc", _i64),
+        ("C2", _p), ("c2_dtype", _i32),
+        ("bias", _p),
+        ("gamma", _p),
+        ("aux", _p), ("aux_dtype", _i32), ("ld_aux", _i64),
+        ("split_k", _i32),
+        ("compute", _i32),
+    ]
+
+
+# name -> argtypes (restype is int for all entry points unless listed in _RESTYPES)
+_SIGS = {
+    "sv_version": [],
+    "sv_last_error_string": [],
+    "sv_build_target": [],
+    "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
+    "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
+    "sv_layernorm_bwd_nparts": [_i64, _i32],
+    "sv_layernorm_bwd": [_p, _p, _i32, _p, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p],
+    "sv_dwconv7_ln_fwd": [_p, _i32, _p, _p, _p, _p, _f32, _p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_weight_nparts": [_i32, _i32, _i32, _i32],
+    "sv_dwconv7_bwd_weight": [_p, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_stem_patchify_ln_fwd": [_p, _p, _p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_stem_patchify_ln_bwd_nparts": [_i32, _i32, _i32, _i32],
+    "sv_stem_patchify_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_downsample_ln_patch2_fwd": [_p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_downsample_ln_patch2_bwd_nparts": [_i32, _i32, _i32, _i32],
+    "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_pool_ln_fwd": [_p, _p, _p, _f32, _p, _p, _p, _p, _i32, _i32, _i32, _p],
+    "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
+    "sv_reduce_partials": [_p, _i32, _i64, _p, _f32, _i32, _p],
+    "sv_colsum_nparts": [_i64, _i32],
+    "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
+    "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
+    "sv_sqnorm_nparts": [_i64],
+    "sv_sqnorm_partial": [_p, _i64, _p, _p],
+    "sv_clip_coef": [_p, _i32, _f32, _p, _p],
+    "sv_adamw_flat": [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _p, _p],
+    "sv_cast_f32_bf16": [_p, _p, _i64, _p],
+}
+_RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p}
+# entry points that return a value (size / count) rather than an sv_status
+_VALUE_FNS = {n for n in _SIGS if n.endswith("_nparts")} | {"sv_version"}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def header_symbols(path: str = HEADER) -> list[str]:
+    """Every ``sv_*`` function declared in include/sv_kernels.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sv_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load the kernel library (once) and bind every declared entry point.  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"spine_vision_amd: native kernel library not found at {LIB_PATH}; "
+                "run `python __graft_entry__.py` (hipcc --offload-arch=gfx950) first"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        missing = [s for s in header_symbols() if not hasattr(L, s)]
+        if missing:
+            raise RuntimeError(f"spine_vision_amd: {LIB_PATH} lacks symbols {missing}")
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = L
+        return L
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def call(name: str, *args):
+    """Invoke an sv_* entry point on the current stream; raise RuntimeError on a non-zero status."""
+    L = lib()
+    fn = getattr(L, name)
+    if name in _VALUE_FNS:
+        return fn(*args)
+    rc = fn(*args, _stream())
+    if rc != 0:
+        msg = L.sv_last_error_string().decode()
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def value(name: str, *args) -> int:
+    return getattr(lib(), name)(*args)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    """Device pointer of a tensor (None -> NULL); refuses CPU tensors loudly."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("spine_vision_amd kernels need device tensors (got a CPU tensor)")
+    return t.data_ptr()
+
+
+def dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return SV_F32
+    if t.dtype == torch.bfloat16:
+        return SV_BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")

@@ -1,0 +1,263 @@
+"""Per-kernel parity on the MI355X: every HIP entry point against a plain PyTorch fp32 CPU
+reference of the same op (fp32/f32-MFMA mode to ~1e-5, bf16 mode to bf16 tolerances)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from spine_vision_amd import kernels as K
+from spine_vision_amd import native as nv
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def maxrel(a, b, floor=1e-3):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return ((a - b).abs() / (b.abs() + floor * b.abs().max())).max().item()
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+# ---------------------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("compute_bf16", [False, True])
+@pytest.mark.parametrize("a_kmajor", [True, False])
+@pytest.mark.parametrize("b_kmajor", [True, False])
+@pytest.mark.parametrize("shape", [(256, 128, 64), (200, 136, 96), (8, 512, 40), (1000, 24, 1024)])
+def test_gemm_layouts(dev, compute_bf16, a_kmajor, b_kmajor, shape):
+    M, N, Kd = shape
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + Kd)
+    Am = torch.randn(M, Kd, generator=g)
+    Bm = torch.randn(Kd, N, generator=g)
+    ref = (bf(Am) @ bf(Bm)) if compute_bf16 else Am.double() @ Bm.double()
+    dtA = torch.bfloat16 if compute_bf16 else torch.float32
+    Ast = (Am if a_kmajor else Am.t()).contiguous().to(dtA)
+    Bst = (Bm.t() if b_kmajor else Bm).contiguous().to(dtA)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(Ast.to(dev), Bst.to(dev), M=M, N=N, K=Kd, a_kmajor=a_kmajor, b_kmajor=b_kmajor,
+           lda=Kd if a_kmajor else M, ldb=Kd if b_kmajor else N, C=C, compute_bf16=compute_bf16)
+    tol = 2e-3 if compute_bf16 else 1e-5
+    assert rel(C, ref) < tol
+
+
+def test_gemm_f32_operand_bf16_compute_with_scale(dev):
+    M, N, Kd = 300, 256, 128
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(M, Kd, generator=g)
+    W = torch.randn(Kd, N, generator=g)  # stored [K][N] -> b_kmajor False (dgrad layout)
+    s = torch.rand(Kd, generator=g) + 0.5
+    C = torch.empty(M, N, device=dev)
+    K.gemm(A.to(dev), W.to(torch.bfloat16).to(dev), M=M, N=N, K=Kd, a_kmajor=True, b_kmajor=False, lda=Kd, ldb=N,
+           C=C, a_scale_k=s.to(dev), compute_bf16=True)
+    ref = bf(A * s) @ bf(W)
+    assert rel(C, ref) < 2e-3
+
+
+@pytest.mark.parametrize("compute_bf16", [False, True])
+def test_gemm_epilogues(dev, compute_bf16):
+    M, Cc = 384, 128
+    g = torch.Generator().manual_seed(2)
+    y = torch.randn(M, Cc, generator=g)
+    w1 = torch.randn(4 * Cc, Cc, generator=g) * 0.1
+    b1 = torch.randn(4 * Cc, generator=g) * 0.1
+    w2 = torch.randn(Cc, 4 * Cc, generator=g) * 0.05
+    b2 = torch.randn(Cc, generator=g) * 0.1
+    gam = torch.rand(Cc, generator=g) * 0.25 + 0.05
+    x = torch.randn(M, Cc, generator=g)
+    act = torch.bfloat16 if compute_bf16 else torch.float32
+    q = bf if compute_bf16 else (lambda t: t)
+    # fc1 + GELU2
+    h = torch.empty(M, 4 * Cc, device=dev, dtype=act)
+    a = torch.empty_like(h)
+    K.linear_fwd(y.to(act).to(dev), w1.to(act).to(dev), out=h, out2=a, bias=b1.to(dev),
+                 epilogue=nv.SV_EPI_BIAS_GELU2, compute_bf16=compute_bf16)
+    h_ref = q(y) @ q(w1).t() + b1
+    tol = 1e-2 if compute_bf16 else 1e-5
+    assert rel(h, h_ref) < tol
+    assert rel(a, F.gelu(h_ref)) < tol
+    # fc2 + gamma + residual
+    out = torch.empty(M, Cc, device=dev)
+    K.linear_fwd(a, w2.to(act).to(dev), out=out, bias=b2.to(dev), gamma=gam.to(dev), residual=x.to(dev),
+                 epilogue=nv.SV_EPI_BIAS_GAMMA_RES, compute_bf16=compute_bf16)
+    a_used = a.float().cpu()
+    out_ref = x + gam * (a_used @ q(w2).t() + b2)
+    assert rel(out, out_ref) < tol
+    # dgrad through fc2 + GELU'
+    d = torch.randn(M, Cc, generator=g)
+    dh = torch.empty(M, 4 * Cc, device=dev, dtype=act)
+    K.linear_dgrad(d.to(dev), w2.to(act).to(dev), out=dh, epilogue=nv.SV_EPI_GELU_GRAD, a_scale_k=gam.to(dev),
+                   aux=h, compute_bf16=compute_bf16)
+    hh = h.float().cpu().requires_grad_(True)
+    F.gelu(hh).backward(q(d * gam) @ q(w2))
+    assert rel(dh, hh.grad) < tol
+    # wgrad slabs
+    G = K.linear_wgrad(d.to(dev), a, compute_bf16=compute_bf16)
+    G_ref = q(d).t() @ a_used
+    assert rel(G, G_ref) < tol
+
+
+# ---------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("C", [128, 192, 512, 1024])
+def test_layernorm_fwd_bwd(dev, C):
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(333, C, generator=g) * 2 + 0.5
+    w = torch.rand(C, generator=g) + 0.5
+    b = torch.randn(C, generator=g)
+    dy = torch.randn(333, C, generator=g)
+    y, mean, rstd = K.layernorm_fwd(x.to(dev), w.to(dev), b.to(dev), out_dtype=torch.float32)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-6)
+    yr.backward(dy)
+    assert rel(y, yr) < 1e-5
+    dw = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    dx = K.layernorm_bwd(dy.to(dev), x.to(dev), mean, rstd, w.to(dev), dw=dw, db=db)
+    assert rel(dx, xr.grad) < 1e-5
+    assert rel(dw, wr.grad) < 1e-5
+    assert rel(db, br.grad) < 1e-5
+
+
+# ------------------------------------------------------------------------------ depthwise conv
+@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64), (3, 4, 4, 256), (2, 2, 2, 192)])
+def test_dwconv7_fwd_bwd(dev, shape):
+    B, H, W, C = shape
+    g = torch.Generator().manual_seed(B * H * W + C)
+    x = torch.randn(B, H, W, C, generator=g)
+    w = torch.randn(C, 1, 7, 7, generator=g) * 0.1
+    bias = torch.randn(C, generator=g) * 0.1
+    lnw = torch.rand(C, generator=g) + 0.5
+    lnb = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(B, H, W, C, generator=g)
+    z, y, mean, rstd = K.dwconv7_ln_fwd(x.to(dev), w.to(dev), bias.to(dev), lnw.to(dev), lnb.to(dev),
+                                        act_dtype=torch.float32)
+    xr = x.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = bias.clone().requires_grad_(True)
+    zr = F.conv2d(xr, wr, br, padding=3, groups=C)
+    zr_nhwc = zr.permute(0, 2, 3, 1)
+    yr = F.layer_norm(zr_nhwc, (C,), lnw, lnb, 1e-6)
+    assert rel(z, zr_nhwc) < 1e-5
+    assert rel(y.view(B, H, W, C), yr) < 1e-5
+    # backward of the conv alone: dz given
+    zr_nhwc.backward(dy)
+    dx = torch.zeros(B, H, W, C, device=dev)
+    K.dwconv7_bwd_data(dy.to(dev), w.to(dev), dx, accumulate=True)
+    assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-5
+    dw = torch.zeros(C, 49, device=dev)
+    db = torch.zeros(C, device=dev)
+    K.dwconv7_bwd_weight(dy.to(dev), x.to(dev), dw=dw, db=db)
+    assert rel(dw, wr.grad.view(C, 49)) < 1e-5
+    assert rel(db, br.grad) < 1e-5
+
+
+# ------------------------------------------------------------------------ stem / downsample / pool
+@pytest.mark.parametrize("C", [128, 192])
+def test_stem(dev, C):
+    g = torch.Generator().manual_seed(C)
+    B, H, W = 2, 32, 24
+    img = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(C, 3, 4, 4, generator=g) * 0.2
+    b = torch.randn(C, generator=g) * 0.1
+    lnw = torch.rand(C, generator=g) + 0.5
+    lnb = torch.randn(C, generator=g) * 0.1
+    y, mean, rstd = K.stem_fwd(img.to(dev), w.to(dev), b.to(dev), lnw.to(dev), lnb.to(dev))
+    wr, br, lwr, lbr = (t.clone().requires_grad_(True) for t in (w, b, lnw, lnb))
+    zr = F.conv2d(img, wr, br, stride=4).permute(0, 2, 3, 1)
+    yr = F.layer_norm(zr, (C,), lwr, lbr, 1e-6)
+    assert rel(y, yr) < 1e-5
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    grads = [torch.zeros_like(t, device=dev) for t in (w, b, lnw, lnb)]
+    K.stem_bwd(img.to(dev), w.to(dev), b.to(dev), lnw.to(dev), mean, rstd, dy.to(dev),
+               dw=grads[0], db=grads[1], dlnw=grads[2], dlnb=grads[3])
+    for got, ref in zip(grads, (wr.grad, br.grad, lwr.grad, lbr.grad)):
+        assert rel(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_downsample(dev, C):
+    g = torch.Generator().manual_seed(C + 1)
+    B, H, W = 2, 8, 6
+    x = torch.randn(B, H, W, C, generator=g)
+    lnw = torch.rand(C, generator=g) + 0.5
+    lnb = torch.randn(C, generator=g) * 0.1
+    wc = torch.randn(2 * C, C, 2, 2, generator=g) * 0.05
+    bc = torch.randn(2 * C, generator=g) * 0.1
+    patches, mean, rstd = K.downsample_fwd(x.to(dev), lnw.to(dev), lnb.to(dev), act_dtype=torch.float32)
+    out = torch.empty(B * (H // 2) * (W // 2), 2 * C, device=dev)
+    K.linear_fwd(patches, wc.reshape(2 * C, 4 * C).to(dev), out=out, bias=bc.to(dev), compute_bf16=False)
+    xr = x.clone().requires_grad_(True)
+    lwr, lbr = lnw.clone().requires_grad_(True), lnb.clone().requires_grad_(True)
+    n = F.layer_norm(xr, (C,), lwr, lbr, 1e-6).permute(0, 3, 1, 2)
+    o = F.conv2d(n, wc, bc, stride=2).permute(0, 2, 3, 1)
+    assert rel(out.view(o.shape), o) < 1e-5
+    dpatch = torch.randn(patches.shape, generator=g)
+    # autograd of the LN+gather alone: reconstruct patches from n and backprop dpatch
+    Ho, Wo = H // 2, W // 2
+    pr = n.reshape(B, C, Ho, 2, Wo, 2).permute(0, 2, 4, 1, 3, 5).reshape(B * Ho * Wo, 4 * C)
+    assert rel(patches, pr) < 1e-5
+    pr.backward(dpatch)
+    dlnw = torch.zeros(C, device=dev)
+    dlnb = torch.zeros(C, device=dev)
+    dx = K.downsample_bwd(dpatch.to(dev), x.to(dev), mean, rstd, lnw.to(dev), dlnw=dlnw, dlnb=dlnb)
+    assert rel(dx, xr.grad) < 1e-5
+    assert rel(dlnw, lwr.grad) < 1e-5
+    assert rel(dlnb, lbr.grad) < 1e-5
+
+
+def test_pool_ln(dev):
+    g = torch.Generator().manual_seed(5)
+    B, H, W, C = 3, 4, 5, 1024
+    x = torch.randn(B, H, W, C, generator=g)
+    lnw = torch.rand(C, generator=g) + 0.5
+    lnb = torch.randn(C, generator=g) * 0.1
+    feat, pooled, mean, rstd = K.pool_ln_fwd(x.to(dev), lnw.to(dev), lnb.to(dev))
+    xr = x.clone().requires_grad_(True)
+    lwr, lbr = lnw.clone().requires_grad_(True), lnb.clone().requires_grad_(True)
+    fr = F.layer_norm(xr.mean((1, 2)), (C,), lwr, lbr, 1e-6)
+    assert rel(feat, fr) < 1e-5
+    df = torch.randn(B, C, generator=g)
+    fr.backward(df)
+    dlnw = torch.zeros(C, device=dev)
+    dlnb = torch.zeros(C, device=dev)
+    dx = K.pool_ln_bwd(df.to(dev), pooled, mean, rstd, lnw.to(dev), (B, H, W, C), dlnw=dlnw, dlnb=dlnb)
+    assert rel(dx, xr.grad) < 1e-5
+    assert rel(dlnw, lwr.grad) < 1e-5
+    assert rel(dlnb, lbr.grad) < 1e-5
+
+
+# ----------------------------------------------------------------------------------- optimizer
+def test_adamw_and_clip(dev):
+    from oracle.step import adamw_reference
+
+    g = torch.Generator().manual_seed(9)
+    n = 100_003
+    p = torch.randn(n, generator=g)
+    gr = torch.randn(n, generator=g) * 3
+    m = torch.randn(n, generator=g) * 0.1
+    v = torch.rand(n, generator=g) * 0.1
+    out = K.grad_clip_coef(gr.to(dev), 1.0)
+    norm = gr.double().norm().item()
+    assert abs(out[0].item() - norm) / norm < 1e-5
+    coef = min(1.0, 1.0 / (norm + 1e-6))
+    assert abs(out[1].item() - coef) / coef < 1e-5
+    pd, md, vd = p.to(dev), m.to(dev), v.to(dev)
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    K.adamw_flat(pd, gr.to(dev), md, vd, pb, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, step=3,
+                 grad_scale=out[1:2])
+    pr, mr, vr = adamw_reference(p.double(), gr.double() * coef, m.double(), v.double(), lr=1e-3, beta1=0.9,
+                                 beta2=0.999, eps=1e-8, weight_decay=1e-2, step=3)
+    assert maxrel(pd, pr) < 1e-5
+    assert maxrel(md, mr) < 1e-5
+    assert maxrel(vd, vr) < 1e-5
+    assert torch.equal(pb.cpu(), pd.cpu().to(torch.bfloat16))
