@@ -60,7 +60,9 @@ typedef enum {
   SV_EPI_BIAS_GELU2 = 1,     /* C = acc + bias[n]  (pre-activation), C2 = GELU_erf(C)             */
   SV_EPI_BIAS_GAMMA_RES = 2, /* C = aux[m,n] + gamma[n] * (acc + bias[n])   (layer-scale residual) */
   SV_EPI_GELU_GRAD = 3,      /* C = acc * GELU_erf'(aux[m,n])                                      */
-  SV_EPI_SLAB = 4            /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32)       */
+  SV_EPI_SLAB = 4            /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32);      */
+                             /* if C2 != NULL also C2[s][m] = sum_{k in slice s} A(m,k) (f32), i.e.  */
+                             /* the bias gradient of a wgrad GEMM (A = dY^T) without another pass.   */
 } sv_epilogue;
 
 typedef struct {
@@ -70,7 +72,7 @@ typedef struct {
   const float* a_scale_k;    /* optional: A(m,k) *= a_scale_k[k]                                  */
   int32_t epilogue;          /* sv_epilogue                                                       */
   void* C; int32_t c_dtype; int64_t ldc;
-  void* C2; int32_t c2_dtype; /* second output for SV_EPI_BIAS_GELU2 (same ldc)                   */
+  void* C2; int32_t c2_dtype; /* second output: SV_EPI_BIAS_GELU2 (same ldc) / SV_EPI_SLAB colsum  */
   const float* bias;         /* [N] or NULL                                                       */
   const float* gamma;        /* [N]  (SV_EPI_BIAS_GAMMA_RES)                                      */
   const void* aux; int32_t aux_dtype; int64_t ld_aux; /* residual / pre-activation input          */
@@ -149,8 +151,10 @@ int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, c
                    int32_t HW, int32_t C, sv_stream_t stream);
 
 /* ---- reductions used by backward -------------------------------------------------------------
- * out[i] = (accumulate ? out[i] : 0) + alpha * sum_{p<P} part[p*n + i]                             */
-int sv_reduce_partials(const float* part, int32_t P, int64_t n, float* out, float alpha,
+ * Grouped partial-sum reduction (group >= P or <= 0: one group):
+ *   out[g*n + i] = (accumulate ? out[g*n + i] : 0) + alpha * sum_{p in [g*group, (g+1)*group)} part[p*n + i]
+ * The host reduces deep split-K slabs in two passes (groups, then the group sums).                 */
+int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,
                        int32_t accumulate, sv_stream_t stream);
 /* column sums of a [rows][C] matrix into partials [nparts][C]; nparts = sv_colsum_nparts(rows,C). */
 int sv_colsum_nparts(int64_t rows, int32_t C);

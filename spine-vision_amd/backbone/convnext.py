@@ -256,16 +256,16 @@ class ConvNeXtHip(nn.Module):
                 dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
                 K.linear_dgrad(d2, w2, out=dh, epilogue=nv.SV_EPI_GELU_GRAD, a_scale_k=blk.gamma, aux=h,
                                compute_bf16=bf)
-                G = K.linear_wgrad(d2, a, compute_bf16=bf)  # [C, 4C] = d^T a
-                cs = K.colsum(d2)
+                cs = torch.empty(C, device=d.device, dtype=torch.float32)
+                G = K.linear_wgrad(d2, a, bias_out=cs, bias_accumulate=False, compute_bf16=bf)  # [C,4C] = d^T a
                 nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),
                         nv.ptr(blk.gamma), nv.ptr(blk.mlp.fc2.bias), nv.ptr(g(blk.mlp.fc2.weight)),
                         nv.ptr(g(blk.gamma)), nv.ptr(g(blk.mlp.fc2.bias)), C, 4 * C)
                 # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh)
                 dy = torch.empty(M, C, device=d.device, dtype=torch.float32)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
-                K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, compute_bf16=bf)
-                K.colsum_into(dh, g(blk.mlp.fc1.bias))
+                K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
+                               compute_bf16=bf)
                 # LayerNorm + depthwise conv
                 dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
                                      db=g(blk.norm.bias))
@@ -284,8 +284,8 @@ class ConvNeXtHip(nn.Module):
                 wds = self._w(conv.weight, cache).reshape(Cout, 4 * C)
                 dpatch = torch.empty(Mo, 4 * C, device=d.device, dtype=torch.float32)
                 K.linear_dgrad(d2, wds, out=dpatch, compute_bf16=bf)
-                K.linear_wgrad(d2, patches, out=g(conv.weight), accumulate=True, compute_bf16=bf)
-                K.colsum_into(d2, g(conv.bias))
+                K.linear_wgrad(d2, patches, out=g(conv.weight), accumulate=True, bias_out=g(conv.bias),
+                               compute_bf16=bf)
                 d = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight), dlnb=g(ln.bias))
                 self._ready([ln.weight, ln.bias, conv.weight, conv.bias])
         s_mean, s_rstd = tape.stem

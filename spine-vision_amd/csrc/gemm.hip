@@ -178,6 +178,33 @@ __device__ __forceinline__ float frag_f32(const char* __restrict__ img, int base
   return KMAJ ? f[(size_t)(base + (l & 15)) * LD + kk + (l >> 4)] : f[(size_t)(kk + (l >> 4)) * LD + base + (l & 15)];
 }
 
+// sum over the BKT k of A(row, k) from the staged A image (row = one of the BM tile rows)
+template <bool BF16, bool KMAJ>
+__device__ __forceinline__ float colsum_tile(const char* __restrict__ img, int row) {
+  constexpr int LD = Img<BF16, KMAJ>::LD;
+  float s = 0.f;
+  if constexpr (BF16) {
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(img);
+    if (KMAJ) {
+#pragma unroll
+      for (int c = 0; c < BKT; c += 8) {
+        const uint4 v = *reinterpret_cast<const uint4*>(h + (size_t)row * LD + c);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += __uint_as_float(w[j] << 16) + __uint_as_float(w[j] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < BKT; ++k) s += bf2f(h[(size_t)k * LD + row]);
+    }
+  } else {
+    const float* f = reinterpret_cast<const float*>(img);
+#pragma unroll
+    for (int k = 0; k < BKT; ++k) s += KMAJ ? f[(size_t)row * LD + k] : f[(size_t)k * LD + row];
+  }
+  return s;
+}
+
 struct EpiArgs {
   int M, N;
   int epi;
@@ -228,7 +255,8 @@ template <bool BF16, typename TA, typename TB, bool AK, bool BKM>
 __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict__ A, int64_t lda,
                                                             const TB* __restrict__ B, int64_t ldb,
                                                             const float* __restrict__ a_scale, int K,
-                                                            int kper, int tilesM, int tilesN, EpiArgs e) {
+                                                            int kper, int tilesM, int tilesN, EpiArgs e,
+                                                            float* __restrict__ colsum) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ABYTES = Img<BF16, AK>::BYTES, BBYTES = Img<BF16, BKM>::BYTES;
   constexpr int STAGE_BYTES = ABYTES + BBYTES;
@@ -254,6 +282,10 @@ __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fused bias gradient of a wgrad GEMM: sum over this split's k of A(m,k), from the staged tile
+  const bool do_cs = colsum != nullptr && tn == 0;
+  float csum = 0.f;
+
   Stage<BF16, TA, AK> sa;
   Stage<BF16, TB, BKM> sb;
   if (nk > 0) {
@@ -274,6 +306,7 @@ __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict
     }
     const char* ai = cur;
     const char* bi = cur + ABYTES;
+    if (do_cs && threadIdx.x < BM) csum += colsum_tile<BF16, AK>(ai, threadIdx.x);
     if constexpr (BF16) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
@@ -304,6 +337,8 @@ __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict
     }
     __syncthreads();
   }
+
+  if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
 
   // ---- epilogue: per wave, 4 slabs of 16 rows x 64 cols staged through its private LDS region
   float* slab = reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD;
@@ -356,7 +391,7 @@ static int launch(const sv_gemm_desc* d, hipStream_t s) {
   }
   gemm_kernel<BF16, TA, TB, AK, BKM><<<grid, kGemmThreads, lds, s>>>(
       reinterpret_cast<const TA*>(d->A), d->lda, reinterpret_cast<const TB*>(d->B), d->ldb, d->a_scale_k, d->K,
-      kper, tilesM, tilesN, e);
+      kper, tilesM, tilesN, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
   return check_launch("sv_gemm");
 }
 
@@ -392,6 +427,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d->N % 4 == 0, "sv_gemm: N must be a multiple of 4");
   if (d->epilogue == SV_EPI_SLAB) {
     SV_REQUIRE(d->c_dtype == SV_F32, "sv_gemm: slab epilogue writes f32");
+    SV_REQUIRE(!d->C2 || d->c2_dtype == SV_F32, "sv_gemm: slab colsum output is f32");
   } else {
     SV_REQUIRE(d->ldc % 4 == 0, "sv_gemm: ldc must be a multiple of 4");
   }

@@ -14,16 +14,50 @@ namespace sv {
 
 constexpr int kThreads = 256;
 
+// out[g][i] (+)= alpha * sum_{p in group g} part[p][i].  grid = (column tiles, groups); each thread
+// owns 4 consecutive columns (16-B loads) and keeps 8 independent loads in flight per round, so the
+// reduction of deep split-K slabs is bandwidth- rather than latency-bound.
 __global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* __restrict__ part,
-                                                                    int P, int64_t n,
+                                                                    int P, int group, int64_t n,
                                                                     float* __restrict__ out,
                                                                     float alpha, int accumulate) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float s = 0.f;
-    for (int p = 0; p < P; ++p) s += part[(size_t)p * n + i];
-    s *= alpha;
-    out[i] = accumulate ? out[i] + s : s;
+  const int g = blockIdx.y;
+  const int p0 = g * group;
+  int p1 = p0 + group;
+  if (p1 > P) p1 = P;
+  float* o = out + (size_t)g * n;
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  if (i4 + 4 <= n && (n & 3) == 0) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int p = p0;
+    for (; p + 8 <= p1; p += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(part + (size_t)(p + u) * n + i4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; p < p1; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * n + i4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    acc.x *= alpha; acc.y *= alpha; acc.z *= alpha; acc.w *= alpha;
+    float4* op = reinterpret_cast<float4*>(o + i4);
+    if (accumulate) {
+      const float4 q = *op;
+      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+    }
+    *op = acc;
+  } else {
+    for (int64_t i = i4; i < n && i < i4 + 4; ++i) {
+      float s = 0.f;
+      for (int p = p0; p < p1; ++p) s += part[(size_t)p * n + i];
+      s *= alpha;
+      o[i] = accumulate ? o[i] + s : s;
+    }
   }
 }
 
@@ -155,11 +189,16 @@ using namespace sv;
 
 extern "C" {
 
-int sv_reduce_partials(const float* part, int32_t P, int64_t n, float* out, float alpha,
+int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,
                        int32_t accumulate, sv_stream_t stream) {
   SV_REQUIRE(part && out && P >= 1, "sv_reduce_partials: bad args");
+  if (group <= 0 || group > P) group = P;
   if (n <= 0) return SV_OK;
-  reduce_partials_kernel<<<stream_grid(n, 1), kThreads, 0, (hipStream_t)stream>>>(part, P, n, out, alpha, accumulate);
+  const int64_t threads = (n + 3) / 4;
+  const dim3 grid((unsigned)((threads + kThreads - 1) / kThreads), (unsigned)((P + group - 1) / group));
+  if ((n & 3) == 0)
+    SV_REQUIRE((((uintptr_t)part | (uintptr_t)out) & 15) == 0, "sv_reduce_partials: buffers must be 16-B aligned");
+  reduce_partials_kernel<<<grid, kThreads, 0, (hipStream_t)stream>>>(part, P, group, n, out, alpha, accumulate);
   return check_launch("sv_reduce_partials");
 }
 

@@ -18,6 +18,24 @@ from .native import SV_BF16, SV_F32, call, dt, ptr, value
 EPS_LN = 1e-6
 
 
+class GemmProbe:
+    """Times every launch of one GEMM layout class with HIP events on the launching stream
+    (bench.py's live roofline measurement).  key = (a_kmajor, b_kmajor, compute_bf16)."""
+
+    def __init__(self, key: tuple[bool, bool, bool]) -> None:
+        self.key = key
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
+        self.flops = 0.0
+        self.launches = 0
+
+    def elapsed_ms(self) -> float:
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+PROBE: GemmProbe | None = None
+
+
 def _check(cond: bool, msg: str) -> None:
     if not cond:
         raise ValueError(msg)
@@ -80,7 +98,17 @@ def gemm(
         d.aux, d.aux_dtype, d.ld_aux = ptr(aux), dt(aux), ld_aux if ld_aux is not None else N
     d.split_k = split_k
     d.compute = _cdt(compute_bf16)
-    call("sv_gemm", ctypes.byref(d))
+    probe = PROBE
+    if probe is not None and probe.key == (bool(a_kmajor), bool(b_kmajor), bool(compute_bf16)):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        call("sv_gemm", ctypes.byref(d))
+        ev1.record()
+        probe.events.append((ev0, ev1))
+        probe.flops += 2.0 * M * N * K
+        probe.launches += 1
+    else:
+        call("sv_gemm", ctypes.byref(d))
     return C
 
 
@@ -102,37 +130,50 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
 
 
 def _wgrad_split(tiles: int, K: int) -> int:
-    split = max(1, -(-1024 // max(tiles, 1)))
-    return max(1, min(split, -(-K // 256)))
+    """K slices so that tiles*split ~ 512 workgroups (2 per CU), each slice >= 16 k-steps."""
+    split = max(1, -(-512 // max(tiles, 1)))
+    return max(1, min(split, K // 512 if K >= 512 else 1))
 
 
-def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, compute_bf16=True) -> torch.Tensor:
+def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
+                 compute_bf16=True) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
-    writes -- or, with ``accumulate``, adds -- into ``out``)."""
+    writes -- or, with ``accumulate``, adds -- into ``out``).  With ``bias_out`` the column sums of
+    dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     tiles = -(-N // 128) * -(-K // 128)
     split = _wgrad_split(tiles, M)
     slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
+    cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
     gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, epilogue=nv.SV_EPI_SLAB,
-         C=slab, split_k=split, compute_bf16=compute_bf16)
+         C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
+    if cs is not None:
+        reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
     if out is None:
         if split == 1 and not accumulate:
             return slab.view(N, K)
         out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
         accumulate = False
     _check(out.numel() == N * K and out.is_contiguous(), "linear_wgrad: bad out")
-    call("sv_reduce_partials", ptr(slab), split, N * K, ptr(out), 1.0, int(accumulate))
+    reduce_into(slab, split, out, accumulate)
     return out
 
 
 # ----------------------------------------------------------------------------------------------
 # reductions
 def reduce_into(part: torch.Tensor, nparts: int, out: torch.Tensor, accumulate: bool = True, alpha: float = 1.0):
+    """out (+)= alpha * sum of nparts partial rows; deep partial stacks are folded in two passes."""
     n = out.numel()
     _check(part.numel() >= nparts * n, "reduce_into: partial buffer too small")
     _check(out.dtype == torch.float32 and out.is_contiguous(), "reduce_into: out must be contiguous f32")
-    call("sv_reduce_partials", ptr(part), nparts, n, ptr(out), alpha, int(accumulate))
+    if nparts > 32:
+        group = 16
+        G = -(-nparts // group)
+        tmp = torch.empty(G * n, device=out.device, dtype=torch.float32)
+        call("sv_reduce_partials", ptr(part), nparts, group, n, ptr(tmp), 1.0, 0)
+        part, nparts = tmp, G
+    call("sv_reduce_partials", ptr(part), nparts, nparts, n, ptr(out), alpha, int(accumulate))
 
 
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = True):

@@ -65,7 +65,7 @@ _SIGS = {
     "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_pool_ln_fwd": [_p, _p, _p, _f32, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
-    "sv_reduce_partials": [_p, _i32, _i64, _p, _f32, _i32, _p],
+    "sv_reduce_partials": [_p, _i32, _i32, _i64, _p, _f32, _i32, _p],
     "sv_colsum_nparts": [_i64, _i32],
     "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],

@@ -1,0 +1,13 @@
+"""Training path: models, flat-buffer optimizer, RCCL gradient exchange, step engine, trainers."""
+
+from .comm import GradBucketer, broadcast_parameters
+from .engine import StepEngine
+from .flat import FlatArena
+from .models.backbone import BACKBONES, BackboneFactory
+from .models.generic import BaseModel, Classifier, CoordinateRegressor
+from .optim import FlatAdamW
+
+__all__ = [
+    "BACKBONES", "BackboneFactory", "BaseModel", "Classifier", "CoordinateRegressor", "FlatAdamW", "FlatArena",
+    "GradBucketer", "StepEngine", "broadcast_parameters",
+]

@@ -1,0 +1,87 @@
+"""AdamW over the flat arena -- the optimizer behind ``BaseTrainer._create_optimizer``
+(spine_vision/training/trainers/base.py:384-390: ``torch.optim.AdamW(params, lr, weight_decay)``,
+betas (0.9, 0.999), eps 1e-8, one param group, weight decay on every parameter).
+
+It is a ``torch.optim.Optimizer`` so LR schedulers (CosineAnnealingLR etc.) drive
+``param_groups[0]["lr"]`` as in the reference, and its ``state_dict`` has torch's AdamW layout
+(per-parameter ``step``/``exp_avg``/``exp_avg_sq``) so checkpoints interchange with the reference's.
+``step()`` is one HIP kernel per contiguous run of trainable parameters; the clip coefficient is a
+device scalar (no host sync); the bf16 GEMM shadow is refreshed in the same pass.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from .. import kernels as K
+from .flat import FlatArena
+
+
+class FlatAdamW(torch.optim.Optimizer):
+    def __init__(self, arena: FlatArena, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2) -> None:
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(arena.params, defaults)
+        self.arena = arena
+        self.exp_avg = torch.zeros_like(arena.param_flat)
+        self.exp_avg_sq = torch.zeros_like(arena.param_flat)
+        self._step = 0
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: torch.Tensor | None = None):
+        """One AdamW update of every trainable parameter; ``grad_scale`` is an optional device
+        scalar multiplying the gradients first (the clip coefficient)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        group = self.param_groups[0]
+        self._step += 1
+        a = self.arena
+        shadow = a.shadow_flat
+        for s, e in a.trainable_runs():
+            K.adamw_flat(a.param_flat[s:e], a.grad_flat[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e],
+                         shadow[s:e] if shadow is not None else None, lr=group["lr"], beta1=group["betas"][0],
+                         beta2=group["betas"][1], eps=group["eps"], weight_decay=group["weight_decay"],
+                         step=self._step, grad_scale=grad_scale)
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True) -> None:  # grads live in the arena: always zero
+        self.arena.zero_grad()
+
+    # -- torch AdamW-compatible state dict ---------------------------------------------------------
+    def state_dict(self):
+        sd = super().state_dict()
+        a = self.arena
+        state = {}
+        for i, (p, o) in enumerate(zip(a.params, a.offsets)):
+            n = p.numel()
+            state[i] = {
+                "step": torch.tensor(float(self._step)),
+                "exp_avg": self.exp_avg[o : o + n].view_as(p).clone(),
+                "exp_avg_sq": self.exp_avg_sq[o : o + n].view_as(p).clone(),
+            }
+        sd["state"] = state
+        return sd
+
+    def load_state_dict(self, state_dict):
+        groups = state_dict["param_groups"]
+        for g, sg in zip(self.param_groups, groups):
+            for k, v in sg.items():
+                if k != "params":
+                    g[k] = v
+        a = self.arena
+        st = state_dict.get("state", {})
+        steps = []
+        with torch.no_grad():
+            for i, (p, o) in enumerate(zip(a.params, a.offsets)):
+                s = st.get(i)
+                if not s:
+                    continue
+                n = p.numel()
+                self.exp_avg[o : o + n].copy_(s["exp_avg"].reshape(-1).to(self.exp_avg.device))
+                self.exp_avg_sq[o : o + n].copy_(s["exp_avg_sq"].reshape(-1).to(self.exp_avg.device))
+                steps.append(int(float(s["step"])))
+        if steps:
+            self._step = max(steps)

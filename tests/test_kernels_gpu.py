@@ -98,10 +98,34 @@ def test_gemm_epilogues(dev, compute_bf16):
     hh = h.float().cpu().requires_grad_(True)
     F.gelu(hh).backward(q(d * gam) @ q(w2))
     assert rel(dh, hh.grad) < tol
-    # wgrad slabs
-    G = K.linear_wgrad(d.to(dev), a, compute_bf16=compute_bf16)
+    # wgrad slabs (+ fused bias-gradient column sums)
+    cs = torch.zeros(Cc, device=dev)
+    G = K.linear_wgrad(d.to(dev), a, bias_out=cs, compute_bf16=compute_bf16)
     G_ref = q(d).t() @ a_used
     assert rel(G, G_ref) < tol
+    assert rel(cs, q(d).sum(0)) < tol
+
+
+@pytest.mark.parametrize("M", [37, 4096, 70000])
+def test_wgrad_split_and_bias(dev, M):
+    g = torch.Generator().manual_seed(M)
+    N, Kd = 256, 512
+    dy = torch.randn(M, N, generator=g)
+    x = torch.randn(M, Kd, generator=g)
+    out = torch.ones(N, Kd, device=dev)
+    bias = torch.ones(N, device=dev)
+    K.linear_wgrad(dy.to(dev), x.to(dev), out=out, accumulate=True, bias_out=bias, compute_bf16=False)
+    assert rel(out, dy.double().t() @ x.double() + 1) < 1e-5
+    assert rel(bias, dy.double().sum(0) + 1) < 1e-5
+
+
+def test_reduce_partials_deep(dev):
+    g = torch.Generator().manual_seed(3)
+    P, n = 300, 12345 * 4
+    part = torch.randn(P, n, generator=g)
+    out = torch.zeros(n, device=dev)
+    K.reduce_into(part.to(dev).reshape(-1), P, out, accumulate=False)
+    assert rel(out, part.double().sum(0)) < 1e-6
 
 
 # ---------------------------------------------------------------------------------- LayerNorm
