@@ -104,9 +104,10 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
                       const float* lnw, const float* lnb, float eps, void* z, int32_t z_dtype, void* y,
                       int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
                       int32_t C, sv_stream_t stream);
-/* backward-data of the depthwise conv: dx[p] = (accumulate ? dx[p] : 0) + sum_tap w*dz.           */
-int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, int32_t accumulate, int32_t B,
-                        int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+/* backward-data of the depthwise conv: dx[p] = (accumulate ? dx[p] : 0) + sum_tap w*dz; if dx_bf16
+ * != NULL it also receives bf16(dx) -- the GEMM-operand copy of the gradient stream.              */
+int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
+                        int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
 /* backward-weight: per-workgroup partials dw_part [nparts][C*49], db_part [nparts][C].             */
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
 int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float* dw_part,
@@ -136,7 +137,7 @@ int sv_downsample_ln_patch2_fwd(const float* x, const float* lnw, const float* l
 /* dpatches (f32, same layout) -> dx [B,H,W,C] (written), LN weight partials [nparts][C].           */
 int sv_downsample_ln_patch2_bwd_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
 int sv_downsample_ln_patch2_bwd(const float* dpatches, const float* x, const float* mean,
-                                const float* rstd, const float* lnw, float* dx, float* dlnw_part,
+                                const float* rstd, const float* lnw, float* dx, uint16_t* dx_bf16, float* dlnw_part,
                                 float* dlnb_part, int32_t B, int32_t H, int32_t W, int32_t C,
                                 sv_stream_t stream);
 
@@ -145,9 +146,9 @@ int sv_downsample_ln_patch2_bwd(const float* dpatches, const float* x, const flo
 int sv_pool_ln_fwd(const float* x, const float* lnw, const float* lnb, float eps, float* pooled,
                    float* feat, float* mean, float* rstd, int32_t B, int32_t HW, int32_t C,
                    sv_stream_t stream);
-/* dfeat [B,C] -> dx [B,HW,C] (written); dlnw/dlnb partials [B][C].                                */
+/* dfeat [B,C] -> dx [B,HW,C] (written, + optional bf16 copy); dlnw/dlnb partials [B][C].        */
 int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, const float* rstd,
-                   const float* lnw, float* dx, float* dlnw_part, float* dlnb_part, int32_t B,
+                   const float* lnw, float* dx, uint16_t* dx_bf16, float* dlnw_part, float* dlnb_part, int32_t B,
                    int32_t HW, int32_t C, sv_stream_t stream);
 
 /* ---- reductions used by backward -------------------------------------------------------------
@@ -182,6 +183,10 @@ int sv_clip_coef(const float* part, int32_t nparts, float max_norm, float* out, 
 int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n,
                   float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                   const float* grad_scale, sv_stream_t stream);
+/* out[r][k] = bf16(W[r][k] * scale[r]): fc2 weight with the layer-scale gamma folded in, so the fc2
+ * dgrad GEMM reads bf16 operands only.                                                              */
+int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,
+                       sv_stream_t stream);
 /* y = bf16(x) over n elements (weight shadows after load_state_dict / init).                       */
 int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream);
 

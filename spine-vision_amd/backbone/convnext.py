@@ -242,7 +242,9 @@ class ConvNeXtHip(nn.Module):
         cache: dict = tape.wcache
         g = self._grad
         hn = self.head.norm
-        d = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight), dlnb=g(hn.bias))
+        # d: f32 gradient stream (residual accumulation); db: its bf16 copy, the GEMM operand (bf16 mode)
+        d, db = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight),
+                              dlnb=g(hn.bias), with_bf16=bf)
         self._ready([hn.weight, hn.bias])
         for st, (ds_saved, blocks_saved) in zip(reversed(list(self.stages)), reversed(tape.stages)):
             for blk, saved in zip(reversed(list(st.blocks)), reversed(blocks_saved)):
@@ -251,27 +253,32 @@ class ConvNeXtHip(nn.Module):
                 M = B * H * W
                 d2 = d.view(M, C)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
-                w2 = self._w(blk.mlp.fc2.weight, cache)
-                # fc2: dh = ((d * gamma) @ W2) * GELU'(h)
+                # fc2: dh = ((d * gamma) @ W2) * GELU'(h).  bf16 mode folds gamma into a bf16 copy of W2
                 dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
-                K.linear_dgrad(d2, w2, out=dh, epilogue=nv.SV_EPI_GELU_GRAD, a_scale_k=blk.gamma, aux=h,
-                               compute_bf16=bf)
+                if bf:
+                    dsrc = db.view(M, C)
+                    w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+                    K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_GELU_GRAD, aux=h, compute_bf16=True)
+                else:
+                    dsrc = d2
+                    K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_GELU_GRAD,
+                                   a_scale_k=blk.gamma, aux=h, compute_bf16=False)
                 cs = torch.empty(C, device=d.device, dtype=torch.float32)
-                G = K.linear_wgrad(d2, a, bias_out=cs, bias_accumulate=False, compute_bf16=bf)  # [C,4C] = d^T a
+                G = K.linear_wgrad(dsrc, a, bias_out=cs, bias_accumulate=False, compute_bf16=bf)  # [C,4C] = d^T a
                 nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),
                         nv.ptr(blk.gamma), nv.ptr(blk.mlp.fc2.bias), nv.ptr(g(blk.mlp.fc2.weight)),
                         nv.ptr(g(blk.gamma)), nv.ptr(g(blk.mlp.fc2.bias)), C, 4 * C)
-                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh)
+                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM)
                 dy = torch.empty(M, C, device=d.device, dtype=torch.float32)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
                 K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
                                compute_bf16=bf)
-                # LayerNorm + depthwise conv
+                # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
                 dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
                                      db=g(blk.norm.bias))
                 dz4 = dz.view(B, H, W, C)
                 K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
-                K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True)
+                K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
                 self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
                              blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
             if ds_saved is not None:
@@ -280,13 +287,14 @@ class ConvNeXtHip(nn.Module):
                 B, H, W, C = x_prev.shape
                 Cout = conv.weight.shape[0]
                 Mo = B * (H // 2) * (W // 2)
-                d2 = d.view(Mo, Cout)
+                dsrc = db.view(Mo, Cout) if bf else d.view(Mo, Cout)
                 wds = self._w(conv.weight, cache).reshape(Cout, 4 * C)
                 dpatch = torch.empty(Mo, 4 * C, device=d.device, dtype=torch.float32)
-                K.linear_dgrad(d2, wds, out=dpatch, compute_bf16=bf)
-                K.linear_wgrad(d2, patches, out=g(conv.weight), accumulate=True, bias_out=g(conv.bias),
+                K.linear_dgrad(dsrc, wds, out=dpatch, compute_bf16=bf)
+                K.linear_wgrad(dsrc, patches, out=g(conv.weight), accumulate=True, bias_out=g(conv.bias),
                                compute_bf16=bf)
-                d = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight), dlnb=g(ln.bias))
+                d, db = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight),
+                                         dlnb=g(ln.bias), with_bf16=bf)
                 self._ready([ln.weight, ln.bias, conv.weight, conv.bias])
         s_mean, s_rstd = tape.stem
         conv, ln = self.stem[0], self.stem[1]

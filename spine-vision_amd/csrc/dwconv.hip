@@ -45,8 +45,9 @@ template <typename TIN, typename TOUT, bool FLIP, bool ACCUM>
 __global__ void __launch_bounds__(kDwThreads) dwconv7_kernel(const TIN* __restrict__ x,
                                                              const float* __restrict__ wdw,
                                                              const float* __restrict__ bdw,
-                                                             TOUT* __restrict__ out, int B, int H, int W,
-                                                             int C) {
+                                                             TOUT* __restrict__ out,
+                                                             uint16_t* __restrict__ out_bf16, int B, int H,
+                                                             int W, int C) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [TR*TC][64]
   const int tilesW = (W + TW - 1) / TW, tilesH = (H + TH - 1) / TH;
   int t = blockIdx.x;
@@ -86,7 +87,9 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_kernel(const TIN* __restri
         const int w = w0 + o;
         if (w < W) {
           const size_t i = (((size_t)b * H + h) * W + w) * C + c;
-          st(out, i, ACCUM ? ld(out, i) + acc[o] : acc[o]);
+          const float v = ACCUM ? ld(out, i) + acc[o] : acc[o];
+          st(out, i, v);
+          if (out_bf16) out_bf16[i] = f2bf(v);
         }
       }
     }
@@ -193,7 +196,7 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   const dim3 grid(dw_tiles(B, H, W), C / 64);
   const size_t lds = dw_lds_bytes();
 #define LAUNCH(TI, TO) \
-  dwconv7_kernel<TI, TO, false, false><<<grid, kDwThreads, lds, s>>>((const TI*)x, wdw, bdw, (TO*)z, B, H, W, C)
+  dwconv7_kernel<TI, TO, false, false><<<grid, kDwThreads, lds, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, B, H, W, C)
   if (x_dtype == SV_F32 && z_dtype == SV_F32) LAUNCH(float, float);
   else if (x_dtype == SV_F32 && z_dtype == SV_BF16) LAUNCH(float, uint16_t);
   else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) LAUNCH(uint16_t, uint16_t);
@@ -205,8 +208,8 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
 }
 
-int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, int32_t accumulate, int32_t B,
-                        int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
+                        int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dz && wdw && dx, "sv_dwconv7_bwd_data: null pointer");
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_bwd_data: C=%d must be a multiple of 64", C);
   SV_REQUIRE(dz != dx, "sv_dwconv7_bwd_data: dz and dx must not alias");
@@ -215,9 +218,9 @@ int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, int32_t ac
   const dim3 grid(dw_tiles(B, H, W), C / 64);
   const size_t lds = dw_lds_bytes();
   if (accumulate)
-    dwconv7_kernel<float, float, true, true><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, B, H, W, C);
+    dwconv7_kernel<float, float, true, true><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C);
   else
-    dwconv7_kernel<float, float, true, false><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, B, H, W, C);
+    dwconv7_kernel<float, float, true, false><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C);
   return check_launch("sv_dwconv7_bwd_data");
 }
 

@@ -22,16 +22,15 @@
 // The blockIdx -> tile map is XCD-aware (each XCD gets a contiguous run of tiles, which share
 // A row panels in its private L2).
 #include "common.h"
+#include "gemm_common.h"
+
+#include <stdlib.h>
 
 namespace sv {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BKT = 32;
 constexpr int kGemmThreads = 256;
-constexpr int EPI_LD = 64 + 4;  // f32 epilogue slab row stride
 
 // ---------------------------------------------------------------------------------------------
 // LDS images.  bf16 compute: k-major [R][BKT+8] (80 B rows), m-major [BKT][R+16] (288 B rows).
@@ -205,52 +204,6 @@ __device__ __forceinline__ float colsum_tile(const char* __restrict__ img, int r
   return s;
 }
 
-struct EpiArgs {
-  int M, N;
-  int epi;
-  void* C; int c_dtype; int64_t ldc;
-  void* C2; int c2_dtype;
-  const float* bias;
-  const float* gamma;
-  const void* aux; int aux_dtype; int64_t ld_aux;
-};
-
-__device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
-  return dt == SV_F32 ? ld4(reinterpret_cast<const float*>(p), i) : ld4(reinterpret_cast<const uint16_t*>(p), i);
-}
-__device__ __forceinline__ void st4_any(void* p, int dt, size_t i, float4 v) {
-  if (dt == SV_F32) st4(reinterpret_cast<float*>(p), i, v);
-  else st4(reinterpret_cast<uint16_t*>(p), i, v);
-}
-
-// apply the epilogue to 4 consecutive columns n..n+3 of row m
-__device__ __forceinline__ void epi4(const EpiArgs& e, int m, int n, float4 v, int split) {
-  if (e.epi == SV_EPI_SLAB) {
-    float* C = reinterpret_cast<float*>(e.C) + (size_t)split * e.M * e.N;
-    *reinterpret_cast<float4*>(C + (size_t)m * e.N + n) = v;
-    return;
-  }
-  if (e.bias && e.epi != SV_EPI_GELU_GRAD) {
-    const float4 b = *reinterpret_cast<const float4*>(e.bias + n);
-    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-  }
-  const size_t ci = (size_t)m * e.ldc + n;
-  if (e.epi == SV_EPI_STORE) {
-    st4_any(e.C, e.c_dtype, ci, v);
-  } else if (e.epi == SV_EPI_BIAS_GELU2) {
-    st4_any(e.C, e.c_dtype, ci, v);
-    st4_any(e.C2, e.c2_dtype, ci, make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)));
-  } else if (e.epi == SV_EPI_BIAS_GAMMA_RES) {
-    const float4 g = *reinterpret_cast<const float4*>(e.gamma + n);
-    const float4 r = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
-    st4_any(e.C, e.c_dtype, ci, make_float4(r.x + g.x * v.x, r.y + g.y * v.y, r.z + g.z * v.z, r.w + g.w * v.w));
-  } else {  // SV_EPI_GELU_GRAD
-    const float4 h = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
-    st4_any(e.C, e.c_dtype, ci,
-            make_float4(v.x * gelu_grad_f(h.x), v.y * gelu_grad_f(h.y), v.z * gelu_grad_f(h.z), v.w * gelu_grad_f(h.w)));
-  }
-}
-
 template <bool BF16, typename TA, typename TB, bool AK, bool BKM>
 __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict__ A, int64_t lda,
                                                             const TB* __restrict__ B, int64_t ldb,
@@ -340,34 +293,8 @@ __global__ void __launch_bounds__(kGemmThreads) gemm_kernel(const TA* __restrict
 
   if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
 
-  // ---- epilogue: per wave, 4 slabs of 16 rows x 64 cols staged through its private LDS region
-  float* slab = reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD;
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i][j][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const int row = l >> 2, cb = (l & 3) * 16;
-    const int m = m0 + wm * 64 + i * 16 + row;
-    if (m < e.M) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wn * 64 + cb + 4 * g;
-        if (n < e.N) {
-          const float* sp = slab + row * EPI_LD + cb + 4 * g;
-          epi4(e, m, n, make_float4(sp[0], sp[1], sp[2], sp[3]), split);
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  }
+  // ---- epilogue: per wave, 16-row slabs staged through its private LDS region
+  wave_tile_epilogue(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64, n0 + wn * 64, e, split);
 }
 
 template <bool BF16, typename TA, typename TB, bool AK, bool BKM>
@@ -438,6 +365,12 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
   hipStream_t s = (hipStream_t)stream;
   if (!bf) return launch_layout<false, float, float>(d, s);
+  // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
+  static const bool force_v1 = getenv("SV_GEMM_V1") != nullptr;
+  if (!force_v1) {
+    const int rc = launch_gemm2(d, s);
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+  }
   const bool a32 = d->a_dtype == SV_F32, b32 = d->b_dtype == SV_F32;
   SV_REQUIRE((a32 || d->a_dtype == SV_BF16) && (b32 || d->b_dtype == SV_BF16), "sv_gemm: bad operand dtype");
   if (!a32 && !b32) return launch_layout<true, uint16_t, uint16_t>(d, s);

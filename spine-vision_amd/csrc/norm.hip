@@ -367,7 +367,8 @@ template <int CPL>
 __global__ void __launch_bounds__(kLnThreads) ds_bwd_kernel(
     const float* __restrict__ dpatches, const float* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ lnw, float* __restrict__ dx,
-    float* __restrict__ dlnw_part, float* __restrict__ dlnb_part, int B, int H, int W, int C) {
+    uint16_t* __restrict__ dx_bf16, float* __restrict__ dlnw_part, float* __restrict__ dlnb_part, int B, int H,
+    int W, int C) {
   __shared__ float red[kLnThreads / 64][2048];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = (int64_t)blockIdx.x * (kLnThreads / 64) + wid;
@@ -406,7 +407,12 @@ __global__ void __launch_bounds__(kLnThreads) ds_bwd_kernel(
       s1 = wave_sum(s1) * invC;
       s2 = wave_sum(s2) * invC;
 #pragma unroll
-      for (int t = 0; t < CPL; ++t) dx[(size_t)pix * C + lane + 64 * t] = rs * (g[t] - s1 - xh[t] * s2);
+      for (int t = 0; t < CPL; ++t) {
+        const size_t i = (size_t)pix * C + lane + 64 * t;
+        const float v = rs * (g[t] - s1 - xh[t] * s2);
+        dx[i] = v;
+        if (dx_bf16) dx_bf16[i] = f2bf(v);
+      }
     }
   }
 #pragma unroll
@@ -462,7 +468,7 @@ __global__ void __launch_bounds__(kLnThreads) pool_ln_fwd_kernel(const float* __
 __global__ void __launch_bounds__(kLnThreads) pool_ln_bwd_kernel(
     const float* __restrict__ dfeat, const float* __restrict__ pooled, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ lnw, float* __restrict__ dx,
-    float* __restrict__ dlnw_part, float* __restrict__ dlnb_part, int HW, int C) {
+    uint16_t* __restrict__ dx_bf16, float* __restrict__ dlnw_part, float* __restrict__ dlnb_part, int HW, int C) {
   __shared__ float red[kLnThreads / 64];
   extern __shared__ __attribute__((aligned(16))) float dp[];  // [C]
   const int b = blockIdx.x;
@@ -487,7 +493,11 @@ __global__ void __launch_bounds__(kLnThreads) pool_ln_bwd_kernel(
   }
   __syncthreads();
   float* dxb = dx + (size_t)b * HW * C;
-  for (size_t i = threadIdx.x; i < (size_t)HW * C; i += blockDim.x) dxb[i] = dp[i % C];
+  uint16_t* dbb = dx_bf16 ? dx_bf16 + (size_t)b * HW * C : nullptr;
+  for (size_t i = threadIdx.x; i < (size_t)HW * C; i += blockDim.x) {
+    dxb[i] = dp[i % C];
+    if (dbb) dbb[i] = f2bf(dp[i % C]);
+  }
 }
 
 }  // namespace sv
@@ -628,7 +638,7 @@ int sv_downsample_ln_patch2_bwd_nparts(int32_t B, int32_t H, int32_t W, int32_t 
 }
 
 int sv_downsample_ln_patch2_bwd(const float* dpatches, const float* x, const float* mean,
-                                const float* rstd, const float* lnw, float* dx, float* dlnw_part,
+                                const float* rstd, const float* lnw, float* dx, uint16_t* dx_bf16, float* dlnw_part,
                                 float* dlnb_part, int32_t B, int32_t H, int32_t W, int32_t C,
                                 sv_stream_t stream) {
   SV_REQUIRE(dpatches && x && mean && rstd && lnw && dx && dlnw_part && dlnb_part,
@@ -638,7 +648,7 @@ int sv_downsample_ln_patch2_bwd(const float* dpatches, const float* x, const flo
   hipStream_t s = (hipStream_t)stream;
   const int grid = ds_grid(B, H, W);
   SV_CPL_SWITCH(C / 64, ds_bwd_kernel<CPL><<<grid, kLnThreads, 0, s>>>(
-                            dpatches, x, mean, rstd, lnw, dx, dlnw_part, dlnb_part, B, H, W, C));
+                            dpatches, x, mean, rstd, lnw, dx, dx_bf16, dlnw_part, dlnb_part, B, H, W, C));
   return check_launch("sv_downsample_ln_patch2_bwd");
 }
 
@@ -653,13 +663,13 @@ int sv_pool_ln_fwd(const float* x, const float* lnw, const float* lnb, float eps
 }
 
 int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, const float* rstd,
-                   const float* lnw, float* dx, float* dlnw_part, float* dlnb_part, int32_t B,
+                   const float* lnw, float* dx, uint16_t* dx_bf16, float* dlnw_part, float* dlnb_part, int32_t B,
                    int32_t HW, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dfeat && pooled && mean && rstd && lnw && dx && dlnw_part && dlnb_part,
              "sv_pool_ln_bwd: null pointer");
   if (B <= 0) return SV_OK;
   pool_ln_bwd_kernel<<<B, kLnThreads, C * sizeof(float), (hipStream_t)stream>>>(
-      dfeat, pooled, mean, rstd, lnw, dx, dlnw_part, dlnb_part, HW, C);
+      dfeat, pooled, mean, rstd, lnw, dx, dx_bf16, dlnw_part, dlnb_part, HW, C);
   return check_launch("sv_pool_ln_bwd");
 }
 

@@ -172,6 +172,16 @@ __global__ void __launch_bounds__(kThreads) adamw_kernel(float* __restrict__ p, 
   }
 }
 
+// out[r][k] = bf16(W[r][k] * scale[r])   (the layer-scale gamma folded into fc2's weight for dgrad)
+__global__ void __launch_bounds__(kThreads) scale_rows_bf16_kernel(const float* __restrict__ W,
+                                                                   const float* __restrict__ scale,
+                                                                   uint16_t* __restrict__ out, int rows, int cols) {
+  const int64_t n = (int64_t)rows * cols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = f2bf(W[i] * scale[i / cols]);
+}
+
 __global__ void __launch_bounds__(kThreads) cast_bf16_kernel(const float* __restrict__ x,
                                                              uint16_t* __restrict__ y, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -269,6 +279,14 @@ int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16
   adamw_kernel<<<stream_grid(n, 4), kThreads, 0, (hipStream_t)stream>>>(
       p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale);
   return check_launch("sv_adamw_flat");
+}
+
+int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,
+                       sv_stream_t stream) {
+  SV_REQUIRE(W && scale && out && rows > 0 && cols > 0, "sv_scale_rows_bf16: bad args");
+  scale_rows_bf16_kernel<<<stream_grid((int64_t)rows * cols, 1), kThreads, 0, (hipStream_t)stream>>>(W, scale, out,
+                                                                                                      rows, cols);
+  return check_launch("sv_scale_rows_bf16");
 }
 
 int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream) {

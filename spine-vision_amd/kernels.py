@@ -231,10 +231,12 @@ def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN):
     return z, y, mean, rstd
 
 
-def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True):
+def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
     B, H, W, C = dz4d.shape
     _check(dx4d.shape == dz4d.shape and dx4d.dtype == torch.float32, "dwconv7_bwd_data: shape")
-    call("sv_dwconv7_bwd_data", ptr(dz4d), ptr(wdw), ptr(dx4d), int(accumulate), B, H, W, C)
+    if dx_bf16 is not None:
+        _check(dx_bf16.numel() == dx4d.numel() and dx_bf16.dtype == torch.bfloat16, "dwconv7_bwd_data: bf16 copy")
+    call("sv_dwconv7_bwd_data", ptr(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16), int(accumulate), B, H, W, C)
 
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
@@ -287,16 +289,18 @@ def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):
     return patches, mean, rstd
 
 
-def downsample_bwd(dpatches, x4d, mean, rstd, lnw, *, dlnw, dlnb):
+def downsample_bwd(dpatches, x4d, mean, rstd, lnw, *, dlnw, dlnb, with_bf16=False):
+    """-> dx (f32 [B,H,W,C]) and, with ``with_bf16``, its bf16 GEMM-operand copy (else None)."""
     B, H, W, C = x4d.shape
     dx = torch.empty(B, H, W, C, device=x4d.device, dtype=torch.float32)
+    dxb = torch.empty(B, H, W, C, device=x4d.device, dtype=torch.bfloat16) if with_bf16 else None
     P = value("sv_downsample_ln_patch2_bwd_nparts", B, H, W, C)
     pv = torch.empty(2, P * C, device=x4d.device, dtype=torch.float32)
-    call("sv_downsample_ln_patch2_bwd", ptr(dpatches), ptr(x4d), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(pv[0]),
-         ptr(pv[1]), B, H, W, C)
+    call("sv_downsample_ln_patch2_bwd", ptr(dpatches), ptr(x4d), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(dxb),
+         ptr(pv[0]), ptr(pv[1]), B, H, W, C)
     reduce_into(pv[0], P, dlnw)
     reduce_into(pv[1], P, dlnb)
-    return dx
+    return dx, dxb
 
 
 def pool_ln_fwd(x4d, lnw, lnb, *, eps=EPS_LN):
@@ -310,19 +314,30 @@ def pool_ln_fwd(x4d, lnw, lnb, *, eps=EPS_LN):
     return feat, pooled, mean, rstd
 
 
-def pool_ln_bwd(dfeat, pooled, mean, rstd, lnw, shape, *, dlnw, dlnb):
+def pool_ln_bwd(dfeat, pooled, mean, rstd, lnw, shape, *, dlnw, dlnb, with_bf16=False):
+    """-> dx (f32 [B,H,W,C]) and, with ``with_bf16``, its bf16 GEMM-operand copy (else None)."""
     B, H, W, C = shape
     dx = torch.empty(B, H, W, C, device=dfeat.device, dtype=torch.float32)
+    dxb = torch.empty(B, H, W, C, device=dfeat.device, dtype=torch.bfloat16) if with_bf16 else None
     pv = torch.empty(2, B * C, device=dfeat.device, dtype=torch.float32)
-    call("sv_pool_ln_bwd", ptr(dfeat.contiguous()), ptr(pooled), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(pv[0]),
-         ptr(pv[1]), B, H * W, C)
+    call("sv_pool_ln_bwd", ptr(dfeat.contiguous()), ptr(pooled), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(dxb),
+         ptr(pv[0]), ptr(pv[1]), B, H * W, C)
     reduce_into(pv[0], B, dlnw)
     reduce_into(pv[1], B, dlnb)
-    return dx
+    return dx, dxb
 
 
 # ----------------------------------------------------------------------------------------------
 # optimizer pieces
+def scale_rows_bf16(W: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """bf16(W * scale[:, None]) for a 2-D f32 weight (fc2 weight with the layer scale folded in)."""
+    rows, cols = W.shape
+    _check(W.dtype == torch.float32 and W.is_contiguous() and scale.numel() == rows, "scale_rows_bf16: bad args")
+    out = torch.empty(rows, cols, device=W.device, dtype=torch.bfloat16)
+    call("sv_scale_rows_bf16", ptr(W), ptr(scale), ptr(out), rows, cols)
+    return out
+
+
 def cast_bf16(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _check(x.dtype == torch.float32 and x.is_contiguous(), "cast_bf16: need contiguous f32")
     if out is None:

@@ -54,7 +54,7 @@ _SIGS = {
     "sv_layernorm_bwd_nparts": [_i64, _i32],
     "sv_layernorm_bwd": [_p, _p, _i32, _p, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p],
     "sv_dwconv7_ln_fwd": [_p, _i32, _p, _p, _p, _p, _f32, _p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
-    "sv_dwconv7_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_data": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_weight_nparts": [_i32, _i32, _i32, _i32],
     "sv_dwconv7_bwd_weight": [_p, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_fwd": [_p, _p, _p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
@@ -62,9 +62,9 @@ _SIGS = {
     "sv_stem_patchify_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_downsample_ln_patch2_fwd": [_p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_downsample_ln_patch2_bwd_nparts": [_i32, _i32, _i32, _i32],
-    "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_pool_ln_fwd": [_p, _p, _p, _f32, _p, _p, _p, _p, _i32, _i32, _i32, _p],
-    "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
+    "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_reduce_partials": [_p, _i32, _i32, _i64, _p, _f32, _i32, _p],
     "sv_colsum_nparts": [_i64, _i32],
     "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
@@ -73,6 +73,7 @@ _SIGS = {
     "sv_sqnorm_partial": [_p, _i64, _p, _p],
     "sv_clip_coef": [_p, _i32, _f32, _p, _p],
     "sv_adamw_flat": [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _p, _p],
+    "sv_scale_rows_bf16": [_p, _p, _p, _i32, _i32, _p],
     "sv_cast_f32_bf16": [_p, _p, _i64, _p],
 }
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p}

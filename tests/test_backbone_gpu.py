@@ -54,3 +54,21 @@ def test_convnext_bf16_forward(dev):
         f_ref = ref(img)
         f_hip = hip(img.to(dev))
     assert rel(f_hip, f_ref) < 2e-2
+
+
+def test_convnext_bf16_backward(dev):
+    """bf16 mode backward (bf16 GEMM operands incl. the bf16 gradient-stream copy and the gamma-folded
+    fc2 weight) against the fp32 oracle: per-tensor relative L2 of every gradient within bf16 bounds."""
+    ref, hip = _pair("convnext_base", "bf16", dev)
+    img, _, _ = ow.localization_batch(2, 64, 64)
+    f_ref = ref(img)
+    f_hip = hip(img.to(dev))
+    dfeat = torch.from_numpy(ow.uniform("dfeat", f_ref.numel(), -1, 1).reshape(f_ref.shape))
+    f_ref.backward(dfeat)
+    f_hip.backward(dfeat.to(dev))
+    worst = 0.0
+    for (n1, p1), (n2, p2) in zip(ref.named_parameters(), hip.named_parameters()):
+        r = rel(p2.grad, p1.grad)
+        worst = max(worst, r)
+        assert r < 5e-2, f"{n1}: rel {r}"
+    print(f"bf16 worst grad rel {worst:.2e}")

@@ -31,7 +31,8 @@ def bf(t):
 @pytest.mark.parametrize("compute_bf16", [False, True])
 @pytest.mark.parametrize("a_kmajor", [True, False])
 @pytest.mark.parametrize("b_kmajor", [True, False])
-@pytest.mark.parametrize("shape", [(256, 128, 64), (200, 136, 96), (8, 512, 40), (1000, 24, 1024)])
+@pytest.mark.parametrize("shape", [(256, 128, 64), (200, 136, 96), (8, 512, 40), (1000, 24, 1024),
+                                   (1024, 512, 512), (264, 392, 128), (4096, 256, 2048)])
 def test_gemm_layouts(dev, compute_bf16, a_kmajor, b_kmajor, shape):
     M, N, Kd = shape
     g = torch.Generator().manual_seed(M * 7 + N * 3 + Kd)
@@ -107,16 +108,21 @@ def test_gemm_epilogues(dev, compute_bf16):
 
 
 @pytest.mark.parametrize("M", [37, 4096, 70000])
-def test_wgrad_split_and_bias(dev, M):
+@pytest.mark.parametrize("compute_bf16", [False, True])
+def test_wgrad_split_and_bias(dev, M, compute_bf16):
     g = torch.Generator().manual_seed(M)
     N, Kd = 256, 512
     dy = torch.randn(M, N, generator=g)
     x = torch.randn(M, Kd, generator=g)
     out = torch.ones(N, Kd, device=dev)
     bias = torch.ones(N, device=dev)
-    K.linear_wgrad(dy.to(dev), x.to(dev), out=out, accumulate=True, bias_out=bias, compute_bf16=False)
-    assert rel(out, dy.double().t() @ x.double() + 1) < 1e-5
-    assert rel(bias, dy.double().sum(0) + 1) < 1e-5
+    dt = torch.bfloat16 if compute_bf16 else torch.float32
+    q = bf if compute_bf16 else (lambda t: t.double())
+    K.linear_wgrad(dy.to(dt).to(dev), x.to(dt).to(dev), out=out, accumulate=True, bias_out=bias,
+                   compute_bf16=compute_bf16)
+    tol = 2e-3 if compute_bf16 else 1e-5
+    assert rel(out, q(dy).t() @ q(x) + 1) < tol
+    assert rel(bias, q(dy).sum(0) + 1) < tol
 
 
 def test_reduce_partials_deep(dev):
@@ -175,7 +181,9 @@ def test_dwconv7_fwd_bwd(dev, shape):
     # backward of the conv alone: dz given
     zr_nhwc.backward(dy)
     dx = torch.zeros(B, H, W, C, device=dev)
-    K.dwconv7_bwd_data(dy.to(dev), w.to(dev), dx, accumulate=True)
+    dxb = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+    K.dwconv7_bwd_data(dy.to(dev), w.to(dev), dx, accumulate=True, dx_bf16=dxb)
+    assert torch.equal(dxb.cpu(), dx.cpu().to(torch.bfloat16))
     assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-5
     dw = torch.zeros(C, 49, device=dev)
     db = torch.zeros(C, device=dev)
@@ -233,10 +241,20 @@ def test_downsample(dev, C):
     pr.backward(dpatch)
     dlnw = torch.zeros(C, device=dev)
     dlnb = torch.zeros(C, device=dev)
-    dx = K.downsample_bwd(dpatch.to(dev), x.to(dev), mean, rstd, lnw.to(dev), dlnw=dlnw, dlnb=dlnb)
+    dx, dxb = K.downsample_bwd(dpatch.to(dev), x.to(dev), mean, rstd, lnw.to(dev), dlnw=dlnw, dlnb=dlnb,
+                               with_bf16=True)
+    assert torch.equal(dxb.cpu(), dx.cpu().to(torch.bfloat16))
     assert rel(dx, xr.grad) < 1e-5
     assert rel(dlnw, lwr.grad) < 1e-5
     assert rel(dlnb, lbr.grad) < 1e-5
+
+
+def test_scale_rows_bf16(dev):
+    g = torch.Generator().manual_seed(11)
+    W = torch.randn(96, 200, generator=g)
+    sc = torch.rand(96, generator=g)
+    out = K.scale_rows_bf16(W.to(dev), sc.to(dev))
+    assert torch.equal(out.cpu(), (W * sc[:, None]).to(torch.bfloat16))
 
 
 def test_pool_ln(dev):
@@ -254,7 +272,9 @@ def test_pool_ln(dev):
     fr.backward(df)
     dlnw = torch.zeros(C, device=dev)
     dlnb = torch.zeros(C, device=dev)
-    dx = K.pool_ln_bwd(df.to(dev), pooled, mean, rstd, lnw.to(dev), (B, H, W, C), dlnw=dlnw, dlnb=dlnb)
+    dx, dxb = K.pool_ln_bwd(df.to(dev), pooled, mean, rstd, lnw.to(dev), (B, H, W, C), dlnw=dlnw, dlnb=dlnb,
+                            with_bf16=True)
+    assert torch.equal(dxb.cpu(), dx.cpu().to(torch.bfloat16))
     assert rel(dx, xr.grad) < 1e-5
     assert rel(dlnw, lwr.grad) < 1e-5
     assert rel(dlnb, lbr.grad) < 1e-5
