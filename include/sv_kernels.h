@@ -60,9 +60,12 @@ typedef enum {
   SV_EPI_BIAS_GELU2 = 1,     /* C = acc + bias[n]  (pre-activation), C2 = GELU_erf(C)             */
   SV_EPI_BIAS_GAMMA_RES = 2, /* C = aux[m,n] + gamma[n] * (acc + bias[n])   (layer-scale residual) */
   SV_EPI_GELU_GRAD = 3,      /* C = acc * GELU_erf'(aux[m,n])                                      */
-  SV_EPI_SLAB = 4            /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32);      */
+  SV_EPI_SLAB = 4,           /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32);      */
                              /* if C2 != NULL also C2[s][m] = sum_{k in slice s} A(m,k) (f32), i.e.  */
                              /* the bias gradient of a wgrad GEMM (A = dY^T) without another pass.   */
+  SV_EPI_BIAS_GELU_DUAL = 5, /* h = acc + bias[n]: C = GELU_erf'(h), C2 = GELU_erf(h)  (fc1 forward: */
+                             /* the backward then needs no erf, only SV_EPI_MUL_AUX)                 */
+  SV_EPI_MUL_AUX = 6         /* C = acc * aux[m,n]                       (fc2 dgrad through GELU)    */
 } sv_epilogue;
 
 typedef struct {

@@ -206,15 +206,16 @@ class ConvNeXtHip(nn.Module):
                                                     blk.norm.bias, act_dtype=act)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 w2 = self._w(blk.mlp.fc2.weight, cache)
-                h = torch.empty(M, 4 * C, device=x.device, dtype=act)
+                # fc1 epilogue: a = GELU(h) (fc2 operand) and gh = GELU'(h) (for the backward), one erf
+                gh = torch.empty(M, 4 * C, device=x.device, dtype=act)
                 a = torch.empty(M, 4 * C, device=x.device, dtype=act)
-                K.linear_fwd(y, w1, out=h, out2=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU2,
+                K.linear_fwd(y, w1, out=gh, out2=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU_DUAL,
                              compute_bf16=bf)
                 xo = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
                 K.linear_fwd(a, w2, out=xo.view(M, C), bias=blk.mlp.fc2.bias, gamma=blk.gamma,
                              residual=x.view(M, C), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, compute_bf16=bf)
                 if save:
-                    blocks_saved.append((x, z, y, mean, rstd, h, a))
+                    blocks_saved.append((x, z, y, mean, rstd, gh, a))
                 x = xo
             if save:
                 tape.stages.append((ds_saved, blocks_saved))
@@ -248,21 +249,22 @@ class ConvNeXtHip(nn.Module):
         self._ready([hn.weight, hn.bias])
         for st, (ds_saved, blocks_saved) in zip(reversed(list(self.stages)), reversed(tape.stages)):
             for blk, saved in zip(reversed(list(st.blocks)), reversed(blocks_saved)):
-                x, z, y, mean, rstd, h, a = saved
+                x, z, y, mean, rstd, gh, a = saved
                 B, H, W, C = x.shape
                 M = B * H * W
                 d2 = d.view(M, C)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
-                # fc2: dh = ((d * gamma) @ W2) * GELU'(h).  bf16 mode folds gamma into a bf16 copy of W2
+                # fc2: dh = ((d * gamma) @ W2) * GELU'(h).  bf16 mode folds gamma into a bf16 copy of W2;
+                # GELU'(h) was stored by the forward epilogue
                 dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
                 if bf:
                     dsrc = db.view(M, C)
                     w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
-                    K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_GELU_GRAD, aux=h, compute_bf16=True)
+                    K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
                 else:
                     dsrc = d2
-                    K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_GELU_GRAD,
-                                   a_scale_k=blk.gamma, aux=h, compute_bf16=False)
+                    K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_MUL_AUX,
+                                   a_scale_k=blk.gamma, aux=gh, compute_bf16=False)
                 cs = torch.empty(C, device=d.device, dtype=torch.float32)
                 G = K.linear_wgrad(dsrc, a, bias_out=cs, bias_accumulate=False, compute_bf16=bf)  # [C,4C] = d^T a
                 nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),

@@ -59,13 +59,36 @@ template <> __device__ __forceinline__ void st4<uint16_t>(uint16_t* p, size_t i,
   *reinterpret_cast<uint2*>(p + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
 }
 
-// ---- GELU (exact erf form, = torch.nn.GELU() default) ---------------------------------
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// ---- GELU (erf form, = torch.nn.GELU() default) -----------------------------------------
+// Phi(x) = 0.5*erfc(-x/sqrt2) with the branch-free Chebyshev-fitted erfc of Numerical Recipes
+// (erfcc, |relative error| < 1.2e-7 everywhere): one v_exp, one v_rcp and ten FMAs, no divergent
+// ranges -- the GELU epilogues of the fc1/fc2 GEMMs run it on every element.
+__device__ __forceinline__ float phi_cdf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.5f * z);
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float r = t * __expf(fmaf(-z, z, p));  // erfc(|x|/sqrt2)
+  return x >= 0.f ? fmaf(-0.5f, r, 1.0f) : 0.5f * r;
+}
+__device__ __forceinline__ float gelu_f(float x) { return x * phi_cdf(x); }
+// GELU and its derivative from one Phi evaluation (forward epilogue of fc1)
+__device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
+  const float c = phi_cdf(x);
+  g = x * c;
+  dg = c + x * (0.39894228040143268f * __expf(-0.5f * x * x));
+}
 __device__ __forceinline__ float gelu_grad_f(float x) {
   // d/dx [x * Phi(x)] = Phi(x) + x * phi(x)
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  return phi_cdf(x) + x * (0.39894228040143268f * __expf(-0.5f * x * x));
 }
 
 // ---- wave / block reductions (wave64) -------------------------------------------------

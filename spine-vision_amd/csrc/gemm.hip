@@ -340,7 +340,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
-  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_SLAB, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_MUL_AUX, "sv_gemm: bad epilogue %d", d->epilogue);
   if (d->M == 0 || d->N == 0) return SV_OK;
   const bool bf = d->compute == SV_BF16;
   SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
@@ -358,9 +358,10 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   } else {
     SV_REQUIRE(d->ldc % 4 == 0, "sv_gemm: ldc must be a multiple of 4");
   }
-  if (d->epilogue == SV_EPI_BIAS_GELU2) SV_REQUIRE(d->C2 && al16(d->C2), "sv_gemm: GELU2 needs aligned C2");
+  if (d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL)
+    SV_REQUIRE(d->C2 && al16(d->C2), "sv_gemm: GELU epilogue needs an aligned C2");
   if (d->epilogue == SV_EPI_BIAS_GAMMA_RES) SV_REQUIRE(d->gamma && d->aux, "sv_gemm: gamma/residual missing");
-  if (d->epilogue == SV_EPI_GELU_GRAD) SV_REQUIRE(d->aux, "sv_gemm: pre-activation missing");
+  if (d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX) SV_REQUIRE(d->aux, "sv_gemm: aux missing");
   if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
   hipStream_t s = (hipStream_t)stream;

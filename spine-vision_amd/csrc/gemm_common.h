@@ -60,13 +60,82 @@ __device__ __forceinline__ void epi4(const EpiArgs& e, int m, int n, float4 v, i
 }
 
 
+// 8 consecutive elements <-> two float4 (bf16: one 16-B access, f32: two)
+__device__ __forceinline__ void ld8_any(const void* p, int dt, size_t i, float4& a, float4& b) {
+  if (dt == SV_F32) {
+    const float* f = reinterpret_cast<const float*>(p) + i;
+    a = *reinterpret_cast<const float4*>(f);
+    b = *reinterpret_cast<const float4*>(f + 4);
+  } else {
+    const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(p) + i);
+    a = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                    __uint_as_float(u.y & 0xffff0000u));
+    b = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+                    __uint_as_float(u.w & 0xffff0000u));
+  }
+}
+__device__ __forceinline__ void st8_any(void* p, int dt, size_t i, float4 a, float4 b) {
+  if (dt == SV_F32) {
+    float* f = reinterpret_cast<float*>(p) + i;
+    *reinterpret_cast<float4*>(f) = a;
+    *reinterpret_cast<float4*>(f + 4) = b;
+  } else {
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p) + i) =
+        make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
+  }
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 gelu4(float4 v) { return make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)); }
+__device__ __forceinline__ float4 fma4(float4 g, float4 v, float4 r) {
+  return make_float4(fmaf(g.x, v.x, r.x), fmaf(g.y, v.y, r.y), fmaf(g.z, v.z, r.z), fmaf(g.w, v.w, r.w));
+}
+__device__ __forceinline__ float4 ggrad4(float4 v, float4 h) {
+  return make_float4(v.x * gelu_grad_f(h.x), v.y * gelu_grad_f(h.y), v.z * gelu_grad_f(h.z), v.w * gelu_grad_f(h.w));
+}
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+__device__ __forceinline__ void gelu_dual4(float4 v, float4& g, float4& dg) {
+  gelu_and_grad(v.x, g.x, dg.x);
+  gelu_and_grad(v.y, g.y, dg.y);
+  gelu_and_grad(v.z, g.z, dg.z);
+  gelu_and_grad(v.w, g.w, dg.w);
+}
+
 // Store one wave's 64x64 accumulator (acc[i][j]: 16x16 MFMA fragments, C/D map col = lane&15,
 // row = 4*(lane>>4) + r).  Each 16-row slab goes through the wave's private LDS region `slab`
-// (16 x EPI_LD floats) and is re-read row-contiguous: lane -> (row = lane>>2, 16 columns), so every
-// epilogue load/store is a 16-B vector access.
+// (16 x EPI_LD floats) and is re-read as 8-column units: unit u = lane + 64*h (h = 0,1) covers row
+// u>>3 and columns 8*(u&7)..+7, so one wave store instruction writes 8 whole 128-B rows (bf16:
+// 16 B per lane) -- full cache lines instead of 32-B fragments.  All epilogue operands (bias, gamma
+// and the residual / pre-activation of the tile) are loaded before the first slab.
 __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], float* __restrict__ slab, int mb,
                                                    int nb, const EpiArgs& e, int split) {
   const int l = threadIdx.x & 63;
+  const int cu = (l & 7) * 8, r0 = l >> 3;
+  const int n = nb + cu;
+  const bool okn = n < e.N;  // N % 8 == 0 is enforced for bf16-output epilogues; f32 needs N % 4 only
+  const bool okn4 = n + 4 < e.N;
+  const bool slab_out = e.epi == SV_EPI_SLAB;
+  const bool need_aux = e.epi == SV_EPI_BIAS_GAMMA_RES || e.epi == SV_EPI_GELU_GRAD || e.epi == SV_EPI_MUL_AUX;
+  float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, g0 = b0, g1 = b0;
+  if (okn && e.bias && !slab_out && e.epi != SV_EPI_GELU_GRAD && e.epi != SV_EPI_MUL_AUX) {
+    b0 = *reinterpret_cast<const float4*>(e.bias + n);
+    if (okn4) b1 = *reinterpret_cast<const float4*>(e.bias + n + 4);
+  }
+  if (okn && e.epi == SV_EPI_BIAS_GAMMA_RES) {
+    g0 = *reinterpret_cast<const float4*>(e.gamma + n);
+    if (okn4) g1 = *reinterpret_cast<const float4*>(e.gamma + n + 4);
+  }
+  float4 xa[4][2], xb[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      xa[i][h] = xb[i][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int m = mb + i * 16 + r0 + 8 * h;
+      if (need_aux && okn && m < e.M) {
+        if (okn4) ld8_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n, xa[i][h], xb[i][h]);
+        else xa[i][h] = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
+      }
+    }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -76,16 +145,51 @@ __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], flo
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const int row = l >> 2, cb = (l & 3) * 16;
-    const int m = mb + i * 16 + row;
-    if (m < e.M) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = nb + cb + 4 * g;
-        if (n < e.N) {
-          const float* sp = slab + row * EPI_LD + cb + 4 * g;
-          epi4(e, m, n, make_float4(sp[0], sp[1], sp[2], sp[3]), split);
-        }
+    for (int h = 0; h < 2; ++h) {
+      const int row = r0 + 8 * h;
+      const int m = mb + i * 16 + row;
+      if (m >= e.M || !okn) continue;
+      const float* sp = slab + row * EPI_LD + cu;
+      float4 va = make_float4(sp[0], sp[1], sp[2], sp[3]);
+      float4 vb = make_float4(sp[4], sp[5], sp[6], sp[7]);
+      if (slab_out) {
+        float* C = reinterpret_cast<float*>(e.C) + (size_t)split * e.M * e.N + (size_t)m * e.N + n;
+        *reinterpret_cast<float4*>(C) = va;
+        if (okn4) *reinterpret_cast<float4*>(C + 4) = vb;
+        continue;
+      }
+      va = add4(va, b0);
+      vb = add4(vb, b1);
+      float4 oa, ob;
+      if (e.epi == SV_EPI_STORE || e.epi == SV_EPI_BIAS_GELU2) {
+        oa = va;
+        ob = vb;
+      } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
+        float4 ga, gb;
+        gelu_dual4(va, ga, oa);
+        gelu_dual4(vb, gb, ob);
+        va = ga;  // C2 gets GELU, C gets GELU'
+        vb = gb;
+      } else if (e.epi == SV_EPI_MUL_AUX) {
+        oa = mul4(va, xa[i][h]);
+        ob = mul4(vb, xb[i][h]);
+      } else if (e.epi == SV_EPI_BIAS_GAMMA_RES) {
+        oa = fma4(g0, va, xa[i][h]);
+        ob = fma4(g1, vb, xb[i][h]);
+      } else {
+        oa = ggrad4(va, xa[i][h]);
+        ob = ggrad4(vb, xb[i][h]);
+      }
+      const size_t ci = (size_t)m * e.ldc + n;
+      if (okn4) st8_any(e.C, e.c_dtype, ci, oa, ob);
+      else st4_any(e.C, e.c_dtype, ci, oa);
+      if (e.epi == SV_EPI_BIAS_GELU2) {
+        if (okn4) st8_any(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb));
+        else st4_any(e.C2, e.c2_dtype, ci, gelu4(va));
+      } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
+        if (okn4) st8_any(e.C2, e.c2_dtype, ci, va, vb);
+        else st4_any(e.C2, e.c2_dtype, ci, va);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

@@ -84,6 +84,15 @@ def test_gemm_epilogues(dev, compute_bf16):
     tol = 1e-2 if compute_bf16 else 1e-5
     assert rel(h, h_ref) < tol
     assert rel(a, F.gelu(h_ref)) < tol
+    # fc1 + GELU dual: C = GELU'(h), C2 = GELU(h)
+    gh = torch.empty_like(h)
+    a2 = torch.empty_like(h)
+    K.linear_fwd(y.to(act).to(dev), w1.to(act).to(dev), out=gh, out2=a2, bias=b1.to(dev),
+                 epilogue=nv.SV_EPI_BIAS_GELU_DUAL, compute_bf16=compute_bf16)
+    hr = h_ref.clone().requires_grad_(True)
+    F.gelu(hr).sum().backward()
+    assert rel(a2, F.gelu(h_ref)) < tol
+    assert rel(gh, hr.grad) < tol
     # fc2 + gamma + residual
     out = torch.empty(M, Cc, device=dev)
     K.linear_fwd(a, w2.to(act).to(dev), out=out, bias=b2.to(dev), gamma=gam.to(dev), residual=x.to(dev),
@@ -99,6 +108,11 @@ def test_gemm_epilogues(dev, compute_bf16):
     hh = h.float().cpu().requires_grad_(True)
     F.gelu(hh).backward(q(d * gam) @ q(w2))
     assert rel(dh, hh.grad) < tol
+    # the same through the stored GELU' (SV_EPI_MUL_AUX)
+    dh2 = torch.empty_like(dh)
+    K.linear_dgrad(d.to(dev), w2.to(act).to(dev), out=dh2, epilogue=nv.SV_EPI_MUL_AUX, a_scale_k=gam.to(dev),
+                   aux=gh, compute_bf16=compute_bf16)
+    assert rel(dh2, (q(d * gam) @ q(w2)) * gh.float().cpu()) < tol
     # wgrad slabs (+ fused bias-gradient column sums)
     cs = torch.zeros(Cc, device=dev)
     G = K.linear_wgrad(d.to(dev), a, bias_out=cs, compute_bf16=compute_bf16)

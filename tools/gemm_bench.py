@@ -1,0 +1,78 @@
+"""Standalone timing of the ConvNeXt-base @512 bs32 GEMM shapes through sv_gemm (HIP events).
+
+    python tools/gemm_bench.py [--stages S3] [--iters 20]
+"""
+
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import __graft_entry__  # noqa: E402
+
+__graft_entry__.load_package()
+from spine_vision_amd import kernels as K  # noqa: E402
+from spine_vision_amd import native as nv  # noqa: E402
+
+STAGES = {"S1": (524288, 128), "S2": (131072, 256), "S3": (32768, 512), "S4": (8192, 1024)}
+
+
+def cases(M, C, dev):
+    bf = torch.bfloat16
+    y = torch.randn(M, C, device=dev).to(bf)
+    w1 = (torch.randn(4 * C, C, device=dev) * 0.05).to(bf)
+    w2 = (torch.randn(C, 4 * C, device=dev) * 0.05).to(bf)
+    b1 = torch.zeros(4 * C, device=dev)
+    b2 = torch.zeros(C, device=dev)
+    gam = torch.ones(C, device=dev)
+    h = torch.randn(M, 4 * C, device=dev).to(bf)
+    a = torch.randn(M, 4 * C, device=dev).to(bf)
+    x = torch.randn(M, C, device=dev)
+    d = torch.randn(M, C, device=dev).to(bf)
+    dh = torch.randn(M, 4 * C, device=dev).to(bf)
+    outh = torch.empty(M, 4 * C, device=dev, dtype=bf)
+    outa = torch.empty_like(outh)
+    out = torch.empty(M, C, device=dev)
+    fl = 2.0 * M * C * 4 * C
+    return [
+        ("fc1_fwd(gelu2)", fl, lambda: K.linear_fwd(y, w1, out=outh, out2=outa, bias=b1, epilogue=nv.SV_EPI_BIAS_GELU2)),
+        ("fc1_fwd(dual)", fl, lambda: K.linear_fwd(y, w1, out=outh, out2=outa, bias=b1,
+                                                  epilogue=nv.SV_EPI_BIAS_GELU_DUAL)),
+        ("fc1_fwd(store)", fl, lambda: K.linear_fwd(y, w1, out=outh, bias=b1)),
+        ("fc2_fwd(res)", fl, lambda: K.linear_fwd(a, w2, out=out, bias=b2, gamma=gam, residual=x,
+                                                 epilogue=nv.SV_EPI_BIAS_GAMMA_RES)),
+        ("fc2_dgrad(gelu')", fl, lambda: K.linear_dgrad(d, w2, out=outh, epilogue=nv.SV_EPI_GELU_GRAD, aux=h)),
+        ("fc2_dgrad(mul)", fl, lambda: K.linear_dgrad(d, w2, out=outh, epilogue=nv.SV_EPI_MUL_AUX, aux=h)),
+        ("fc1_dgrad", fl, lambda: K.linear_dgrad(dh, w1, out=out)),
+        ("fc2_wgrad", fl, lambda: K.linear_wgrad(d, a)),
+        ("fc1_wgrad", fl, lambda: K.linear_wgrad(dh, y)),
+    ]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stages", default="S1,S2,S3,S4")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for st in args.stages.split(","):
+        M, C = STAGES[st]
+        for name, fl, fn in cases(M, C, dev):
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / args.iters * 1e3
+            print(f"{st} M={M:7d} C={C:5d} {name:18s} {us:8.1f} us  {fl / us / 1e6:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
