@@ -1,0 +1,134 @@
+"""Localization batches (reference: spine_vision/training/datasets/localization.py:41-337)."""
+
+from __future__ import annotations
+
+import csv
+from collections import Counter, defaultdict
+from pathlib import Path
+from typing import Any, Literal
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+LEVELS = ("L1/L2", "L2/L3", "L3/L4", "L4/L5", "L5/S1")
+NUM_LEVELS = len(LEVELS)
+IDX_TO_LEVEL = dict(enumerate(LEVELS))
+LEVEL_TO_IDX = {v: k for k, v in IDX_TO_LEVEL.items()}
+SERIES_TYPE_TO_IDX = {"sag_t1": 0, "sag_t2": 1, "ct": 2}
+_MEAN = torch.tensor([0.485, 0.456, 0.406]).view(3, 1, 1)
+_STD = torch.tensor([0.229, 0.224, 0.225]).view(3, 1, 1)
+
+
+def normalize_u8(img_u8: torch.Tensor) -> torch.Tensor:
+    """uint8 [H,W] or [3,H,W] -> ToTensor (/255) -> ImageNet Normalize, f32 [3,H,W]."""
+    x = img_u8.float() / 255.0
+    if x.dim() == 2:
+        x = x.unsqueeze(0).expand(3, -1, -1)
+    return (x - _MEAN) / _STD
+
+
+class LocalizationDataset(Dataset):
+    """annotations.csv (image_path, level, relative_x, relative_y, series_type, source) + images.
+    Per sample: image [3,H,W] (Resize -> ToTensor -> Normalize), coords [5,2], mask [5],
+    series_type_idx, metadata -- the reference's record layout and patient-free image split."""
+
+    def __init__(self, data_path: Path, split: Literal["train", "val", "test", "all"] = "all", val_ratio: float = 0.15,
+                 test_ratio: float = 0.05, series_types: list[str] | None = None, sources: list[str] | None = None,
+                 image_size: tuple[int, int] = (256, 256), augment: bool = True, normalize: bool = True,
+                 seed: int = 42) -> None:
+        self.data_path = Path(data_path)
+        self.split = split
+        self.image_size = tuple(image_size)
+        self.augment = augment and split == "train"
+        self.normalize = normalize
+        ann = self.data_path / "annotations.csv"
+        if not ann.exists():
+            raise FileNotFoundError(f"Annotations not found: {ann}")
+        with open(ann, newline="") as f:
+            recs = list(csv.DictReader(f))
+        if series_types:
+            recs = [r for r in recs if r["series_type"] in series_types]
+        if sources:
+            recs = [r for r in recs if r["source"] in sources]
+        self.image_records: dict[str, dict[str, Any]] = {}
+        for r in recs:
+            d = self.image_records.setdefault(r["image_path"], {"coords": {}, "series_type": r["series_type"],
+                                                                "source": r["source"]})
+            lvl = LEVEL_TO_IDX.get(r["level"], None)
+            if lvl is None:
+                lvl = int(r["level"])
+            d["coords"][lvl] = (float(r["relative_x"]), float(r["relative_y"]))
+        images = list(self.image_records)
+        perm = np.random.RandomState(seed).permutation(len(images))
+        n_test, n_val = int(len(images) * test_ratio), int(len(images) * val_ratio)
+        idx = {"test": perm[:n_test], "val": perm[n_test:n_test + n_val], "train": perm[n_test + n_val:]}
+        keep = set(images[i] for i in idx[split]) if split != "all" else set(images)
+        self.image_list = [im for im in images if im in keep]
+
+    def __len__(self) -> int:
+        return len(self.image_list)
+
+    def _load(self, rel: str) -> torch.Tensor:
+        from PIL import Image
+
+        im = Image.open(self.data_path / rel).convert("L").resize((self.image_size[1], self.image_size[0]),
+                                                                  Image.BILINEAR)
+        return torch.from_numpy(np.asarray(im, dtype=np.uint8).copy())
+
+    def __getitem__(self, i: int) -> dict[str, Any]:
+        rel = self.image_list[i]
+        rec = self.image_records[rel]
+        u8 = self._load(rel)
+        image = normalize_u8(u8) if self.normalize else u8.float().div(255).unsqueeze(0).expand(3, -1, -1)
+        coords = torch.zeros(NUM_LEVELS, 2)
+        mask = torch.zeros(NUM_LEVELS)
+        for lvl, (x, y) in rec["coords"].items():
+            coords[lvl, 0], coords[lvl, 1], mask[lvl] = x, y, 1.0
+        return {"image": image, "coords": coords, "mask": mask,
+                "series_type_idx": SERIES_TYPE_TO_IDX.get(rec["series_type"], 0),
+                "metadata": {"image_path": rel, "source": rec["source"], "series_type": rec["series_type"]}}
+
+    def get_stats(self) -> dict[str, Any]:
+        lc: dict[int, int] = defaultdict(int)
+        for rel in self.image_list:
+            for lvl in self.image_records[rel]["coords"]:
+                lc[lvl] += 1
+        return {"num_images": len(self.image_list), "num_annotations": sum(lc.values()),
+                "levels": {IDX_TO_LEVEL[k]: v for k, v in sorted(lc.items())},
+                "series_types": dict(Counter(self.image_records[r]["series_type"] for r in self.image_list)),
+                "sources": dict(Counter(self.image_records[r]["source"] for r in self.image_list)),
+                "split": self.split}
+
+
+class SyntheticLocalizationDataset(Dataset):
+    """Seeded synthetic samples with the BASELINE input spec: uint8 grayscale U{0..255} -> RGB ->
+    /255 -> ImageNet normalise; coords U(0.05, 0.95); ~10% of levels masked."""
+
+    def __init__(self, n: int, image_size: tuple[int, int] = (512, 512), seed: int = 42) -> None:
+        self.n, self.image_size, self.seed = n, tuple(image_size), seed
+
+    def __len__(self) -> int:
+        return self.n
+
+    def __getitem__(self, i: int) -> dict[str, Any]:
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
+        u8 = torch.randint(0, 256, self.image_size, generator=g, dtype=torch.uint8)
+        coords = torch.rand(NUM_LEVELS, 2, generator=g) * 0.9 + 0.05
+        mask = (torch.rand(NUM_LEVELS, generator=g) >= 0.1).float()
+        return {"image": normalize_u8(u8), "coords": coords, "mask": mask, "series_type_idx": 1,
+                "metadata": {"image_path": f"synthetic_{i}.png", "source": "synthetic", "series_type": "sag_t2"}}
+
+    def get_stats(self) -> dict[str, Any]:
+        return {"num_images": self.n, "source": "synthetic"}
+
+
+class LocalizationCollator:
+    def __call__(self, samples: list[dict[str, Any]]) -> dict[str, Any]:
+        return {
+            "image": torch.stack([s["image"] for s in samples]),
+            "coords": torch.stack([s["coords"] for s in samples]),
+            "mask": torch.stack([s["mask"] for s in samples]),
+            "series_type_idx": torch.tensor([s["series_type_idx"] for s in samples], dtype=torch.long),
+            "metadata": [s["metadata"] for s in samples],
+        }

@@ -1,0 +1,148 @@
+"""CPU: trainer host logic (loop, history, scheduler quirk, checkpoints, early stop, sharding).
+
+The product backbone needs the HIP library, so these tests inject a small CPU model and a torch
+optimizer through the reference's own override points (``model=`` and ``_create_optimizer``,
+spine_vision/training/trainers/base.py:384-390) -- exactly what a reference user can do."""
+
+import pytest
+import torch
+
+from oracle import convnext as oc
+from oracle import heads as oh
+from spine_vision_amd.training.datasets import SyntheticClassificationDataset, SyntheticLocalizationDataset
+from spine_vision_amd.training.trainers import (
+    ClassificationConfig,
+    ClassificationTrainer,
+    LocalizationConfig,
+    LocalizationTrainer,
+    ShardedBatchSampler,
+)
+
+
+class TinyLoc(oh.CoordinateRegressor):
+    name = "tiny"
+
+    def __init__(self):
+        super().__init__(oc.ConvNeXt((1, 1, 1, 1), (64, 64, 64, 64)), 64, dropout=0.0)
+
+    def get_loss(self, pred, target, mask=None):
+        return super().get_loss(pred, target, mask)
+
+    def unfreeze_backbone(self):
+        for p in self.backbone.parameters():
+            p.requires_grad = True
+
+
+class CpuLocTrainer(LocalizationTrainer):
+    def _create_optimizer(self):
+        return torch.optim.AdamW(self.model.parameters(), lr=self.config.learning_rate,
+                                 weight_decay=self.config.weight_decay)
+
+
+def _cfg(tmp_path, **kw):
+    base = dict(output_path=tmp_path, batch_size=4, num_epochs=3, num_workers=0, pin_memory=False,
+                image_size=(32, 32), pretrained=False, save_frequency=2, log_frequency=1)
+    base.update(kw)
+    return LocalizationConfig(**base)
+
+
+def test_localization_trainer_loop(tmp_path):
+    cfg = _cfg(tmp_path)
+    tr = CpuLocTrainer(cfg, model=TinyLoc(), train_dataset=SyntheticLocalizationDataset(12, (32, 32), seed=1),
+                       val_dataset=SyntheticLocalizationDataset(8, (32, 32), seed=2))
+    assert len(tr.train_loader) == 3  # drop_last on train
+    res = tr.train()
+    assert len(res.history["train_loss"]) >= 1 and res.final_train_loss > 0
+    assert (tmp_path / "best_model.pt").exists()
+    assert (tmp_path / "checkpoint_epoch_2.pt").exists()
+    assert (tmp_path / "config.yaml").exists()
+    ck = torch.load(tmp_path / "checkpoint_epoch_2.pt", weights_only=False)  # our own file
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "best_metric",
+                       "best_epoch", "history", "config"}
+    assert "med" in res.history and "pck@0.05" in res.history
+
+
+def test_cosine_scheduler_quirk(tmp_path):
+    """T_max counted in steps, stepped once per epoch (reference base.py:397-404 vs 471-478)."""
+    cfg = _cfg(tmp_path, num_epochs=2, early_stopping=False)
+    tr = CpuLocTrainer(cfg, model=TinyLoc(), train_dataset=SyntheticLocalizationDataset(16, (32, 32)),
+                       val_dataset=SyntheticLocalizationDataset(4, (32, 32), seed=9))
+    assert tr.scheduler.T_max == len(tr.train_loader) * 2 == 8
+    seen = []
+    tr.on_epoch_end = lambda epoch, m: seen.append(tr.optimizer.param_groups[0]["lr"])
+    res = tr.train()
+    lrs = [1e-4] + seen
+    assert lrs[0] == pytest.approx(1e-4)  # recorded before the epoch's scheduler step
+    import math
+    expected = 1e-6 + (1e-4 - 1e-6) * (1 + math.cos(math.pi * 1 / 8)) / 2
+    assert lrs[1] == pytest.approx(expected)
+
+
+def test_resume_from_checkpoint(tmp_path):
+    cfg = _cfg(tmp_path, num_epochs=2, early_stopping=False, save_frequency=1)
+    val = SyntheticLocalizationDataset(4, (32, 32), seed=9)
+    tr = CpuLocTrainer(cfg, model=TinyLoc(), train_dataset=SyntheticLocalizationDataset(8, (32, 32)), val_dataset=val)
+    tr.train()
+    cfg2 = _cfg(tmp_path / "b", num_epochs=3, checkpoint_path=tmp_path / "checkpoint_epoch_2.pt")
+    tr2 = CpuLocTrainer(cfg2, model=TinyLoc(), train_dataset=SyntheticLocalizationDataset(8, (32, 32)),
+                        val_dataset=val)
+    r = tr2.train()
+    assert len(r.history["train_loss"]) == 3
+
+
+class TinyCls(torch.nn.Module):
+    name = "tinycls"
+
+    def __init__(self, tasks):
+        super().__init__()
+        from spine_vision_amd.core.tasks import create_loss_functions, get_strategy
+
+        self.tasks = tasks
+        self.backbone = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 4, 4), torch.nn.AdaptiveAvgPool2d(1),
+                                            torch.nn.Flatten())
+        self.heads = torch.nn.ModuleDict({t.name: torch.nn.Linear(8, t.num_classes) for t in tasks})
+        self.losses, self.weights = create_loss_functions(tasks)
+        self._strategy = get_strategy
+
+    def forward(self, x):
+        f = self.backbone(x)
+        return {k: h(f) for k, h in self.heads.items()}
+
+    def get_loss(self, preds, targets):
+        return sum(self.weights[t.name] * self.losses[t.name](preds[t.name], self._strategy(t).format_target(
+            targets[t.name])) for t in self.tasks)
+
+
+def test_classification_trainer_plumbing(tmp_path):
+    """BASELINE configs[0] plumbing: 32 synthetic crops, bs4, 2 epochs, weighted sampling, CPU."""
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    class CpuCls(ClassificationTrainer):
+        def _create_optimizer(self):
+            return torch.optim.AdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-5)
+
+    labels = ["pfirrmann", "modic", "herniation"]
+    tasks = _create_tasks_for_training(labels)
+    cfg = ClassificationConfig(output_path=tmp_path, batch_size=4, num_epochs=2, num_workers=0, pin_memory=False,
+                               target_labels=labels, output_size=(32, 32), pretrained=False)
+    tr = CpuCls(cfg, model=TinyCls(tasks), train_dataset=SyntheticClassificationDataset(32, (32, 32), seed=3,
+                                                                                       target_labels=labels),
+                val_dataset=SyntheticClassificationDataset(8, (32, 32), seed=4, target_labels=labels))
+    res = tr.train()
+    # reference quirk: history is replaced by the best checkpoint's (base.py:521-524)
+    assert len(res.history["train_loss"]) == res.best_epoch + 1
+    assert "macro_f1" in res.history
+
+
+@pytest.mark.parametrize("world,n,bs,drop", [(2, 37, 4, True), (2, 37, 4, False), (4, 64, 8, True), (3, 10, 3, False)])
+def test_sharding_matches_accelerate(world, n, bs, drop):
+    from accelerate.data_loader import BatchSamplerShard
+    from torch.utils.data import BatchSampler, SequentialSampler
+
+    for r in range(world):
+        ours = list(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
+        ref = list(BatchSamplerShard(BatchSampler(SequentialSampler(range(n)), bs, drop), num_processes=world,
+                                     process_index=r, split_batches=False, even_batches=False))
+        m = min(len(ours), len(ref))
+        assert ours[:m] == ref[:m]
+        assert len(ours) == len(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
