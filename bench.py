@@ -191,6 +191,7 @@ def main():
             "launches_timed": probe.launches,
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
+            "algorithmic_bytes_per_launch": int(probe.bytes / max(probe.launches, 1)),
             "step_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
         },
         "loss": round(final_loss, 6),

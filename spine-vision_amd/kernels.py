@@ -26,6 +26,7 @@ class GemmProbe:
         self.key = key
         self.events: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self.flops = 0.0
+        self.bytes = 0.0  # algorithmic HBM bytes: A, B read once; C (+C2, aux) once
         self.launches = 0
 
     def elapsed_ms(self) -> float:
@@ -106,6 +107,13 @@ def gemm(
         ev1.record()
         probe.events.append((ev0, ev1))
         probe.flops += 2.0 * M * N * K
+        nbytes = M * K * A.element_size() + N * K * B.element_size()
+        nbytes += (split_k if epilogue == nv.SV_EPI_SLAB else 1) * M * N * C.element_size()
+        if C2 is not None:
+            nbytes += (split_k * M if epilogue == nv.SV_EPI_SLAB else M * N) * C2.element_size()
+        if aux is not None:
+            nbytes += M * N * aux.element_size()
+        probe.bytes += nbytes
         probe.launches += 1
     else:
         call("sv_gemm", ctypes.byref(d))
