@@ -193,6 +193,87 @@ int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_
 /* y = bf16(x) over n elements (weight shadows after load_state_dict / init).                       */
 int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream);
 
+/* ---- ResNet-18/50 (ClassificationTrainer backbone) -------------------------------------------
+ * Replaces timm ResNet (BasicBlock / Bottleneck, timm/models/resnet.py, not vendored) built at
+ * spine_vision/training/models/backbone.py:166 for "resnet18"/"resnet50" (backbone.py:27,29) and run
+ * by Classifier.forward (generic.py:134-145) / ClassificationTrainer._train_step
+ * (trainers/classification.py:269-290): Conv2d (cuDNN) as implicit GEMM on MFMA, BatchNorm2d in
+ * train mode (batch statistics, eps 1e-5, momentum 0.1, unbiased running_var), ReLU, MaxPool2d(3,2,1),
+ * global average pool.
+ *
+ * Convolutions (all tensors NHWC; `dtype` is both operand and MFMA type: SV_BF16 or SV_F32):
+ *   x   [B][H][W][Cs]    input, Cs = stored channels (power of two; >= the real Cin, zero padded)
+ *   y   [B][OH][OW][Cout]  OH = (H + 2 pad - KH)/stride + 1
+ *   wp  [Cout][KH*KW][Cs]  packed weight (sv_conv_weight_pack), dtype
+ * Cout must be a multiple of 8 (bf16) / 4 (f32).                                                   */
+typedef struct sv_conv_shape {
+  int32_t B, H, W, Cs;  /* input                                      */
+  int32_t Cout;         /* output channels                            */
+  int32_t KH, KW, stride, pad;
+  int32_t Cin;          /* real input channels (<= Cs), torch weight  */
+} sv_conv_shape;
+/* wp[co][t][c] = w[co][c][t] (c < Cin) else 0, cast to `dtype`; w = torch [Cout][Cin][KH][KW] f32. */
+int sv_conv_weight_pack(const float* w, void* wp, int32_t dtype, const sv_conv_shape* s, sv_stream_t stream);
+/* y = conv(x, w).  y_dtype may differ from dtype (f32 or bf16 store).                             */
+int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
+                sv_stream_t stream);
+/* dx (+)= conv_transpose(dy, w): dy [B][OH][OW][Cout] (dtype), dx [B][H][W][Cs] (dx_dtype). Stride-2
+ * convolutions run as four stride-1 sub-convolutions, one per output parity class.                 */
+int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                     int32_t dtype, const sv_conv_shape* s, sv_stream_t stream);
+/* dw (+)= dy^T * im2col(x) into torch layout [Cout][Cin][KH][KW] f32, through split-K f32 slabs in
+ * `work` (sv_conv_bwd_weight_work_floats(s) floats).                                              */
+int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s);
+int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate, int32_t dtype,
+                       const sv_conv_shape* s, sv_stream_t stream);
+/* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
+int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
+                     int32_t Cs, sv_stream_t stream);
+
+/* BatchNorm2d, train mode.  stats: part [nparts][2][C] (shifted sums, shift = row 0), then
+ * finish -> mean[C], rstd[C] and (running_mean, running_var) updated in place with `momentum`
+ * (unbiased variance, torch semantics) when they are non-NULL.                                    */
+int sv_bn_nparts(int64_t rows, int32_t C);
+int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream);
+int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows, int32_t C,
+                       float eps, float momentum, float* mean, float* rstd, float* running_mean,
+                       float* running_var, sv_stream_t stream);
+/* eval mode: mean = running_mean, rstd = 1/sqrt(running_var + eps).                               */
+int sv_bn_eval_params(const float* running_mean, const float* running_var, float eps, float* mean, float* rstd,
+                      int32_t C, sv_stream_t stream);
+/* out = act( gamma (y - mean) rstd + beta  + res ),  act = ReLU if relu;
+ * res = 0 (res == NULL) | res (res_mean == NULL) | res_gamma (res - res_mean) res_rstd + res_beta
+ * (the BN'd downsample shortcut).                                                                  */
+int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                  const float* beta, const void* res, int32_t res_dtype, const float* res_mean,
+                  const float* res_rstd, const float* res_gamma, const float* res_beta, int32_t relu, void* out,
+                  int32_t out_dtype, int64_t rows, int32_t C, sv_stream_t stream);
+/* backward.  g = dout * (act > 0) (act == NULL: no mask); xhat = (y - mean) rstd.
+ * bn_bwd_stats: part [nparts][2][C] = (sum g, sum g xhat);  bn_bwd_finish: sums[2][C], and
+ * dgamma += sum g xhat, dbeta += sum g;  bn_bwd_apply: dx = gamma rstd (g - sum g/n - xhat sum gx/n);
+ * if gmask != NULL it also stores g itself there (the masked gradient, for the block shortcut).    */
+int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                    int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
+                    sv_stream_t stream);
+int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
+                     sv_stream_t stream);
+int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                    int32_t y_dtype, const float* mean, const float* rstd, const float* gamma, const float* sums,
+                    void* dx, int32_t dx_dtype, float* gmask, int64_t rows, int32_t C, sv_stream_t stream);
+/* g = dout * (act > 0), f32 out (block-output ReLU of the residual join).                         */
+int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g, int64_t n,
+                 sv_stream_t stream);
+/* MaxPool2d(3, stride 2, pad 1) NHWC; idx [B][OH][OW][C] uint8 = argmax tap (first max in (kh,kw)
+ * order, torch semantics); bwd gathers dout into dx [B][H][W][C] (dx_dtype; overwrite).           */
+int sv_maxpool3s2_fwd(const void* x, int32_t x_dtype, void* y, uint8_t* idx, int32_t B, int32_t H, int32_t W,
+                      int32_t C, sv_stream_t stream);
+int sv_maxpool3s2_bwd(const void* dout, int32_t dout_dtype, const uint8_t* idx, void* dx, int32_t dx_dtype,
+                      int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+/* global average pool: feat[b][c] = mean_hw x; bwd: dx[b][hw][c] = dfeat[b][c] / HW (f32).        */
+int sv_avgpool_fwd(const void* x, int32_t x_dtype, float* feat, int32_t B, int32_t HW, int32_t C,
+                   sv_stream_t stream);
+int sv_avgpool_bwd(const float* dfeat, float* dx, int32_t B, int32_t HW, int32_t C, sv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,302 @@
+"""ResNet-18 / ResNet-50 backbone on the gfx950 kernel library -- drop-in for
+``timm.create_model("resnet18.a1_in1k" | "resnet50.a1_in1k", num_classes=0)`` as called at
+spine_vision/training/models/backbone.py:166-170 (names at backbone.py:27,29; timm 1.0.22
+``timm/models/resnet.py``: BasicBlock [2,2,2,2] / Bottleneck [3,4,6,3], stride on the 3x3 conv,
+1x1 conv + BN downsample, conv7x7/s2 stem + BN + ReLU + MaxPool(3,2,1), global average pool).
+
+* Same module tree / ``state_dict`` keys as timm (``conv1``, ``bn1``, ``layerN.i.{conv1,bn1,conv2,bn2,
+  conv3,bn3,downsample.{0,1}}``), ``num_features``, ``forward([B,3,H,W] f32) -> [B,F]``.  Sub-modules
+  are parameter/buffer containers; their own ``forward`` is never called.
+* Every convolution is an implicit GEMM on MFMA over NHWC activations (``sv_conv_*``; no im2col
+  buffers); BatchNorm uses train-mode batch statistics (and updates running_mean / running_var /
+  num_batches_tracked exactly like torch) or the running statistics in eval mode; BN + ReLU (+ the
+  residual add, including the BN of the downsample shortcut) is one fused pass.
+* Backward is an explicit kernel sequence writing the parameter gradients into ``p.grad`` (views of
+  the trainer's flat gradient buffer) and calling ``grad_ready_hook`` after each block so the DDP
+  bucketer can start all-reducing while earlier blocks are still being differentiated.
+* ``precision="bf16"``: bf16 MFMA and bf16 activations, f32 statistics / block-input gradient stream /
+  master weights.  ``precision="fp32"``: f32 everywhere with exact f32 MFMA (parity mode).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable
+
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+
+RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
+BN_EPS = 1e-5
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def convs(self):
+        """(conv, bn, kernel, stride, pad, relu) of the main path, in forward order."""
+        return [(self.conv1, self.bn1, 3, self.stride, 1, True), (self.conv2, self.bn2, 3, 1, 1, False)]
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.downsample = downsample
+        self.stride = stride
+
+    def convs(self):
+        return [(self.conv1, self.bn1, 1, 1, 0, True), (self.conv2, self.bn2, 3, self.stride, 1, True),
+                (self.conv3, self.bn3, 1, 1, 0, False)]
+
+
+class _ResNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, model):  # noqa: D401 - autograd signature
+        feat, tape = model._forward_impl(x, save=True)
+        ctx.model = model
+        ctx.tape = tape
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        ctx.model._backward_impl(ctx.tape, dfeat)
+        ctx.tape = None
+        return None, None, None
+
+
+@dataclass
+class _Tape:
+    stem: tuple = ()
+    blocks: list = field(default_factory=list)
+    out_shape: tuple = ()
+
+
+class ResNetHip(nn.Module):
+    def __init__(self, kind: str = "bottleneck", layers=(3, 4, 6, 3), precision: str = "bf16") -> None:
+        super().__init__()
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        self.precision = precision
+        block = BasicBlock if kind == "basic" else Bottleneck
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        inplanes = 64
+        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for j in range(n):
+                s = stride if j == 0 else 1
+                ds = None
+                if j == 0 and (s != 1 or inplanes != planes * block.expansion):
+                    ds = nn.Sequential(nn.Conv2d(inplanes, planes * block.expansion, 1, stride=s, bias=False),
+                                       nn.BatchNorm2d(planes * block.expansion))
+                blocks.append(block(inplanes, planes, s, ds))
+                inplanes = planes * block.expansion
+            setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
+        self.num_features = inplanes
+        self.grad_ready_hook: Callable[[list], None] | None = None
+        self._init_weights()
+
+    # timm ResNet.init_weights: kaiming_normal_(fan_out, relu) for convs, BN weight 1 / bias 0, and
+    # zero_init_last=True: the last BN of every block starts at weight 0
+    def _init_weights(self) -> None:
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        for blk in self.blocks():
+            nn.init.zeros_(blk.convs()[-1][1].weight)
+
+    @property
+    def compute_bf16(self) -> bool:
+        return self.precision == "bf16"
+
+    @property
+    def act_dtype(self) -> torch.dtype:
+        return torch.bfloat16 if self.compute_bf16 else torch.float32
+
+    def blocks(self):
+        for i in range(1, 5):
+            yield from getattr(self, f"layer{i}")
+
+    # -- forward -----------------------------------------------------------------------------------
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("ResNetHip runs on the MI355X kernel library only (got a CPU tensor)")
+        x = x.float().contiguous()
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if need_grad:
+            anchor = torch.zeros((), device=x.device, requires_grad=True)
+            return _ResNetFn.apply(x, anchor, self)
+        feat, _ = self._forward_impl(x, save=False)
+        return feat
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward(x)
+
+    def _bn(self, bn: nn.BatchNorm2d, y2d: torch.Tensor):
+        """(mean, rstd) of a BatchNorm: batch statistics (+ running update) in train mode."""
+        if self.training:
+            momentum = 0.1 if bn.momentum is None else bn.momentum
+            mean, rstd = K.bn_stats(y2d, eps=bn.eps, momentum=momentum, running_mean=bn.running_mean,
+                                    running_var=bn.running_var)
+            bn.num_batches_tracked.add_(1)
+            return mean, rstd
+        return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
+
+    def _conv(self, x4d, conv, k, stride, pad, Cin=None):
+        """conv(x) -> (y, packed weight, shape); y in the activation dtype."""
+        B, H, W, Cs = x4d.shape
+        s = K.conv_shape(B, H, W, Cs, conv.weight.shape[0], k, stride, pad, Cin)
+        wp = K.conv_weight_pack(conv.weight.detach(), Cs, self.act_dtype)
+        return K.conv_fwd(x4d, wp, s, self.act_dtype), wp, s
+
+    @torch.no_grad()
+    def _forward_impl(self, img: torch.Tensor, save: bool):
+        act = self.act_dtype
+        cs0 = 8 if self.compute_bf16 else 4
+        x0 = K.image_to_nhwc(img, cs0, act)
+        y0, wp0, s0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3)
+        B, H, W, C = y0.shape
+        m0, r0 = self._bn(self.bn1, y0.view(-1, C))
+        a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act).view(B, H, W, C)
+        x, idx = K.maxpool_fwd(a0)
+        tape = _Tape() if save else None
+        if save:
+            tape.stem = (x0, y0, m0, r0, a0, idx, wp0, s0)
+        for blk in self.blocks():
+            x_in = x
+            cur = x
+            saved = []
+            convs = blk.convs()
+            for ci, (conv, bn, k, st, pad, relu) in enumerate(convs):
+                y, wp, s = self._conv(cur, conv, k, st, pad)
+                Bq, Hq, Wq, Cq = y.shape
+                mean, rstd = self._bn(bn, y.view(-1, Cq))
+                last = ci == len(convs) - 1
+                if not last:
+                    a = K.bn_act(y.view(-1, Cq), mean, rstd, bn.weight, bn.bias, relu=True, out_dtype=act)
+                    a = a.view(Bq, Hq, Wq, Cq)
+                    saved.append((cur, y, mean, rstd, a, wp, s))
+                    cur = a
+                else:
+                    saved.append((cur, y, mean, rstd, None, wp, s))
+            # residual join: out = relu(bn_last(y) + shortcut), shortcut = x or BN(conv_ds(x))
+            _, y_last, m_last, r_last, _, _, _ = saved[-1]
+            bn_last = convs[-1][1]
+            Bq, Hq, Wq, Cq = y_last.shape
+            ds_saved = None
+            if blk.downsample is not None:
+                dconv, dbn = blk.downsample[0], blk.downsample[1]
+                yd, wpd, sd = self._conv(x_in, dconv, 1, blk.stride, 0)
+                md, rd = self._bn(dbn, yd.view(-1, Cq))
+                out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias, res=yd.view(-1, Cq),
+                               res_bn=(md, rd, dbn.weight, dbn.bias), relu=True, out_dtype=act)
+                ds_saved = (yd, md, rd, wpd, sd)
+            else:
+                out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias,
+                               res=x_in.view(-1, Cq), relu=True, out_dtype=act)
+            out = out.view(Bq, Hq, Wq, Cq)
+            if save:
+                tape.blocks.append((x_in, saved, ds_saved, out))
+            x = out
+        feat = K.avgpool_fwd(x)
+        if save:
+            tape.out_shape = tuple(x.shape)
+        return feat, tape
+
+    # -- backward ----------------------------------------------------------------------------------
+    @staticmethod
+    def _grad(p: torch.Tensor) -> torch.Tensor:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        return p.grad
+
+    def _ready(self, params: list) -> None:
+        if self.grad_ready_hook is not None:
+            self.grad_ready_hook(params)
+
+    @torch.no_grad()
+    def _backward_impl(self, tape: _Tape, dfeat: torch.Tensor) -> None:
+        act = self.act_dtype
+        g = self._grad
+        d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
+        for blk, (x_in, saved, ds_saved, out) in zip(reversed(list(self.blocks())), reversed(tape.blocks)):
+            convs = blk.convs()
+            Bq, Hq, Wq, Cq = out.shape
+            rows = Bq * Hq * Wq
+            # last BN of the main path, with the block-output ReLU mask; gm = the masked gradient
+            gm = torch.empty(rows, Cq, device=d.device, dtype=torch.float32)
+            conv, bn, _, _, _, _ = convs[-1]
+            cur_in, y, mean, rstd, _, wp, s = saved[-1]
+            dy = K.bn_bwd(d.view(rows, Cq), y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
+                          dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm)
+            params = [bn.weight, bn.bias]
+            for ci in range(len(convs) - 1, -1, -1):
+                conv, bn, _, _, _, _ = convs[ci]
+                cur_in, y, mean, rstd, a, wp, s = saved[ci]
+                dy4 = dy.view(y.shape)
+                K.conv_bwd_weight(dy4, cur_in, s, dw=g(conv.weight), accumulate=True)
+                params.append(conv.weight)
+                if ci == 0:
+                    break
+                da = K.conv_bwd_data(dy4, wp, s, dx_dtype=act)
+                pconv, pbn, _, _, _, _ = convs[ci - 1]
+                _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
+                Cp = py.shape[-1]
+                dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, act=pa.view(-1, Cp),
+                              dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act)
+                params += [pbn.weight, pbn.bias]
+            # dy is now the gradient at conv1's output; conv1's input is x_in
+            s1, wp1 = saved[0][6], saved[0][5]
+            if ds_saved is not None:
+                yd, md, rd, wpd, sd = ds_saved
+                dconv, dbn = blk.downsample[0], blk.downsample[1]
+                dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
+                               dx_dtype=act)
+                dyd4 = dyd.view(yd.shape)
+                K.conv_bwd_weight(dyd4, x_in, sd, dw=g(dconv.weight), accumulate=True)
+                dx = K.conv_bwd_data(dyd4, wpd, sd, dx_dtype=torch.float32)
+                params += [dconv.weight, dbn.weight, dbn.bias]
+            else:
+                dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
+            K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
+            d = dx
+            self._ready(params)
+        # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
+        x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
+        B, H, W, C = a0.shape
+        da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
+        dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, act=a0.view(-1, C),
+                       dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act)
+        K.conv_bwd_weight(dy0.view(y0.shape), x0, s0, dw=g(self.conv1.weight), accumulate=True)
+        self._ready([self.conv1.weight, self.bn1.weight, self.bn1.bias])
+
+
+def create_resnet(name: str, precision: str = "bf16") -> ResNetHip:
+    key = name.split(".")[0]
+    if key not in RESNET_CFGS:
+        raise ValueError(f"unsupported ResNet variant {name!r}")
+    kind, layers = RESNET_CFGS[key]
+    return ResNetHip(kind, layers, precision=precision)

@@ -1,0 +1,492 @@
+// BatchNorm2d (train-mode batch statistics), ReLU, MaxPool2d(3,2,1) and global average pooling for
+// the ResNet-18/50 classification backbone (gfx950), NHWC.
+//
+// Replaces timm ResNet's nn.BatchNorm2d / nn.ReLU / nn.MaxPool2d / SelectAdaptivePool2d
+// (timm/models/resnet.py, built at spine_vision/training/models/backbone.py:166) and their autograd
+// backward.  All kernels are HBM-bound streaming passes: one thread owns 4 consecutive channels
+// (16-B f32 / 8-B bf16 accesses), channel statistics are reduced per block into deterministic
+// partials [nparts][2][C] and finished by a one-thread-per-channel pass (no atomics, bit-stable).
+// Batch statistics use shifted sums (shift = the channel's value in row 0) so mean^2 >> var does
+// not cancel catastrophically in f32.
+#include <math.h>
+
+#include "common.h"
+
+namespace sv {
+namespace bn {
+
+constexpr int kThreads = 256;
+
+template <typename T>
+__device__ __forceinline__ float4 ld4t(const void* p, size_t i) {
+  return ld4(reinterpret_cast<const T*>(p), i);
+}
+__device__ __forceinline__ float4 ld4d(const void* p, int dt, size_t i) {
+  return dt == SV_F32 ? ld4t<float>(p, i) : ld4t<uint16_t>(p, i);
+}
+__device__ __forceinline__ void st4d(void* p, int dt, size_t i, float4 v) {
+  if (dt == SV_F32) st4(reinterpret_cast<float*>(p), i, v);
+  else st4(reinterpret_cast<uint16_t*>(p), i, v);
+}
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 ld4f(const float* p, int c) { return *reinterpret_cast<const float4*>(p + c); }
+
+// Block layout for per-channel reductions: tpr threads cover one row (4 channels each), rp rows in
+// parallel; grid.x = channel slices of 4*tpr channels, grid.y = row parts.
+struct RedGeo {
+  int tpr, rp, cslices;
+};
+static RedGeo red_geo(int C) {
+  const int cg = C / 4;
+  RedGeo g;
+  g.tpr = cg < kThreads ? cg : kThreads;
+  g.rp = kThreads / g.tpr;
+  g.cslices = cg / g.tpr;
+  return g;
+}
+
+static int nparts_for(int64_t rows, int C) {
+  const RedGeo g = red_geo(C);
+  int64_t p = rows / (8 * g.rp);  // >= 8 rows per thread
+  const int64_t cap = 1024 / g.cslices;
+  if (p > cap) p = cap;
+  if (p < 1) p = 1;
+  return (int)p;
+}
+
+// block-level reduce of two float4 per thread over the rp row-groups; writes part[p][0|1][c..c+3]
+__device__ __forceinline__ void reduce_write(float4 s1, float4 s2, int tpr, int rp, int c, int C, float* part) {
+  __shared__ float4 red[2][kThreads];
+  const int t = threadIdx.x;
+  red[0][t] = s1;
+  red[1][t] = s2;
+  __syncthreads();
+  if (t < tpr) {
+    for (int r = 1; r < rp; ++r) {
+      const float4 a = red[0][r * tpr + t], b = red[1][r * tpr + t];
+      s1.x += a.x; s1.y += a.y; s1.z += a.z; s1.w += a.w;
+      s2.x += b.x; s2.y += b.y; s2.z += b.z; s2.w += b.w;
+    }
+    float* o = part + (size_t)blockIdx.y * 2 * C;
+    *reinterpret_cast<float4*>(o + c) = s1;
+    *reinterpret_cast<float4*>(o + C + c) = s2;
+  }
+}
+
+// forward statistics: shifted sums S1 = sum (y - y0), S2 = sum (y - y0)^2
+__global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict__ y, int ydt, int64_t rows, int C,
+                                                         int tpr, int rp, int64_t rpp, float* __restrict__ part) {
+  const int t = threadIdx.x;
+  const int c = (blockIdx.x * tpr + t % tpr) * 4;
+  const int rsub = t / tpr;
+  const float4 k = ld4d(y, ydt, (size_t)c);
+  float4 s1 = f4(0.f), s2 = f4(0.f);
+  const int64_t r0 = (int64_t)blockIdx.y * rpp;
+  int64_t r1 = r0 + rpp;
+  if (r1 > rows) r1 = rows;
+  for (int64_t r = r0 + rsub; r < r1; r += rp) {
+    const float4 v = ld4d(y, ydt, (size_t)r * C + c);
+    const float dx = v.x - k.x, dy = v.y - k.y, dz = v.z - k.z, dw = v.w - k.w;
+    s1.x += dx; s1.y += dy; s1.z += dz; s1.w += dw;
+    s2.x = fmaf(dx, dx, s2.x); s2.y = fmaf(dy, dy, s2.y); s2.z = fmaf(dz, dz, s2.z); s2.w = fmaf(dw, dw, s2.w);
+  }
+  reduce_write(s1, s2, tpr, rp, c, C, part);
+}
+
+__global__ void stats_finish_kernel(const void* __restrict__ y, int ydt, const float* __restrict__ part, int P,
+                                    int64_t rows, int C, float eps, float momentum, float* __restrict__ mean,
+                                    float* __restrict__ rstd, float* __restrict__ rmean, float* __restrict__ rvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int p = 0; p < P; ++p) {
+    s1 += part[(size_t)p * 2 * C + c];
+    s2 += part[(size_t)p * 2 * C + C + c];
+  }
+  const float k = ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
+  const float n = (float)rows;
+  const float m1 = s1 / n;
+  const float var = fmaxf(s2 / n - m1 * m1, 0.f);
+  const float mu = k + m1;
+  mean[c] = mu;
+  rstd[c] = 1.0f / sqrtf(var + eps);
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (rows > 1 ? var * n / (n - 1.f) : var);
+}
+
+__global__ void eval_params_kernel(const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                   float* __restrict__ mean, float* __restrict__ rstd, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  rstd[c] = 1.0f / sqrtf(rv[c] + eps);
+}
+
+struct ActArgs {
+  const void* y; int ydt;
+  const float *mean, *rstd, *gamma, *beta;
+  const void* res; int rdt;
+  const float *rmean, *rrstd, *rgamma, *rbeta;
+  int relu;
+  void* out; int odt;
+  int64_t rows; int C;
+};
+
+__global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
+  const int64_t n4 = a.rows * a.C / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t e = (size_t)i * 4;
+    const int c = (int)(e % a.C);
+    const float4 v = ld4d(a.y, a.ydt, e);
+    const float4 mu = ld4f(a.mean, c), rs = ld4f(a.rstd, c), g = ld4f(a.gamma, c), b = ld4f(a.beta, c);
+    float4 o = make_float4(fmaf(g.x * rs.x, v.x - mu.x, b.x), fmaf(g.y * rs.y, v.y - mu.y, b.y),
+                           fmaf(g.z * rs.z, v.z - mu.z, b.z), fmaf(g.w * rs.w, v.w - mu.w, b.w));
+    if (a.res) {
+      float4 r = ld4d(a.res, a.rdt, e);
+      if (a.rmean) {
+        const float4 rm = ld4f(a.rmean, c), rr = ld4f(a.rrstd, c), rg = ld4f(a.rgamma, c), rb = ld4f(a.rbeta, c);
+        r = make_float4(fmaf(rg.x * rr.x, r.x - rm.x, rb.x), fmaf(rg.y * rr.y, r.y - rm.y, rb.y),
+                        fmaf(rg.z * rr.z, r.z - rm.z, rb.z), fmaf(rg.w * rr.w, r.w - rm.w, rb.w));
+      }
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    if (a.relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    st4d(a.out, a.odt, e, o);
+  }
+}
+
+__device__ __forceinline__ float4 masked(float4 g, const void* act, int adt, size_t e) {
+  if (act) {
+    const float4 m = ld4d(act, adt, e);
+    g.x = m.x > 0.f ? g.x : 0.f;
+    g.y = m.y > 0.f ? g.y : 0.f;
+    g.z = m.z > 0.f ? g.z : 0.f;
+    g.w = m.w > 0.f ? g.w : 0.f;
+  }
+  return g;
+}
+
+// backward statistics: sum g and sum g * xhat, g = dout * (act > 0)
+__global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restrict__ dout, int ddt,
+                                                             const void* __restrict__ act, int adt,
+                                                             const void* __restrict__ y, int ydt,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd, int64_t rows, int C,
+                                                             int tpr, int rp, int64_t rpp, float* __restrict__ part) {
+  const int t = threadIdx.x;
+  const int c = (blockIdx.x * tpr + t % tpr) * 4;
+  const int rsub = t / tpr;
+  const float4 mu = ld4f(mean, c), rs = ld4f(rstd, c);
+  float4 s1 = f4(0.f), s2 = f4(0.f);
+  const int64_t r0 = (int64_t)blockIdx.y * rpp;
+  int64_t r1 = r0 + rpp;
+  if (r1 > rows) r1 = rows;
+  for (int64_t r = r0 + rsub; r < r1; r += rp) {
+    const size_t e = (size_t)r * C + c;
+    const float4 g = masked(ld4d(dout, ddt, e), act, adt, e);
+    const float4 v = ld4d(y, ydt, e);
+    s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
+    s2.x = fmaf(g.x, (v.x - mu.x) * rs.x, s2.x);
+    s2.y = fmaf(g.y, (v.y - mu.y) * rs.y, s2.y);
+    s2.z = fmaf(g.z, (v.z - mu.z) * rs.z, s2.z);
+    s2.w = fmaf(g.w, (v.w - mu.w) * rs.w, s2.w);
+  }
+  reduce_write(s1, s2, tpr, rp, c, C, part);
+}
+
+__global__ void bwd_finish_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ sums,
+                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int p = 0; p < P; ++p) {
+    s1 += part[(size_t)p * 2 * C + c];
+    s2 += part[(size_t)p * 2 * C + C + c];
+  }
+  sums[c] = s1;
+  sums[C + c] = s2;
+  if (dgamma) dgamma[c] += s2;
+  if (dbeta) dbeta[c] += s1;
+}
+
+struct BwdArgs {
+  const void* dout; int ddt;
+  const void* act; int adt;
+  const void* y; int ydt;
+  const float *mean, *rstd, *gamma, *sums;
+  void* dx; int xdt;
+  float* gmask;
+  int64_t rows; int C;
+};
+
+__global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
+  const int64_t n4 = a.rows * a.C / 4;
+  const float inv_n = 1.0f / (float)a.rows;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t e = (size_t)i * 4;
+    const int c = (int)(e % a.C);
+    const float4 g = masked(ld4d(a.dout, a.ddt, e), a.act, a.adt, e);
+    const float4 v = ld4d(a.y, a.ydt, e);
+    const float4 mu = ld4f(a.mean, c), rs = ld4f(a.rstd, c), ga = ld4f(a.gamma, c);
+    const float4 sg = ld4f(a.sums, c), sgx = ld4f(a.sums + a.C, c);
+    float4 o;
+    o.x = ga.x * rs.x * (g.x - sg.x * inv_n - (v.x - mu.x) * rs.x * sgx.x * inv_n);
+    o.y = ga.y * rs.y * (g.y - sg.y * inv_n - (v.y - mu.y) * rs.y * sgx.y * inv_n);
+    o.z = ga.z * rs.z * (g.z - sg.z * inv_n - (v.z - mu.z) * rs.z * sgx.z * inv_n);
+    o.w = ga.w * rs.w * (g.w - sg.w * inv_n - (v.w - mu.w) * rs.w * sgx.w * inv_n);
+    st4d(a.dx, a.xdt, e, o);
+    if (a.gmask) *reinterpret_cast<float4*>(a.gmask + e) = g;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) relu_mask_kernel(const void* __restrict__ dout, int ddt,
+                                                             const void* __restrict__ act, int adt, float* __restrict__ g,
+                                                             int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t e = (size_t)i * 4;
+    *reinterpret_cast<float4*>(g + e) = masked(ld4d(dout, ddt, e), act, adt, e);
+  }
+}
+
+// ---- pooling -------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int pool_out(int n) { return (n + 2 - 3) / 2 + 1; }
+
+__global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y,
+                                                               uint8_t* __restrict__ idx, int B, int H, int W, int C) {
+  const int OH = pool_out(H), OW = pool_out(W);
+  const int64_t n4 = (int64_t)B * OH * OW * C / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % C);
+    const int64_t pix = e / C;
+    const int ox = (int)(pix % OW), oy = (int)((pix / OW) % OH);
+    const int64_t b = pix / ((int64_t)OW * OH);
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int arg[4] = {-1, -1, -1, -1};
+    for (int kh = 0; kh < 3; ++kh) {
+      const int iy = 2 * oy - 1 + kh;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ix = 2 * ox - 1 + kw;
+        if ((unsigned)ix >= (unsigned)W) continue;
+        const float4 v = ld4d(x, xdt, (size_t)((b * H + iy) * W + ix) * C + c);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (arg[u] < 0 || vv[u] > best[u] || vv[u] != vv[u]) {
+            best[u] = vv[u];
+            arg[u] = kh * 3 + kw;
+          }
+      }
+    }
+    st4d(y, xdt, (size_t)e, make_float4(best[0], best[1], best[2], best[3]));
+    *reinterpret_cast<uchar4*>(idx + e) = make_uchar4((uint8_t)arg[0], (uint8_t)arg[1], (uint8_t)arg[2], (uint8_t)arg[3]);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(const void* __restrict__ dout, int ddt,
+                                                               const uint8_t* __restrict__ idx, void* __restrict__ dx,
+                                                               int xdt, int B, int H, int W, int C) {
+  const int OH = pool_out(H), OW = pool_out(W);
+  const int64_t n4 = (int64_t)B * H * W * C / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % C);
+    const int64_t pix = e / C;
+    const int ix = (int)(pix % W), iy = (int)((pix / W) % H);
+    const int64_t b = pix / ((int64_t)W * H);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    // windows oy with 2 oy - 1 <= iy <= 2 oy + 1
+    const int oy0 = iy / 2, oy1 = (iy + 1) / 2;
+    const int ox0 = ix / 2, ox1 = (ix + 1) / 2;
+    for (int oy = oy0; oy <= oy1 && oy < OH; ++oy) {
+      const int kh = iy - (2 * oy - 1);
+      if (kh < 0 || kh > 2) continue;
+      for (int ox = ox0; ox <= ox1 && ox < OW; ++ox) {
+        const int kw = ix - (2 * ox - 1);
+        if (kw < 0 || kw > 2) continue;
+        const size_t o = (size_t)((b * OH + oy) * OW + ox) * C + c;
+        const uchar4 a = *reinterpret_cast<const uchar4*>(idx + o);
+        const float4 g = ld4d(dout, ddt, o);
+        const int tap = kh * 3 + kw;
+        if (a.x == tap) acc[0] += g.x;
+        if (a.y == tap) acc[1] += g.y;
+        if (a.z == tap) acc[2] += g.z;
+        if (a.w == tap) acc[3] += g.w;
+      }
+    }
+    st4d(dx, xdt, (size_t)e, make_float4(acc[0], acc[1], acc[2], acc[3]));
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) avgpool_fwd_kernel(const void* __restrict__ x, int xdt, float* __restrict__ feat,
+                                                               int B, int HW, int C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*C/4
+  if (i >= (int64_t)B * C / 4) return;
+  const int c = (int)((i * 4) % C);
+  const int64_t b = i * 4 / C;
+  float4 s = f4(0.f);
+  for (int p = 0; p < HW; ++p) {
+    const float4 v = ld4d(x, xdt, (size_t)((b * HW + p) * C + c));
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float inv = 1.0f / (float)HW;
+  *reinterpret_cast<float4*>(feat + b * C + c) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+}
+
+__global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const float* __restrict__ dfeat, float* __restrict__ dx,
+                                                               int B, int HW, int C) {
+  const int64_t n4 = (int64_t)B * HW * C / 4;
+  const float inv = 1.0f / (float)HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % C);
+    const int64_t b = e / ((int64_t)HW * C);
+    const float4 g = *reinterpret_cast<const float4*>(dfeat + b * C + c);
+    *reinterpret_cast<float4*>(dx + e) = make_float4(g.x * inv, g.y * inv, g.z * inv, g.w * inv);
+  }
+}
+
+static int grid_for(int64_t n4) {
+  int64_t b = (n4 + kThreads - 1) / kThreads;
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+static bool dt_ok(int dt) { return dt == SV_F32 || dt == SV_BF16; }
+
+}  // namespace bn
+}  // namespace sv
+
+using namespace sv;
+using namespace sv::bn;
+
+#define BN_REQUIRE_C(C, who) SV_REQUIRE((C) >= 4 && (C) % 4 == 0 && (((C) / 4) <= kThreads || ((C) / 4) % kThreads == 0), \
+                                         "%s: C=%d must be a multiple of 4 (and of 1024 above 1024)", who, (int)(C))
+
+extern "C" int sv_bn_nparts(int64_t rows, int32_t C) {
+  if (rows <= 0 || C < 4 || C % 4) return 1;
+  return nparts_for(rows, C);
+}
+
+extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_stats");
+  SV_REQUIRE(y && part && rows > 0 && dt_ok(y_dtype), "sv_bn_stats: bad arguments");
+  const RedGeo g = red_geo(C);
+  const int P = nparts_for(rows, C);
+  const int64_t rpp = (rows + P - 1) / P;
+  stats_kernel<<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(y, y_dtype, rows, C, g.tpr, g.rp, rpp, part);
+  return check_launch("sv_bn_stats");
+}
+
+extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows,
+                                  int32_t C, float eps, float momentum, float* mean, float* rstd, float* running_mean,
+                                  float* running_var, sv_stream_t stream) {
+  SV_REQUIRE(y && part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
+             "sv_bn_stats_finish: bad arguments");
+  stats_finish_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
+                                                                        momentum, mean, rstd, running_mean, running_var);
+  return check_launch("sv_bn_stats_finish");
+}
+
+extern "C" int sv_bn_eval_params(const float* running_mean, const float* running_var, float eps, float* mean,
+                                 float* rstd, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(running_mean && running_var && mean && rstd && C > 0, "sv_bn_eval_params: bad arguments");
+  eval_params_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(running_mean, running_var, eps, mean, rstd, C);
+  return check_launch("sv_bn_eval_params");
+}
+
+extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                             const float* beta, const void* res, int32_t res_dtype, const float* res_mean,
+                             const float* res_rstd, const float* res_gamma, const float* res_beta, int32_t relu,
+                             void* out, int32_t out_dtype, int64_t rows, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(C % 4 == 0 && C > 0 && rows > 0, "sv_bn_act_fwd: C must be a multiple of 4");
+  SV_REQUIRE(y && mean && rstd && gamma && beta && out && dt_ok(y_dtype) && dt_ok(out_dtype),
+             "sv_bn_act_fwd: bad arguments");
+  SV_REQUIRE(!res || dt_ok(res_dtype), "sv_bn_act_fwd: bad residual dtype");
+  SV_REQUIRE(!res_mean || (res && res_rstd && res_gamma && res_beta), "sv_bn_act_fwd: incomplete residual BN");
+  ActArgs a{y, y_dtype, mean, rstd, gamma, beta, res, res_dtype, res_mean, res_rstd, res_gamma, res_beta,
+            relu, out, out_dtype, rows, C};
+  act_kernel<<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
+  return check_launch("sv_bn_act_fwd");
+}
+
+extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                               int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C,
+                               float* part, sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_bwd_stats");
+  SV_REQUIRE(dout && y && mean && rstd && part && rows > 0 && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
+                 (!act || dt_ok(act_dtype)),
+             "sv_bn_bwd_stats: bad arguments");
+  const RedGeo g = red_geo(C);
+  const int P = nparts_for(rows, C);
+  const int64_t rpp = (rows + P - 1) / P;
+  bwd_stats_kernel<<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(dout, dout_dtype, act, act_dtype, y,
+                                                                            y_dtype, mean, rstd, rows, C, g.tpr, g.rp,
+                                                                            rpp, part);
+  return check_launch("sv_bn_bwd_stats");
+}
+
+extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
+                                sv_stream_t stream) {
+  SV_REQUIRE(part && sums && nparts > 0 && C > 0, "sv_bn_bwd_finish: bad arguments");
+  bwd_finish_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
+  return check_launch("sv_bn_bwd_finish");
+}
+
+extern "C" int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                               int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                               const float* sums, void* dx, int32_t dx_dtype, float* gmask, int64_t rows, int32_t C,
+                               sv_stream_t stream) {
+  SV_REQUIRE(C % 4 == 0 && C > 0 && rows > 0, "sv_bn_bwd_apply: C must be a multiple of 4");
+  SV_REQUIRE(dout && y && mean && rstd && gamma && sums && dx && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
+                 dt_ok(dx_dtype) && (!act || dt_ok(act_dtype)),
+             "sv_bn_bwd_apply: bad arguments");
+  BwdArgs a{dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, sums, dx, dx_dtype, gmask, rows, C};
+  bwd_apply_kernel<<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
+  return check_launch("sv_bn_bwd_apply");
+}
+
+extern "C" int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g,
+                            int64_t n, sv_stream_t stream) {
+  SV_REQUIRE(dout && act && g && n >= 0 && n % 4 == 0 && dt_ok(dout_dtype) && dt_ok(act_dtype),
+             "sv_relu_mask: bad arguments");
+  if (n == 0) return SV_OK;
+  relu_mask_kernel<<<grid_for(n / 4), kThreads, 0, (hipStream_t)stream>>>(dout, dout_dtype, act, act_dtype, g, n / 4);
+  return check_launch("sv_relu_mask");
+}
+
+extern "C" int sv_maxpool3s2_fwd(const void* x, int32_t x_dtype, void* y, uint8_t* idx, int32_t B, int32_t H, int32_t W,
+                                 int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(x && y && idx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && dt_ok(x_dtype),
+             "sv_maxpool3s2_fwd: bad arguments");
+  const int64_t n4 = (int64_t)B * pool_out(H) * pool_out(W) * C / 4;
+  maxpool_fwd_kernel<<<grid_for(n4), kThreads, 0, (hipStream_t)stream>>>(x, x_dtype, y, idx, B, H, W, C);
+  return check_launch("sv_maxpool3s2_fwd");
+}
+
+extern "C" int sv_maxpool3s2_bwd(const void* dout, int32_t dout_dtype, const uint8_t* idx, void* dx, int32_t dx_dtype,
+                                 int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(dout && idx && dx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && dt_ok(dout_dtype) &&
+                 dt_ok(dx_dtype),
+             "sv_maxpool3s2_bwd: bad arguments");
+  maxpool_bwd_kernel<<<grid_for((int64_t)B * H * W * C / 4), kThreads, 0, (hipStream_t)stream>>>(
+      dout, dout_dtype, idx, dx, dx_dtype, B, H, W, C);
+  return check_launch("sv_maxpool3s2_bwd");
+}
+
+extern "C" int sv_avgpool_fwd(const void* x, int32_t x_dtype, float* feat, int32_t B, int32_t HW, int32_t C,
+                              sv_stream_t stream) {
+  SV_REQUIRE(x && feat && B > 0 && HW > 0 && C % 4 == 0 && C > 0 && dt_ok(x_dtype), "sv_avgpool_fwd: bad arguments");
+  const int64_t n = (int64_t)B * C / 4;
+  avgpool_fwd_kernel<<<(int)((n + kThreads - 1) / kThreads), kThreads, 0, (hipStream_t)stream>>>(x, x_dtype, feat, B,
+                                                                                                 HW, C);
+  return check_launch("sv_avgpool_fwd");
+}
+
+extern "C" int sv_avgpool_bwd(const float* dfeat, float* dx, int32_t B, int32_t HW, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(dfeat && dx && B > 0 && HW > 0 && C % 4 == 0 && C > 0, "sv_avgpool_bwd: bad arguments");
+  avgpool_bwd_kernel<<<grid_for((int64_t)B * HW * C / 4), kThreads, 0, (hipStream_t)stream>>>(dfeat, dx, B, HW, C);
+  return check_launch("sv_avgpool_bwd");
+}

@@ -1,0 +1,647 @@
+// Implicit-GEMM convolution on MFMA for the ResNet-18/50 classification backbone (gfx950).
+//
+// Replaces the cuDNN convolutions timm's ResNet (BasicBlock / Bottleneck, stem conv7x7/s2, 1x1
+// downsample) runs under the reference (spine_vision/training/models/backbone.py:166 ->
+// timm/models/resnet.py) and their autograd data / weight gradients.  Nothing is materialised: the
+// im2col matrix exists only as the per-chunk address arithmetic of the operand loaders.
+//
+//   FPROP  y[m = (b,oy,ox)][co]  = sum_{t,c} x[b, oy*s + kh_t - p, ox*s + kw_t - p, c] * wp[co][t][c]
+//          A = gathered activations (K-major, k = t*Cs + c), B = packed weight (K-major)
+//   DGRAD  dx[b, oy*so+py, ox*so+px][c] = sum_{j,co} dy[b, oy + dy_j, ox + dx_j, co] * wp[co][t_j][c]
+//          one launch per output parity class (py, px) of a stride-2 conv: every tap of the class
+//          hits a real dy pixel, so no MFMA work is spent on the zeros of the transposed conv;
+//          A = gathered gradient (K-major, k = j*Cout + co), B = weight read N-contiguous
+//   WGRAD  dw[co][t][c] = sum_pix dy[pix][co] * x[gather(pix, t)][c]
+//          A = dy (M-contiguous: the pixel-major NHWC gradient), B = gathered activations
+//          (N-contiguous), split-K over pixels into f32 slabs, reduced + permuted to torch layout.
+//
+// Tiles: the v1 register-staged MFMA structure (mfma_v1.h): 128x128 per 256-thread workgroup,
+// 4 waves of 64x64, BK = 32, double-buffered padded LDS images, bf16 (16x16x32) or exact f32
+// (16x16x4) MFMA; channel counts are powers of two so tap/channel split of k is a shift and a mask.
+// Padding / out-of-image taps are zero-filled in registers.  XCD-aware tile order.
+#include "common.h"
+#include "gemm_common.h"
+#include "mfma_v1.h"
+
+#include <type_traits>
+
+namespace sv {
+namespace conv {
+
+enum { FPROP = 0, DGRAD = 1, WGRAD = 2 };
+constexpr int MAX_TAPS = 64;
+
+// unsigned division by a run-time constant d >= 1 (n < 2^31): q = (umulhi(n, mul) + n) >> shift
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{d, 0, 0};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shift = l;
+  f.mul = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)__umulhi(n, f.mul) + n) >> f.shift);
+}
+
+struct Args {
+  const void* A;
+  const void* B;
+  int M, N, K;
+  int64_t lda, ldb;
+  // gather source image [Bn][SH][SW][SC] and the pixel grid the gathered operand is indexed by
+  int SH, SW, SC, lsc;  // lsc = log2(SC)
+  int GH, GW;           // grid of the decoded index (FPROP/DGRAD: GEMM rows; WGRAD: k)
+  FastDiv dGW, dGHW;
+  int si;               // source step per grid step
+  int ntaps;
+  int8_t tdy[MAX_TAPS], tdx[MAX_TAPS];
+  uint8_t twt[MAX_TAPS];  // DGRAD: weight tap of gather tap j
+  int Tw;                 // DGRAD: taps per output channel in wp
+  // epilogue
+  void* C;
+  int c_dtype;
+  int accumulate;
+  int so, py, px, DH, DW;  // DGRAD scatter of GEMM row (b,oy,ox) -> pixel (b, oy*so+py, ox*so+px)
+  int kper;
+};
+
+// ---- operand stages (register-staged, 16-B chunks: 8 bf16 or 4 f32) ----------------------------
+template <bool BF16>
+struct Chunks {
+  static constexpr int EPC = BF16 ? 8 : 4;
+  static constexpr int PER_THREAD = BM * BKT / EPC / kGemmThreads;
+};
+
+template <typename T>
+__device__ __forceinline__ uint4 load16(const T* p) {
+  return *reinterpret_cast<const uint4*>(p);
+}
+
+// A of FPROP / DGRAD: rows = gathered pixels, K-major.
+template <bool BF16, typename T>
+struct StageGatherK {
+  using CH = Chunks<BF16>;
+  uint4 r[CH::PER_THREAD];
+  int boff[CH::PER_THREAD], iy0[CH::PER_THREAD], ix0[CH::PER_THREAD];
+
+  __device__ __forceinline__ void init(const Args& a, int m0) {
+#pragma unroll
+    for (int s = 0; s < CH::PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      const int m = m0 + q / (BKT / CH::EPC);
+      if (m < a.M) {
+        const uint32_t b = fdiv((uint32_t)m, a.dGHW);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(a.GH * a.GW);
+        const uint32_t oy = fdiv(rem, a.dGW);
+        const uint32_t ox = rem - oy * (uint32_t)a.GW;
+        boff[s] = (int)b * a.SH;
+        iy0[s] = (int)oy * a.si;
+        ix0[s] = (int)ox * a.si;
+      } else {
+        boff[s] = -1;
+        iy0[s] = ix0[s] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ void load(const Args& a, int k0) {
+    const T* X = reinterpret_cast<const T*>(a.A);
+#pragma unroll
+    for (int s = 0; s < CH::PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      const int k = k0 + (q % (BKT / CH::EPC)) * CH::EPC;
+      const int j = k >> a.lsc, c = k & (a.SC - 1);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (boff[s] >= 0 && k < a.K && j < a.ntaps) {
+        const int iy = iy0[s] + a.tdy[j], ix = ix0[s] + a.tdx[j];
+        if ((unsigned)iy < (unsigned)a.SH && (unsigned)ix < (unsigned)a.SW)
+          v = load16(X + ((int64_t)(boff[s] + iy) * a.SW + ix) * a.SC + c);
+      }
+      r[s] = v;
+    }
+  }
+};
+
+// B of FPROP: packed weight [N][K] (K-major), or A of WGRAD (dy: [K][M], M-major): plain operands.
+template <bool BF16, typename T, bool KMAJ>
+struct StagePlain {
+  using CH = Chunks<BF16>;
+  uint4 r[CH::PER_THREAD];
+  __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int row0, int k0, int R, int K) {
+#pragma unroll
+    for (int s = 0; s < CH::PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      int row, kk;
+      if (KMAJ) {
+        row = q / (BKT / CH::EPC);
+        kk = (q % (BKT / CH::EPC)) * CH::EPC;
+      } else {
+        kk = q / (BM / CH::EPC);
+        row = (q % (BM / CH::EPC)) * CH::EPC;
+      }
+      const int gr = row0 + row, gk = k0 + kk;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gr < R && gk < K) v = load16(KMAJ ? p + (int64_t)gr * ld + gk : p + (int64_t)gk * ld + gr);
+      r[s] = v;
+    }
+  }
+};
+
+// B of DGRAD: B(k = j*Cout + co, n = c) = wp[(co*Tw + t_j)*N + c]  (N-contiguous)
+template <bool BF16, typename T>
+struct StageWeightN {
+  using CH = Chunks<BF16>;
+  uint4 r[CH::PER_THREAD];
+  __device__ __forceinline__ void load(const Args& a, int n0, int k0) {
+    const T* W = reinterpret_cast<const T*>(a.B);
+#pragma unroll
+    for (int s = 0; s < CH::PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      const int k = k0 + q / (BN / CH::EPC);
+      const int n = n0 + (q % (BN / CH::EPC)) * CH::EPC;
+      const int j = k >> a.lsc, co = k & (a.SC - 1);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k < a.K && n < a.N) v = load16(W + ((int64_t)co * a.Tw + a.twt[j]) * a.N + n);
+      r[s] = v;
+    }
+  }
+};
+
+// B of WGRAD: B(k = pix, n = t*SC + c) = x[b, oy*si + dy_t, ox*si + dx_t, c]  (N-contiguous)
+template <bool BF16, typename T>
+struct StageGatherN {
+  using CH = Chunks<BF16>;
+  uint4 r[CH::PER_THREAD];
+  __device__ __forceinline__ void load(const Args& a, int n0, int k0) {
+    const T* X = reinterpret_cast<const T*>(a.B);
+#pragma unroll
+    for (int s = 0; s < CH::PER_THREAD; ++s) {
+      const int q = threadIdx.x + kGemmThreads * s;
+      const int k = k0 + q / (BN / CH::EPC);
+      const int n = n0 + (q % (BN / CH::EPC)) * CH::EPC;
+      const int t = n >> a.lsc, c = n & (a.SC - 1);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k < a.K && n < a.N && t < a.ntaps) {
+        const uint32_t b = fdiv((uint32_t)k, a.dGHW);
+        const uint32_t rem = (uint32_t)k - b * (uint32_t)(a.GH * a.GW);
+        const uint32_t oy = fdiv(rem, a.dGW);
+        const uint32_t ox = rem - oy * (uint32_t)a.GW;
+        const int iy = (int)oy * a.si + a.tdy[t], ix = (int)ox * a.si + a.tdx[t];
+        if ((unsigned)iy < (unsigned)a.SH && (unsigned)ix < (unsigned)a.SW)
+          v = load16(X + (((int64_t)b * a.SH + iy) * a.SW + ix) * a.SC + c);
+      }
+      r[s] = v;
+    }
+  }
+};
+
+// registers -> LDS image (same images as the v1 GEMM)
+template <bool BF16, bool KMAJ, int PT>
+__device__ __forceinline__ void store_img(const uint4 (&r)[PT], char* __restrict__ img) {
+  constexpr int EPC = BF16 ? 8 : 4, ES = BF16 ? 2 : 4;
+  constexpr int LD = Img<BF16, KMAJ>::LD;
+#pragma unroll
+  for (int s = 0; s < PT; ++s) {
+    const int q = threadIdx.x + kGemmThreads * s;
+    if (KMAJ) {
+      const int row = q / (BKT / EPC), kk = (q % (BKT / EPC)) * EPC;
+      *reinterpret_cast<uint4*>(img + ((size_t)row * LD + kk) * ES) = r[s];
+    } else {
+      const int kk = q / (BM / EPC), row = (q % (BM / EPC)) * EPC;
+      *reinterpret_cast<uint4*>(img + ((size_t)kk * LD + row) * ES) = r[s];
+    }
+  }
+}
+
+// ---- epilogue: 16-row LDS slabs re-read as 8-column units (16-B / 32-B row-contiguous stores) ----
+template <int MODE>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][4], float* __restrict__ slab, int mb, int nb,
+                                         const Args& a, int split) {
+  const int l = threadIdx.x & 63;
+  const int cu = (l & 7) * 8, r0 = l >> 3;
+  const int n = nb + cu;
+  const bool okn = n < a.N, okn4 = n + 4 < a.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = r0 + 8 * h;
+      const int m = mb + i * 16 + row;
+      if (m >= a.M || !okn) continue;
+      const float* sp = slab + row * EPI_LD + cu;
+      float4 va = make_float4(sp[0], sp[1], sp[2], sp[3]);
+      float4 vb = make_float4(sp[4], sp[5], sp[6], sp[7]);
+      size_t ci;
+      if (MODE == WGRAD) {
+        float* C = reinterpret_cast<float*>(a.C) + (size_t)split * a.M * a.N + (size_t)m * a.N + n;
+        *reinterpret_cast<float4*>(C) = va;
+        if (okn4) *reinterpret_cast<float4*>(C + 4) = vb;
+        continue;
+      } else if (MODE == FPROP) {
+        ci = (size_t)m * a.N + n;
+      } else {
+        const uint32_t b = fdiv((uint32_t)m, a.dGHW);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(a.GH * a.GW);
+        const uint32_t oy = fdiv(rem, a.dGW);
+        const uint32_t ox = rem - oy * (uint32_t)a.GW;
+        const size_t pix = ((size_t)b * a.DH + oy * a.so + a.py) * a.DW + ox * a.so + a.px;
+        ci = pix * a.N + n;
+        if (a.accumulate) {
+          float4 xa, xb = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (okn4) ld8_any(a.C, a.c_dtype, ci, xa, xb);
+          else xa = ld4_any(a.C, a.c_dtype, ci);
+          va = add4(va, xa);
+          vb = add4(vb, xb);
+        }
+      }
+      if (okn4) st8_any(a.C, a.c_dtype, ci, va, vb);
+      else st4_any(a.C, a.c_dtype, ci, va);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
+template <bool BF16, int MODE>
+__global__ void __launch_bounds__(kGemmThreads) conv_kernel(const Args a, int tilesM, int tilesN) {
+  using T = typename std::conditional<BF16, uint16_t, float>::type;
+  constexpr bool AK = MODE != WGRAD;   // A K-major (gathered pixels) except WGRAD (dy, M-contiguous)
+  constexpr bool BKM = MODE == FPROP;  // B K-major only for the packed weight of FPROP
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ABYTES = Img<BF16, AK>::BYTES, BBYTES = Img<BF16, BKM>::BYTES;
+  constexpr int STAGE_BYTES = ABYTES + BBYTES;
+  constexpr int PT = Chunks<BF16>::PER_THREAD;
+
+  const int nwg = tilesM * tilesN;
+  const int pid = blockIdx.x;
+  const int xcd = pid & 7, loc = pid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = wg / tilesN, tn = wg % tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * a.kper;
+  int kend = kbeg + a.kper;
+  if (kend > a.K) kend = a.K;
+  const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
+
+  const int wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  StageGatherK<BF16, T> ga;      // FPROP / DGRAD A
+  StagePlain<BF16, T, false> pa;  // WGRAD A
+  StagePlain<BF16, T, true> pb;   // FPROP B
+  StageWeightN<BF16, T> wb;       // DGRAD B
+  StageGatherN<BF16, T> gb;       // WGRAD B
+  if (MODE != WGRAD) ga.init(a, m0);
+
+  auto load = [&](int k0) {
+    if constexpr (MODE == WGRAD) {
+      pa.load(reinterpret_cast<const T*>(a.A), a.lda, m0, k0, a.M, kend);
+      gb.load(a, n0, k0);
+    } else {
+      ga.load(a, k0);
+      if constexpr (MODE == FPROP) pb.load(reinterpret_cast<const T*>(a.B), a.ldb, n0, k0, a.N, a.K);
+      else wb.load(a, n0, k0);
+    }
+  };
+  auto store = [&](char* st) {
+    if constexpr (MODE == WGRAD) {
+      store_img<BF16, AK, PT>(pa.r, st);
+      store_img<BF16, BKM, PT>(gb.r, st + ABYTES);
+    } else {
+      store_img<BF16, AK, PT>(ga.r, st);
+      if constexpr (MODE == FPROP) store_img<BF16, BKM, PT>(pb.r, st + ABYTES);
+      else store_img<BF16, BKM, PT>(wb.r, st + ABYTES);
+    }
+  };
+
+  if (nk > 0) {
+    load(kbeg);
+    store(smem);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+    const bool more = kt + 1 < nk;
+    if (more) load(kbeg + (kt + 1) * BKT);
+    const char* ai = cur;
+    const char* bi = cur + ABYTES;
+    if constexpr (BF16) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_bf16<AK>(ai, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag_bf16<BKM>(bi, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BKT; kk += 4) {
+        float af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = frag_f32<AK>(ai, wm * 64 + i * 16, kk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag_f32<BKM>(bi, wn * 64 + j * 16, kk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store(nxt);
+    __syncthreads();
+  }
+  epilogue<MODE>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64, n0 + wn * 64, a, split);
+}
+
+template <bool BF16, int MODE>
+static int launch(const Args& a, int split, hipStream_t s) {
+  const int tilesM = ceil_div(a.M, BM), tilesN = ceil_div(a.N, BN);
+  constexpr bool AK = MODE != WGRAD, BKM = MODE == FPROP;
+  constexpr size_t main_lds = 2 * (size_t)(Img<BF16, AK>::BYTES + Img<BF16, BKM>::BYTES);
+  constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
+  constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
+  static_assert(lds <= 160 * 1024, "conv kernel LDS");
+  if (lds > 65536) {
+    static bool attr_set = false;  // per template instantiation
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel<BF16, MODE>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+  }
+  dim3 grid(tilesM * tilesN, 1, split);
+  conv_kernel<BF16, MODE><<<grid, kGemmThreads, lds, s>>>(a, tilesM, tilesN);
+  return check_launch(MODE == FPROP ? "sv_conv_fwd" : MODE == DGRAD ? "sv_conv_bwd_data" : "sv_conv_bwd_weight");
+}
+
+template <int MODE>
+static int launch_dt(const Args& a, int dtype, int split, hipStream_t s) {
+  return dtype == SV_BF16 ? launch<true, MODE>(a, split, s) : launch<false, MODE>(a, split, s);
+}
+
+// ---- small helper kernels --------------------------------------------------------------------
+template <typename T>
+__global__ void weight_pack_kernel(const float* __restrict__ w, T* __restrict__ wp, int Cout, int Cin, int T_,
+                                   int Cs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over wp [Cout][T][Cs]
+  const int64_t n = (int64_t)Cout * T_ * Cs;
+  if (i >= n) return;
+  const int c = (int)(i % Cs);
+  const int t = (int)((i / Cs) % T_);
+  const int co = (int)(i / ((int64_t)Cs * T_));
+  const float v = c < Cin ? w[((int64_t)co * Cin + c) * T_ + t] : 0.f;
+  st(wp, (size_t)i, v);
+}
+
+template <typename T>
+__global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restrict__ out, int C, int H, int W, int Cs,
+                                     int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over out [B][H][W][Cs]
+  if (i >= n) return;
+  const int c = (int)(i % Cs);
+  const int64_t pix = i / Cs;
+  const int64_t hw = pix % ((int64_t)H * W), b = pix / ((int64_t)H * W);
+  const float v = c < C ? img[(b * C + c) * H * W + hw] : 0.f;
+  st(out, (size_t)i, v);
+}
+
+// dw[co][c][t] (+)= sum_s slab[s][co][t*Cs + c]   (c < Cin)
+__global__ void wgrad_finish_kernel(const float* __restrict__ slab, int split, int Cout, int Cin, int T_, int Cs,
+                                    float* __restrict__ dw, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over dw [Cout][Cin][T]
+  const int64_t n = (int64_t)Cout * Cin * T_;
+  if (i >= n) return;
+  const int t = (int)(i % T_);
+  const int c = (int)((i / T_) % Cin);
+  const int co = (int)(i / ((int64_t)T_ * Cin));
+  const int64_t MN = (int64_t)Cout * T_ * Cs;
+  const int64_t off = (int64_t)co * T_ * Cs + (int64_t)t * Cs + c;
+  float s = 0.f;
+  for (int p = 0; p < split; ++p) s += slab[p * MN + off];
+  dw[i] = accumulate ? dw[i] + s : s;
+}
+
+// ---- host helpers -----------------------------------------------------------------------------
+static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+static int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
+
+static int check_shape(const sv_conv_shape* s, int dtype, const char* who) {
+  SV_REQUIRE(s, "%s: null shape", who);
+  SV_REQUIRE(dtype == SV_BF16 || dtype == SV_F32, "%s: dtype must be SV_BF16 or SV_F32", who);
+  const int epc = dtype == SV_BF16 ? 8 : 4;
+  SV_REQUIRE(s->B > 0 && s->H > 0 && s->W > 0 && s->KH > 0 && s->KW > 0 && s->stride > 0 && s->pad >= 0,
+             "%s: bad geometry", who);
+  SV_REQUIRE(pow2(s->Cs) && s->Cs >= epc, "%s: stored channels Cs=%d must be a power of two >= %d", who, s->Cs, epc);
+  SV_REQUIRE(s->Cin > 0 && s->Cin <= s->Cs, "%s: Cin=%d must be in [1, Cs=%d]", who, s->Cin, s->Cs);
+  SV_REQUIRE(s->Cout > 0 && s->Cout % 8 == 0, "%s: Cout=%d must be a multiple of 8", who, s->Cout);
+  SV_REQUIRE(s->KH * s->KW <= MAX_TAPS, "%s: at most %d taps", who, MAX_TAPS);
+  SV_REQUIRE(s->stride <= 2, "%s: stride must be 1 or 2", who);
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  SV_REQUIRE(OH > 0 && OW > 0, "%s: empty output", who);
+  SV_REQUIRE((int64_t)s->B * s->H * s->W * s->Cs < (1ll << 31) &&
+                 (int64_t)s->B * OH * OW * (s->Cout > s->Cs ? s->Cout : s->Cs) < (1ll << 31),
+             "%s: tensor too large for 32-bit pixel indexing", who);
+  return SV_OK;
+}
+
+static void set_grid(Args& a, int GH, int GW) {
+  a.GH = GH;
+  a.GW = GW;
+  a.dGW = make_fastdiv((uint32_t)GW);
+  a.dGHW = make_fastdiv((uint32_t)(GH * GW));
+}
+
+static int wgrad_split(const sv_conv_shape* s) {
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  const int64_t K = (int64_t)s->B * OH * OW;
+  const int tiles = ceil_div(s->Cout, BM) * ceil_div((int64_t)s->KH * s->KW * s->Cs, BN);
+  int split = ceil_div(768, tiles);
+  const int64_t maxs = K / 256 > 0 ? K / 256 : 1;  // >= 256 pixels (8 k-steps) per split
+  if (split > maxs) split = (int)maxs;
+  if (split > 256) split = 256;
+  return split < 1 ? 1 : split;
+}
+
+}  // namespace conv
+}  // namespace sv
+
+using namespace sv;
+using namespace sv::conv;
+
+extern "C" int sv_conv_weight_pack(const float* w, void* wp, int32_t dtype, const sv_conv_shape* s,
+                                   sv_stream_t stream) {
+  if (int rc = check_shape(s, dtype, "sv_conv_weight_pack")) return rc;
+  SV_REQUIRE(w && wp, "sv_conv_weight_pack: null pointer");
+  const int T_ = s->KH * s->KW;
+  const int64_t n = (int64_t)s->Cout * T_ * s->Cs;
+  const int blocks = (int)((n + 255) / 256);
+  if (dtype == SV_BF16)
+    weight_pack_kernel<uint16_t><<<blocks, 256, 0, (hipStream_t)stream>>>(w, (uint16_t*)wp, s->Cout, s->Cin, T_, s->Cs);
+  else
+    weight_pack_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>(w, (float*)wp, s->Cout, s->Cin, T_, s->Cs);
+  return check_launch("sv_conv_weight_pack");
+}
+
+extern "C" int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
+                                int32_t Cs, sv_stream_t stream) {
+  SV_REQUIRE(img && out, "sv_image_to_nhwc: null pointer");
+  SV_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0 && Cs >= C, "sv_image_to_nhwc: bad shape");
+  SV_REQUIRE(dtype == SV_BF16 || dtype == SV_F32, "sv_image_to_nhwc: bad dtype");
+  const int64_t n = (int64_t)B * H * W * Cs;
+  const int blocks = (int)((n + 255) / 256);
+  if (dtype == SV_BF16)
+    image_to_nhwc_kernel<uint16_t><<<blocks, 256, 0, (hipStream_t)stream>>>(img, (uint16_t*)out, C, H, W, Cs, n);
+  else
+    image_to_nhwc_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>(img, (float*)out, C, H, W, Cs, n);
+  return check_launch("sv_image_to_nhwc");
+}
+
+extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
+                           const sv_conv_shape* s, sv_stream_t stream) {
+  if (int rc = check_shape(s, dtype, "sv_conv_fwd")) return rc;
+  SV_REQUIRE(x && wp && y, "sv_conv_fwd: null pointer");
+  SV_REQUIRE(y_dtype == SV_BF16 || y_dtype == SV_F32, "sv_conv_fwd: bad y dtype");
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  Args a{};
+  a.A = x;
+  a.B = wp;
+  a.M = s->B * OH * OW;
+  a.N = s->Cout;
+  a.K = s->KH * s->KW * s->Cs;
+  a.ldb = a.K;
+  a.SH = s->H;
+  a.SW = s->W;
+  a.SC = s->Cs;
+  a.lsc = ilog2(s->Cs);
+  set_grid(a, OH, OW);
+  a.si = s->stride;
+  a.ntaps = s->KH * s->KW;
+  for (int kh = 0; kh < s->KH; ++kh)
+    for (int kw = 0; kw < s->KW; ++kw) {
+      a.tdy[kh * s->KW + kw] = (int8_t)(kh - s->pad);
+      a.tdx[kh * s->KW + kw] = (int8_t)(kw - s->pad);
+    }
+  a.C = y;
+  a.c_dtype = y_dtype;
+  a.kper = ceil_div(a.K, BKT) * BKT;
+  return launch_dt<FPROP>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                                int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
+  if (int rc = check_shape(s, dtype, "sv_conv_bwd_data")) return rc;
+  SV_REQUIRE(dy && wp && dx, "sv_conv_bwd_data: null pointer");
+  SV_REQUIRE(dx_dtype == SV_BF16 || dx_dtype == SV_F32, "sv_conv_bwd_data: bad dx dtype");
+  SV_REQUIRE(pow2(s->Cout), "sv_conv_bwd_data: Cout=%d must be a power of two", s->Cout);
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  const int st = s->stride;
+  for (int py = 0; py < st; ++py)
+    for (int px = 0; px < st; ++px) {
+      Args a{};
+      a.A = dy;
+      a.B = wp;
+      const int GH = (s->H - py + st - 1) / st, GW = (s->W - px + st - 1) / st;
+      if (GH <= 0 || GW <= 0) continue;
+      a.M = s->B * GH * GW;
+      a.N = s->Cs;
+      a.SH = OH;
+      a.SW = OW;
+      a.SC = s->Cout;
+      a.lsc = ilog2(s->Cout);
+      set_grid(a, GH, GW);
+      a.si = 1;
+      a.Tw = s->KH * s->KW;
+      int nt = 0;
+      for (int kh = 0; kh < s->KH; ++kh) {
+        const int ry = py + s->pad - kh;
+        if (((ry % st) + st) % st) continue;
+        for (int kw = 0; kw < s->KW; ++kw) {
+          const int rx = px + s->pad - kw;
+          if (((rx % st) + st) % st) continue;
+          a.tdy[nt] = (int8_t)(ry >= 0 ? ry / st : -((-ry) / st));
+          a.tdx[nt] = (int8_t)(rx >= 0 ? rx / st : -((-rx) / st));
+          a.twt[nt] = (uint8_t)(kh * s->KW + kw);
+          ++nt;
+        }
+      }
+      if (nt == 0 && accumulate) continue;  // this parity class receives no gradient
+      a.ntaps = nt;
+      a.K = nt * s->Cout;
+      a.C = dx;
+      a.c_dtype = dx_dtype;
+      a.accumulate = accumulate;
+      a.so = st;
+      a.py = py;
+      a.px = px;
+      a.DH = s->H;
+      a.DW = s->W;
+      a.kper = a.K > 0 ? ceil_div(a.K, BKT) * BKT : 0;
+      if (int rc = launch_dt<DGRAD>(a, dtype, 1, (hipStream_t)stream)) return rc;
+    }
+  return SV_OK;
+}
+
+extern "C" int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s) {
+  if (!s) return -1;
+  return (int64_t)wgrad_split(s) * s->Cout * s->KH * s->KW * s->Cs;
+}
+
+extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate,
+                                  int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
+  if (int rc = check_shape(s, dtype, "sv_conv_bwd_weight")) return rc;
+  SV_REQUIRE(dy && x && work && dw, "sv_conv_bwd_weight: null pointer");
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  const int split = wgrad_split(s);
+  Args a{};
+  a.A = dy;
+  a.B = x;
+  a.M = s->Cout;
+  a.N = s->KH * s->KW * s->Cs;
+  a.K = s->B * OH * OW;
+  a.lda = s->Cout;
+  a.SH = s->H;
+  a.SW = s->W;
+  a.SC = s->Cs;
+  a.lsc = ilog2(s->Cs);
+  set_grid(a, OH, OW);
+  a.si = s->stride;
+  a.ntaps = s->KH * s->KW;
+  for (int kh = 0; kh < s->KH; ++kh)
+    for (int kw = 0; kw < s->KW; ++kw) {
+      a.tdy[kh * s->KW + kw] = (int8_t)(kh - s->pad);
+      a.tdx[kh * s->KW + kw] = (int8_t)(kw - s->pad);
+    }
+  a.C = work;
+  a.c_dtype = SV_F32;
+  a.kper = ceil_div(ceil_div(a.K, split), BKT) * BKT;
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = launch_dt<WGRAD>(a, dtype, split, st)) return rc;
+  const int T_ = s->KH * s->KW;
+  const int64_t n = (int64_t)s->Cout * s->Cin * T_;
+  wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, split, s->Cout, s->Cin, T_, s->Cs, dw, accumulate);
+  return check_launch("sv_conv_bwd_weight(finish)");
+}

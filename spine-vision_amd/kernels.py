@@ -370,3 +370,184 @@ def adamw_flat(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, weight_decay, step,
     _check(g.numel() == n and m.numel() == n and v.numel() == n, "adamw_flat: size mismatch")
     call("sv_adamw_flat", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(lr), float(beta1), float(beta2),
          float(eps), float(weight_decay), int(step), ptr(grad_scale))
+
+
+# ----------------------------------------------------------------------------------------------
+# ResNet-18/50: implicit-GEMM convolution, BatchNorm (train-mode batch statistics), pooling
+EPS_BN = 1e-5
+
+
+def _is_pow2(v: int) -> bool:
+    return v > 0 and (v & (v - 1)) == 0
+
+
+def conv_out_hw(H: int, W: int, k: int, stride: int, pad: int) -> tuple[int, int]:
+    return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+
+
+def conv_shape(B, H, W, Cs, Cout, k, stride, pad, Cin=None) -> nv.ConvShape:
+    s = nv.ConvShape()
+    s.B, s.H, s.W, s.Cs, s.Cout = B, H, W, Cs, Cout
+    s.KH = s.KW = k
+    s.stride, s.pad = stride, pad
+    s.Cin = Cs if Cin is None else Cin
+    _check(_is_pow2(Cs) and Cs >= 4 and Cout % 8 == 0 and 0 < s.Cin <= Cs and stride in (1, 2),
+           f"conv: unsupported shape Cs={Cs} Cout={Cout} Cin={s.Cin} stride={stride}")
+    return s
+
+
+def conv_weight_pack(w: torch.Tensor, Cs: int, dtype: torch.dtype) -> torch.Tensor:
+    """torch weight [Cout][Cin][k][k] f32 -> packed [Cout][k*k][Cs] (`dtype`), channels >= Cin zero."""
+    Cout, Cin, KH, KW = w.shape
+    _check(w.dtype == torch.float32 and w.is_contiguous() and KH == KW, "conv_weight_pack: need contiguous f32 [Co,Ci,k,k]")
+    s = conv_shape(1, KH, KW, Cs, Cout, KH, 1, 0, Cin)
+    wp = torch.empty(Cout, KH * KW, Cs, device=w.device, dtype=dtype)
+    call("sv_conv_weight_pack", ptr(w), ptr(wp), dt(wp), ctypes.byref(s))
+    return wp
+
+
+def _conv_check_x(x: torch.Tensor, s: nv.ConvShape, dtype: torch.dtype, who: str) -> None:
+    _check(x.is_contiguous() and tuple(x.shape) == (s.B, s.H, s.W, s.Cs) and x.dtype == dtype,
+           f"{who}: x must be contiguous {dtype} [B,H,W,Cs]={(s.B, s.H, s.W, s.Cs)}, got {tuple(x.shape)} {x.dtype}")
+
+
+def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype) -> torch.Tensor:
+    _conv_check_x(x, s, wp.dtype, "conv_fwd")
+    _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
+    OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
+    y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
+    call("sv_conv_fwd", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s))
+    return y
+
+
+def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: torch.Tensor | None = None,
+                  accumulate: bool = False, dx_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
+    _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout) and dy.dtype == wp.dtype,
+           "conv_bwd_data: dy must be contiguous [B,OH,OW,Cout] in the compute dtype")
+    _check(_is_pow2(s.Cout), "conv_bwd_data: Cout must be a power of two")
+    if dx is None:
+        _check(not accumulate, "conv_bwd_data: accumulate needs dx")
+        dx = torch.empty(s.B, s.H, s.W, s.Cs, device=dy.device, dtype=dx_dtype)
+    _check(dx.is_contiguous() and tuple(dx.shape) == (s.B, s.H, s.W, s.Cs), "conv_bwd_data: dx shape")
+    call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s))
+    return dx
+
+
+def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: torch.Tensor,
+                    accumulate: bool = True) -> torch.Tensor:
+    OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
+    _conv_check_x(x, s, dy.dtype, "conv_bwd_weight")
+    _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout), "conv_bwd_weight: dy shape")
+    _check(dw.dtype == torch.float32 and dw.is_contiguous() and tuple(dw.shape) == (s.Cout, s.Cin, s.KH, s.KW),
+           "conv_bwd_weight: dw must be f32 [Cout,Cin,k,k]")
+    nwork = value("sv_conv_bwd_weight_work_floats", ctypes.byref(s))
+    work = torch.empty(nwork, device=dy.device, dtype=torch.float32)
+    call("sv_conv_bwd_weight", ptr(dy), ptr(x), ptr(work), ptr(dw), int(accumulate), dt(dy), ctypes.byref(s))
+    return dw
+
+
+def image_to_nhwc(img: torch.Tensor, Cs: int, dtype: torch.dtype) -> torch.Tensor:
+    B, C, H, W = img.shape
+    _check(img.dtype == torch.float32 and img.is_contiguous() and Cs >= C, "image_to_nhwc: need contiguous f32 NCHW")
+    out = torch.empty(B, H, W, Cs, device=img.device, dtype=dtype)
+    call("sv_image_to_nhwc", ptr(img), ptr(out), dt(out), B, C, H, W, Cs)
+    return out
+
+
+def _bn_c_ok(C: int) -> bool:
+    return C >= 4 and C % 4 == 0 and (C // 4 <= 256 or (C // 4) % 256 == 0)
+
+
+def bn_stats(y2d: torch.Tensor, *, eps: float = EPS_BN, momentum: float = 0.1, running_mean=None, running_var=None):
+    """Train-mode batch statistics of y [rows, C] -> (mean, rstd) f32; running stats updated in place."""
+    rows, C = y2d.shape
+    _check(_bn_c_ok(C) and y2d.is_contiguous() and rows > 0, f"bn_stats: unsupported C={C}")
+    P = value("sv_bn_nparts", rows, C)
+    part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_stats", ptr(y2d), dt(y2d), rows, C, ptr(part))
+    mean = torch.empty(C, device=y2d.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_bn_stats_finish", ptr(y2d), dt(y2d), ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var))
+    return mean, rstd
+
+
+def bn_eval_params(running_mean: torch.Tensor, running_var: torch.Tensor, eps: float = EPS_BN):
+    C = running_mean.numel()
+    mean = torch.empty(C, device=running_mean.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_bn_eval_params", ptr(running_mean), ptr(running_var), float(eps), ptr(mean), ptr(rstd), C)
+    return mean, rstd
+
+
+def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, out_dtype=torch.float32,
+           out=None) -> torch.Tensor:
+    """act(gamma (y-mean) rstd + beta + r), r = res or BN(res) with res_bn = (mean, rstd, gamma, beta)."""
+    rows, C = y2d.shape
+    _check(C % 4 == 0 and y2d.is_contiguous(), "bn_act: C must be a multiple of 4")
+    if res is not None:
+        _check(res.is_contiguous() and res.numel() == rows * C, "bn_act: residual shape")
+    rm, rr, rg, rb = res_bn if res_bn is not None else (None, None, None, None)
+    if out is None:
+        out = torch.empty(rows, C, device=y2d.device, dtype=out_dtype)
+    call("sv_bn_act_fwd", ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), ptr(res),
+         nv.dt_none(res), ptr(rm), ptr(rr), ptr(rg), ptr(rb), int(relu), ptr(out), dt(out), rows, C)
+    return out
+
+
+def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, dgamma=None, dbeta=None, dx_dtype=torch.float32,
+           gmask=None) -> torch.Tensor:
+    """BatchNorm (train) backward with an optional ReLU mask (act > 0) on dout; dgamma/dbeta accumulate."""
+    rows, C = y2d.shape
+    _check(_bn_c_ok(C) and dout2d.numel() == rows * C and dout2d.is_contiguous(), "bn_bwd: bad shapes")
+    if act is not None:
+        _check(act.numel() == rows * C and act.is_contiguous(), "bn_bwd: act shape")
+    if gmask is not None:
+        _check(gmask.dtype == torch.float32 and gmask.numel() == rows * C, "bn_bwd: gmask must be f32 [rows,C]")
+    P = value("sv_bn_nparts", rows, C)
+    part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
+         ptr(rstd), rows, C, ptr(part))
+    sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
+    dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+    call("sv_bn_bwd_apply", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
+         ptr(rstd), ptr(gamma), ptr(sums), ptr(dx), dt(dx), ptr(gmask), rows, C)
+    return dx
+
+
+def maxpool_fwd(x4d: torch.Tensor):
+    B, H, W, C = x4d.shape
+    _check(x4d.is_contiguous() and C % 4 == 0, "maxpool_fwd: need contiguous NHWC, C % 4 == 0")
+    OH, OW = conv_out_hw(H, W, 3, 2, 1)
+    y = torch.empty(B, OH, OW, C, device=x4d.device, dtype=x4d.dtype)
+    idx = torch.empty(B, OH, OW, C, device=x4d.device, dtype=torch.uint8)
+    call("sv_maxpool3s2_fwd", ptr(x4d), dt(x4d), ptr(y), ptr(idx), B, H, W, C)
+    return y, idx
+
+
+def maxpool_bwd(dout4d: torch.Tensor, idx: torch.Tensor, H: int, W: int, dx_dtype=torch.float32) -> torch.Tensor:
+    B, OH, OW, C = dout4d.shape
+    _check(dout4d.is_contiguous() and idx.shape == dout4d.shape and (OH, OW) == conv_out_hw(H, W, 3, 2, 1),
+           "maxpool_bwd: shape mismatch")
+    dx = torch.empty(B, H, W, C, device=dout4d.device, dtype=dx_dtype)
+    call("sv_maxpool3s2_bwd", ptr(dout4d), dt(dout4d), ptr(idx), ptr(dx), dt(dx), B, H, W, C)
+    return dx
+
+
+def avgpool_fwd(x4d: torch.Tensor) -> torch.Tensor:
+    B, H, W, C = x4d.shape
+    _check(x4d.is_contiguous() and C % 4 == 0, "avgpool_fwd: need contiguous NHWC, C % 4 == 0")
+    feat = torch.empty(B, C, device=x4d.device, dtype=torch.float32)
+    call("sv_avgpool_fwd", ptr(x4d), dt(x4d), ptr(feat), B, H * W, C)
+    return feat
+
+
+def avgpool_bwd(dfeat: torch.Tensor, shape: tuple) -> torch.Tensor:
+    B, H, W, C = shape
+    dfeat = dfeat.float().contiguous()
+    _check(tuple(dfeat.shape) == (B, C), "avgpool_bwd: dfeat shape")
+    dx = torch.empty(B, H, W, C, device=dfeat.device, dtype=torch.float32)
+    call("sv_avgpool_bwd", ptr(dfeat), ptr(dx), B, H * W, C)
+    return dx

@@ -45,6 +45,13 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class ConvShape(ctypes.Structure):
+    _fields_ = [("B", _i32), ("H", _i32), ("W", _i32), ("Cs", _i32), ("Cout", _i32), ("KH", _i32), ("KW", _i32),
+                ("stride", _i32), ("pad", _i32), ("Cin", _i32)]
+
+
+_CS = ctypes.POINTER(ConvShape)
+
 # name -> argtypes (restype is int for all entry points unless listed in _RESTYPES)
 _SIGS = {
     "sv_version": [],
@@ -76,10 +83,31 @@ _SIGS = {
     "sv_adamw_flat": [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _p, _p],
     "sv_scale_rows_bf16": [_p, _p, _p, _i32, _i32, _p],
     "sv_cast_f32_bf16": [_p, _p, _i64, _p],
+    # ResNet
+    "sv_conv_weight_pack": [_p, _p, _i32, _CS, _p],
+    "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _p],
+    "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],
+    "sv_conv_bwd_weight_work_floats": [_CS],
+    "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],
+    "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_bn_nparts": [_i64, _i32],
+    "sv_bn_stats": [_p, _i32, _i64, _i32, _p, _p],
+    "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p],
+    "sv_bn_eval_params": [_p, _p, _f32, _p, _p, _i32, _p],
+    "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
+    "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
+    "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
+    "sv_bn_bwd_apply": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _i64, _i32, _p],
+    "sv_relu_mask": [_p, _i32, _p, _i32, _p, _i64, _p],
+    "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_maxpool3s2_bwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_avgpool_fwd": [_p, _i32, _p, _i32, _i32, _i32, _p],
+    "sv_avgpool_bwd": [_p, _p, _i32, _i32, _i32, _p],
 }
-_RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p}
+_RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
+             "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith("_nparts")} | {"sv_version"}
+_VALUE_FNS = {n for n in _SIGS if n.endswith("_nparts")} | {"sv_version", "sv_conv_bwd_weight_work_floats"}
 
 _lib = None
 _lock = threading.Lock()
@@ -145,6 +173,10 @@ def ptr(t: torch.Tensor | None) -> int | None:
     if not t.is_cuda:
         raise RuntimeError("spine_vision_amd kernels need device tensors (got a CPU tensor)")
     return t.data_ptr()
+
+
+def dt_none(t: torch.Tensor | None) -> int:
+    return SV_F32 if t is None else dt(t)
 
 
 def dt(t: torch.Tensor) -> int:

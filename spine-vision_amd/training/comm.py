@@ -113,6 +113,38 @@ class GradBucketer:
         self.reset()
 
 
+class BufferSync:
+    """DDP's per-forward ``broadcast_buffers=True`` (the reference's accelerate default): rank 0's
+    floating buffers -- the ResNet BatchNorm running statistics -- overwrite every rank's before
+    each step.  The buffers are rebound as views of ONE flat f32 tensor so the sync is a single
+    broadcast (ResNet-50: 53k floats) instead of ~160 small ones.  Integer buffers
+    (num_batches_tracked) advance identically on every rank and are not sent."""
+
+    def __init__(self, model: torch.nn.Module, src: int = 0, group=None) -> None:
+        self.src, self.group = src, group
+        slots = []
+        for mod in model.modules():
+            for name, b in mod._buffers.items():
+                if b is not None and b.is_floating_point():
+                    slots.append((mod, name, b))
+        self.flat = None
+        if not slots:
+            return
+        total = sum(b.numel() for _, _, b in slots)
+        self.flat = torch.empty(total, device=slots[0][2].device, dtype=torch.float32)
+        off = 0
+        with torch.no_grad():
+            for mod, name, b in slots:
+                v = self.flat[off : off + b.numel()].view_as(b)
+                v.copy_(b)
+                mod._buffers[name] = v
+                off += b.numel()
+
+    def sync(self) -> None:
+        if self.flat is not None:
+            dist.broadcast(self.flat, self.src, group=self.group)
+
+
 def broadcast_parameters(arena: FlatArena, model: torch.nn.Module, src: int = 0, group=None) -> None:
     """DDP's constructor-time broadcast: rank 0's parameters and buffers to every rank."""
     dist.broadcast(arena.param_flat, src, group=group)

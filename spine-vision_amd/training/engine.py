@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import kernels as K
-from .comm import GradBucketer, broadcast_parameters
+from .comm import BufferSync, GradBucketer, broadcast_parameters
 from .flat import FlatArena
 from .optim import FlatAdamW
 
@@ -36,15 +36,19 @@ class StepEngine:
             distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.distributed = distributed
         self.bucketer = None
+        self.buffer_sync = None
         if distributed:
             broadcast_parameters(self.arena, model)
             self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb)
             self.bucketer.attach(model)
+            self.buffer_sync = BufferSync(model)
         self.last_grad_norm: torch.Tensor | None = None
 
     def step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
         """Run one optimisation step; returns the (device) loss tensor."""
         self.optimizer.zero_grad()
+        if self.buffer_sync is not None:
+            self.buffer_sync.sync()
         loss = loss_fn(self.model)
         loss.backward()
         if self.bucketer is not None:

@@ -35,7 +35,7 @@ from pydantic import BaseModel, ConfigDict, model_validator
 from torch.utils.data import DataLoader, Dataset, Sampler
 
 from .. import optim as flat_optim
-from ..comm import GradBucketer, broadcast_parameters
+from ..comm import BufferSync, GradBucketer, broadcast_parameters
 from ..flat import FlatArena
 
 logger = logging.getLogger("spine_vision_amd")
@@ -190,7 +190,9 @@ class BaseTrainer:
         self.optimizer = self._create_optimizer()
         self.scheduler = self._create_scheduler()
         self.bucketer = None
+        self.buffer_sync = None
         if self.world > 1:
+            self.buffer_sync = BufferSync(self.model)
             if isinstance(self.optimizer, flat_optim.FlatAdamW):
                 broadcast_parameters(self.optimizer.arena, self.model)
                 self.bucketer = GradBucketer(self.optimizer.arena, bucket_mb=config.bucket_mb)
@@ -286,6 +288,8 @@ class BaseTrainer:
         """zero_grad -> forward/loss -> backward (+bucketed all-reduce) -> clip -> optimizer step."""
         opt = self.optimizer
         opt.zero_grad()
+        if self.buffer_sync is not None:
+            self.buffer_sync.sync()
         loss = loss_fn()
         loss.backward()
         if isinstance(opt, flat_optim.FlatAdamW):

@@ -74,3 +74,49 @@ def test_bucketed_allreduce_gloo_world2():
         assert ok_bcast
         assert nb >= 2
         assert err < 1e-5, (rank, err)
+
+
+def _bn_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    from spine_vision_amd.training.comm import BufferSync
+
+    torch.manual_seed(rank)
+    model = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8), torch.nn.ReLU(),
+                                torch.nn.Conv2d(8, 8, 1), torch.nn.BatchNorm2d(8))
+    model.train()
+    sync = BufferSync(model)
+    ok = True
+    for step in range(3):
+        sync.sync()  # DDP broadcast_buffers: rank 0's running stats before every forward
+        got = torch.cat([model[1].running_mean, model[1].running_var, model[4].running_mean, model[4].running_var])
+        all_ = [torch.empty_like(got) for _ in range(world)]
+        dist.all_gather(all_, got)
+        ok &= all(torch.equal(all_[0], a) for a in all_)
+        # each rank sees different data -> running stats diverge until the next sync
+        model(torch.randn(4, 3, 8, 8, generator=torch.Generator().manual_seed(10 * step + rank)))
+    ok &= model[1].running_mean.data_ptr() == sync.flat.data_ptr()  # still bound to the flat buffer
+    q.put((rank, ok, int(model[1].num_batches_tracked)))
+    dist.destroy_process_group()
+
+
+def test_bn_buffer_broadcast_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, nbt in res:
+        assert ok, rank
+        assert nbt == 3
