@@ -238,52 +238,61 @@ class ResNetHip(nn.Module):
             self.grad_ready_hook(params)
 
     @torch.no_grad()
+    def _block_backward(self, blk, saved_block, d: torch.Tensor) -> torch.Tensor:
+        """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
+        block's parameter gradients and returns dL/d(block input) (f32)."""
+        act = self.act_dtype
+        g = self._grad
+        x_in, saved, ds_saved, out = saved_block
+        convs = blk.convs()
+        Bq, Hq, Wq, Cq = out.shape
+        rows = Bq * Hq * Wq
+        # last BN of the main path, with the block-output ReLU mask; gm = the masked gradient
+        gm = torch.empty(rows, Cq, device=d.device, dtype=torch.float32)
+        conv, bn, _, _, _, _ = convs[-1]
+        cur_in, y, mean, rstd, _, wp, s = saved[-1]
+        dy = K.bn_bwd(d.reshape(rows, Cq), y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
+                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm)
+        params = [bn.weight, bn.bias]
+        for ci in range(len(convs) - 1, -1, -1):
+            conv, bn, _, _, _, _ = convs[ci]
+            cur_in, y, mean, rstd, a, wp, s = saved[ci]
+            dy4 = dy.view(y.shape)
+            K.conv_bwd_weight(dy4, cur_in, s, dw=g(conv.weight), accumulate=True)
+            params.append(conv.weight)
+            if ci == 0:
+                break
+            da = K.conv_bwd_data(dy4, wp, s, dx_dtype=act)
+            pconv, pbn, _, _, _, _ = convs[ci - 1]
+            _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
+            Cp = py.shape[-1]
+            dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, act=pa.view(-1, Cp),
+                          dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act)
+            params += [pbn.weight, pbn.bias]
+        # dy is now the gradient at conv1's output; conv1's input is x_in
+        s1, wp1 = saved[0][6], saved[0][5]
+        if ds_saved is not None:
+            yd, md, rd, wpd, sd = ds_saved
+            dconv, dbn = blk.downsample[0], blk.downsample[1]
+            dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
+                           dx_dtype=act)
+            dyd4 = dyd.view(yd.shape)
+            K.conv_bwd_weight(dyd4, x_in, sd, dw=g(dconv.weight), accumulate=True)
+            dx = K.conv_bwd_data(dyd4, wpd, sd, dx_dtype=torch.float32)
+            params += [dconv.weight, dbn.weight, dbn.bias]
+        else:
+            dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
+        K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
+        self._ready(params)
+        return dx
+
+    @torch.no_grad()
     def _backward_impl(self, tape: _Tape, dfeat: torch.Tensor) -> None:
         act = self.act_dtype
         g = self._grad
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
-        for blk, (x_in, saved, ds_saved, out) in zip(reversed(list(self.blocks())), reversed(tape.blocks)):
-            convs = blk.convs()
-            Bq, Hq, Wq, Cq = out.shape
-            rows = Bq * Hq * Wq
-            # last BN of the main path, with the block-output ReLU mask; gm = the masked gradient
-            gm = torch.empty(rows, Cq, device=d.device, dtype=torch.float32)
-            conv, bn, _, _, _, _ = convs[-1]
-            cur_in, y, mean, rstd, _, wp, s = saved[-1]
-            dy = K.bn_bwd(d.view(rows, Cq), y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
-                          dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm)
-            params = [bn.weight, bn.bias]
-            for ci in range(len(convs) - 1, -1, -1):
-                conv, bn, _, _, _, _ = convs[ci]
-                cur_in, y, mean, rstd, a, wp, s = saved[ci]
-                dy4 = dy.view(y.shape)
-                K.conv_bwd_weight(dy4, cur_in, s, dw=g(conv.weight), accumulate=True)
-                params.append(conv.weight)
-                if ci == 0:
-                    break
-                da = K.conv_bwd_data(dy4, wp, s, dx_dtype=act)
-                pconv, pbn, _, _, _, _ = convs[ci - 1]
-                _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
-                Cp = py.shape[-1]
-                dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, act=pa.view(-1, Cp),
-                              dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act)
-                params += [pbn.weight, pbn.bias]
-            # dy is now the gradient at conv1's output; conv1's input is x_in
-            s1, wp1 = saved[0][6], saved[0][5]
-            if ds_saved is not None:
-                yd, md, rd, wpd, sd = ds_saved
-                dconv, dbn = blk.downsample[0], blk.downsample[1]
-                dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
-                               dx_dtype=act)
-                dyd4 = dyd.view(yd.shape)
-                K.conv_bwd_weight(dyd4, x_in, sd, dw=g(dconv.weight), accumulate=True)
-                dx = K.conv_bwd_data(dyd4, wpd, sd, dx_dtype=torch.float32)
-                params += [dconv.weight, dbn.weight, dbn.bias]
-            else:
-                dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
-            K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
-            d = dx
-            self._ready(params)
+        for blk, saved_block in zip(reversed(list(self.blocks())), reversed(tape.blocks)):
+            d = self._block_backward(blk, saved_block, d)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
