@@ -39,15 +39,45 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="localization", choices=["localization", "classification"],
+                    help="localization = the BASELINE metric (ConvNeXt-base 512); classification = ResNet-50 "
+                         "256x256 3-head ClassificationTrainer step (configs[3], secondary line)")
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
-    ap.add_argument("--image-size", type=int, default=512)
-    ap.add_argument("--backbone", default="convnext_base")
+    ap.add_argument("--image-size", type=int, default=None, help="default 512 (localization) / 256 (classification)")
+    ap.add_argument("--backbone", default=None, help="default convnext_base / resnet50")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--probe", default="fwd", choices=sorted(PROBE_KEYS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU sample budget")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    return ap.parse_args()
+    args = ap.parse_args()
+    cls = args.workload == "classification"
+    if args.image_size is None:
+        args.image_size = 256 if cls else 512
+    if args.backbone is None:
+        args.backbone = "resnet50" if cls else "convnext_base"
+    return args
+
+
+# fwd+bwd GFLOP per image (SURVEY.md section 8d, counted with torch.utils.flop_counter)
+STEP_GFLOP = {("convnext_base", 512): 481.3, ("convnext_large", 512): 1077.0, ("resnet50", 256): 31.7,
+              ("resnet18", 256): 13.9}
+CLS_TASKS = ["pfirrmann", "modic", "herniation"]
+
+
+def synthetic_cls_batch(B, H, W, device, seed):
+    """[T2, T1, T2] uint8 planes -> /255 -> ImageNet normalise (reference datasets/classification.py
+    crops), labels pfirrmann U{0..4}, modic U{0..3}, herniation Bernoulli(0.3)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    u8 = torch.randint(0, 256, (B, 2, H, W), generator=g, device=device, dtype=torch.uint8)
+    x = (u8.float() / 255.0)[:, [0, 1, 0]]
+    mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1)
+    img = ((x - mean) / std).contiguous()
+    targets = {"pfirrmann": torch.randint(0, 5, (B,), generator=g, device=device),
+               "modic": torch.randint(0, 4, (B,), generator=g, device=device),
+               "herniation": (torch.rand(B, generator=g, device=device) < 0.3).float()}
+    return img, targets
 
 
 def synthetic_batch(B, H, W, device, seed):
@@ -73,14 +103,27 @@ def cpu_baseline(args):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     B = 4
-    model = oh.CoordinateRegressor(oc.create(args.backbone), 1024 if args.backbone == "convnext_base" else 1536)
+    if args.workload == "classification":
+        from oracle import resnet as orn
+
+        model = oh.Classifier(orn.create(args.backbone), 2048 if args.backbone == "resnet50" else 512, dropout=0.3)
+        img, targets = synthetic_cls_batch(B, args.image_size, args.image_size, "cpu", 7)
+        opt = ostep.make_optimizer(model)
+
+        def one():
+            ostep.train_step_classification(model, opt, img, targets)
+    else:
+        model = oh.CoordinateRegressor(oc.create(args.backbone), 1024 if args.backbone == "convnext_base" else 1536)
+        img, coords, mask = synthetic_batch(B, args.image_size, args.image_size, "cpu", 7)
+        opt = ostep.make_optimizer(model)
+
+        def one():
+            ostep.train_step_localization(model, opt, img, coords, mask)
     model.train()
-    opt = ostep.make_optimizer(model)
-    img, coords, mask = synthetic_batch(B, args.image_size, args.image_size, "cpu", 7)
-    ostep.train_step_localization(model, opt, img, coords, mask)  # warmup
+    one()  # warmup
     n, t0 = 0, time.perf_counter()
     while True:
-        ostep.train_step_localization(model, opt, img, coords, mask)
+        one()
         n += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or n >= 8:
@@ -111,16 +154,32 @@ def main():
 
     pkg = __graft_entry__.load_package()
     from spine_vision_amd import kernels as K
-    from spine_vision_amd.training import CoordinateRegressor, StepEngine
+    from spine_vision_amd.training import Classifier, CoordinateRegressor, StepEngine
 
     torch.manual_seed(42)
-    model = CoordinateRegressor(args.backbone, pretrained=False, precision=args.precision).to(device)
-    model.train()
+    cls = args.workload == "classification"
+    if cls:
+        from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+        tasks = _create_tasks_for_training(target_labels=CLS_TASKS, label_smoothing=0.1)
+        model = Classifier(args.backbone, tasks=tasks, pretrained=False, dropout=0.3, precision=args.precision)
+    else:
+        model = CoordinateRegressor(args.backbone, pretrained=False, precision=args.precision)
+    model = model.to(device).train()
     engine = StepEngine(model, device, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
-    img, coords, mask = synthetic_batch(args.batch, args.image_size, args.image_size, device, 1234 + rank)
+    if cls:
+        img, targets = synthetic_cls_batch(args.batch, args.image_size, args.image_size, device, 1234 + rank)
+
+        def run_step():
+            return engine.step_classification(img, targets)
+    else:
+        img, coords, mask = synthetic_batch(args.batch, args.image_size, args.image_size, device, 1234 + rank)
+
+        def run_step():
+            return engine.step_localization(img, coords, mask)
 
     for _ in range(args.warmup):
-        engine.step_localization(img, coords, mask)
+        run_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -131,7 +190,7 @@ def main():
     K.PROBE = probe
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = engine.step_localization(img, coords, mask)
+        loss = run_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,28 +218,24 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
-    step_tflops = 481.3 * args.batch / (ms * 1e-3) / 1e3 if args.backbone == "convnext_base" else None
-    result = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "images/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": args.precision,
-        "data": "synthetic uint8 512x512 grayscale->RGB, ImageNet-normalised, resident in HBM; random-init weights",
-        "config": {
-            "workload": f"CoordinateRegressor({args.backbone}) localization train step fwd+bwd+allreduce+clip+AdamW",
-            "image_size": args.image_size,
-            "batch_per_gpu": args.batch,
-            "global_batch": args.batch * world,
-            "parallelism": f"dp{world}",
-        },
-        "roofline": {
+    gflop = STEP_GFLOP.get((args.backbone, args.image_size))
+    step_tflops = gflop * args.batch / (ms * 1e-3) / 1e3 if gflop else None
+    if cls:
+        metric = f"images/sec training, {args.backbone} {args.image_size}x{args.image_size} 3-head cls, bs{args.batch}"
+        workload = f"Classifier({args.backbone}, pfirrmann+modic+herniation) train step fwd+bwd+allreduce+clip+AdamW"
+        data = (f"synthetic uint8 {args.image_size}x{args.image_size} [T2,T1,T2] crops, ImageNet-normalised, "
+                "resident in HBM; random-init weights")
+    else:
+        metric = METRIC
+        workload = f"CoordinateRegressor({args.backbone}) localization train step fwd+bwd+allreduce+clip+AdamW"
+        data = "synthetic uint8 512x512 grayscale->RGB, ImageNet-normalised, resident in HBM; random-init weights"
+    if cls:
+        # the conv kernels are not GEMM-probed: report the whole-step model FLOP rate against the peak
+        roof = {"bound": "mfma", "kernel": "whole training step (implicit-GEMM conv + BN), model FLOPs",
+                "achieved": round(step_tflops, 2) if step_tflops else None, "peak": peak, "unit": "TFLOP/s",
+                "frac": round(step_tflops / peak, 4) if step_tflops else None, "traffic": None}
+    else:
+        roof = {
             "bound": "mfma",
             "kernel": f"gemm_kernel {args.probe} ({'bf16' if bf else 'f32'} MFMA)",
             "achieved": round(achieved, 2),
@@ -193,7 +248,28 @@ def main():
             "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
             "algorithmic_bytes_per_launch": int(probe.bytes / max(probe.launches, 1)),
             "step_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
+        }
+    result = {
+        "metric": metric,
+        "value": round(value, 3),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": data,
+        "config": {
+            "workload": workload,
+            "image_size": args.image_size,
+            "batch_per_gpu": args.batch,
+            "global_batch": args.batch * world,
+            "parallelism": f"dp{world}",
         },
+        "roofline": roof,
         "loss": round(final_loss, 6),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
