@@ -1,20 +1,24 @@
 // Depthwise 7x7 convolution (pad 3, stride 1) on NHWC activations -- ConvNeXtBlock.conv_dw
 // (timm convnext.py; HF equivalent transformers/models/convnext/modeling_convnext.py:130,144).
 //
-// Layout/tiling (gfx950): a workgroup owns an 8x8 output tile of one image for one 64-channel
-// chunk.  The (8+6)x(8+6)x64 f32 input halo tile is staged in LDS as [pixel][64 ch] (16 lanes x
-// 16 B per pixel on the global side -> 256 contiguous bytes per pixel, fully coalesced; on the
-// LDS side lane == channel, so the per-tap ds_read_b32 of 64 consecutive floats is bank-conflict
-// free).  Each wave computes two output rows; a lane keeps its channel's 49 taps in registers and
-// slides a 14-wide input row window along W (7 FMAs per input value read from LDS).
+// Layout/tiling (gfx950): one WAVE owns a 16-row x 8-column output strip of one image for one
+// 64-channel group (lane == channel, so every global access of a wave is 64 consecutive channels:
+// 256 B f32 / 128 B bf16, fully coalesced).  The wave streams the 22 input rows of its strip
+// through registers once, top to bottom: each 14-wide input row feeds the 7 output rows it touches
+// (7 x 8 x 7 FMAs per 14 loads), with a rolling set of 7 output-row accumulators -- an output row
+// is stored as soon as its 7th input row has been consumed.  No LDS and no barriers: the 3.6x halo
+// re-read of an 8x8 tile becomes 2.4x row re-reads that the CU's L1 / the XCD's L2 absorb, and the
+// HBM traffic is one read of the input and one write of the output.
 //
-// The op is HBM-bound (49 FMA per 4-8 bytes moved): per output element it reads the input once
-// (+halo re-read ~ (14*14)/(8*8) from LDS, not HBM) and writes the output once.
+// The op is HBM-bound (49 FMA per 4-8 bytes moved).
 //
 //   fwd          z = b + sum_tap w[tap] * x[p + tap]               (+ LayerNorm via ln_fwd)
 //   bwd-data     dx = (acc ? dx : 0) + sum_tap w[48 - tap] * dz[p + tap]   (flipped kernel)
 //   bwd-weight   dW[c][tap] = sum_p dz[p,c] * x[p + tap, c],  db[c] = sum_p dz[p,c]
+//                (same streaming with a rolling set of 7 dz rows; per-workgroup partials)
 #include "common.h"
+
+#include <stdlib.h>
 
 extern "C" int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
                                 int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C,
@@ -22,138 +26,169 @@ extern "C" int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, 
 
 namespace sv {
 
-constexpr int TH = 8, TW = 8;            // output tile
-constexpr int TR = TH + 6, TC = TW + 6;  // halo tile
-constexpr int kDwThreads = 256;          // 4 waves x 2 output rows
-constexpr int RPW = TH / 4;
+constexpr int TH = 16;          // output rows per wave strip
+constexpr int TR = TH + 6;      // input rows the strip reads
+constexpr int kDwThreads = 256;  // 4 independent waves per workgroup
 
-template <typename TIN>
-__device__ __forceinline__ void load_halo_tile(float* __restrict__ lds, const TIN* __restrict__ x, int b,
-                                               int h0, int w0, int c0, int H, int W, int C) {
-  const int sub = threadIdx.x & 15;
-  for (int p = threadIdx.x >> 4; p < TR * TC; p += kDwThreads / 16) {
-    const int r = p / TC, q = p - r * TC;
-    const int h = h0 - 3 + r, w = w0 - 3 + q;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (h >= 0 && h < H && w >= 0 && w < W) v = ld4(x, (((size_t)b * H + h) * W + w) * C + c0 + sub * 4);
-    *reinterpret_cast<float4*>(lds + p * 64 + sub * 4) = v;
+struct DwGeo {
+  int B, H, W, C, tw, tilesW, tilesH, ntiles;  // tw = strip width (output columns per lane)
+};
+
+__device__ __forceinline__ void dw_tile(const DwGeo& g, int tile, int& b, int& h0, int& w0) {
+  const int tw = tile % g.tilesW;
+  const int t = tile / g.tilesW;
+  const int th = t % g.tilesH;
+  b = t / g.tilesH;
+  h0 = th * TH;
+  w0 = tw * g.tw;
+}
+
+// one (TW+6)-wide input row (zero outside the image) of channel c
+template <int TC, typename TIN>
+__device__ __forceinline__ void load_row(float (&in)[TC], const TIN* __restrict__ x, const DwGeo& g, int b, int h,
+                                         int w0, int c) {
+  const bool okh = h >= 0 && h < g.H;
+  const size_t base = (((size_t)b * g.H + (okh ? h : 0)) * g.W) * g.C + c;
+#pragma unroll
+  for (int j = 0; j < TC; ++j) {
+    const int w = w0 - 3 + j;
+    in[j] = (okh && w >= 0 && w < g.W) ? ld(x, base + (size_t)w * g.C) : 0.f;
   }
 }
 
-// z (or dx) for one 8x8 tile x 64 channels.  FLIP: use w[48 - tap] (backward-data).
-template <typename TIN, typename TOUT, bool FLIP, bool ACCUM>
-__global__ void __launch_bounds__(kDwThreads) dwconv7_kernel(const TIN* __restrict__ x,
+// z (or dx) for one 16x8 strip x 64 channels per wave.  FLIP: use w[48 - tap] (backward-data).
+template <int TW, typename TIN, typename TOUT, bool FLIP, bool ACCUM>
+__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_kernel(const TIN* __restrict__ x,
                                                              const float* __restrict__ wdw,
                                                              const float* __restrict__ bdw,
                                                              TOUT* __restrict__ out,
-                                                             uint16_t* __restrict__ out_bf16, int B, int H,
-                                                             int W, int C) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [TR*TC][64]
-  const int tilesW = (W + TW - 1) / TW, tilesH = (H + TH - 1) / TH;
-  int t = blockIdx.x;
-  const int tw = t % tilesW;
-  t /= tilesW;
-  const int th = t % tilesH;
-  const int b = t / tilesH;
-  const int h0 = th * TH, w0 = tw * TW, c0 = blockIdx.y * 64;
-  load_halo_tile(lds, x, b, h0, w0, c0, H, W, C);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = c0 + lane;
+                                                             uint16_t* __restrict__ out_bf16, DwGeo g) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * (kDwThreads / 64) + (threadIdx.x >> 6);
+  const int ncg = g.C / 64;
+  if (gw >= g.ntiles * ncg) return;  // whole wave; the kernel has no barriers
+  const int tile = gw % g.ntiles, c = (gw / g.ntiles) * 64 + lane;
+  int b, h0, w0;
+  dw_tile(g, tile, b, h0, w0);
   float wk[49];
 #pragma unroll
   for (int i = 0; i < 49; ++i) wk[i] = wdw[(size_t)c * 49 + (FLIP ? 48 - i : i)];
   const float bias = bdw ? bdw[c] : 0.f;
-  __syncthreads();
+  constexpr int TC = TW + 6;
+  float acc[7][TW];
 #pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int r = wv * RPW + rr;
-    float acc[TW];
+  for (int r = 0; r < 7; ++r)
 #pragma unroll
-    for (int o = 0; o < TW; ++o) acc[o] = bias;
+    for (int o = 0; o < TW; ++o) acc[r][o] = bias;
+  float in[TC], nxt[TC];
+  load_row(nxt, x, g, b, h0 - 3, w0, c);
+  // input rows in blocks of 7: inside a block, the accumulator slot of output row ir - kh is the
+  // compile-time (u - kh) mod 7 (ib is a multiple of 7); sched_barrier keeps each row's loads one
+  // row ahead instead of letting the scheduler hoist all 308 of them
+#pragma nounroll
+  for (int ib = 0; ib < TR; ib += 7) {
 #pragma unroll
-    for (int kh = 0; kh < 7; ++kh) {
-      float in[TC];
+    for (int u = 0; u < 7; ++u) {
+      const int ir = ib + u;
+      if (ir >= TR) break;
 #pragma unroll
-      for (int j = 0; j < TC; ++j) in[j] = lds[((r + kh) * TC + j) * 64 + lane];
+      for (int j = 0; j < TC; ++j) in[j] = nxt[j];
+      if (ir + 1 < TR) load_row(nxt, x, g, b, h0 - 3 + ir + 1, w0, c);  // next row in flight
 #pragma unroll
-      for (int o = 0; o < TW; ++o)
+      for (int kh = 0; kh < 7; ++kh) {
+        const int orow = ir - kh;
+        if (orow < 0 || orow >= TH) continue;
+        const int sl = (u - kh + 7) % 7;
 #pragma unroll
-        for (int kw = 0; kw < 7; ++kw) acc[o] = fmaf(wk[kh * 7 + kw], in[o + kw], acc[o]);
-    }
-    const int h = h0 + r;
-    if (h < H) {
+        for (int o = 0; o < TW; ++o)
 #pragma unroll
-      for (int o = 0; o < TW; ++o) {
-        const int w = w0 + o;
-        if (w < W) {
-          const size_t i = (((size_t)b * H + h) * W + w) * C + c;
-          const float v = ACCUM ? ld(out, i) + acc[o] : acc[o];
-          st(out, i, v);
-          if (out_bf16) out_bf16[i] = f2bf(v);
-        }
+          for (int kw = 0; kw < 7; ++kw) acc[sl][o] = fmaf(wk[kh * 7 + kw], in[o + kw], acc[sl][o]);
       }
+      if (ir >= 6) {
+        const int orow = ir - 6;  // its 7th (last) input row was just consumed
+        const int sl = (u + 1) % 7;  // == (u - 6) mod 7
+        const int h = h0 + orow;
+        if (h < g.H) {
+#pragma unroll
+          for (int o = 0; o < TW; ++o) {
+            const int w = w0 + o;
+            if (w < g.W) {
+              const size_t i = (((size_t)b * g.H + h) * g.W + w) * g.C + c;
+              const float v = ACCUM ? ld(out, i) + acc[sl][o] : acc[sl][o];
+              st(out, i, v);
+              if (out_bf16) out_bf16[i] = f2bf(v);
+            }
+          }
+        }
+#pragma unroll
+        for (int o = 0; o < TW; ++o) acc[sl][o] = bias;  // reused by output row orow + 7
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
-// backward-weight partials.  grid = (nparts, C/64); part p visits tiles p, p+nparts, ...
-template <typename TIN>
-__global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_kernel(const float* __restrict__ dz,
+// backward-weight partials.  grid = (nparts, C/64); wave v of workgroup p visits strips
+// 4p + v, 4p + v + 4 nparts, ...; the 4 waves are combined through LDS into part p.
+template <int TW, typename TIN>
+__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_wgrad_kernel(const float* __restrict__ dz,
                                                                    const TIN* __restrict__ x,
                                                                    float* __restrict__ dw_part,
-                                                                   float* __restrict__ db_part, int B,
-                                                                   int H, int W, int C) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [TR*TC][64], reused for combine
-  const int tilesW = (W + TW - 1) / TW, tilesH = (H + TH - 1) / TH;
-  const int ntiles = B * tilesH * tilesW;
+                                                                   float* __restrict__ db_part, DwGeo g) {
+  __shared__ float red[4 * 49 * 64 + 4 * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c0 = blockIdx.y * 64, c = c0 + lane;
   float acc[49];
 #pragma unroll
   for (int i = 0; i < 49; ++i) acc[i] = 0.f;
   float dbacc = 0.f;
-  for (int t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-    int t = t0;
-    const int tw = t % tilesW;
-    t /= tilesW;
-    const int th = t % tilesH;
-    const int b = t / tilesH;
-    const int h0 = th * TH, w0 = tw * TW;
-    __syncthreads();  // previous tile's LDS reads are done
-    load_halo_tile(lds, x, b, h0, w0, c0, H, W, C);
-    __syncthreads();
+  for (int tile = blockIdx.x * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
+    int b, h0, w0;
+    dw_tile(g, tile, b, h0, w0);
+    constexpr int TC = TW + 6;
+    float dzb[7][TW];
+    float in[TC], nxt[TC];
+    load_row(nxt, x, g, b, h0 - 3, w0, c);
+#pragma nounroll
+    for (int ib = 0; ib < TR; ib += 7) {
 #pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) {
-      const int r = wv * RPW + rr;
-      const int h = h0 + r;
-      float d[TW];
+      for (int u = 0; u < 7; ++u) {
+        const int ir = ib + u;
+        if (ir >= TR) break;
 #pragma unroll
-      for (int o = 0; o < TW; ++o) {
-        const int w = w0 + o;
-        d[o] = (h < H && w < W) ? dz[(((size_t)b * H + h) * W + w) * C + c] : 0.f;
-        dbacc += d[o];
-      }
+        for (int j = 0; j < TC; ++j) in[j] = nxt[j];
+        if (ir + 1 < TR) load_row(nxt, x, g, b, h0 - 3 + ir + 1, w0, c);
+        if (ir < TH) {  // output-gradient row ir enters the rolling set (slot u)
+          const int h = h0 + ir;
 #pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        float in[TC];
-#pragma unroll
-        for (int j = 0; j < TC; ++j) in[j] = lds[((r + kh) * TC + j) * 64 + lane];
-#pragma unroll
-        for (int kw = 0; kw < 7; ++kw) {
-          float s = acc[kh * 7 + kw];
-#pragma unroll
-          for (int o = 0; o < TW; ++o) s = fmaf(d[o], in[o + kw], s);
-          acc[kh * 7 + kw] = s;
+          for (int o = 0; o < TW; ++o) {
+            const int w = w0 + o;
+            const float v = (h < g.H && w < g.W) ? dz[(((size_t)b * g.H + h) * g.W + w) * g.C + c] : 0.f;
+            dzb[u][o] = v;
+            dbacc += v;
+          }
         }
+#pragma unroll
+        for (int kh = 0; kh < 7; ++kh) {
+          const int orow = ir - kh;
+          if (orow < 0 || orow >= TH) continue;
+          const int sl = (u - kh + 7) % 7;
+#pragma unroll
+          for (int kw = 0; kw < 7; ++kw) {
+            float s = acc[kh * 7 + kw];
+#pragma unroll
+            for (int o = 0; o < TW; ++o) s = fmaf(dzb[sl][o], in[o + kw], s);
+            acc[kh * 7 + kw] = s;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
   // deterministic combine of the 4 waves through LDS: red[wave][tap][64]
-  __syncthreads();
-  float* red = lds;
 #pragma unroll
   for (int i = 0; i < 49; ++i) red[(wv * 49 + i) * 64 + lane] = acc[i];
-  float* redb = lds + 4 * 49 * 64;
+  float* redb = red + 4 * 49 * 64;
   redb[wv * 64 + lane] = dbacc;
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 49; i += kDwThreads) {
@@ -161,23 +196,31 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_kernel(const float* 
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) s += red[(k * 49 + tap) * 64 + ch];
-    dw_part[(size_t)blockIdx.x * C * 49 + (size_t)(c0 + ch) * 49 + tap] = s;
+    dw_part[(size_t)blockIdx.x * g.C * 49 + (size_t)(c0 + ch) * 49 + tap] = s;
   }
   if (threadIdx.x < 64) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) s += redb[k * 64 + threadIdx.x];
-    db_part[(size_t)blockIdx.x * C + c0 + threadIdx.x] = s;
+    db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = s;
   }
 }
 
-static size_t dw_lds_bytes() {
-  size_t a = (size_t)TR * TC * 64 * sizeof(float);
-  size_t b = (size_t)(4 * 49 * 64 + 4 * 64) * sizeof(float);
-  return a > b ? a : b;
+// strip width: 4 columns keeps a lane within 3 waves/SIMD (143 VGPRs); SV_DW_TW=8 trades occupancy for
+// fewer horizontal halo reads
+static int dw_tw() {
+  static const int tw = getenv("SV_DW_TW") && atoi(getenv("SV_DW_TW")) == 8 ? 8 : 4;
+  return tw;
 }
 
-static int dw_tiles(int B, int H, int W) { return B * ((H + TH - 1) / TH) * ((W + TW - 1) / TW); }
+static DwGeo dw_geo(int B, int H, int W, int C) {
+  const int tw = dw_tw();
+  DwGeo g{B, H, W, C, tw, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
+  g.ntiles = B * g.tilesW * g.tilesH;
+  return g;
+}
+
+static int dw_blocks(const DwGeo& g) { return ceil_div((long long)g.ntiles * (g.C / 64), kDwThreads / 64); }
 
 }  // namespace sv
 
@@ -193,10 +236,13 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_ln_fwd: C=%d must be a multiple of 64", C);
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(dw_tiles(B, H, W), C / 64);
-  const size_t lds = dw_lds_bytes();
-#define LAUNCH(TI, TO) \
-  dwconv7_kernel<TI, TO, false, false><<<grid, kDwThreads, lds, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, B, H, W, C)
+  const DwGeo g = dw_geo(B, H, W, C);
+  const int grid = dw_blocks(g);
+#define LAUNCH(TI, TO)                                                                                      \
+  if (g.tw == 8)                                                                                           \
+    dwconv7_kernel<8, TI, TO, false, false><<<grid, kDwThreads, 0, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, g); \
+  else                                                                                                     \
+    dwconv7_kernel<4, TI, TO, false, false><<<grid, kDwThreads, 0, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
   if (x_dtype == SV_F32 && z_dtype == SV_F32) LAUNCH(float, float);
   else if (x_dtype == SV_F32 && z_dtype == SV_BF16) LAUNCH(float, uint16_t);
   else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) LAUNCH(uint16_t, uint16_t);
@@ -215,20 +261,29 @@ int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, uint16_t* 
   SV_REQUIRE(dz != dx, "sv_dwconv7_bwd_data: dz and dx must not alias");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(dw_tiles(B, H, W), C / 64);
-  const size_t lds = dw_lds_bytes();
-  if (accumulate)
-    dwconv7_kernel<float, float, true, true><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C);
-  else
-    dwconv7_kernel<float, float, true, false><<<grid, kDwThreads, lds, s>>>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C);
+  const DwGeo g = dw_geo(B, H, W, C);
+  const int grid = dw_blocks(g);
+  if (g.tw == 8) {
+    if (accumulate)
+      dwconv7_kernel<8, float, float, true, true><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+    else
+      dwconv7_kernel<8, float, float, true, false><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+  } else {
+    if (accumulate)
+      dwconv7_kernel<4, float, float, true, true><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+    else
+      dwconv7_kernel<4, float, float, true, false><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+  }
   return check_launch("sv_dwconv7_bwd_data");
 }
 
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
-  const int tiles = dw_tiles(B, H, W);
-  int np = 2048 / (C / 64 > 0 ? C / 64 : 1);
+  const DwGeo g = dw_geo(B, H, W, C);
+  const int ncg = C / 64 > 0 ? C / 64 : 1;
+  int np = 512 / ncg;  // ~2048 waves over all channel groups
   if (np < 1) np = 1;
-  return tiles < np ? tiles : np;
+  const int need = ceil_div(g.ntiles, 4);
+  return need < np ? need : np;
 }
 
 int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float* dw_part,
@@ -238,14 +293,17 @@ int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_bwd_weight: C=%d must be a multiple of 64", C);
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
+  const DwGeo g = dw_geo(B, H, W, C);
   const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
-  const size_t lds = dw_lds_bytes();
-  if (x_dtype == SV_F32)
-    dwconv7_wgrad_kernel<float><<<grid, kDwThreads, lds, s>>>(dz, (const float*)x, dw_part, db_part, B, H, W, C);
-  else if (x_dtype == SV_BF16)
-    dwconv7_wgrad_kernel<uint16_t><<<grid, kDwThreads, lds, s>>>(dz, (const uint16_t*)x, dw_part, db_part, B, H, W, C);
+  if (x_dtype != SV_F32 && x_dtype != SV_BF16) return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_bwd_weight: bad dtype");
+  if (x_dtype == SV_F32 && g.tw == 8)
+    dwconv7_wgrad_kernel<8, float><<<grid, kDwThreads, 0, s>>>(dz, (const float*)x, dw_part, db_part, g);
+  else if (x_dtype == SV_F32)
+    dwconv7_wgrad_kernel<4, float><<<grid, kDwThreads, 0, s>>>(dz, (const float*)x, dw_part, db_part, g);
+  else if (g.tw == 8)
+    dwconv7_wgrad_kernel<8, uint16_t><<<grid, kDwThreads, 0, s>>>(dz, (const uint16_t*)x, dw_part, db_part, g);
   else
-    return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_bwd_weight: bad dtype");
+    dwconv7_wgrad_kernel<4, uint16_t><<<grid, kDwThreads, 0, s>>>(dz, (const uint16_t*)x, dw_part, db_part, g);
   return check_launch("sv_dwconv7_bwd_weight");
 }
 

@@ -324,8 +324,16 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (!bf) return launch_layout<false, float, float>(d, s);
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
   static const bool force_v1 = getenv("SV_GEMM_V1") != nullptr;
+  static const int impl = getenv("SV_GEMM_IMPL") ? atoi(getenv("SV_GEMM_IMPL")) : 0;
   if (!force_v1) {
-    const int rc = launch_gemm2(d, s);
+    // v3 (two workgroups per CU, BK 32) hides VALU-heavy epilogues and short K behind the other
+    // workgroup's MFMAs; v2 (one workgroup, BK 64, half the barriers) wins on long-K GEMMs with light
+    // epilogues (measured per ConvNeXt shape: tools/gemm_bench.py, profiles/)
+    const bool heavy_epi = d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
+                           d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
+    const bool use_v3 =
+        impl == 3 || (impl == 0 && (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048)));
+    const int rc = use_v3 ? launch_gemm3(d, s) : launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   const bool a32 = d->a_dtype == SV_F32, b32 = d->b_dtype == SV_F32;

@@ -18,14 +18,28 @@
 #include "common.h"
 #include "gemm_common.h"
 
+#include <stdlib.h>
+
 namespace sv {
 namespace g2 {
 
-constexpr int BM = 256, BN = 128, BK = 64, STAGES = 3, THREADS = 512;
-constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-constexpr int A_PIECES = A_BYTES / 1024, B_PIECES = B_BYTES / 1024;  // 1 KiB LDS-DMA pieces
-constexpr int A_PER_WAVE = A_PIECES / 8, B_PER_WAVE = B_PIECES / 8;
-constexpr int LOADS_PER_STAGE = A_PER_WAVE + B_PER_WAVE;  // per wave: 4 + 2 = 6
+constexpr int BM = 256, BK = 64, THREADS = 512;
+constexpr int A_BYTES = BM * BK * 2;
+constexpr int A_PER_WAVE = A_BYTES / 1024 / 8;  // 1 KiB LDS-DMA pieces per wave per stage
+
+// Tile configurations: BN = 128 -> 8 waves as 4(M) x 2(N) of 64x64, 3-stage ring (144 KiB);
+//                      BN = 256 -> 8 waves as 2(M) x 4(N) of 128x64, 2-stage ring (128 KiB): half the
+//                      L2->LDS bytes per FLOP, used when the grid still fills the chip.
+template <int BN>
+struct Cfg {
+  static constexpr int B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int B_PER_WAVE = B_BYTES / 1024 / 8;
+  static constexpr int LOADS = A_PER_WAVE + B_PER_WAVE;  // LDS-DMA instructions per wave per stage
+  static constexpr int STAGES = BN == 128 ? 3 : 2;
+  static constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
+  static constexpr int FM = BM / WAVES_M / 16;  // fragment rows per wave (4 or 8)
+  static constexpr size_t LDS = (size_t)STAGES * STAGE_BYTES;
+};
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -109,11 +123,43 @@ __device__ __forceinline__ float colsum64(const char* __restrict__ img, int row)
   return s;
 }
 
-template <bool AK, bool BKM>
+// wgrad bias gradient for an m-major A image [64 k][BM m]: thread t owns the 16-B chunk t&31 (8 m)
+// of k rows 4(t>>5)..+3, accumulated over the k-steps with ds_read_b128 (4 per k-step); the 16
+// k-groups are folded through LDS once after the main loop (colsum_fold).
+__device__ __forceinline__ void colsum_mmajor(const char* __restrict__ img, float (&cs)[8]) {
+  constexpr int RB = BM * 2;
+  const int gc = threadIdx.x & 31, kg = threadIdx.x >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = kg * 4 + j;
+    const uint4 v = *reinterpret_cast<const uint4*>(img + r * RB + ((gc ^ mswz(r)) << 4));
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cs[2 * q] += __uint_as_float(w[q] << 16);
+      cs[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+}
+// after the main loop (LDS free): fold the 16 k-groups, thread m < BM returns the sum for row m
+__device__ __forceinline__ float colsum_fold(const float (&cs)[8], float* red) {
+  const int gc = threadIdx.x & 31, kg = threadIdx.x >> 5;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[kg * BM + gc * 8 + q] = cs[q];
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x < BM)
+    for (int g = 0; g < 16; ++g) s += red[g * BM + threadIdx.x];
+  __syncthreads();
+  return s;
+}
+
+template <bool AK, bool BKM, int BN>
 __global__ void __launch_bounds__(THREADS) gemm2_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                        const uint16_t* __restrict__ B, int64_t ldb, int K,
                                                        int kper, int tilesM, int tilesN, EpiArgs e,
                                                        float* __restrict__ colsum) {
+  using C = Cfg<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = tilesM * tilesN;
   const int pid = blockIdx.x;
@@ -127,74 +173,99 @@ __global__ void __launch_bounds__(THREADS) gemm2_kernel(const uint16_t* __restri
   if (kend > K) kend = K;
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
-  const int wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  const int wid = threadIdx.x >> 6, wm = wid / C::WAVES_N, wn = wid % C::WAVES_N;
   const bool do_cs = colsum != nullptr && tn == 0;
   float csum = 0.f;
-  f32x4 acc[4][4];
+  float cs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[C::FM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt) {
-    char* st = smem + (kt % STAGES) * STAGE_BYTES;
+    char* st = smem + (kt % C::STAGES) * C::STAGE_BYTES;
     const int k0 = kbeg + kt * BK;
     issue_tile<AK, BM, A_PER_WAVE>(A, lda, m0, k0, e.M, st);
-    issue_tile<BKM, BN, B_PER_WAVE>(B, ldb, n0, k0, e.N, st + A_BYTES);
+    issue_tile<BKM, BN, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + A_BYTES);
   };
 
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
+  for (int p = 0; p < C::STAGES - 1 && p < nk; ++p) issue(p);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // == LOADS_PER_STAGE: tile kt+1 stays in flight
+    // tile kt must have landed; the (STAGES - 2) younger tiles may stay in flight
+    if constexpr (C::STAGES == 3) {
+      static_assert(C::LOADS == 6, "vmcnt immediate below assumes 6 LDS-DMA pieces per wave per stage");
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kt + 2);  // into the slot of tile kt-1, which every wave has finished
-    const char* ai = smem + (kt % STAGES) * STAGE_BYTES;
+    // into the slot of tile kt-1, which every wave has finished reading
+    if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
+    const char* ai = smem + (kt % C::STAGES) * C::STAGE_BYTES;
     const char* bi = ai + A_BYTES;
-    if (do_cs && threadIdx.x < BM) csum += colsum64<AK>(ai, threadIdx.x);
+    if constexpr (AK) {
+      if (do_cs && threadIdx.x < BM) csum += colsum64<AK>(ai, threadIdx.x);
+    } else {
+      static_assert(THREADS == 512 && BK == 64, "colsum_mmajor thread map");
+      if (do_cs) colsum_mmajor(ai, cs8);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[C::FM], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<AK, BM>(ai, wm * 64 + i * 16, kk);
+      for (int i = 0; i < C::FM; ++i) af[i] = frag<AK, BM>(ai, wm * (16 * C::FM) + i * 16, kk);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM, BN>(bi, wn * 64 + j * 16, kk);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
-  static_assert(LOADS_PER_STAGE == 6, "vmcnt immediate above assumes 6 LDS-DMA pieces per wave per stage");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (!AK) {
+    if (do_cs) csum = colsum_fold(cs8, reinterpret_cast<float*>(smem));  // block-uniform branch
+  }
   if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
-  wave_tile_epilogue(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64, n0 + wn * 64, e, split);
+  wave_tile_epilogue<C::FM>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * (16 * C::FM),
+                            n0 + wn * 64, e, split);
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int BN>
 static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  constexpr size_t lds = (size_t)STAGES * STAGE_BYTES;
+  constexpr size_t lds = Cfg<BN>::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm2_kernel<AK, BKM>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm2_kernel<AK, BKM, BN>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   dim3 grid(tilesM * tilesN, 1, split);
-  gemm2_kernel<AK, BKM><<<grid, THREADS, lds, s>>>(
+  gemm2_kernel<AK, BKM, BN><<<grid, THREADS, lds, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
       tilesM, tilesN, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
   return check_launch("sv_gemm(v2)");
+}
+
+template <bool AK, bool BKM>
+static int launch_bn(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
+  // 256-wide tiles (SV_GEMM_BN=256) halve the L2->LDS bytes per FLOP
+  static const int force = getenv("SV_GEMM_BN") ? atoi(getenv("SV_GEMM_BN")) : 0;
+  const long tiles256 = (long)ceil_div(d->M, BM) * ceil_div(d->N, 256) * split;
+  // measured slower than 128-wide tiles on every ConvNeXt shape (2-stage ring exposes the DMA
+  // latency at one workgroup per CU): opt-in only
+  bool wide = false;
+  (void)tiles256;
+  if (force == 256) wide = d->N >= 256;
+  return wide ? launch<AK, BKM, 256>(d, split, kper, s) : launch<AK, BKM, 128>(d, split, kper, s);
 }
 
 }  // namespace g2
@@ -208,10 +279,10 @@ int launch_gemm2(const sv_gemm_desc* d, hipStream_t s) {
   if (d->K % BK != 0 || d->K < BK) return SV_ERR_UNSUPPORTED;
   // m-major operands need whole 16-B chunks along the tile width: M/N multiples of 8 (checked by
   // sv_gemm); k-major need K multiple of 64 (above)
-  if (d->a_kmajor && d->b_kmajor) return launch<true, true>(d, split, kper, s);
-  if (d->a_kmajor && !d->b_kmajor) return launch<true, false>(d, split, kper, s);
-  if (!d->a_kmajor && d->b_kmajor) return launch<false, true>(d, split, kper, s);
-  return launch<false, false>(d, split, kper, s);
+  if (d->a_kmajor && d->b_kmajor) return launch_bn<true, true>(d, split, kper, s);
+  if (d->a_kmajor && !d->b_kmajor) return launch_bn<true, false>(d, split, kper, s);
+  if (!d->a_kmajor && d->b_kmajor) return launch_bn<false, true>(d, split, kper, s);
+  return launch_bn<false, false>(d, split, kper, s);
 }
 
 }  // namespace sv

@@ -100,14 +100,12 @@ __device__ __forceinline__ void gelu_dual4(float4 v, float4& g, float4& dg) {
   gelu_and_grad(v.w, g.w, dg.w);
 }
 
-// Store one wave's 64x64 accumulator (acc[i][j]: 16x16 MFMA fragments, C/D map col = lane&15,
-// row = 4*(lane>>4) + r).  Each 16-row slab goes through the wave's private LDS region `slab`
-// (16 x EPI_LD floats) and is re-read as 8-column units: unit u = lane + 64*h (h = 0,1) covers row
-// u>>3 and columns 8*(u&7)..+7, so one wave store instruction writes 8 whole 128-B rows (bf16:
-// 16 B per lane) -- full cache lines instead of 32-B fragments.  All epilogue operands (bias, gamma
-// and the residual / pre-activation of the tile) are loaded before the first slab.
-__device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], float* __restrict__ slab, int mb,
-                                                   int nb, const EpiArgs& e, int split) {
+// Store one 64-row group (4 fragment rows) of a wave's accumulator; see wave_tile_epilogue.
+// PRE: load the group's residual / pre-activation operands before its first slab (more loads in
+// flight, 64 more VGPRs) or per slab (for kernels that must stay within 128 VGPRs).
+template <int FM, bool PRE = true>
+__device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][4], int i0, float* __restrict__ slab,
+                                                    int mb, int nb, const EpiArgs& e, int split) {
   const int l = threadIdx.x & 63;
   const int cu = (l & 7) * 8, r0 = l >> 3;
   const int n = nb + cu;
@@ -124,24 +122,31 @@ __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], flo
     g0 = *reinterpret_cast<const float4*>(e.gamma + n);
     if (okn4) g1 = *reinterpret_cast<const float4*>(e.gamma + n + 4);
   }
-  float4 xa[4][2], xb[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
+  constexpr int NP = PRE ? 4 : 1;
+  float4 xa[NP][2], xb[NP][2];
+  auto load_aux = [&](int i, int slot) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      xa[i][h] = xb[i][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      xa[slot][h] = xb[slot][h] = make_float4(0.f, 0.f, 0.f, 0.f);
       const int m = mb + i * 16 + r0 + 8 * h;
       if (need_aux && okn && m < e.M) {
-        if (okn4) ld8_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n, xa[i][h], xb[i][h]);
-        else xa[i][h] = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
+        if (okn4) ld8_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n, xa[slot][h], xb[slot][h]);
+        else xa[slot][h] = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
       }
     }
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_aux(i, i);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    const int si = PRE ? i : 0;
+    if constexpr (!PRE) load_aux(i, 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i0 + i][j][r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -172,14 +177,14 @@ __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], flo
         va = ga;  // C2 gets GELU, C gets GELU'
         vb = gb;
       } else if (e.epi == SV_EPI_MUL_AUX) {
-        oa = mul4(va, xa[i][h]);
-        ob = mul4(vb, xb[i][h]);
+        oa = mul4(va, xa[si][h]);
+        ob = mul4(vb, xb[si][h]);
       } else if (e.epi == SV_EPI_BIAS_GAMMA_RES) {
-        oa = fma4(g0, va, xa[i][h]);
-        ob = fma4(g1, vb, xb[i][h]);
+        oa = fma4(g0, va, xa[si][h]);
+        ob = fma4(g1, vb, xb[si][h]);
       } else {
-        oa = ggrad4(va, xa[i][h]);
-        ob = ggrad4(vb, xb[i][h]);
+        oa = ggrad4(va, xa[si][h]);
+        ob = ggrad4(vb, xb[si][h]);
       }
       const size_t ci = (size_t)m * e.ldc + n;
       if (okn4) st8_any(e.C, e.c_dtype, ci, oa, ob);
@@ -198,7 +203,24 @@ __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[4][4], flo
   }
 }
 
+// Store one wave's (16 FM) x 64 accumulator (acc[i][j]: 16x16 MFMA fragments, C/D map col =
+// lane&15, row = 4*(lane>>4) + r), 64 rows at a time.  Each 16-row slab goes through the wave's
+// private LDS region `slab` (16 x EPI_LD floats) and is re-read as 8-column units: unit
+// u = lane + 64*h (h = 0,1) covers row u>>3 and columns 8*(u&7)..+7, so one wave store instruction
+// writes 8 whole 128-B rows (bf16: 16 B per lane) -- full cache lines instead of 32-B fragments.
+// The epilogue operands of each 64-row group (bias, gamma, residual / pre-activation) are loaded
+// before its first slab.
+template <int FM, bool PRE = true>
+__device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[FM][4], float* __restrict__ slab, int mb,
+                                                   int nb, const EpiArgs& e, int split) {
+  static_assert(FM % 4 == 0, "64-row groups");
+#pragma unroll
+  for (int i0 = 0; i0 < FM; i0 += 4) wave_group_epilogue<FM, PRE>(acc, i0, slab, mb + 16 * i0, nb, e, split);
+}
+
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
+// v3 entry (gemm3.hip, two workgroups per CU): same contract with K % 32 == 0
+int launch_gemm3(const sv_gemm_desc* d, hipStream_t s);
 
 }  // namespace sv

@@ -15,7 +15,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsv_kernels.so")
+LIB_PATH = os.environ.get("SV_LIB_PATH") or os.path.join(_HERE, "libsv_kernels.so")  # override: A/B experiments
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 
 SV_F32, SV_BF16 = 0, 1

@@ -49,9 +49,15 @@ def test_classification_trainer_gpu(dev, tmp_path, backbone, precision):
 
 
 def test_classification_step_matches_oracle(dev):
-    """One full ClassificationTrainer step (ResNet-50, 3 heads, fp32 parity mode): loss, gradient
-    norm, every clipped gradient, the AdamW update bound and the BN running statistics against the
-    fp32 CPU oracle step (oracle pinned to the reference by tests/golden/classification_resnet50_64.npz)."""
+    """One full ClassificationTrainer step (ResNet-50, 3 heads, fp32 parity mode) against the CPU
+    oracle step (pinned to the reference by tests/golden/classification_resnet50_64.npz): loss and
+    gradient norm within 1e-3; every clipped parameter gradient against the oracle run in float64,
+    within max(1e-3, 3x the fp32 oracle's own error) -- at B=4, 64x64 the train-mode BatchNorm of
+    layer4 normalises over 16 values per channel and some gradients are ill-conditioned (the fp32 CPU
+    oracle itself is up to 4e-2 away from float64 on them); the AdamW update bound (2 lr) and the BN
+    running statistics."""
+    import copy
+
     from oracle import heads as oh
     from oracle import resnet as orn
     from oracle import step as ostep
@@ -64,6 +70,7 @@ def test_classification_step_matches_oracle(dev):
     ow.fill_module(m)
     ora = oh.Classifier(orn.create("resnet50"), 2048, dropout=0.0)
     ora.load_state_dict(m.state_dict(), strict=False)
+    o64 = copy.deepcopy(ora).double().train()
     m = m.to(dev).train()
     ora.train()
     img, targets = ow.classification_batch(4, 64, 64)
@@ -73,15 +80,23 @@ def test_classification_step_matches_oracle(dev):
     loss = eng.step_classification(img.to(dev), {k: v.to(dev) for k, v in targets.items()})
     opt = ostep.make_optimizer(ora, lr=lr, weight_decay=1e-5)
     l_ref, _, norm = ostep.train_step_classification(ora, opt, img, targets)
+    l64 = o64.get_loss(o64(img.double()), targets)
+    l64.backward()
+    n64 = torch.nn.utils.clip_grad_norm_(o64.parameters(), 1.0)
     assert abs(float(loss) - l_ref) / abs(l_ref) < 1e-3
     assert abs(float(eng.last_grad_norm) - float(norm)) / float(norm) < 1e-3
-    # gradients: HIP keeps the unclipped gradient (the clip is a scale inside the fused AdamW), the
-    # oracle's clip_grad_norm_ scaled its gradients in place
+    e_norm_ora = abs(float(norm) - float(n64)) / float(n64)
+    assert abs(float(eng.last_grad_norm) - float(n64)) / float(n64) < max(1e-3, 3.0 * e_norm_ora)
+    # HIP keeps the unclipped gradient (the clip is a scale inside the fused AdamW)
     coef = min(1.0, 1.0 / (float(eng.last_grad_norm) + 1e-6))
     hp = dict(m.named_parameters())
+    p64 = dict(o64.named_parameters())
     for n, p in ora.named_parameters():
-        r = float((hp[n].grad.cpu() * coef - p.grad).norm() / (p.grad.norm() + 1e-30))
-        assert r < 1e-3, (n, r)
+        g64 = p64[n].grad
+        scale = float(g64.norm()) + 1e-30
+        e_hip = float((hp[n].grad.cpu().double() * coef - g64).norm()) / scale
+        e_ora = float((p.grad.double() - g64).norm()) / scale
+        assert e_hip < max(1e-3, 3.0 * e_ora), (n, e_hip, e_ora)
     sd_ref = ora.state_dict()
     for k, v in m.state_dict().items():
         ref = sd_ref[k]

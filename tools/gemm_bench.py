@@ -48,6 +48,7 @@ def cases(M, C, dev):
         ("fc2_dgrad(mul)", fl, lambda: K.linear_dgrad(d, w2, out=outh, epilogue=nv.SV_EPI_MUL_AUX, aux=h)),
         ("fc1_dgrad", fl, lambda: K.linear_dgrad(dh, w1, out=out)),
         ("fc2_wgrad", fl, lambda: K.linear_wgrad(d, a)),
+        ("fc2_wgrad+bias", fl, lambda: K.linear_wgrad(d, a, bias_out=b2, bias_accumulate=False)),
         ("fc1_wgrad", fl, lambda: K.linear_wgrad(dh, y)),
     ]
 
