@@ -95,9 +95,10 @@ int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float
                      int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C, float eps,
                      sv_stream_t stream);
 int sv_layernorm_bwd_nparts(int64_t rows, int32_t C);
-int sv_layernorm_bwd(const float* dy, const void* x, int32_t x_dtype, const float* mean,
-                     const float* rstd, const float* w, float* dx, int32_t accumulate, float* dw_part,
-                     float* db_part, int64_t rows, int32_t C, sv_stream_t stream);
+/* dy/x/dx dtype combinations: (f32,f32,f32), (f32,bf16,f32), (bf16,bf16,f32), (bf16,bf16,bf16).     */
+int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_dtype, const float* mean,
+                     const float* rstd, const float* w, void* dx, int32_t dx_dtype, int32_t accumulate,
+                     float* dw_part, float* db_part, int64_t rows, int32_t C, sv_stream_t stream);
 
 /* ---- ConvNeXt block head: depthwise 7x7 (pad 3, bias) fused with the channels-last LayerNorm --
  * Replaces ConvNeXtBlock.conv_dw + permute + ConvNeXtBlock.norm (timm convnext.py).
@@ -108,12 +109,13 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
                       int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
                       int32_t C, sv_stream_t stream);
 /* backward-data of the depthwise conv: dx[p] = (accumulate ? dx[p] : 0) + sum_tap w*dz; if dx_bf16
- * != NULL it also receives bf16(dx) -- the GEMM-operand copy of the gradient stream.              */
-int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
-                        int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+ * != NULL it also receives bf16(dx) -- the GEMM-operand copy of the gradient stream.  dz: f32 or bf16
+ * (dz_dtype), dx: f32.                                                                             */
+int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, float* dx, uint16_t* dx_bf16,
+                        int32_t accumulate, int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
 /* backward-weight: per-workgroup partials dw_part [nparts][C*49], db_part [nparts][C].             */
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
-int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float* dw_part,
+int sv_dwconv7_bwd_weight(const void* dz, int32_t dz_dtype, const void* x, int32_t x_dtype, float* dw_part,
                           float* db_part, int32_t B, int32_t H, int32_t W, int32_t C,
                           sv_stream_t stream);
 
@@ -158,6 +160,10 @@ int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, c
  * Grouped partial-sum reduction (group >= P or <= 0: one group):
  *   out[g*n + i] = (accumulate ? out[g*n + i] : 0) + alpha * sum_{p in [g*group, (g+1)*group)} part[p*n + i]
  * The host reduces deep split-K slabs in two passes (groups, then the group sums).                 */
+/* one-launch variant for two independent segments sharing the partial count P (a weight gradient and
+ * its bias gradient): out_s[i] (+)= alpha * sum_p part_s[p*n_s + i]; n_b = 0 for a single segment.   */
+int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, const float* part_b, int64_t n_b,
+                            float* out_b, int32_t P, float alpha, int32_t accumulate, sv_stream_t stream);
 int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,
                        int32_t accumulate, sv_stream_t stream);
 /* column sums of a [rows][C] matrix into partials [nparts][C]; nparts = sv_colsum_nparts(rows,C). */

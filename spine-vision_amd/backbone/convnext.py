@@ -270,8 +270,10 @@ class ConvNeXtHip(nn.Module):
                 nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),
                         nv.ptr(blk.gamma), nv.ptr(blk.mlp.fc2.bias), nv.ptr(g(blk.mlp.fc2.weight)),
                         nv.ptr(g(blk.gamma)), nv.ptr(g(blk.mlp.fc2.bias)), C, 4 * C)
-                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM)
-                dy = torch.empty(M, C, device=d.device, dtype=torch.float32)
+                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM).
+                # bf16 mode: dy travels as bf16; dz stays f32 (the depthwise backward streams it with
+                # 4-byte lane loads, measured faster than 2-byte ones)
+                dy = torch.empty(M, C, device=d.device, dtype=act)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
                 K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
                                compute_bf16=bf)

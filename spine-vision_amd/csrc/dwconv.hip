@@ -130,8 +130,8 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
 
 // backward-weight partials.  grid = (nparts, C/64); wave v of workgroup p visits strips
 // 4p + v, 4p + v + 4 nparts, ...; the 4 waves are combined through LDS into part p.
-template <int TW, typename TIN>
-__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_wgrad_kernel(const float* __restrict__ dz,
+template <int TW, typename TDZ, typename TIN>
+__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_wgrad_kernel(const TDZ* __restrict__ dz,
                                                                    const TIN* __restrict__ x,
                                                                    float* __restrict__ dw_part,
                                                                    float* __restrict__ db_part, DwGeo g) {
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
           for (int o = 0; o < TW; ++o) {
             const int w = w0 + o;
-            const float v = (h < g.H && w < g.W) ? dz[(((size_t)b * g.H + h) * g.W + w) * g.C + c] : 0.f;
+            const float v = (h < g.H && w < g.W) ? ld(dz, (((size_t)b * g.H + h) * g.W + w) * g.C + c) : 0.f;
             dzb[u][o] = v;
             dbacc += v;
           }
@@ -254,26 +254,27 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
 }
 
-int sv_dwconv7_bwd_data(const float* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
-                        int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, float* dx, uint16_t* dx_bf16,
+                        int32_t accumulate, int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dz && wdw && dx, "sv_dwconv7_bwd_data: null pointer");
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_bwd_data: C=%d must be a multiple of 64", C);
-  SV_REQUIRE(dz != dx, "sv_dwconv7_bwd_data: dz and dx must not alias");
+  SV_REQUIRE(dz != (const void*)dx, "sv_dwconv7_bwd_data: dz and dx must not alias");
+  SV_REQUIRE(dz_dtype == SV_F32 || dz_dtype == SV_BF16, "sv_dwconv7_bwd_data: bad dz dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
-  if (g.tw == 8) {
-    if (accumulate)
-      dwconv7_kernel<8, float, float, true, true><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
-    else
-      dwconv7_kernel<8, float, float, true, false><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+#define BWD(TWV, TD, ACC) \
+  dwconv7_kernel<TWV, TD, float, true, ACC><<<grid, kDwThreads, 0, s>>>((const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
+#define BWD_TW(TD, ACC) \
+  if (g.tw == 8) BWD(8, TD, ACC); else BWD(4, TD, ACC)
+  if (dz_dtype == SV_F32) {
+    if (accumulate) { BWD_TW(float, true); } else { BWD_TW(float, false); }
   } else {
-    if (accumulate)
-      dwconv7_kernel<4, float, float, true, true><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
-    else
-      dwconv7_kernel<4, float, float, true, false><<<grid, kDwThreads, 0, s>>>(dz, wdw, nullptr, dx, dx_bf16, g);
+    if (accumulate) { BWD_TW(uint16_t, true); } else { BWD_TW(uint16_t, false); }
   }
+#undef BWD_TW
+#undef BWD
   return check_launch("sv_dwconv7_bwd_data");
 }
 
@@ -286,24 +287,27 @@ int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
   return need < np ? need : np;
 }
 
-int sv_dwconv7_bwd_weight(const float* dz, const void* x, int32_t x_dtype, float* dw_part,
+int sv_dwconv7_bwd_weight(const void* dz, int32_t dz_dtype, const void* x, int32_t x_dtype, float* dw_part,
                           float* db_part, int32_t B, int32_t H, int32_t W, int32_t C,
                           sv_stream_t stream) {
   SV_REQUIRE(dz && x && dw_part && db_part, "sv_dwconv7_bwd_weight: null pointer");
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_bwd_weight: C=%d must be a multiple of 64", C);
+  SV_REQUIRE((dz_dtype == SV_F32 || dz_dtype == SV_BF16) && (x_dtype == SV_F32 || x_dtype == SV_BF16),
+             "sv_dwconv7_bwd_weight: bad dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const DwGeo g = dw_geo(B, H, W, C);
   const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
-  if (x_dtype != SV_F32 && x_dtype != SV_BF16) return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_bwd_weight: bad dtype");
-  if (x_dtype == SV_F32 && g.tw == 8)
-    dwconv7_wgrad_kernel<8, float><<<grid, kDwThreads, 0, s>>>(dz, (const float*)x, dw_part, db_part, g);
-  else if (x_dtype == SV_F32)
-    dwconv7_wgrad_kernel<4, float><<<grid, kDwThreads, 0, s>>>(dz, (const float*)x, dw_part, db_part, g);
-  else if (g.tw == 8)
-    dwconv7_wgrad_kernel<8, uint16_t><<<grid, kDwThreads, 0, s>>>(dz, (const uint16_t*)x, dw_part, db_part, g);
-  else
-    dwconv7_wgrad_kernel<4, uint16_t><<<grid, kDwThreads, 0, s>>>(dz, (const uint16_t*)x, dw_part, db_part, g);
+#define WG(TWV, TD, TX) \
+  dwconv7_wgrad_kernel<TWV, TD, TX><<<grid, kDwThreads, 0, s>>>((const TD*)dz, (const TX*)x, dw_part, db_part, g)
+#define WG_TW(TD, TX) \
+  if (g.tw == 8) WG(8, TD, TX); else WG(4, TD, TX)
+  if (dz_dtype == SV_F32 && x_dtype == SV_F32) { WG_TW(float, float); }
+  else if (dz_dtype == SV_F32) { WG_TW(float, uint16_t); }
+  else if (x_dtype == SV_F32) { WG_TW(uint16_t, float); }
+  else { WG_TW(uint16_t, uint16_t); }
+#undef WG_TW
+#undef WG
   return check_launch("sv_dwconv7_bwd_weight");
 }
 

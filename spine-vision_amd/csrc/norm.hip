@@ -61,13 +61,15 @@ __global__ void __launch_bounds__(kLnThreads) ln_fwd_kernel(const TX* __restrict
 }
 
 // LayerNorm backward over rows.  dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w.
-template <typename TX, int CPL>
-__global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const float* __restrict__ dy,
+// dy / x / dx may each be f32 or bf16 (bf16 mode: the fc1 dgrad output and the dwconv input
+// gradient travel as bf16); statistics and parameter gradients stay f32.
+template <typename TDY, typename TX, typename TDX, int CPL>
+__global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const TDY* __restrict__ dy,
                                                             const TX* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ w,
-                                                            float* __restrict__ dx, int accumulate,
+                                                            TDX* __restrict__ dx, int accumulate,
                                                             float* __restrict__ dw_part,
                                                             float* __restrict__ db_part, int64_t rows,
                                                             int C) {
@@ -90,7 +92,7 @@ __global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const float* __restr
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       const int c = lane + 64 * t;
-      const float d = dy[(size_t)r * C + c];
+      const float d = ld(dy, (size_t)r * C + c);
       xh[t] = (ld(x, (size_t)r * C + c) - mu) * rs;
       g[t] = d * wr[t];
       s1 += g[t];
@@ -104,7 +106,7 @@ __global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const float* __restr
     for (int t = 0; t < CPL; ++t) {
       const size_t i = (size_t)r * C + lane + 64 * t;
       const float v = rs * (g[t] - s1 - xh[t] * s2);
-      dx[i] = accumulate ? dx[i] + v : v;
+      st(dx, i, accumulate ? ld(dx, i) + v : v);
     }
   }
   // combine the 4 waves of this workgroup deterministically (fixed order) -> one partial row
@@ -528,23 +530,31 @@ int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float
 
 int sv_layernorm_bwd_nparts(int64_t rows, int32_t C) { (void)C; return ln_grid(rows); }
 
-int sv_layernorm_bwd(const float* dy, const void* x, int32_t x_dtype, const float* mean,
-                     const float* rstd, const float* w, float* dx, int32_t accumulate, float* dw_part,
-                     float* db_part, int64_t rows, int32_t C, sv_stream_t stream) {
+int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_dtype, const float* mean,
+                     const float* rstd, const float* w, void* dx, int32_t dx_dtype, int32_t accumulate,
+                     float* dw_part, float* db_part, int64_t rows, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dy && x && mean && rstd && w && dx && dw_part && db_part, "sv_layernorm_bwd: null pointer");
   SV_REQUIRE(cpl_ok(C) && C <= 2048, "sv_layernorm_bwd: C=%d unsupported", C);
   if (rows <= 0) return SV_OK;
   const int grid = ln_grid(rows);
   hipStream_t s = (hipStream_t)stream;
-  if (x_dtype == SV_F32) {
-    SV_CPL_SWITCH(C / 64, ln_bwd_kernel<float, CPL><<<grid, kLnThreads, 0, s>>>(
-                              dy, (const float*)x, mean, rstd, w, dx, accumulate, dw_part, db_part, rows, C));
-  } else if (x_dtype == SV_BF16) {
-    SV_CPL_SWITCH(C / 64, ln_bwd_kernel<uint16_t, CPL><<<grid, kLnThreads, 0, s>>>(
-                              dy, (const uint16_t*)x, mean, rstd, w, dx, accumulate, dw_part, db_part, rows, C));
+#define LNB(TDY, TX, TDX)                                                                              \
+  SV_CPL_SWITCH(C / 64, ln_bwd_kernel<TDY, TX, TDX, CPL><<<grid, kLnThreads, 0, s>>>(                 \
+                            (const TDY*)dy, (const TX*)x, mean, rstd, w, (TDX*)dx, accumulate, dw_part, \
+                            db_part, rows, C))
+  if (dy_dtype == SV_F32 && x_dtype == SV_F32 && dx_dtype == SV_F32) {
+    LNB(float, float, float);
+  } else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_F32) {
+    LNB(float, uint16_t, float);
+  } else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_F32) {
+    LNB(uint16_t, uint16_t, float);
+  } else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) {
+    LNB(uint16_t, uint16_t, uint16_t);
   } else {
-    return set_error(SV_ERR_INVALID_ARG, "sv_layernorm_bwd: bad dtype");
+    return set_error(SV_ERR_UNSUPPORTED, "sv_layernorm_bwd: dtype combination (dy %d, x %d, dx %d) unsupported",
+                     dy_dtype, x_dtype, dx_dtype);
   }
+#undef LNB
   return check_launch("sv_layernorm_bwd");
 }
 

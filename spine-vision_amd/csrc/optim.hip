@@ -61,6 +61,61 @@ __global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* 
   }
 }
 
+// One-launch partial reduction for up to two segments (e.g. a weight and its bias gradient):
+// out_s[i] (+)= alpha * sum_p part_s[p][i].  A workgroup owns 64 columns of one segment: 16 float4
+// column lanes x 16 partial groups (p = g, g+16, ...), folded through LDS in a fixed order
+// (deterministic).  Works for any partial depth P in one pass: small column counts with deep P (the
+// LayerNorm / depthwise / bias partials) get P-parallelism, wide slabs get column parallelism.
+struct RedSeg {
+  const float* part;
+  int64_t n;
+  float* out;
+};
+
+__global__ void __launch_bounds__(kThreads) reduce_pair_kernel(RedSeg a, RedSeg b, int64_t blocks_a, int P,
+                                                               float alpha, int accumulate) {
+  __shared__ float4 red[16][16];
+  const bool sb = blockIdx.x >= blocks_a;
+  const RedSeg sg = sb ? b : a;
+  const int64_t blk = sb ? blockIdx.x - blocks_a : blockIdx.x;
+  const int c4 = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int64_t col = blk * 64 + c4 * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col + 4 <= sg.n) {
+    int p = pg;
+    for (; p + 48 < P; p += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sg.part + (size_t)(p + 16 * u) * sg.n + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(sg.part + (size_t)p * sg.n + col);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  } else if (col < sg.n) {  // ragged tail (n % 4 != 0)
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = pg; p < P; p += 16)
+      for (int j = 0; j < 4 && col + j < sg.n; ++j) t[j] += sg.part[(size_t)p * sg.n + col + j];
+    acc = make_float4(t[0], t[1], t[2], t[3]);
+  }
+  red[pg][c4] = acc;
+  __syncthreads();
+  if (threadIdx.x < 16 && col < sg.n) {
+    float4 s = red[0][c4];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) {
+      const float4 v = red[g][c4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const float r[4] = {s.x * alpha, s.y * alpha, s.z * alpha, s.w * alpha};
+    for (int j = 0; j < 4 && col + j < sg.n; ++j) sg.out[col + j] = accumulate ? sg.out[col + j] + r[j] : r[j];
+  }
+}
+
 // column sums: workgroup b sums rows [b*rpb, (b+1)*rpb) of all C columns -> part[b][C]
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, int64_t rows, int C,
@@ -198,6 +253,19 @@ static int stream_grid(int64_t n, int per_thread) {
 using namespace sv;
 
 extern "C" {
+
+int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, const float* part_b, int64_t n_b,
+                            float* out_b, int32_t P, float alpha, int32_t accumulate, sv_stream_t stream) {
+  SV_REQUIRE(part_a && out_a && P >= 1 && n_a >= 0, "sv_reduce_partials_pair: bad args");
+  SV_REQUIRE(!n_b || (part_b && out_b), "sv_reduce_partials_pair: bad second segment");
+  if (n_a % 4 == 0) SV_REQUIRE((((uintptr_t)part_a) & 15) == 0, "sv_reduce_partials_pair: part_a must be 16-B aligned");
+  if (n_b % 4 == 0 && n_b) SV_REQUIRE((((uintptr_t)part_b) & 15) == 0, "sv_reduce_partials_pair: part_b must be 16-B aligned");
+  const int64_t ba = (n_a + 63) / 64, bb = (n_b + 63) / 64;
+  if (ba + bb == 0) return SV_OK;
+  RedSeg a{part_a, n_a, out_a}, b{part_b, n_b, out_b};
+  reduce_pair_kernel<<<(unsigned)(ba + bb), kThreads, 0, (hipStream_t)stream>>>(a, b, ba, P, alpha, accumulate);
+  return check_launch("sv_reduce_partials_pair");
+}
 
 int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,
                        int32_t accumulate, sv_stream_t stream) {

@@ -156,32 +156,43 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
     gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
-    if cs is not None:
-        reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
     if out is None:
         if split == 1 and not accumulate:
+            if cs is not None:
+                reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
             return slab.view(N, K)
         out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
         accumulate = False
     _check(out.numel() == N * K and out.is_contiguous(), "linear_wgrad: bad out")
-    reduce_into(slab, split, out, accumulate)
+    if cs is not None and bias_accumulate == accumulate:
+        reduce_pair(slab, out, cs, bias_out, split, accumulate=accumulate)
+    else:
+        if cs is not None:
+            reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
+        reduce_into(slab, split, out, accumulate)
     return out
 
 
 # ----------------------------------------------------------------------------------------------
 # reductions
 def reduce_into(part: torch.Tensor, nparts: int, out: torch.Tensor, accumulate: bool = True, alpha: float = 1.0):
-    """out (+)= alpha * sum of nparts partial rows; deep partial stacks are folded in two passes."""
-    n = out.numel()
-    _check(part.numel() >= nparts * n, "reduce_into: partial buffer too small")
-    _check(out.dtype == torch.float32 and out.is_contiguous(), "reduce_into: out must be contiguous f32")
-    if nparts > 32:
-        group = 16
-        G = -(-nparts // group)
-        tmp = torch.empty(G * n, device=out.device, dtype=torch.float32)
-        call("sv_reduce_partials", ptr(part), nparts, group, n, ptr(tmp), 1.0, 0)
-        part, nparts = tmp, G
-    call("sv_reduce_partials", ptr(part), nparts, nparts, n, ptr(out), alpha, int(accumulate))
+    """out (+)= alpha * sum of nparts partial rows -- one launch for any depth (sv_reduce_partials_pair)."""
+    reduce_pair(part, out, None, None, nparts, accumulate=accumulate, alpha=alpha)
+
+
+def reduce_pair(part_a: torch.Tensor, out_a: torch.Tensor, part_b: torch.Tensor | None, out_b: torch.Tensor | None,
+                nparts: int, accumulate: bool = True, alpha: float = 1.0):
+    """Two independent partial reductions with the same depth in ONE launch (weight + bias gradients)."""
+    na = out_a.numel()
+    _check(part_a.numel() >= nparts * na, "reduce_pair: partial buffer a too small")
+    _check(out_a.dtype == torch.float32 and out_a.is_contiguous(), "reduce_pair: out must be contiguous f32")
+    nb = 0
+    if out_b is not None:
+        nb = out_b.numel()
+        _check(part_b is not None and part_b.numel() >= nparts * nb, "reduce_pair: partial buffer b too small")
+        _check(out_b.dtype == torch.float32 and out_b.is_contiguous(), "reduce_pair: out must be contiguous f32")
+    call("sv_reduce_partials_pair", ptr(part_a), na, ptr(out_a), ptr(part_b), nb, ptr(out_b), nparts, float(alpha),
+         int(accumulate))
 
 
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = True):
@@ -209,18 +220,20 @@ def layernorm_fwd(x2d, w, b, *, out_dtype, eps=EPS_LN):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=False):
+def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=False, out_dtype=torch.float32):
     rows, C = x2d.shape
-    _check(dy2d.dtype == torch.float32 and dy2d.shape == (rows, C), "layernorm_bwd: dy must be f32 [rows,C]")
+    _check(tuple(dy2d.shape) == (rows, C) and dy2d.is_contiguous(), "layernorm_bwd: dy must be contiguous [rows,C]")
     if dx is None:
-        dx = torch.empty(rows, C, device=x2d.device, dtype=torch.float32)
+        dx = torch.empty(rows, C, device=x2d.device, dtype=out_dtype)
     P = value("sv_layernorm_bwd_nparts", rows, C)
     pw = torch.empty(2, P * C, device=x2d.device, dtype=torch.float32)
-    call("sv_layernorm_bwd", ptr(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx),
+    call("sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx), dt(dx),
          int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
-    if dw is not None:
+    if dw is not None and db is not None:
+        reduce_pair(pw[0], dw, pw[1], db, P)
+    elif dw is not None:
         reduce_into(pw[0], P, dw)
-    if db is not None:
+    elif db is not None:
         reduce_into(pw[1], P, db)
     return dx
 
@@ -244,7 +257,7 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
     _check(dx4d.shape == dz4d.shape and dx4d.dtype == torch.float32, "dwconv7_bwd_data: shape")
     if dx_bf16 is not None:
         _check(dx_bf16.numel() == dx4d.numel() and dx_bf16.dtype == torch.bfloat16, "dwconv7_bwd_data: bf16 copy")
-    call("sv_dwconv7_bwd_data", ptr(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16), int(accumulate), B, H, W, C)
+    call("sv_dwconv7_bwd_data", ptr(dz4d), dt(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16), int(accumulate), B, H, W, C)
 
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
@@ -252,9 +265,8 @@ def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
     P = value("sv_dwconv7_bwd_weight_nparts", B, H, W, C)
     pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
     pb = torch.empty(P * C, device=dz4d.device, dtype=torch.float32)
-    call("sv_dwconv7_bwd_weight", ptr(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb), B, H, W, C)
-    reduce_into(pw, P, dw)
-    reduce_into(pb, P, db)
+    call("sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb), B, H, W, C)
+    reduce_pair(pw, dw, pb, db, P)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -280,10 +292,8 @@ def stem_bwd(img, w, b, lnw, mean, rstd, dy, *, dw, db, dlnw, dlnb):
     pv = torch.empty(3, P * C, device=img.device, dtype=torch.float32)
     call("sv_stem_patchify_ln_bwd", ptr(img), ptr(w), ptr(b), ptr(lnw), ptr(mean), ptr(rstd), ptr(dy), ptr(pw),
          ptr(pv[0]), ptr(pv[1]), ptr(pv[2]), B, H, W, C)
-    reduce_into(pw, P, dw)
-    reduce_into(pv[0], P, db)
-    reduce_into(pv[1], P, dlnw)
-    reduce_into(pv[2], P, dlnb)
+    reduce_pair(pw, dw, pv[0], db, P)
+    reduce_pair(pv[1], dlnw, pv[2], dlnb, P)
 
 
 def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):
@@ -306,8 +316,7 @@ def downsample_bwd(dpatches, x4d, mean, rstd, lnw, *, dlnw, dlnb, with_bf16=Fals
     pv = torch.empty(2, P * C, device=x4d.device, dtype=torch.float32)
     call("sv_downsample_ln_patch2_bwd", ptr(dpatches), ptr(x4d), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(dxb),
          ptr(pv[0]), ptr(pv[1]), B, H, W, C)
-    reduce_into(pv[0], P, dlnw)
-    reduce_into(pv[1], P, dlnb)
+    reduce_pair(pv[0], dlnw, pv[1], dlnb, P)
     return dx, dxb
 
 
@@ -330,8 +339,7 @@ def pool_ln_bwd(dfeat, pooled, mean, rstd, lnw, shape, *, dlnw, dlnb, with_bf16=
     pv = torch.empty(2, B * C, device=dfeat.device, dtype=torch.float32)
     call("sv_pool_ln_bwd", ptr(dfeat.contiguous()), ptr(pooled), ptr(mean), ptr(rstd), ptr(lnw), ptr(dx), ptr(dxb),
          ptr(pv[0]), ptr(pv[1]), B, H * W, C)
-    reduce_into(pv[0], B, dlnw)
-    reduce_into(pv[1], B, dlnb)
+    reduce_pair(pv[0], dlnw, pv[1], dlnb, B)
     return dx, dxb
 
 

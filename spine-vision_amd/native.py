@@ -60,11 +60,11 @@ _SIGS = {
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
     "sv_layernorm_bwd_nparts": [_i64, _i32],
-    "sv_layernorm_bwd": [_p, _p, _i32, _p, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p],
+    "sv_layernorm_bwd": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _i64, _i32, _p],
     "sv_dwconv7_ln_fwd": [_p, _i32, _p, _p, _p, _p, _f32, _p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
-    "sv_dwconv7_bwd_data": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_data": [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_weight_nparts": [_i32, _i32, _i32, _i32],
-    "sv_dwconv7_bwd_weight": [_p, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_weight": [_p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_fwd": [_p, _p, _p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_bwd_nparts": [_i32, _i32, _i32, _i32],
     "sv_stem_patchify_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
@@ -74,6 +74,7 @@ _SIGS = {
     "sv_pool_ln_fwd": [_p, _p, _p, _f32, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_reduce_partials": [_p, _i32, _i32, _i64, _p, _f32, _i32, _p],
+    "sv_reduce_partials_pair": [_p, _i64, _p, _p, _i64, _p, _i32, _f32, _i32, _p],
     "sv_colsum_nparts": [_i64, _i32],
     "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],

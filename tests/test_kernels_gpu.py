@@ -319,3 +319,47 @@ def test_adamw_and_clip(dev):
     assert maxrel(md, mr) < 1e-5
     assert maxrel(vd, vr) < 1e-5
     assert torch.equal(pb.cpu(), pd.cpu().to(torch.bfloat16))
+
+
+# ------------------------------------------------- bf16 gradient paths (bf16 mode: dy, dz in bf16)
+@pytest.mark.parametrize("C", [128, 512])
+def test_layernorm_bwd_bf16_io(dev, C):
+    g = torch.Generator().manual_seed(C + 1)
+    x = (torch.randn(333, C, generator=g) * 2 + 0.5).to(torch.bfloat16)
+    w = torch.rand(C, generator=g) + 0.5
+    dy = torch.randn(333, C, generator=g).to(torch.bfloat16)
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), wr, None, 1e-6)
+    yr.backward(dy.double())
+    xd = x.to(dev)
+    _, mean, rstd = K.layernorm_fwd(xd, w.to(dev), torch.zeros(C, device=dev), out_dtype=torch.float32)
+    dw = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    dx = K.layernorm_bwd(dy.to(dev), xd, mean, rstd, w.to(dev), dw=dw, db=db, out_dtype=torch.bfloat16)
+    assert dx.dtype == torch.bfloat16
+    assert rel(dx, xr.grad) < 8e-3  # output rounded to bf16
+    assert rel(dw, wr.grad) < 1e-5
+    assert rel(db, dy.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64)])
+def test_dwconv7_bwd_bf16_dz(dev, shape):
+    B, H, W, C = shape
+    g = torch.Generator().manual_seed(B * H * W + C + 7)
+    x = torch.randn(B, H, W, C, generator=g)
+    w = torch.randn(C, 1, 7, 7, generator=g) * 0.1
+    dz = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    xr = x.permute(0, 3, 1, 2).double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    zr = F.conv2d(xr, wr, None, padding=3, groups=C)
+    zr.permute(0, 2, 3, 1).backward(dz.double())
+    base = torch.randn(B, H, W, C, generator=g)
+    dx = base.clone().to(dev)
+    K.dwconv7_bwd_data(dz.to(dev), w.to(dev), dx, accumulate=True)
+    assert rel(dx - base.to(dev), xr.grad.permute(0, 2, 3, 1)) < 1e-5
+    dw = torch.zeros(C, 49, device=dev)
+    db = torch.zeros(C, device=dev)
+    K.dwconv7_bwd_weight(dz.to(dev), x.to(dev), dw=dw, db=db)
+    assert rel(dw, wr.grad.view(C, 49)) < 1e-5
+    assert rel(db, dz.double().sum((0, 1, 2))) < 1e-5
