@@ -81,6 +81,9 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int o = 0; o < TW; ++o) acc[r][o] = bias;
   float in[TC], nxt[TC];
+  float pcur[TW], pnew[TW];  // ACCUM: the old values of the next output row, loaded one row early
+#pragma unroll
+  for (int o = 0; o < TW; ++o) pcur[o] = pnew[o] = 0.f;
   load_row(nxt, x, g, b, h0 - 3, w0, c);
   // input rows in blocks of 7: inside a block, the accumulator slot of output row ir - kh is the
   // compile-time (u - kh) mod 7 (ib is a multiple of 7); sched_barrier keeps each row's loads one
@@ -94,6 +97,14 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int j = 0; j < TC; ++j) in[j] = nxt[j];
       if (ir + 1 < TR) load_row(nxt, x, g, b, h0 - 3 + ir + 1, w0, c);  // next row in flight
+      if (ACCUM && ir >= 5 && ir - 5 < TH) {
+        const int h = h0 + ir - 5;
+#pragma unroll
+        for (int o = 0; o < TW; ++o) {
+          const int w = w0 + o;
+          pnew[o] = (h < g.H && w < g.W) ? ld(out, (((size_t)b * g.H + h) * g.W + w) * g.C + c) : 0.f;
+        }
+      }
 #pragma unroll
       for (int kh = 0; kh < 7; ++kh) {
         const int orow = ir - kh;
@@ -114,7 +125,7 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
             const int w = w0 + o;
             if (w < g.W) {
               const size_t i = (((size_t)b * g.H + h) * g.W + w) * g.C + c;
-              const float v = ACCUM ? ld(out, i) + acc[sl][o] : acc[sl][o];
+              const float v = ACCUM ? pcur[o] + acc[sl][o] : acc[sl][o];
               st(out, i, v);
               if (out_bf16) out_bf16[i] = f2bf(v);
             }
@@ -122,6 +133,10 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
         }
 #pragma unroll
         for (int o = 0; o < TW; ++o) acc[sl][o] = bias;  // reused by output row orow + 7
+      }
+      if (ACCUM) {
+#pragma unroll
+        for (int o = 0; o < TW; ++o) pcur[o] = pnew[o];
       }
       __builtin_amdgcn_sched_barrier(0);
     }
