@@ -60,35 +60,36 @@ template <> __device__ __forceinline__ void st4<uint16_t>(uint16_t* p, size_t i,
 }
 
 // ---- GELU (erf form, = torch.nn.GELU() default) -----------------------------------------
-// Phi(x) = 0.5*erfc(-x/sqrt2) with the branch-free Chebyshev-fitted erfc of Numerical Recipes
-// (erfcc, |relative error| < 1.2e-7 everywhere): one v_exp, one v_rcp and ten FMAs, no divergent
-// ranges -- the GELU epilogues of the fc1/fc2 GEMMs run it on every element.
-__device__ __forceinline__ float phi_cdf(float x) {
+// Phi(x) = 1 - 0.5 erfc(|x|/sqrt2) (x >= 0), 0.5 erfc(|x|/sqrt2) (x < 0) with the Abramowitz-Stegun
+// 7.1.26 erfc: t = 1/(1 + 0.3275911 z), erfc(z) = t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) e^{-z^2},
+// |error of erf| <= 1.5e-7.  e^{-z^2} = e^{-x^2/2} is also the Gaussian density's exponential, so
+// GELU(x) = x Phi(x) and GELU'(x) = Phi(x) + x e^{-x^2/2}/sqrt(2 pi) cost ONE v_exp_f32, ONE v_rcp_f32
+// and ~14 FMA/MUL -- the fc1 epilogue evaluates both for every element of the 4C-wide hidden layer.
+struct GeluParts {
+  float phi, e;  // Phi(x), exp(-x^2/2)
+};
+__device__ __forceinline__ GeluParts gelu_parts(float x) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.0f + 0.5f * z);
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float r = t * __expf(fmaf(-z, z, p));  // erfc(|x|/sqrt2)
-  return x >= 0.f ? fmaf(-0.5f, r, 1.0f) : 0.5f * r;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float e = __builtin_amdgcn_exp2f(-(z * z) * 1.4426950408889634f);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float h = 0.5f * (p * t) * e;  // 0.5 erfc(z)
+  return {x >= 0.f ? 1.0f - h : h, e};
 }
-__device__ __forceinline__ float gelu_f(float x) { return x * phi_cdf(x); }
-// GELU and its derivative from one Phi evaluation (forward epilogue of fc1)
+__device__ __forceinline__ float phi_cdf(float x) { return gelu_parts(x).phi; }
+__device__ __forceinline__ float gelu_f(float x) { return x * gelu_parts(x).phi; }
+// GELU and its derivative from one evaluation (forward epilogue of fc1)
 __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
-  const float c = phi_cdf(x);
-  g = x * c;
-  dg = c + x * (0.39894228040143268f * __expf(-0.5f * x * x));
+  const GeluParts q = gelu_parts(x);
+  g = x * q.phi;
+  dg = fmaf(x, q.e * 0.39894228040143268f, q.phi);
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  // d/dx [x * Phi(x)] = Phi(x) + x * phi(x)
-  return phi_cdf(x) + x * (0.39894228040143268f * __expf(-0.5f * x * x));
+  const GeluParts q = gelu_parts(x);
+  return fmaf(x, q.e * 0.39894228040143268f, q.phi);
 }
 
 // ---- wave / block reductions (wave64) -------------------------------------------------

@@ -57,11 +57,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stages", default="S1,S2,S3,S4")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cases", default="", help="comma-separated case-name substrings to run")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     for st in args.stages.split(","):
         M, C = STAGES[st]
         for name, fl, fn in cases(M, C, dev):
+            if args.cases and not any(c in name for c in args.cases.split(",")):
+                continue
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
