@@ -331,8 +331,9 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     // epilogues (measured per ConvNeXt shape: tools/gemm_bench.py, profiles/)
     const bool heavy_epi = d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
                            d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
-    const bool use_v3 =
-        impl == 3 || (impl == 0 && (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048)));
+    static const bool slab_v3 = getenv("SV_WGRAD_V3") != nullptr;
+    const bool use_v3 = impl == 3 || (impl == 0 && (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048) ||
+                                                     (slab_v3 && d->epilogue == SV_EPI_SLAB)));
     const int rc = use_v3 ? launch_gemm3(d, s) : launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }

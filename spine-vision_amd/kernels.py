@@ -137,9 +137,12 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
                 a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16)
 
 
+_WGRAD_TARGET = int(__import__("os").environ.get("SV_WGRAD_TARGET", "512"))
+
+
 def _wgrad_split(tiles: int, K: int) -> int:
     """K slices so that tiles*split ~ 512 workgroups (2 per CU), each slice >= 16 k-steps."""
-    split = max(1, -(-512 // max(tiles, 1)))
+    split = max(1, -(-_WGRAD_TARGET // max(tiles, 1)))
     return max(1, min(split, K // 512 if K >= 512 else 1))
 
 

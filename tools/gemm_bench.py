@@ -50,6 +50,11 @@ def cases(M, C, dev):
         ("fc2_wgrad", fl, lambda: K.linear_wgrad(d, a)),
         ("fc2_wgrad+bias", fl, lambda: K.linear_wgrad(d, a, bias_out=b2, bias_accumulate=False)),
         ("fc1_wgrad", fl, lambda: K.linear_wgrad(dh, y)),
+        # calibration: the vendor library (hipBLASLt via torch.matmul) on the same shapes, plain store
+        ("torch_fc1_fwd", fl, lambda: torch.matmul(y, w1.t(), out=outh)),
+        ("torch_fc2_fwd", fl, lambda: torch.matmul(a, w2.t())),
+        ("torch_fc1_dgrad", fl, lambda: torch.matmul(dh, w1)),
+        ("torch_fc1_wgrad", fl, lambda: torch.matmul(dh.t(), y)),
     ]
 
 
