@@ -265,11 +265,10 @@ class ConvNeXtHip(nn.Module):
                     dsrc = d2
                     K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_MUL_AUX,
                                    a_scale_k=blk.gamma, aux=gh, compute_bf16=False)
-                cs = torch.empty(C, device=d.device, dtype=torch.float32)
-                G = K.linear_wgrad(dsrc, a, bias_out=cs, bias_accumulate=False, compute_bf16=bf)  # [C,4C] = d^T a
-                nv.call("sv_layerscale_wgrad_finish", nv.ptr(G), nv.ptr(cs), nv.ptr(blk.mlp.fc2.weight),
-                        nv.ptr(blk.gamma), nv.ptr(blk.mlp.fc2.bias), nv.ptr(g(blk.mlp.fc2.weight)),
-                        nv.ptr(g(blk.gamma)), nv.ptr(g(blk.mlp.fc2.bias)), C, 4 * C)
+                # dW2 = gamma (.) d^T a, dgamma = rowdot(W2, d^T a) + b2 (.) colsum(d), db2 = gamma (.) colsum(d)
+                K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(),
+                                   blk.mlp.fc2.bias.detach(), dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma),
+                                   db2=g(blk.mlp.fc2.bias), compute_bf16=bf)
                 # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM).
                 # bf16 mode: dy travels as bf16; dz stays f32 (the depthwise backward streams it with
                 # 4-byte lane loads, measured faster than 2-byte ones)

@@ -129,6 +129,235 @@ __global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const TDY* __restric
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Vectorised LayerNorm for C = 8 * LPR * NV with LPR in {16, 32, 64}: every lane owns NV runs of
+// 8 consecutive channels (one 16-B bf16 / two 16-B f32 accesses per run), a row is spread over LPR
+// lanes, a wave covers 64/LPR rows at once.  ConvNeXt-base's C = 128/256/512/1024 all fit; the
+// per-lane-channel kernels above serve the other widths (e.g. ConvNeXt-large's 192/384/768/1536).
+template <typename T>
+__device__ __forceinline__ void ld8v(const T* __restrict__ p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8v(T* __restrict__ p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(p) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
+}
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename TX, typename TY, int LPR, int NV>
+__global__ void __launch_bounds__(kLnThreads) ln_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w,
+                                                                const float* __restrict__ b, TY* __restrict__ y,
+                                                                float* __restrict__ mean, float* __restrict__ rstd,
+                                                                int64_t rows, int C, float eps) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, l = lane % LPR;
+  const int64_t r = ((int64_t)blockIdx.x * (kLnThreads / 64) + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool ok = r < rows;
+  const size_t base = (size_t)(ok ? r : 0) * C;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    ld8v(x + base + (size_t)(l + LPR * j) * 8, v[j]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[j][e];
+  }
+  const float invC = 1.0f / (float)C;
+  const float mu = group_sum<LPR>(s) * invC;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q += (v[j][e] - mu) * (v[j][e] - mu);
+  const float rs = rsqrtf(group_sum<LPR>(q) * invC + eps);
+  if (!ok) return;  // after the last shuffle
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (l + LPR * j) * 8;
+    float wv[8], bv[8], o[8];
+    ld8v(w + c, wv);
+    ld8v(b + c, bv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[j][e] - mu) * rs * wv[e] + bv[e];
+    st8v(y + base + c, o);
+  }
+  if (l == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+// backward: grid-stride over row groups with the next group's operands loaded before the current
+// one is reduced; dw/db partials per workgroup (lanes of one wave that hold the same channels are
+// folded with shuffles, the 4 waves through LDS, fixed order)
+template <typename TDY, typename TX, typename TDX, int LPR, int NV>
+__global__ void __launch_bounds__(kLnThreads) ln_bwd_vec_kernel(const TDY* __restrict__ dy, const TX* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ w, TDX* __restrict__ dx,
+                                                                int accumulate, float* __restrict__ dw_part,
+                                                                float* __restrict__ db_part, int64_t rows, int C) {
+  constexpr int RPW = 64 / LPR;
+  __shared__ float red[kLnThreads / 64][2][8 * LPR * NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l = lane % LPR, sub = lane / LPR;
+  const int64_t ngroups = (rows + RPW - 1) / RPW;
+  const int64_t nw = (int64_t)gridDim.x * (kLnThreads / 64);
+  const float invC = 1.0f / (float)C;
+  float wr[NV][8], adw[NV][8], adb[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    ld8v(w + (l + LPR * j) * 8, wr[j]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) adw[j][e] = adb[j][e] = 0.f;
+  }
+  float nd[NV][8], nx[NV][8], nmu = 0.f, nrs = 0.f;
+  auto load = [&](int64_t g) {
+    int64_t r = g * RPW + sub;
+    const bool ok = g < ngroups && r < rows;
+    if (!ok) r = 0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      ld8v(dy + (size_t)r * C + (l + LPR * j) * 8, nd[j]);
+      ld8v(x + (size_t)r * C + (l + LPR * j) * 8, nx[j]);
+      if (!ok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nd[j][e] = 0.f;  // contributes nothing to dw/db
+      }
+    }
+    nmu = mean[r];
+    nrs = rstd[r];
+  };
+  int64_t g = (int64_t)blockIdx.x * (kLnThreads / 64) + wid;
+  load(g);
+  for (; g < ngroups; g += nw) {
+    float d[NV][8], xh[NV][8];
+    const float mu = nmu, rs = nrs;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        d[j][e] = nd[j][e];
+        xh[j][e] = (nx[j][e] - mu) * rs;
+      }
+    load(g + nw);  // next group in flight while this one is reduced
+    const int64_t r = g * RPW + sub;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gg = d[j][e] * wr[j][e];
+        s1 += gg;
+        s2 += gg * xh[j][e];
+        adw[j][e] += d[j][e] * xh[j][e];
+        adb[j][e] += d[j][e];
+      }
+    s1 = group_sum<LPR>(s1) * invC;
+    s2 = group_sum<LPR>(s2) * invC;
+    if (r < rows) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        TDX* p = dx + (size_t)r * C + (l + LPR * j) * 8;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = rs * (d[j][e] * wr[j][e] - s1 - xh[j][e] * s2);
+        if (accumulate) {
+          float old[8];
+          ld8v(p, old);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += old[e];
+        }
+        st8v(p, o);
+      }
+    }
+  }
+  // fold the RPW row slots of this wave (lanes l, l+LPR, ... hold the same channels)
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        adw[j][e] += __shfl_xor(adw[j][e], o, 64);
+        adb[j][e] += __shfl_xor(adb[j][e], o, 64);
+      }
+  if (sub == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wid][0][(l + LPR * j) * 8 + e] = adw[j][e];
+        red[wid][1][(l + LPR * j) * 8 + e] = adb[j][e];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kLnThreads) {
+    float sw = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLnThreads / 64; ++k) {
+      sw += red[k][0][c];
+      sb += red[k][1][c];
+    }
+    dw_part[(size_t)blockIdx.x * C + c] = sw;
+    db_part[(size_t)blockIdx.x * C + c] = sb;
+  }
+}
+
+// fast-path geometry: C = 8 * LPR * NV, LPR in {16,32,64}, NV in {1,2,4}; returns LPR*16+NV or 0
+static int ln_vec_kind(int C) {
+  if (C % 8) return 0;
+  const int u = C / 8;
+  if (u == 16 || u == 32 || u == 64) return u * 16 + 1;
+  if (u == 128) return 64 * 16 + 2;
+  if (u == 256) return 64 * 16 + 4;
+  return 0;
+}
+#define SV_LNVEC_SWITCH(KIND, ...)                                           \
+  switch (KIND) {                                                            \
+    case 16 * 16 + 1: { constexpr int LPR = 16, NV = 1; __VA_ARGS__; } break; \
+    case 32 * 16 + 1: { constexpr int LPR = 32, NV = 1; __VA_ARGS__; } break; \
+    case 64 * 16 + 1: { constexpr int LPR = 64, NV = 1; __VA_ARGS__; } break; \
+    case 64 * 16 + 2: { constexpr int LPR = 64, NV = 2; __VA_ARGS__; } break; \
+    case 64 * 16 + 4: { constexpr int LPR = 64, NV = 4; __VA_ARGS__; } break; \
+    default: break;                                                          \
+  }
+static int ln_vec_fwd_grid(int64_t rows, int C) {
+  const int rpw = 64 / (C / 8 < 64 ? C / 8 : 64);
+  const int64_t waves = (rows + rpw - 1) / rpw;
+  return (int)((waves + kLnThreads / 64 - 1) / (kLnThreads / 64));
+}
+static int ln_vec_bwd_grid(int64_t rows, int C) {
+  const int rpw = 64 / (C / 8 < 64 ? C / 8 : 64);
+  const int64_t groups = (rows + rpw - 1) / rpw;
+  // ~8 row groups per wave: enough loop trip for the prefetch, partials stay small
+  int64_t g = (groups + 8 * (kLnThreads / 64) - 1) / (8 * (kLnThreads / 64));
+  if (g > 2048) g = 2048;
+  return (int)(g < 1 ? 1 : g);
+}
+
 static int ln_grid(int64_t rows) {
   const int64_t g = (rows + 3) / 4;
   return (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
@@ -431,51 +660,67 @@ __global__ void __launch_bounds__(kLnThreads) ds_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// Head: global average pool over HW, then LayerNorm over C.  One workgroup per image.
-__global__ void __launch_bounds__(kLnThreads) pool_ln_fwd_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ lnw,
-                                                                 const float* __restrict__ lnb,
-                                                                 float eps, float* __restrict__ pooled,
-                                                                 float* __restrict__ feat,
-                                                                 float* __restrict__ mean,
-                                                                 float* __restrict__ rstd, int HW,
-                                                                 int C) {
+// Head: global average pool over HW, then LayerNorm over C.
+//   pool_sum_kernel   grid (C/64, B): 4 waves split the HW rows of one 64-channel group of one
+//                     image (256-B coalesced row reads, 8 in flight per lane), LDS fold -> pooled
+//   pool_norm_kernel  grid B: LayerNorm of the pooled [C] vector
+//   pool_bwd_kernel   grid (HW/kPoolRows, B): every workgroup re-derives the [C] input gradient of
+//                     its image (two block sums over C, cheap) and broadcasts it over its rows
+constexpr int kPoolRows = 16;
+
+__global__ void __launch_bounds__(kLnThreads) pool_sum_kernel(const float* __restrict__ x, float* __restrict__ pooled,
+                                                              int HW, int C) {
+  __shared__ float red[kLnThreads / 64][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b = blockIdx.y, c = blockIdx.x * 64 + lane;
+  const float* xb = x + (size_t)b * HW * C + c;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int p = wid;
+  for (; p + 28 < HW; p += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += xb[(size_t)(p + 4 * u) * C];
+  }
+  for (; p < HW; p += 4) acc[0] += xb[(size_t)p * C];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += acc[u];
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0) pooled[(size_t)b * C + c] = (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]) / (float)HW;
+}
+
+__global__ void __launch_bounds__(kLnThreads) pool_norm_kernel(const float* __restrict__ pooled,
+                                                               const float* __restrict__ lnw,
+                                                               const float* __restrict__ lnb, float eps,
+                                                               float* __restrict__ feat, float* __restrict__ mean,
+                                                               float* __restrict__ rstd, int C) {
   __shared__ float red[kLnThreads / 64];
   const int b = blockIdx.x;
-  const float* xb = x + (size_t)b * HW * C;
-  const float invHW = 1.0f / (float)HW, invC = 1.0f / (float)C;
+  const float* pb = pooled + (size_t)b * C;
+  const float invC = 1.0f / (float)C;
   float s = 0.f;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f;
-    for (int p = 0; p < HW; ++p) a += xb[(size_t)p * C + c];
-    a *= invHW;
-    pooled[(size_t)b * C + c] = a;
-    s += a;
-  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) s += pb[c];
   const float mu = block_sum(s, red) * invC;
   float q = 0.f;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float d = pooled[(size_t)b * C + c] - mu;
-    q += d * d;
-  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) q += (pb[c] - mu) * (pb[c] - mu);
   const float rs = rsqrtf(block_sum(q, red) * invC + eps);
-  for (int c = threadIdx.x; c < C; c += blockDim.x)
-    feat[(size_t)b * C + c] = (pooled[(size_t)b * C + c] - mu) * rs * lnw[c] + lnb[c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) feat[(size_t)b * C + c] = (pb[c] - mu) * rs * lnw[c] + lnb[c];
   if (threadIdx.x == 0) {
     mean[b] = mu;
     rstd[b] = rs;
   }
 }
 
-__global__ void __launch_bounds__(kLnThreads) pool_ln_bwd_kernel(
+__global__ void __launch_bounds__(kLnThreads) pool_bwd_kernel(
     const float* __restrict__ dfeat, const float* __restrict__ pooled, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ lnw, float* __restrict__ dx,
     uint16_t* __restrict__ dx_bf16, float* __restrict__ dlnw_part, float* __restrict__ dlnb_part, int HW, int C) {
   __shared__ float red[kLnThreads / 64];
   extern __shared__ __attribute__((aligned(16))) float dp[];  // [C]
-  const int b = blockIdx.x;
+  const int b = blockIdx.y;
   const float mu = mean[b], rs = rstd[b];
   const float invC = 1.0f / (float)C, invHW = 1.0f / (float)HW;
+  const bool first = blockIdx.x == 0;
   float s1 = 0.f, s2 = 0.f;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float d = dfeat[(size_t)b * C + c];
@@ -483,8 +728,10 @@ __global__ void __launch_bounds__(kLnThreads) pool_ln_bwd_kernel(
     const float g = d * lnw[c];
     s1 += g;
     s2 += g * xh;
-    dlnw_part[(size_t)b * C + c] = d * xh;
-    dlnb_part[(size_t)b * C + c] = d;
+    if (first) {
+      dlnw_part[(size_t)b * C + c] = d * xh;
+      dlnb_part[(size_t)b * C + c] = d;
+    }
   }
   s1 = block_sum(s1, red) * invC;
   s2 = block_sum(s2, red) * invC;
@@ -494,11 +741,15 @@ __global__ void __launch_bounds__(kLnThreads) pool_ln_bwd_kernel(
     dp[c] = rs * (g - s1 - xh * s2) * invHW;
   }
   __syncthreads();
-  float* dxb = dx + (size_t)b * HW * C;
-  uint16_t* dbb = dx_bf16 ? dx_bf16 + (size_t)b * HW * C : nullptr;
-  for (size_t i = threadIdx.x; i < (size_t)HW * C; i += blockDim.x) {
-    dxb[i] = dp[i % C];
-    if (dbb) dbb[i] = f2bf(dp[i % C]);
+  const int p0 = blockIdx.x * kPoolRows;
+  const int p1 = p0 + kPoolRows < HW ? p0 + kPoolRows : HW;
+  const size_t base = ((size_t)b * HW + p0) * C;
+  const size_t n4 = (size_t)(p1 - p0) * C / 4;  // C % 4 == 0
+  for (size_t i = threadIdx.x; i < n4; i += blockDim.x) {
+    const int c = (int)((i * 4) % C);
+    const float4 v = *reinterpret_cast<const float4*>(dp + c);
+    *reinterpret_cast<float4*>(dx + base + i * 4) = v;
+    if (dx_bf16) st4(dx_bf16, base + i * 4, v);
   }
 }
 
@@ -512,10 +763,23 @@ int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float
                      int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C, float eps,
                      sv_stream_t stream) {
   SV_REQUIRE(x && w && b && y && mean && rstd, "sv_layernorm_fwd: null pointer");
-  SV_REQUIRE(cpl_ok(C), "sv_layernorm_fwd: C=%d must be 64*{1,2,3,4,6,8,12,16,24}", C);
+  SV_REQUIRE(ln_vec_kind(C) || cpl_ok(C), "sv_layernorm_fwd: C=%d must be 64*{1,2,3,4,6,8,12,16,24} or 2048", C);
   if (rows <= 0) return SV_OK;
-  const int grid = ln_grid(rows);
   hipStream_t s = (hipStream_t)stream;
+  if (const int kind = ln_vec_kind(C)) {
+    const int vg = ln_vec_fwd_grid(rows, C);
+#define LAUNCHV(TX, TY)                                                                                    \
+  SV_LNVEC_SWITCH(kind, ln_fwd_vec_kernel<TX, TY, LPR, NV><<<vg, kLnThreads, 0, s>>>((const TX*)x, w, b, (TY*)y, \
+                                                                                      mean, rstd, rows, C, eps))
+    if (x_dtype == SV_F32 && y_dtype == SV_F32) { LAUNCHV(float, float); }
+    else if (x_dtype == SV_F32 && y_dtype == SV_BF16) { LAUNCHV(float, uint16_t); }
+    else if (x_dtype == SV_BF16 && y_dtype == SV_F32) { LAUNCHV(uint16_t, float); }
+    else if (x_dtype == SV_BF16 && y_dtype == SV_BF16) { LAUNCHV(uint16_t, uint16_t); }
+    else return set_error(SV_ERR_INVALID_ARG, "sv_layernorm_fwd: bad dtype");
+#undef LAUNCHV
+    return check_launch("sv_layernorm_fwd");
+  }
+  const int grid = ln_grid(rows);
 #define LAUNCH(TX, TY)                                                                            \
   SV_CPL_SWITCH(C / 64, ln_fwd_kernel<TX, TY, CPL><<<grid, kLnThreads, 0, s>>>(                  \
                             (const TX*)x, w, b, (TY*)y, mean, rstd, rows, C, eps))
@@ -528,16 +792,33 @@ int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float
   return check_launch("sv_layernorm_fwd");
 }
 
-int sv_layernorm_bwd_nparts(int64_t rows, int32_t C) { (void)C; return ln_grid(rows); }
+int sv_layernorm_bwd_nparts(int64_t rows, int32_t C) {
+  return ln_vec_kind(C) ? ln_vec_bwd_grid(rows, C) : ln_grid(rows);
+}
 
 int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_dtype, const float* mean,
                      const float* rstd, const float* w, void* dx, int32_t dx_dtype, int32_t accumulate,
                      float* dw_part, float* db_part, int64_t rows, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dy && x && mean && rstd && w && dx && dw_part && db_part, "sv_layernorm_bwd: null pointer");
-  SV_REQUIRE(cpl_ok(C) && C <= 2048, "sv_layernorm_bwd: C=%d unsupported", C);
+  SV_REQUIRE(ln_vec_kind(C) || (cpl_ok(C) && C <= 2048), "sv_layernorm_bwd: C=%d unsupported", C);
   if (rows <= 0) return SV_OK;
-  const int grid = ln_grid(rows);
   hipStream_t s = (hipStream_t)stream;
+  if (const int kind = ln_vec_kind(C)) {
+    const int vg = ln_vec_bwd_grid(rows, C);
+#define LNBV(TDY, TX, TDX)                                                                                  \
+  SV_LNVEC_SWITCH(kind, ln_bwd_vec_kernel<TDY, TX, TDX, LPR, NV><<<vg, kLnThreads, 0, s>>>(                 \
+                            (const TDY*)dy, (const TX*)x, mean, rstd, w, (TDX*)dx, accumulate, dw_part, db_part, \
+                            rows, C))
+    if (dy_dtype == SV_F32 && x_dtype == SV_F32 && dx_dtype == SV_F32) { LNBV(float, float, float); }
+    else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_F32) { LNBV(float, uint16_t, float); }
+    else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_F32) { LNBV(uint16_t, uint16_t, float); }
+    else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) { LNBV(uint16_t, uint16_t, uint16_t); }
+    else return set_error(SV_ERR_UNSUPPORTED, "sv_layernorm_bwd: dtype combination (dy %d, x %d, dx %d) unsupported",
+                          dy_dtype, x_dtype, dx_dtype);
+#undef LNBV
+    return check_launch("sv_layernorm_bwd");
+  }
+  const int grid = ln_grid(rows);
 #define LNB(TDY, TX, TDX)                                                                              \
   SV_CPL_SWITCH(C / 64, ln_bwd_kernel<TDY, TX, TDX, CPL><<<grid, kLnThreads, 0, s>>>(                 \
                             (const TDY*)dy, (const TX*)x, mean, rstd, w, (TDX*)dx, accumulate, dw_part, \
@@ -666,9 +947,11 @@ int sv_pool_ln_fwd(const float* x, const float* lnw, const float* lnb, float eps
                    float* feat, float* mean, float* rstd, int32_t B, int32_t HW, int32_t C,
                    sv_stream_t stream) {
   SV_REQUIRE(x && lnw && lnb && pooled && feat && mean && rstd, "sv_pool_ln_fwd: null pointer");
+  SV_REQUIRE(C % 64 == 0, "sv_pool_ln_fwd: C=%d must be a multiple of 64", C);
   if (B <= 0) return SV_OK;
-  pool_ln_fwd_kernel<<<B, kLnThreads, 0, (hipStream_t)stream>>>(x, lnw, lnb, eps, pooled, feat, mean,
-                                                                 rstd, HW, C);
+  hipStream_t s = (hipStream_t)stream;
+  pool_sum_kernel<<<dim3(C / 64, B), kLnThreads, 0, s>>>(x, pooled, HW, C);
+  pool_norm_kernel<<<B, kLnThreads, 0, s>>>(pooled, lnw, lnb, eps, feat, mean, rstd, C);
   return check_launch("sv_pool_ln_fwd");
 }
 
@@ -677,8 +960,9 @@ int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, c
                    int32_t HW, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dfeat && pooled && mean && rstd && lnw && dx && dlnw_part && dlnb_part,
              "sv_pool_ln_bwd: null pointer");
+  SV_REQUIRE(C % 4 == 0, "sv_pool_ln_bwd: C=%d must be a multiple of 4", C);
   if (B <= 0) return SV_OK;
-  pool_ln_bwd_kernel<<<B, kLnThreads, C * sizeof(float), (hipStream_t)stream>>>(
+  pool_bwd_kernel<<<dim3(ceil_div(HW, kPoolRows), B), kLnThreads, C * sizeof(float), (hipStream_t)stream>>>(
       dfeat, pooled, mean, rstd, lnw, dx, dx_bf16, dlnw_part, dlnb_part, HW, C);
   return check_launch("sv_pool_ln_bwd");
 }

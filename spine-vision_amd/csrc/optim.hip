@@ -153,6 +153,88 @@ __global__ void __launch_bounds__(kThreads) layerscale_finish_kernel(
   }
 }
 
+
+// fc2 wgrad split-K reduction fused with the layer-scale finish (replaces reduce_pair + finish):
+// workgroup `blk` < blocks_a sums the P slabs of 64 consecutive columns of one row c of G (K4 % 64
+// == 0), writes dW2 += gamma_c G and a partial row dot sum(W2 G) -> dot_part[blk]; the remaining
+// workgroups reduce the P colsum partials into cs_out.  layerscale_final folds the dots.
+__global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float* __restrict__ slab,
+                                                                     const float* __restrict__ cs_part, int P,
+                                                                     const float* __restrict__ W2,
+                                                                     const float* __restrict__ gamma,
+                                                                     float* __restrict__ dW2,
+                                                                     float* __restrict__ dot_part,
+                                                                     float* __restrict__ cs_out, int64_t nA, int K4,
+                                                                     int C, int64_t blocks_a) {
+  __shared__ float4 red[16][16];
+  const int c4 = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const bool seg_b = blockIdx.x >= blocks_a;
+  const int64_t blk = seg_b ? blockIdx.x - blocks_a : blockIdx.x;
+  const int64_t col = blk * 64 + c4 * 4;
+  const int64_t n = seg_b ? C : nA;
+  const float* part = seg_b ? cs_part : slab;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col + 4 <= n) {
+    int p = pg;
+    for (; p + 48 < P; p += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (size_t)(p + 16 * u) * n + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * n + col);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  } else if (col < n) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = pg; p < P; p += 16)
+      for (int j = 0; j < 4 && col + j < n; ++j) t[j] += part[(size_t)p * n + col + j];
+    acc = make_float4(t[0], t[1], t[2], t[3]);
+  }
+  red[pg][c4] = acc;
+  __syncthreads();
+  if (threadIdx.x >= 16) return;
+  float4 s = red[0][c4];
+#pragma unroll
+  for (int g = 1; g < 16; ++g) {
+    const float4 v = red[g][c4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  if (seg_b) {
+    const float r[4] = {s.x, s.y, s.z, s.w};
+    for (int j = 0; j < 4 && col + j < n; ++j) cs_out[col + j] = r[j];
+    return;
+  }
+  const int c = (int)(col / K4);
+  const float gc = gamma[c];
+  const float4 w = *reinterpret_cast<const float4*>(W2 + col);
+  float4 o = *reinterpret_cast<const float4*>(dW2 + col);
+  o.x += gc * s.x; o.y += gc * s.y; o.z += gc * s.z; o.w += gc * s.w;
+  *reinterpret_cast<float4*>(dW2 + col) = o;
+  float d = w.x * s.x + w.y * s.y + w.z * s.z + w.w * s.w;
+#pragma unroll
+  for (int o2 = 8; o2 > 0; o2 >>= 1) d += __shfl_xor(d, o2, 16);
+  if (c4 == 0) dot_part[blk] = d;
+}
+
+__global__ void __launch_bounds__(kThreads) layerscale_final_kernel(const float* __restrict__ dot_part,
+                                                                    const float* __restrict__ cs,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ b2,
+                                                                    float* __restrict__ dgamma, float* __restrict__ db2,
+                                                                    int C, int nb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int j = 0; j < nb; ++j) s += dot_part[(size_t)c * nb + j];
+  dgamma[c] += s + b2[c] * cs[c];
+  db2[c] += gamma[c] * cs[c];
+}
+
 constexpr int kSqBlocks = 1024;
 
 __global__ void __launch_bounds__(kThreads) sqnorm_kernel(const float* __restrict__ g, int64_t n,
@@ -313,6 +395,28 @@ int sv_layerscale_wgrad_finish(const float* G, const float* cs, const float* W2,
   layerscale_finish_kernel<<<ceil_div(C, kThreads / 64), kThreads, 0, (hipStream_t)stream>>>(
       G, cs, W2, gamma, b2, dW2, dgamma, db2, C, K4);
   return check_launch("sv_layerscale_wgrad_finish");
+}
+
+int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4) { return C * (K4 / 64) + C; }
+
+int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t P, const float* W2,
+                               const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2,
+                               float* ws, int32_t C, int32_t K4, sv_stream_t stream) {
+  SV_REQUIRE(slab && cs_part && W2 && gamma && b2 && dW2 && dgamma && db2 && ws && P >= 1,
+             "sv_layerscale_wgrad_reduce: bad arguments");
+  SV_REQUIRE(K4 % 64 == 0 && C > 0, "sv_layerscale_wgrad_reduce: K4=%d must be a multiple of 64", K4);
+  SV_REQUIRE((((uintptr_t)slab | (uintptr_t)cs_part | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
+             "sv_layerscale_wgrad_reduce: buffers must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nA = (int64_t)C * K4;
+  const int64_t ba = nA / 64, bb = (C + 63) / 64;
+  float* dot_part = ws;
+  float* cs = ws + (size_t)C * (K4 / 64);
+  layerscale_reduce_kernel<<<(unsigned)(ba + bb), kThreads, 0, s>>>(slab, cs_part, P, W2, gamma, dW2, dot_part, cs,
+                                                                  nA, K4, C, ba);
+  layerscale_final_kernel<<<ceil_div(C, kThreads), kThreads, 0, s>>>(dot_part, cs, gamma, b2, dgamma, db2, C,
+                                                                   K4 / 64);
+  return check_launch("sv_layerscale_wgrad_reduce");
 }
 
 int sv_sqnorm_nparts(int64_t n) {

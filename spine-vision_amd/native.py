@@ -78,6 +78,8 @@ _SIGS = {
     "sv_colsum_nparts": [_i64, _i32],
     "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
+    "sv_layerscale_wgrad_reduce_ws": [_i32, _i32],
+    "sv_layerscale_wgrad_reduce": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_sqnorm_nparts": [_i64],
     "sv_sqnorm_partial": [_p, _i64, _p, _p],
     "sv_clip_coef": [_p, _i32, _f32, _p, _p],
@@ -108,7 +110,7 @@ _SIGS = {
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith("_nparts")} | {"sv_version", "sv_conv_bwd_weight_work_floats"}
+_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats"}
 
 _lib = None
 _lock = threading.Lock()

@@ -149,13 +149,14 @@ def test_reduce_partials_deep(dev):
 
 
 # ---------------------------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("C", [128, 192, 512, 1024])
-def test_layernorm_fwd_bwd(dev, C):
-    g = torch.Generator().manual_seed(C)
-    x = torch.randn(333, C, generator=g) * 2 + 0.5
+@pytest.mark.parametrize("C,rows", [(128, 333), (128, 9001), (192, 333), (256, 333), (512, 333), (512, 9001),
+                                    (1024, 333), (2048, 77)])
+def test_layernorm_fwd_bwd(dev, C, rows):
+    g = torch.Generator().manual_seed(C + rows)
+    x = torch.randn(rows, C, generator=g) * 2 + 0.5
     w = torch.rand(C, generator=g) + 0.5
     b = torch.randn(C, generator=g)
-    dy = torch.randn(333, C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
     y, mean, rstd = K.layernorm_fwd(x.to(dev), w.to(dev), b.to(dev), out_dtype=torch.float32)
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
@@ -271,9 +272,10 @@ def test_scale_rows_bf16(dev):
     assert torch.equal(out.cpu(), (W * sc[:, None]).to(torch.bfloat16))
 
 
-def test_pool_ln(dev):
+@pytest.mark.parametrize("shape", [(3, 4, 5, 1024), (2, 16, 16, 512)])
+def test_pool_ln(dev, shape):
     g = torch.Generator().manual_seed(5)
-    B, H, W, C = 3, 4, 5, 1024
+    B, H, W, C = shape
     x = torch.randn(B, H, W, C, generator=g)
     lnw = torch.rand(C, generator=g) + 0.5
     lnb = torch.randn(C, generator=g) * 0.1
@@ -363,3 +365,29 @@ def test_dwconv7_bwd_bf16_dz(dev, shape):
     K.dwconv7_bwd_weight(dz.to(dev), x.to(dev), dw=dw, db=db)
     assert rel(dw, wr.grad.view(C, 49)) < 1e-5
     assert rel(db, dz.double().sum((0, 1, 2))) < 1e-5
+
+
+# ------------------------------------------------- fc2 wgrad + layer-scale finish (fused reduce)
+@pytest.mark.parametrize("M,C,compute_bf16", [(4096, 128, True), (2048, 192, False), (1024, 512, True)])
+def test_layerscale_wgrad_fused(dev, M, C, compute_bf16):
+    g = torch.Generator().manual_seed(M + C)
+    d = torch.randn(M, C, generator=g)
+    a = torch.randn(M, 4 * C, generator=g)
+    w2 = torch.randn(C, 4 * C, generator=g) * 0.05
+    gam = torch.rand(C, generator=g) + 0.1
+    b2 = torch.randn(C, generator=g) * 0.1
+    base = [torch.randn(C, 4 * C, generator=g), torch.randn(C, generator=g), torch.randn(C, generator=g)]
+    dt_ = torch.bfloat16 if compute_bf16 else torch.float32
+    dq, aq = d.to(dt_), a.to(dt_)
+    G = dq.double().t() @ aq.double()
+    cs = dq.double().sum(0)
+    ref_w = base[0].double() + gam.double()[:, None] * G
+    ref_g = base[1].double() + (w2.double() * G).sum(1) + b2.double() * cs
+    ref_b = base[2].double() + gam.double() * cs
+    dw2, dgam, db2 = (t.clone().to(dev) for t in base)
+    K.layerscale_wgrad(dq.to(dev), aq.to(dev), w2.to(dev), gam.to(dev), b2.to(dev), dw2=dw2, dgamma=dgam, db2=db2,
+                       compute_bf16=compute_bf16)
+    tol = 1e-4 if compute_bf16 else 1e-5
+    assert rel(dw2, ref_w) < tol
+    assert rel(dgam, ref_g) < tol
+    assert rel(db2, ref_b) < tol

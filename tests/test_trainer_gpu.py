@@ -52,10 +52,10 @@ def test_classification_step_matches_oracle(dev):
     """One full ClassificationTrainer step (ResNet-50, 3 heads, fp32 parity mode) against the CPU
     oracle step (pinned to the reference by tests/golden/classification_resnet50_64.npz): loss and
     gradient norm within 1e-3; every clipped parameter gradient against the oracle run in float64,
-    within max(1e-3, 3x the fp32 oracle's own error) -- at B=4, 64x64 the train-mode BatchNorm of
-    layer4 normalises over 16 values per channel and some gradients are ill-conditioned (the fp32 CPU
-    oracle itself is up to 4e-2 away from float64 on them); the AdamW update bound (2 lr) and the BN
-    running statistics."""
+    within max(1e-3, 3x the fp32 oracle's own error); the AdamW update bound (2 lr) and the BN running
+    statistics.  Input 128x128 (B=4): the train-mode BatchNorm of layer4 then normalises over 64 values
+    per channel -- at 64x64 it sees 16 and its gamma gradient is so ill-conditioned that two fp32
+    summation orders (CPU oracle vs HIP) land 3e-3 and 1.4e-2 away from float64."""
     import copy
 
     from oracle import heads as oh
@@ -73,7 +73,7 @@ def test_classification_step_matches_oracle(dev):
     o64 = copy.deepcopy(ora).double().train()
     m = m.to(dev).train()
     ora.train()
-    img, targets = ow.classification_batch(4, 64, 64)
+    img, targets = ow.classification_batch(4, 128, 128)
     lr = 1e-4
     before = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     eng = StepEngine(m, dev, lr=lr, weight_decay=1e-5, grad_clip=1.0)

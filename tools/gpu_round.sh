@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 STEPS=${STEPS:-10}
 ROOTDIR=$(pwd)
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/tests.log" 2>&1
   rc=$?; echo "tests rc=$rc" | tee -a "$OUT/status"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
