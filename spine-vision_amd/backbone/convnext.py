@@ -270,15 +270,15 @@ class ConvNeXtHip(nn.Module):
                                    blk.mlp.fc2.bias.detach(), dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma),
                                    db2=g(blk.mlp.fc2.bias), compute_bf16=bf)
                 # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM).
-                # bf16 mode: dy travels as bf16; dz stays f32 (the depthwise backward streams it with
-                # 4-byte lane loads, measured faster than 2-byte ones)
+                # bf16 mode: dy and dz travel as bf16 (the depthwise backward reads dz through its LDS-DMA
+                # ring, where 2-byte columns cost no more than 4-byte ones)
                 dy = torch.empty(M, C, device=d.device, dtype=act)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
                 K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
                                compute_bf16=bf)
                 # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
                 dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
-                                     db=g(blk.norm.bias))
+                                     db=g(blk.norm.bias), out_dtype=act)
                 dz4 = dz.view(B, H, W, C)
                 K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
                 K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)

@@ -221,11 +221,299 @@ __global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ring variants (default): the same per-wave strip streaming, but the input rows arrive through a
+// wave-private LDS ring filled by LDS-DMA (global_load_lds, one 64-lane column per instruction)
+// PF-1 rows ahead of the row being consumed; the prefetch costs no VGPRs.  Everything except the
+// channel is wave-uniform, so the strip geometry lives in SGPRs (readfirstlane'd wave id) and every
+// global address is an SGPR base + the lane's channel offset: the per-row address arithmetic and the
+// bounds checks run on the scalar unit.  Padding costs nothing in the FMA stream: an out-of-image
+// column or row is DMA'd from a zero page, so the consumer reads LDS unconditionally.  No barriers:
+// each wave only reads rows its own DMA wrote, ordered by a counted `s_waitcnt vmcnt` (the DMA rows
+// issued after row ir may stay in flight; stores and loads interleaved with them only make the wait
+// conservative).
+typedef __attribute__((address_space(3))) void dw_lds_void;
+
+__device__ __attribute__((aligned(256))) float dw_zero_page[64];  // zero-initialised, never written
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until only the DMA rows issued after the current one (`younger` rows of NL instructions) may
+// still be outstanding
+template <int PF, int NL>
+__device__ __forceinline__ void wait_rows(int younger) {
+  static_assert((PF - 1) * NL <= 63, "vmcnt immediate");
+  if (PF > 3 && younger >= 3) vm_wait<(PF > 3 ? 3 * NL : 0)>();
+  else if (PF > 2 && younger >= 2) vm_wait<(PF > 2 ? 2 * NL : 0)>();
+  else if (younger >= 1) vm_wait<NL>();
+  else vm_wait<0>();
+}
+
+__device__ __forceinline__ int wave_id_uniform() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Column offsets of a strip (uniform, computed once): colo[j] = (wstart + j) * C, or -1 when the
+// column lies outside the image.
+template <int NCOL>
+__device__ __forceinline__ void dw_cols(const DwGeo& g, int wstart, int (&colo)[NCOL]) {
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) {
+    const int w = wstart + j;
+    colo[j] = (w >= 0 && w < g.W) ? w * g.C : -1;
+  }
+}
+
+// DMA NCOL columns of row h of the wave's 64-channel group into dst (one dword per lane per
+// column: LDS-DMA writes M0 + 4*lane whatever the load size, a bf16 lands zero-extended in the low
+// half).  xg = x + c0 (uniform); out-of-image columns/rows read the zero page.  Per column: one
+// scalar add + select for the address, one M0 write, one DMA.
+template <int NCOL, typename T>
+__device__ __forceinline__ void dma_row(const T* __restrict__ xg, const DwGeo& g, int b, int h, const int (&colo)[NCOL],
+                                        int lane, char* dst) {
+  const bool okh = h >= 0 && h < g.H;
+  const T* rowp = xg + (size_t)((b * g.H + (okh ? h : 0)) * g.W) * g.C;
+  const T* zero = reinterpret_cast<const T*>(dw_zero_page);
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) {
+    const T* src = (okh && colo[j] >= 0) ? rowp + colo[j] : zero;
+    if constexpr (sizeof(T) == 4)
+      __builtin_amdgcn_global_load_lds((const void*)(src + lane), (dw_lds_void*)(dst + j * 256), 4, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(src + lane), (dw_lds_void*)(dst + j * 256), 2, 0, 0);
+  }
+}
+template <typename T>
+__device__ __forceinline__ float lds_ld(const char* col, int lane) {
+  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const float*>(col + lane * 4);
+  else return bf2f(*reinterpret_cast<const uint16_t*>(col + lane * 4));
+}
+
+template <int PF, int TW, typename TIN>
+constexpr size_t dw_ring_lds() {
+  return (size_t)(kDwThreads / 64) * PF * (TW + 6) * 256;
+}
+
+template <int PF, int TW, typename TIN, typename TOUT, bool FLIP, bool ACCUM>
+__global__ void __launch_bounds__(kDwThreads) dwconv7_ring_kernel(const TIN* __restrict__ x,
+                                                                  const float* __restrict__ wdw,
+                                                                  const float* __restrict__ bdw,
+                                                                  TOUT* __restrict__ out,
+                                                                  uint16_t* __restrict__ out_bf16, DwGeo g) {
+  extern __shared__ __attribute__((aligned(16))) char dw_smem[];
+  constexpr int TC = TW + 6;
+  constexpr int ROWB = TC * 256;
+  const int lane = threadIdx.x & 63, wv = wave_id_uniform();
+  const int gw = blockIdx.x * (kDwThreads / 64) + wv;
+  const int ncg = g.C / 64;
+  if (gw >= g.ntiles * ncg) return;  // whole wave; no barriers below
+  char* ring = dw_smem + wv * PF * ROWB;
+  const int tile = gw % g.ntiles, c0 = (gw / g.ntiles) * 64, c = c0 + lane;
+  int b, h0, w0;
+  dw_tile(g, tile, b, h0, w0);
+  const TIN* xg = x + c0;
+  TOUT* og = out + c0;
+  uint16_t* obg = out_bf16 ? out_bf16 + c0 : nullptr;
+  float wk[49];
+#pragma unroll
+  for (int i = 0; i < 49; ++i) wk[i] = wdw[(size_t)c * 49 + (FLIP ? 48 - i : i)];
+  const float bias = bdw ? bdw[c] : 0.f;
+  float acc[7][TW];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int o = 0; o < TW; ++o) acc[r][o] = bias;
+  float in[TC];
+  float pcur[TW], pnew[TW];
+#pragma unroll
+  for (int o = 0; o < TW; ++o) pcur[o] = pnew[o] = 0.f;
+  int colo[TC];
+  dw_cols(g, w0 - 3, colo);
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) dma_row<TC>(xg, g, b, h0 - 3 + p, colo, lane, ring + p * ROWB);
+#pragma nounroll
+  for (int ib = 0; ib < TR; ib += 7) {
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      const int ir = ib + u;
+      if (ir >= TR) break;
+      if (ir + PF - 1 < TR) dma_row<TC>(xg, g, b, h0 - 3 + ir + PF - 1, colo, lane, ring + ((ir + PF - 1) % PF) * ROWB);
+      const int rem = TR - 1 - ir;
+      wait_rows<PF, TC>(rem < PF - 1 ? rem : PF - 1);
+      const char* row = ring + (ir % PF) * ROWB;
+#pragma unroll
+      for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row + j * 256, lane);
+      if (ACCUM && ir >= 5 && ir - 5 < TH) {
+        const int h = h0 + ir - 5;
+        if (h < g.H) {
+          const TOUT* prow = og + ((size_t)b * g.H + h) * g.W * g.C;
+#pragma unroll
+          for (int o = 0; o < TW; ++o) pnew[o] = (w0 + o < g.W) ? ld(prow + (size_t)(w0 + o) * g.C, lane) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int kh = 0; kh < 7; ++kh) {
+        const int orow = ir - kh;
+        if (orow < 0 || orow >= TH) continue;
+        const int sl = (u - kh + 7) % 7;
+#pragma unroll
+        for (int o = 0; o < TW; ++o)
+#pragma unroll
+          for (int kw = 0; kw < 7; ++kw) acc[sl][o] = fmaf(wk[kh * 7 + kw], in[o + kw], acc[sl][o]);
+      }
+      if (ir >= 6) {
+        const int orow = ir - 6;
+        const int sl = (u + 1) % 7;
+        const int h = h0 + orow;
+        if (h < g.H) {
+          const size_t rbase = ((size_t)b * g.H + h) * g.W;
+#pragma unroll
+          for (int o = 0; o < TW; ++o) {
+            if (w0 + o < g.W) {
+              const size_t i = (rbase + w0 + o) * g.C;
+              const float v = ACCUM ? pcur[o] + acc[sl][o] : acc[sl][o];
+              st(og + i, lane, v);
+              if (obg) obg[i + lane] = f2bf(v);
+            }
+          }
+        }
+#pragma unroll
+        for (int o = 0; o < TW; ++o) acc[sl][o] = bias;
+      }
+      if (ACCUM) {
+#pragma unroll
+        for (int o = 0; o < TW; ++o) pcur[o] = pnew[o];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// backward-weight with the ring: per input row ir the wave DMAs the TC-wide x row h0-3+ir and the
+// TW-wide dz row h0+ir (rows past the strip's TH read the zero page, which keeps the per-row
+// instruction count fixed and contributes nothing)
+template <int PF, int TW, typename TDZ, typename TIN>
+constexpr size_t dw_wgrad_ring_lds() {
+  return (size_t)(kDwThreads / 64) * PF * (2 * TW + 6) * 256;
+}
+
+template <int PF, int TW, typename TDZ, typename TIN>
+__global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TDZ* __restrict__ dz,
+                                                                        const TIN* __restrict__ x,
+                                                                        float* __restrict__ dw_part,
+                                                                        float* __restrict__ db_part, DwGeo g) {
+  extern __shared__ __attribute__((aligned(16))) char dw_smem[];
+  constexpr int TC = TW + 6;
+  constexpr int ROWB = (TC + TW) * 256;
+  const int lane = threadIdx.x & 63, wv = wave_id_uniform();
+  const int c0 = blockIdx.y * 64, c = c0 + lane;
+  const TIN* xg = x + c0;
+  const TDZ* dg = dz + c0;
+  char* ring = dw_smem + wv * PF * ROWB;
+  float acc[49];
+#pragma unroll
+  for (int i = 0; i < 49; ++i) acc[i] = 0.f;
+  float dbacc = 0.f;
+  for (int tile = blockIdx.x * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
+    int b, h0, w0;
+    dw_tile(g, tile, b, h0, w0);
+    int colx[TC], cold[TW];
+    dw_cols(g, w0 - 3, colx);
+    dw_cols(g, w0, cold);
+    auto issue = [&](int ir) {
+      char* slot = ring + (ir % PF) * ROWB;
+      dma_row<TC>(xg, g, b, h0 - 3 + ir, colx, lane, slot);
+      dma_row<TW>(dg, g, b, ir < TH ? h0 + ir : -1, cold, lane, slot + TC * 256);
+    };
+    float dzb[7][TW];
+    float in[TC];
+#pragma unroll
+    for (int p = 0; p < PF - 1; ++p) issue(p);
+#pragma nounroll
+    for (int ib = 0; ib < TR; ib += 7) {
+#pragma unroll
+      for (int u = 0; u < 7; ++u) {
+        const int ir = ib + u;
+        if (ir >= TR) break;
+        if (ir + PF - 1 < TR) issue(ir + PF - 1);
+        const int rem = TR - 1 - ir;
+        wait_rows<PF, TC + TW>(rem < PF - 1 ? rem : PF - 1);
+        const char* row = ring + (ir % PF) * ROWB;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row + j * 256, lane);
+        if (ir < TH) {
+#pragma unroll
+          for (int o = 0; o < TW; ++o) {
+            const float v = lds_ld<TDZ>(row + (TC + o) * 256, lane);
+            dzb[u][o] = v;
+            dbacc += v;
+          }
+        }
+#pragma unroll
+        for (int kh = 0; kh < 7; ++kh) {
+          const int orow = ir - kh;
+          if (orow < 0 || orow >= TH) continue;
+          const int sl = (u - kh + 7) % 7;
+#pragma unroll
+          for (int kw = 0; kw < 7; ++kw) {
+            float s = acc[kh * 7 + kw];
+#pragma unroll
+            for (int o = 0; o < TW; ++o) s = fmaf(dzb[sl][o], in[o + kw], s);
+            acc[kh * 7 + kw] = s;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // every wave's DMAs have landed (its last row waited with vmcnt(0)); reuse LDS as the combine
+  // buffer [49 taps][64] + [64], the 4 waves adding in turn (fixed order, 12.8 KiB)
+  float* red = reinterpret_cast<float*>(dw_smem);
+  float* redb = red + 49 * 64;
+  __syncthreads();
+  for (int k = 0; k < 4; ++k) {
+    if (wv == k) {
+#pragma unroll
+      for (int i = 0; i < 49; ++i) red[i * 64 + lane] = (k ? red[i * 64 + lane] : 0.f) + acc[i];
+      redb[lane] = (k ? redb[lane] : 0.f) + dbacc;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < 64 * 49; i += kDwThreads) {
+    const int ch = i / 49, tap = i - ch * 49;
+    dw_part[(size_t)blockIdx.x * g.C * 49 + (size_t)(c0 + ch) * 49 + tap] = red[tap * 64 + ch];
+  }
+  if (threadIdx.x < 64) db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = redb[threadIdx.x];
+}
+
+// implementation switch (A/B): SV_DW_IMPL=0 -> register-prefetch kernels; default ring, SV_DW_PF
+// = ring depth (2..4)
+static int dw_impl() {
+  static const int v = getenv("SV_DW_IMPL") ? atoi(getenv("SV_DW_IMPL")) : 1;
+  return v;
+}
+static int dw_pf() {
+  static const int v = getenv("SV_DW_PF") ? atoi(getenv("SV_DW_PF")) : 4;
+  return v < 2 ? 2 : (v > 4 ? 4 : v);
+}
+// wgrad ring depth: its ring holds x AND dz rows (14 columns), so depth 2 keeps 4 workgroups per CU
+// (measured: 2 >= 3, 4 on the S1/S3 shapes)
+static int dw_wgrad_pf() {
+  static const int v = getenv("SV_DW_WGRAD_PF") ? atoi(getenv("SV_DW_WGRAD_PF")) : 2;
+  return v < 2 ? 2 : (v > 4 ? 4 : v);
+}
+
 // strip width: 4 columns keeps a lane within 3 waves/SIMD (143 VGPRs); SV_DW_TW=8 trades occupancy for
 // fewer horizontal halo reads
 static int dw_tw() {
   static const int tw = getenv("SV_DW_TW") && atoi(getenv("SV_DW_TW")) == 8 ? 8 : 4;
   return tw;
+}
+
+static DwGeo dw_geo_tw(int B, int H, int W, int C, int tw) {
+  DwGeo g{B, H, W, C, tw, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
+  g.ntiles = B * g.tilesW * g.tilesH;
+  return g;
 }
 
 static DwGeo dw_geo(int B, int H, int W, int C) {
@@ -251,6 +539,26 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_ln_fwd: C=%d must be a multiple of 64", C);
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (dw_impl() == 1) {
+    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
+    const int grid = dw_blocks(g);
+    const int pf = dw_pf();
+#define RLAUNCH(PFV, TI, TO)                                                                              \
+  dwconv7_ring_kernel<PFV, 4, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<PFV, 4, TI>(), s>>>(   \
+      (const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
+#define RLAUNCH_PF(TI, TO) \
+  if (pf == 4) RLAUNCH(4, TI, TO); else if (pf == 3) RLAUNCH(3, TI, TO); else RLAUNCH(2, TI, TO)
+    if (x_dtype == SV_F32 && z_dtype == SV_F32) { RLAUNCH_PF(float, float); }
+    else if (x_dtype == SV_F32 && z_dtype == SV_BF16) { RLAUNCH_PF(float, uint16_t); }
+    else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) { RLAUNCH_PF(uint16_t, uint16_t); }
+    else if (x_dtype == SV_BF16 && z_dtype == SV_F32) { RLAUNCH_PF(uint16_t, float); }
+    else return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_ln_fwd: bad dtype");
+#undef RLAUNCH_PF
+#undef RLAUNCH
+    int rc = check_launch("sv_dwconv7_ln_fwd(dwconv)");
+    if (rc) return rc;
+    return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
+  }
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
 #define LAUNCH(TI, TO)                                                                                      \
@@ -277,6 +585,24 @@ int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, floa
   SV_REQUIRE(dz_dtype == SV_F32 || dz_dtype == SV_BF16, "sv_dwconv7_bwd_data: bad dz dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (dw_impl() == 1) {
+    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
+    const int grid = dw_blocks(g);
+    const int pf = dw_pf();
+#define RBWD(PFV, TD, ACC)                                                                                    \
+  dwconv7_ring_kernel<PFV, 4, TD, float, true, ACC><<<grid, kDwThreads, dw_ring_lds<PFV, 4, TD>(), s>>>(       \
+      (const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
+#define RBWD_PF(TD, ACC) \
+  if (pf == 4) RBWD(4, TD, ACC); else if (pf == 3) RBWD(3, TD, ACC); else RBWD(2, TD, ACC)
+    if (dz_dtype == SV_F32) {
+      if (accumulate) { RBWD_PF(float, true); } else { RBWD_PF(float, false); }
+    } else {
+      if (accumulate) { RBWD_PF(uint16_t, true); } else { RBWD_PF(uint16_t, false); }
+    }
+#undef RBWD_PF
+#undef RBWD
+    return check_launch("sv_dwconv7_bwd_data");
+  }
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
 #define BWD(TWV, TD, ACC) \
@@ -294,7 +620,7 @@ int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, floa
 }
 
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
-  const DwGeo g = dw_geo(B, H, W, C);
+  const DwGeo g = dw_impl() == 1 ? dw_geo_tw(B, H, W, C, 4) : dw_geo(B, H, W, C);
   const int ncg = C / 64 > 0 ? C / 64 : 1;
   int np = 512 / ncg;  // ~2048 waves over all channel groups
   if (np < 1) np = 1;
@@ -311,6 +637,28 @@ int sv_dwconv7_bwd_weight(const void* dz, int32_t dz_dtype, const void* x, int32
              "sv_dwconv7_bwd_weight: bad dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (dw_impl() == 1) {
+    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
+    const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
+    const int pf = dw_wgrad_pf();
+    constexpr size_t red_bytes = (49 * 64 + 64) * sizeof(float);
+#define RWG(PFV, TD, TX)                                                                                      \
+  {                                                                                                           \
+    const size_t lds = dw_wgrad_ring_lds<PFV, 4, TD, TX>() > red_bytes ? dw_wgrad_ring_lds<PFV, 4, TD, TX>()  \
+                                                                       : red_bytes;                          \
+    dwconv7_wgrad_ring_kernel<PFV, 4, TD, TX><<<grid, kDwThreads, lds, s>>>((const TD*)dz, (const TX*)x, dw_part, \
+                                                                            db_part, g);                     \
+  }
+#define RWG_PF(TD, TX) \
+  if (pf == 4) RWG(4, TD, TX) else if (pf == 3) RWG(3, TD, TX) else RWG(2, TD, TX)
+    if (dz_dtype == SV_F32 && x_dtype == SV_F32) { RWG_PF(float, float); }
+    else if (dz_dtype == SV_F32) { RWG_PF(float, uint16_t); }
+    else if (x_dtype == SV_F32) { RWG_PF(uint16_t, float); }
+    else { RWG_PF(uint16_t, uint16_t); }
+#undef RWG_PF
+#undef RWG
+    return check_launch("sv_dwconv7_bwd_weight");
+  }
   const DwGeo g = dw_geo(B, H, W, C);
   const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
 #define WG(TWV, TD, TX) \

@@ -173,7 +173,8 @@ def test_layernorm_fwd_bwd(dev, C, rows):
 
 
 # ------------------------------------------------------------------------------ depthwise conv
-@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64), (3, 4, 4, 256), (2, 2, 2, 192)])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64), (3, 4, 4, 256), (2, 2, 2, 192), (2, 32, 32, 512),
+                                   (1, 37, 45, 128)])
 def test_dwconv7_fwd_bwd(dev, shape):
     B, H, W, C = shape
     g = torch.Generator().manual_seed(B * H * W + C)

@@ -1,0 +1,91 @@
+"""Standalone timing of the depthwise-conv kernels at the ConvNeXt-base @512 bs32 stage shapes
+(HIP events).  Variants are selected by the SV_DW_* environment variables of the process.
+
+    SV_DW_IMPL=1 SV_DW_PF=4 python tools/dw_bench.py [--stages S1,S3] [--iters 20]
+"""
+
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import __graft_entry__  # noqa: E402
+
+__graft_entry__.load_package()
+from spine_vision_amd import kernels as K  # noqa: E402
+from spine_vision_amd import native as nv  # noqa: E402
+
+STAGES = {"S1": (128, 128), "S2": (64, 256), "S3": (32, 512), "S4": (16, 1024)}
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stages", default="S1,S2,S3,S4")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=32)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    tag = f"impl={os.environ.get('SV_DW_IMPL', '1')} pf={os.environ.get('SV_DW_PF', '4')}"
+    B = args.batch
+    for st in args.stages.split(","):
+        S, C = STAGES[st]
+        x = torch.randn(B, S, S, C, device=dev)
+        w = torch.randn(C, 49, device=dev) * 0.1
+        bias = torch.zeros(C, device=dev)
+        z = torch.empty(B, S, S, C, device=dev, dtype=torch.bfloat16)
+        dz = torch.randn(B, S, S, C, device=dev)
+        dzb = dz.to(torch.bfloat16)
+        dx = torch.zeros(B, S, S, C, device=dev)
+        dxb = torch.empty(B, S, S, C, device=dev, dtype=torch.bfloat16)
+        n = B * S * S * C
+        P = nv.value("sv_dwconv7_bwd_weight_nparts", B, S, S, C)
+        pw = torch.empty(P * C * 49, device=dev)
+        pb = torch.empty(P * C, device=dev)
+
+        def fwd():  # dwconv only (the LN half of sv_dwconv7_ln_fwd is timed by ln below)
+            nv.call("sv_dwconv7_bwd_data", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(dx), None, 0, B, S, S, C)
+
+        cases = [
+            ("bwd_data f32 acc+bf16", 4 * n + 4 * n + 4 * n + 2 * n,
+             lambda: K.dwconv7_bwd_data(dz, w, dx, accumulate=True, dx_bf16=dxb)),
+            ("bwd_data bf16dz acc+bf16", 2 * n + 4 * n + 4 * n + 2 * n,
+             lambda: K.dwconv7_bwd_data(dzb, w, dx, accumulate=True, dx_bf16=dxb)),
+            ("conv f32->f32 (no acc)", 8 * n, fwd),
+            ("wgrad f32 (kernel only)", 8 * n,
+             lambda: nv.call("sv_dwconv7_bwd_weight", nv.ptr(dz), nv.SV_F32, nv.ptr(x), nv.SV_F32, nv.ptr(pw),
+                             nv.ptr(pb), B, S, S, C)),
+            ("wgrad bf16dz (kernel only)", 6 * n,
+             lambda: nv.call("sv_dwconv7_bwd_weight", nv.ptr(dzb), nv.SV_BF16, nv.ptr(x), nv.SV_F32, nv.ptr(pw),
+                             nv.ptr(pb), B, S, S, C)),
+        ]
+        lnw = torch.ones(C, device=dev)
+        y = torch.empty(B * S * S, C, device=dev, dtype=torch.bfloat16)
+        mean = torch.empty(B * S * S, device=dev)
+        rstd = torch.empty_like(mean)
+        cases.append(("fwd f32->bf16 + LN", 4 * n + 2 * n + 2 * n + 2 * n,
+                      lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
+                                      nv.ptr(bias), 1e-6, nv.ptr(z), nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
+                                      nv.ptr(rstd), B, S, S, C)))
+        for name, nbytes, fn in cases:
+            us = timeit(fn, args.iters)
+            print(f"{tag} {st} {name:28s} {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
