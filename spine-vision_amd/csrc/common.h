@@ -29,8 +29,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
   return __builtin_bit_cast(uint16_t, b);
 }
+// two floats -> one bf16x2 word in ONE v_cvt_pk_bf16_f32 (RNE); the shift/or form costs three
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // typed element load/store used by dtype-generic kernels (T = float or uint16_t=bf16)
@@ -62,22 +66,28 @@ template <> __device__ __forceinline__ void st4<uint16_t>(uint16_t* p, size_t i,
 // ---- GELU (erf form, = torch.nn.GELU() default) -----------------------------------------
 // Phi(x) = 1 - 0.5 erfc(|x|/sqrt2) (x >= 0), 0.5 erfc(|x|/sqrt2) (x < 0) with the Abramowitz-Stegun
 // 7.1.26 erfc: t = 1/(1 + 0.3275911 z), erfc(z) = t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) e^{-z^2},
-// |error of erf| <= 1.5e-7.  e^{-z^2} = e^{-x^2/2} is also the Gaussian density's exponential, so
-// GELU(x) = x Phi(x) and GELU'(x) = Phi(x) + x e^{-x^2/2}/sqrt(2 pi) cost ONE v_exp_f32, ONE v_rcp_f32
-// and ~14 FMA/MUL -- the fc1 epilogue evaluates both for every element of the 4C-wide hidden layer.
+// |error of erf| <= 1.5e-7.  With z = |x|/sqrt2, e^{-z^2} = sqrt(2 pi) * phi(x), phi the Gaussian
+// density, so ONE v_exp_f32 gives both pieces:
+//     phi(x)  = exp2(x^2 * (-log2(e)/2) + log2(1/sqrt(2 pi)))        (one fma + v_exp)
+//     h       = 0.5 erfc(z) = t * P(t) * phi(x),  P = 0.5 sqrt(2 pi) (a1 + ... )  (coefficients folded)
+//     Phi(x)  = 0.5 + copysign(0.5 - h, x)                          (v_sub + v_bfi + v_add)
+//     GELU(x) = x Phi(x),   GELU'(x) = Phi(x) + x phi(x)            (v_mul, v_fma)
+// = 2 transcendental + ~14 VALU per element for GELU and GELU' together; the fc1 epilogue evaluates
+// them for every element of the 4C-wide hidden layer.
 struct GeluParts {
-  float phi, e;  // Phi(x), exp(-x^2/2)
+  float phi, dens;  // Phi(x), phi(x)
 };
 __device__ __forceinline__ GeluParts gelu_parts(float x) {
+  constexpr float K = 1.2533141373155003f;  // 0.5 * sqrt(2 pi)
   const float z = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  const float e = __builtin_amdgcn_exp2f(-(z * z) * 1.4426950408889634f);
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float h = 0.5f * (p * t) * e;  // 0.5 erfc(z)
-  return {x >= 0.f ? 1.0f - h : h, e};
+  const float dens = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170f, -1.3257480647361593f));
+  float p = fmaf(1.061405429f * K, t, -1.453152027f * K);
+  p = fmaf(p, t, 1.421413741f * K);
+  p = fmaf(p, t, -0.284496736f * K);
+  p = fmaf(p, t, 0.254829592f * K);
+  const float h = (p * t) * dens;  // 0.5 erfc(|x|/sqrt2)
+  return {0.5f + copysignf(0.5f - h, x), dens};
 }
 __device__ __forceinline__ float phi_cdf(float x) { return gelu_parts(x).phi; }
 __device__ __forceinline__ float gelu_f(float x) { return x * gelu_parts(x).phi; }
@@ -85,11 +95,11 @@ __device__ __forceinline__ float gelu_f(float x) { return x * gelu_parts(x).phi;
 __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
   const GeluParts q = gelu_parts(x);
   g = x * q.phi;
-  dg = fmaf(x, q.e * 0.39894228040143268f, q.phi);
+  dg = fmaf(x, q.dens, q.phi);
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const GeluParts q = gelu_parts(x);
-  return fmaf(x, q.e * 0.39894228040143268f, q.phi);
+  return fmaf(x, q.dens, q.phi);
 }
 
 // ---- wave / block reductions (wave64) -------------------------------------------------

@@ -334,7 +334,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     static const bool slab_v3 = getenv("SV_WGRAD_V3") != nullptr;
     const bool use_v3 = impl == 3 || (impl == 0 && (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048) ||
                                                      (slab_v3 && d->epilogue == SV_EPI_SLAB)));
-    const int rc = use_v3 ? launch_gemm3(d, s) : launch_gemm2(d, s);
+    const int rc = impl == 6 ? launch_gemm6(d, s) : use_v3 ? launch_gemm3(d, s) : launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   const bool a32 = d->a_dtype == SV_F32, b32 = d->b_dtype == SV_F32;

@@ -13,8 +13,8 @@
 //         -> every 16-lane group of a ds_read_b128 fragment read hits 16 distinct bank quads;
 //       m-major tile [32 k][rows]: LDS chunk = m-chunk ^ (2(r&3) ^ 8((r>>3)&1)) as in v2
 //         -> conflict-free ds_read_b64_tr_b16;
-//   * epilogue operands are loaded per 16-row slab (register budget), the other workgroup hides
-//     their latency.
+//   * one kernel per epilogue kind; bf16 epilogue operands (GELU'(h)) are prefetched packed for a
+//     whole 64-row group before its first store (a per-slab load would drain all earlier stores).
 #include "common.h"
 #include "gemm_common.h"
 
@@ -105,88 +105,136 @@ __device__ __forceinline__ float colsum32(const char* __restrict__ img, int row)
   return s;
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int EPI>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
 gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
-             int tilesM, int tilesN, EpiArgs e, float* __restrict__ colsum) {
+             int tilesM, int tilesN, int nsplit, int stagger, EpiArgs e, float* __restrict__ colsum) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nwg = tilesM * tilesN;
-  const int pid = blockIdx.x;
-  const int xcd = pid & 7, loc = pid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = wg / tilesN, tn = wg % tilesN;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int split = blockIdx.z;
-  const int kbeg = split * kper;
-  int kend = kbeg + kper;
-  if (kend > K) kend = K;
-  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  // Persistent: gridDim.x workgroups (two per CU) walk the tiles t = blockIdx.x, + gridDim.x, ...
+  // The second workgroup of every CU starts `stagger` cycles late, so the two co-resident
+  // workgroups stay out of phase and one's epilogue (VALU + stores) runs beside the other's MFMAs.
+  const int nwg = tilesM * tilesN, total = nwg * nsplit;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 1, wn = wid & 1;
+  if (stagger > 0 && blockIdx.x >= gridDim.x / 2) {
+    for (int c = 0; c < stagger; c += 2048) __builtin_amdgcn_s_sleep(32);
+  }
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    // XCD-aware order: tiles t = x (mod 8) run on XCD x; each XCD walks a contiguous tile range so
+    // concurrently resident tiles share A row panels in that XCD's L2
+    const int xcd = t & 7, loc = t >> 3, q8 = total >> 3, r8 = total & 7;
+    const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const int split = wgi / nwg, wg = wgi - split * nwg;
+    const int tm = wg / tilesN, tn = wg % tilesN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = split * kper;
+    int kend = kbeg + kper;
+    if (kend > K) kend = K;
+    const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
-  const int wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
-  const bool do_cs = colsum != nullptr && tn == 0;
-  float csum = 0.f;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int kt) {
-    char* st = smem + (kt % STAGES) * STAGE_BYTES;
-    const int k0 = kbeg + kt * BK;
-    issue_tile<AK, BM, A_PER_WAVE>(A, lda, m0, k0, e.M, st);
-    issue_tile<BKM, BN, B_PER_WAVE>(B, ldb, n0, k0, e.N, st + A_BYTES);
-  };
-
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
-  for (int kt = 0; kt < nk; ++kt) {
-    static_assert(A_PER_WAVE + B_PER_WAVE == 3, "vmcnt immediate below assumes 3 LDS-DMA pieces per wave per stage");
-    if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // tile kt landed, tile kt+1 stays in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kt + 2);  // into the slot of tile kt-1, which every wave has finished
-    const char* ai = smem + (kt % STAGES) * STAGE_BYTES;
-    const char* bi = ai + A_BYTES;
-    if (do_cs && threadIdx.x < BM) csum += colsum32<AK>(ai, threadIdx.x);
-    bf16x8 af[4], bfr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = frag<AK, BM>(ai, wm * 64 + i * 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM, BN>(bi, wn * 64 + j * 16);
+    const bool do_cs = colsum != nullptr && tn == 0;
+    float csum = 0.f;
+    f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int kt) {
+      char* st = smem + (kt % STAGES) * STAGE_BYTES;
+      const int k0 = kbeg + kt * BK;
+      issue_tile<AK, BM, A_PER_WAVE>(A, lda, m0, k0, e.M, st);
+      issue_tile<BKM, BN, B_PER_WAVE>(B, ldb, n0, k0, e.N, st + A_BYTES);
+    };
+
+    __syncthreads();  // the previous tile's epilogue slabs overlap the ring
+    if (nk > 0) issue(0);
+    if (nk > 1) issue(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      static_assert(A_PER_WAVE + B_PER_WAVE == 3, "vmcnt immediate below assumes 3 LDS-DMA pieces per wave per stage");
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // tile kt landed, tile kt+1 stays in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk) issue(kt + 2);  // into the slot of tile kt-1, which every wave has finished
+      const char* ai = smem + (kt % STAGES) * STAGE_BYTES;
+      const char* bi = ai + A_BYTES;
+      if (do_cs && threadIdx.x < BM) csum += colsum32<AK>(ai, threadIdx.x);
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<AK, BM>(ai, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM, BN>(bi, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
+    wave_tile_epilogue<4, 2, EPI>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64,
+                                  n0 + wn * 64, e, split);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
-  wave_tile_epilogue<4, false>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64, n0 + wn * 64,
-                               e, split);
 }
 
-template <bool AK, bool BKM>
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <bool AK, bool BKM, int EPI>
 static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
     attr_set = true;
   }
-  dim3 grid(tilesM * tilesN, 1, split);
-  gemm3_kernel<AK, BKM><<<grid, THREADS, LDS, s>>>(
+  // SV_GEMM3_PERSIST=0: one workgroup per tile (no stagger); default persistent, 2 per CU
+  static const int persist = getenv("SV_GEMM3_PERSIST") ? atoi(getenv("SV_GEMM3_PERSIST")) : 1;
+  static const int stag_env = getenv("SV_GEMM3_STAGGER") ? atoi(getenv("SV_GEMM3_STAGGER")) : -1;
+  const int total = tilesM * tilesN * split;
+  int grid = total, stagger = 0;
+  if (persist) {
+    const int slots = 2 * num_cus();
+    if (total > slots) {
+      grid = slots;
+      const int nk = kper / BK;
+      stagger = stag_env >= 0 ? stag_env * nk : 384 * nk;  // ~half a tile's main loop
+    }
+  }
+  gemm3_kernel<AK, BKM, EPI><<<grid, THREADS, LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
-      tilesM, tilesN, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
+      tilesM, tilesN, split, stagger, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
   return check_launch("sv_gemm(v3)");
+}
+
+// one kernel per epilogue kind: each carries only its own epilogue's registers
+template <bool AK, bool BKM>
+static int launch_epi(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
+  switch (d->epilogue) {
+    case SV_EPI_STORE: return launch<AK, BKM, SV_EPI_STORE>(d, split, kper, s);
+    case SV_EPI_BIAS_GELU2: return launch<AK, BKM, SV_EPI_BIAS_GELU2>(d, split, kper, s);
+    case SV_EPI_BIAS_GAMMA_RES: return launch<AK, BKM, SV_EPI_BIAS_GAMMA_RES>(d, split, kper, s);
+    case SV_EPI_GELU_GRAD: return launch<AK, BKM, SV_EPI_GELU_GRAD>(d, split, kper, s);
+    case SV_EPI_SLAB: return launch<AK, BKM, SV_EPI_SLAB>(d, split, kper, s);
+    case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL>(d, split, kper, s);
+    case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX>(d, split, kper, s);
+    default: return SV_ERR_UNSUPPORTED;
+  }
 }
 
 }  // namespace g3
@@ -198,10 +246,10 @@ int launch_gemm3(const sv_gemm_desc* d, hipStream_t s) {
   const int split = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
   const int kper = ceil_div(ceil_div(d->K, split), BK) * BK;
   if (d->K % BK != 0 || d->K < BK) return SV_ERR_UNSUPPORTED;
-  if (d->a_kmajor && d->b_kmajor) return launch<true, true>(d, split, kper, s);
-  if (d->a_kmajor && !d->b_kmajor) return launch<true, false>(d, split, kper, s);
-  if (!d->a_kmajor && d->b_kmajor) return launch<false, true>(d, split, kper, s);
-  return launch<false, false>(d, split, kper, s);
+  if (d->a_kmajor && d->b_kmajor) return launch_epi<true, true>(d, split, kper, s);
+  if (d->a_kmajor && !d->b_kmajor) return launch_epi<true, false>(d, split, kper, s);
+  if (!d->a_kmajor && d->b_kmajor) return launch_epi<false, true>(d, split, kper, s);
+  return launch_epi<false, false>(d, split, kper, s);
 }
 
 }  // namespace sv

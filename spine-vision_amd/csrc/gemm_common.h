@@ -103,9 +103,16 @@ __device__ __forceinline__ void gelu_dual4(float4 v, float4& g, float4& dg) {
 // Store one 64-row group (4 fragment rows) of a wave's accumulator; see wave_tile_epilogue.
 // PRE: load the group's residual / pre-activation operands before its first slab (more loads in
 // flight, 64 more VGPRs) or per slab (for kernels that must stay within 128 VGPRs).
-template <int FM, bool PRE = true>
-__device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][4], int i0, float* __restrict__ slab,
-                                                    int mb, int nb, const EpiArgs& e, int split) {
+// PRE: 1 = load the group's residual / pre-activation operands (as f32) before its first slab,
+//      0 = per slab (each such load costs a `s_waitcnt vmcnt(0)` that also drains every store issued
+//      before it), 2 = raw operand words one slab ahead (see fetch_raw).
+// EPI >= 0: the epilogue kind is a compile-time constant (kernels specialised per epilogue carry
+// only that epilogue's registers); EPI = -1: read e.epi at run time.
+template <int FM, int PRE = 1, int FN = 4, int J0 = 0, int EPI = -1>
+__device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], int i0, float* __restrict__ slab,
+                                                    int mb, int nb, const EpiArgs& e_in, int split) {
+  EpiArgs e = e_in;
+  if constexpr (EPI >= 0) e.epi = EPI;
   const int l = threadIdx.x & 63;
   const int cu = (l & 7) * 8, r0 = l >> 3;
   const int n = nb + cu;
@@ -122,8 +129,44 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][4], i
     g0 = *reinterpret_cast<const float4*>(e.gamma + n);
     if (okn4) g1 = *reinterpret_cast<const float4*>(e.gamma + n + 4);
   }
-  constexpr int NP = PRE ? 4 : 1;
+  constexpr int NP = PRE == 1 ? 4 : 1;
   float4 xa[NP][2], xb[NP][2];
+  // PRE == 2: raw operand words of slab i+1 are fetched before slab i is stored (one slab ahead,
+  // 8 VGPRs bf16 / 16 f32), so the wait for them never covers the stores issued after them
+  uint4 rcur[2][2], rnxt[2][2];
+  auto fetch_raw = [&](int i, uint4 (&r)[2][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = mb + i * 16 + r0 + 8 * h;
+      r[h][0] = r[h][1] = make_uint4(0, 0, 0, 0);
+      if (need_aux && okn && m < e.M) {
+        if (e.aux_dtype == SV_BF16) {
+          if (okn4) r[h][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n);
+          else r[h][0] = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n),
+                                    *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n + 2), 0, 0);
+        } else {
+          const float* f = reinterpret_cast<const float*>(e.aux) + (size_t)m * e.ld_aux + n;
+          r[h][0] = *reinterpret_cast<const uint4*>(f);
+          if (okn4) r[h][1] = *reinterpret_cast<const uint4*>(f + 4);
+        }
+      }
+    }
+  };
+  auto unpack_raw = [&](const uint4 (&r)[2][2], int h, float4& a, float4& b) {
+    if (e.aux_dtype == SV_BF16) {
+      const uint4 u = r[h][0];
+      a = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                      __uint_as_float(u.y & 0xffff0000u));
+      b = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+                      __uint_as_float(u.w & 0xffff0000u));
+    } else {
+      a = make_float4(__uint_as_float(r[h][0].x), __uint_as_float(r[h][0].y), __uint_as_float(r[h][0].z),
+                      __uint_as_float(r[h][0].w));
+      b = make_float4(__uint_as_float(r[h][1].x), __uint_as_float(r[h][1].y), __uint_as_float(r[h][1].z),
+                      __uint_as_float(r[h][1].w));
+    }
+  };
+  if constexpr (PRE == 2) fetch_raw(0, rcur);
   auto load_aux = [&](int i, int slot) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -135,18 +178,27 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][4], i
       }
     }
   };
-  if constexpr (PRE) {
+  if constexpr (PRE == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) load_aux(i, i);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int si = PRE ? i : 0;
-    if constexpr (!PRE) load_aux(i, 0);
+    const int si = PRE == 1 ? i : 0;
+    if constexpr (PRE == 0) load_aux(i, 0);
+    if constexpr (PRE == 2) {
+      if (i + 1 < 4) fetch_raw(i + 1, rnxt);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) unpack_raw(rcur, h, xa[0][h], xb[0][h]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) rcur[h][q] = rnxt[h][q];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i0 + i][j][r];
+      for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i0 + i][J0 + j][r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -210,17 +262,34 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][4], i
 // writes 8 whole 128-B rows (bf16: 16 B per lane) -- full cache lines instead of 32-B fragments.
 // The epilogue operands of each 64-row group (bias, gamma, residual / pre-activation) are loaded
 // before its first slab.
-template <int FM, bool PRE = true>
+template <int FM, int PRE = 1, int EPI = -1>
 __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[FM][4], float* __restrict__ slab, int mb,
                                                    int nb, const EpiArgs& e, int split) {
   static_assert(FM % 4 == 0, "64-row groups");
 #pragma unroll
-  for (int i0 = 0; i0 < FM; i0 += 4) wave_group_epilogue<FM, PRE>(acc, i0, slab, mb + 16 * i0, nb, e, split);
+  for (int i0 = 0; i0 < FM; i0 += 4) wave_group_epilogue<FM, PRE, 4, 0, EPI>(acc, i0, slab, mb + 16 * i0, nb, e, split);
+}
+
+// (16 FM) x (16 FN) wave tile, FN a multiple of 4: 64-column groups stored one after the other
+template <int FM, int FN, int PRE = 1>
+__device__ __forceinline__ void wave_tile_epilogue_wide(const f32x4 (&acc)[FM][FN], float* __restrict__ slab, int mb,
+                                                        int nb, const EpiArgs& e, int split) {
+  static_assert(FM % 4 == 0 && FN % 4 == 0 && FM <= 8 && FN <= 8, "64x64 groups");
+  // written out (no loop): the unroller refuses a loop this large, and a rolled loop would index the
+  // accumulator array dynamically and push it to scratch
+  wave_group_epilogue<FM, PRE, FN, 0>(acc, 0, slab, mb, nb, e, split);
+  if constexpr (FN >= 8) wave_group_epilogue<FM, PRE, FN, 4>(acc, 0, slab, mb, nb + 64, e, split);
+  if constexpr (FM >= 8) {
+    wave_group_epilogue<FM, PRE, FN, 0>(acc, 4, slab, mb + 64, nb, e, split);
+    if constexpr (FN >= 8) wave_group_epilogue<FM, PRE, FN, 4>(acc, 4, slab, mb + 64, nb + 64, e, split);
+  }
 }
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
 // v3 entry (gemm3.hip, two workgroups per CU): same contract with K % 32 == 0
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s);
+// v6 entry (gemm6.hip, 256x256 tile, one 4-wave workgroup per CU): same contract as v2
+int launch_gemm6(const sv_gemm_desc* d, hipStream_t s);
 
 }  // namespace sv
