@@ -326,15 +326,20 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   static const bool force_v1 = getenv("SV_GEMM_V1") != nullptr;
   static const int impl = getenv("SV_GEMM_IMPL") ? atoi(getenv("SV_GEMM_IMPL")) : 0;
   if (!force_v1) {
-    // v3 (two workgroups per CU, BK 32) hides VALU-heavy epilogues and short K behind the other
-    // workgroup's MFMAs; v2 (one workgroup, BK 64, half the barriers) wins on long-K GEMMs with light
-    // epilogues (measured per ConvNeXt shape: tools/gemm_bench.py, profiles/)
+    // Measured per ConvNeXt shape (tools/gemm_bench.py, profiles/r1s2_gemm_cfg.txt):
+    //   v3 32x3 (two workgroups per CU, one's epilogue beside the other's MFMAs): VALU-heavy and
+    //     operand-reading epilogues and plain stores with K <= 2048 (fc1 fwd, fc2 dgrad, fc1 dgrad);
+    //   v3 32x4 (one workgroup per CU, two tiles in flight): the split-K wgrads (-10..25% vs v2);
+    //   v2 (BK 64, 3 stages): long-K residual epilogue (fc2 fwd).
     const bool heavy_epi = d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
                            d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
-    static const bool slab_v3 = getenv("SV_WGRAD_V3") != nullptr;
-    const bool use_v3 = impl == 3 || (impl == 0 && (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048) ||
-                                                     (slab_v3 && d->epilogue == SV_EPI_SLAB)));
-    const int rc = impl == 6 ? launch_gemm6(d, s) : use_v3 ? launch_gemm3(d, s) : launch_gemm2(d, s);
+    int rc;
+    if (impl == 6) rc = launch_gemm6(d, s);
+    else if (impl == 2) rc = launch_gemm2(d, s);
+    else if (impl == 3) rc = launch_gemm3(d, s);
+    else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, "32x4");
+    else if (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048)) rc = launch_gemm3(d, s);
+    else rc = launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   const bool a32 = d->a_dtype == SV_F32, b32 = d->b_dtype == SV_F32;

@@ -108,11 +108,13 @@ __device__ __forceinline__ void gelu_dual4(float4 v, float4& g, float4& dg) {
 //      before it), 2 = raw operand words one slab ahead (see fetch_raw).
 // EPI >= 0: the epilogue kind is a compile-time constant (kernels specialised per epilogue carry
 // only that epilogue's registers); EPI = -1: read e.epi at run time.
-template <int FM, int PRE = 1, int FN = 4, int J0 = 0, int EPI = -1>
+// AUXT: dtype of the epilogue operand when known at compile time (SV_F32 / SV_BF16), -1 = e.aux_dtype
+template <int FM, int PRE = 1, int FN = 4, int J0 = 0, int EPI = -1, int AUXT = -1>
 __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], int i0, float* __restrict__ slab,
                                                     int mb, int nb, const EpiArgs& e_in, int split) {
   EpiArgs e = e_in;
   if constexpr (EPI >= 0) e.epi = EPI;
+  if constexpr (AUXT >= 0) e.aux_dtype = AUXT;
   const int l = threadIdx.x & 63;
   const int cu = (l & 7) * 8, r0 = l >> 3;
   const int n = nb + cu;
@@ -133,26 +135,28 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
   float4 xa[NP][2], xb[NP][2];
   // PRE == 2: raw operand words of slab i+1 are fetched before slab i is stored (one slab ahead,
   // 8 VGPRs bf16 / 16 f32), so the wait for them never covers the stores issued after them
-  uint4 rcur[2][2], rnxt[2][2];
-  auto fetch_raw = [&](int i, uint4 (&r)[2][2]) {
+  constexpr int RW = AUXT == SV_BF16 ? 1 : 2;  // raw words per 8 operands: bf16 1 x uint4, f32 2
+  uint4 rcur[2][RW], rnxt[2][RW];
+  auto fetch_raw = [&](int i, uint4 (&r)[2][RW]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int m = mb + i * 16 + r0 + 8 * h;
-      r[h][0] = r[h][1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < RW; ++q) r[h][q] = make_uint4(0, 0, 0, 0);
       if (need_aux && okn && m < e.M) {
         if (e.aux_dtype == SV_BF16) {
           if (okn4) r[h][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n);
           else r[h][0] = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n),
                                     *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n + 2), 0, 0);
-        } else {
+        } else if constexpr (RW == 2) {
           const float* f = reinterpret_cast<const float*>(e.aux) + (size_t)m * e.ld_aux + n;
           r[h][0] = *reinterpret_cast<const uint4*>(f);
-          if (okn4) r[h][1] = *reinterpret_cast<const uint4*>(f + 4);
+          if (okn4) r[h][RW - 1] = *reinterpret_cast<const uint4*>(f + 4);
         }
       }
     }
   };
-  auto unpack_raw = [&](const uint4 (&r)[2][2], int h, float4& a, float4& b) {
+  auto unpack_raw = [&](const uint4 (&r)[2][RW], int h, float4& a, float4& b) {
     if (e.aux_dtype == SV_BF16) {
       const uint4 u = r[h][0];
       a = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
@@ -162,8 +166,8 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
     } else {
       a = make_float4(__uint_as_float(r[h][0].x), __uint_as_float(r[h][0].y), __uint_as_float(r[h][0].z),
                       __uint_as_float(r[h][0].w));
-      b = make_float4(__uint_as_float(r[h][1].x), __uint_as_float(r[h][1].y), __uint_as_float(r[h][1].z),
-                      __uint_as_float(r[h][1].w));
+      b = make_float4(__uint_as_float(r[h][RW - 1].x), __uint_as_float(r[h][RW - 1].y),
+                      __uint_as_float(r[h][RW - 1].z), __uint_as_float(r[h][RW - 1].w));
     }
   };
   if constexpr (PRE == 2) fetch_raw(0, rcur);
@@ -193,7 +197,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) rcur[h][q] = rnxt[h][q];
+        for (int q = 0; q < RW; ++q) rcur[h][q] = rnxt[h][q];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -262,12 +266,13 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
 // writes 8 whole 128-B rows (bf16: 16 B per lane) -- full cache lines instead of 32-B fragments.
 // The epilogue operands of each 64-row group (bias, gamma, residual / pre-activation) are loaded
 // before its first slab.
-template <int FM, int PRE = 1, int EPI = -1>
+template <int FM, int PRE = 1, int EPI = -1, int AUXT = -1>
 __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[FM][4], float* __restrict__ slab, int mb,
                                                    int nb, const EpiArgs& e, int split) {
   static_assert(FM % 4 == 0, "64-row groups");
 #pragma unroll
-  for (int i0 = 0; i0 < FM; i0 += 4) wave_group_epilogue<FM, PRE, 4, 0, EPI>(acc, i0, slab, mb + 16 * i0, nb, e, split);
+  for (int i0 = 0; i0 < FM; i0 += 4)
+    wave_group_epilogue<FM, PRE, 4, 0, EPI, AUXT>(acc, i0, slab, mb + 16 * i0, nb, e, split);
 }
 
 // (16 FM) x (16 FN) wave tile, FN a multiple of 4: 64-column groups stored one after the other
@@ -287,8 +292,8 @@ __device__ __forceinline__ void wave_tile_epilogue_wide(const f32x4 (&acc)[FM][F
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
-// v3 entry (gemm3.hip, two workgroups per CU): same contract with K % 32 == 0
-int launch_gemm3(const sv_gemm_desc* d, hipStream_t s);
+// v3 entry (gemm3.hip): same contract with K % BK == 0; cfg = "BKxSTAGES" (nullptr: 32x3)
+int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg = nullptr);
 // v6 entry (gemm6.hip, 256x256 tile, one 4-wave workgroup per CU): same contract as v2
 int launch_gemm6(const sv_gemm_desc* d, hipStream_t s);
 
