@@ -84,6 +84,11 @@ typedef struct {
 } sv_gemm_desc;
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
+/* Residency policy for the bf16 GEMMs launched after this call (host-side, process-wide):
+ * 0 (default) = one workgroup per output tile; n > 0 = persistent grids of n workgroups per CU, so
+ * that GEMMs issued concurrently on two streams (data gradients + weight gradients) are co-resident
+ * on every CU instead of the first one filling the chip.  Returns the previous value.               */
+int sv_gemm_set_workgroups_per_cu(int32_t n);
 
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.

@@ -19,6 +19,8 @@ spine_vision/training/models/backbone.py:166-170 (timm 1.0.22 ``timm/models/conv
 
 from __future__ import annotations
 
+import os
+from contextlib import nullcontext as _nullctx
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -117,6 +119,10 @@ class ConvNeXtHip(nn.Module):
         self.num_features = self.head_hidden_size = prev
         self.grad_ready_hook: Callable[[list], None] | None = None
         self._shadow: dict[int, torch.Tensor] | None = None  # id(param) -> bf16 shadow view
+        # weight-gradient kernels on a side stream beside the data-gradient chain (SV_SIDE_STREAM=0: off)
+        self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
+        self.side_wg_per_cu = int(os.environ.get("SV_SIDE_WG_PER_CU", "1"))
+        self._side: dict = {}
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -226,6 +232,11 @@ class ConvNeXtHip(nn.Module):
         return feat, tape
 
     # -- backward ----------------------------------------------------------------------------------
+    def _side_stream(self, device) -> torch.cuda.Stream:
+        if device not in self._side:
+            self._side[device] = torch.cuda.Stream(device=device)
+        return self._side[device]
+
     @staticmethod
     def _grad(p: torch.Tensor) -> torch.Tensor:
         if p.grad is None:
@@ -243,6 +254,10 @@ class ConvNeXtHip(nn.Module):
         cache: dict = tape.wcache
         g = self._grad
         hn = self.head.norm
+        main = torch.cuda.current_stream()
+        side = self._side_stream(main.device) if self.overlap_wgrad else None
+        # block GEMMs of the two streams: one persistent workgroup per CU each, so they share every CU
+        prev_res = nv.value("sv_gemm_set_workgroups_per_cu", self.side_wg_per_cu if side is not None else 0)
         # d: f32 gradient stream (residual accumulation); db: its bf16 copy, the GEMM operand (bf16 mode)
         d, db = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight),
                               dlnb=g(hn.bias), with_bf16=bf)
@@ -254,36 +269,59 @@ class ConvNeXtHip(nn.Module):
                 M = B * H * W
                 d2 = d.view(M, C)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
+                dsrc = db.view(M, C) if bf else d2
+                # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
+                # stream beside the data-gradient chain of the main stream: the wgrads are MFMA-bound
+                # with small outputs, the dgrads epilogue/HBM-bound, so the two overlap on the chip
+                if side is not None:
+                    side.wait_event(main.record_event())
+                    for t_ in (dsrc, a):
+                        t_.record_stream(side)
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    # dW2 = gamma (.) d^T a, dgamma = rowdot(W2, d^T a) + b2 (.) colsum(d), db2 = gamma (.) colsum(d)
+                    K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(),
+                                       blk.mlp.fc2.bias.detach(), dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma),
+                                       db2=g(blk.mlp.fc2.bias), compute_bf16=bf)
+                ev_w2 = side.record_event() if side is not None else None
                 # fc2: dh = ((d * gamma) @ W2) * GELU'(h).  bf16 mode folds gamma into a bf16 copy of W2;
                 # GELU'(h) was stored by the forward epilogue
                 dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
                 if bf:
-                    dsrc = db.view(M, C)
                     w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
                     K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
                 else:
-                    dsrc = d2
                     K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_MUL_AUX,
                                    a_scale_k=blk.gamma, aux=gh, compute_bf16=False)
-                # dW2 = gamma (.) d^T a, dgamma = rowdot(W2, d^T a) + b2 (.) colsum(d), db2 = gamma (.) colsum(d)
-                K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(),
-                                   blk.mlp.fc2.bias.detach(), dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma),
-                                   db2=g(blk.mlp.fc2.bias), compute_bf16=bf)
-                # fc1: dy = dh @ W1 ; dW1 = dh^T y ; db1 = colsum(dh) (fused in the wgrad GEMM).
+                # fc1: dy = dh @ W1 (main) ; dW1 = dh^T y, db1 = colsum(dh) (side, fused in the wgrad GEMM).
                 # bf16 mode: dy and dz travel as bf16 (the depthwise backward reads dz through its LDS-DMA
                 # ring, where 2-byte columns cost no more than 4-byte ones)
+                if side is not None:
+                    side.wait_event(main.record_event())
+                    for t_ in (dh, y):
+                        t_.record_stream(side)
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True,
+                                   bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf)
                 dy = torch.empty(M, C, device=d.device, dtype=act)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
-                K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
-                               compute_bf16=bf)
                 # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
                 dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
                                      db=g(blk.norm.bias), out_dtype=act)
                 dz4 = dz.view(B, H, W, C)
-                K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+                blk_params = [blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
+                              blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma]
+                if side is not None:
+                    side.wait_event(main.record_event())
+                    for t_ in (dz, x):
+                        t_.record_stream(side)
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+                    # every gradient of the block is final on this stream now (the LN ones were made on
+                    # the main stream before the wait above): the bucketer's event covers them all
+                    self._ready(blk_params)
+                if side is not None:
+                    main.wait_event(ev_w2)  # fc2 wgrad has read db before the depthwise backward rewrites it
                 K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
-                self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
-                             blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
             if ds_saved is not None:
                 x_prev, patches, d_mean, d_rstd = ds_saved
                 ln, conv = st.downsample[0], st.downsample[1]
@@ -303,6 +341,9 @@ class ConvNeXtHip(nn.Module):
         conv, ln = self.stem[0], self.stem[1]
         K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
                    db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
+        nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
+        if side is not None:
+            main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
         self._ready([conv.weight, conv.bias, ln.weight, ln.bias])
 
 

@@ -292,6 +292,16 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace sv;
 
+namespace sv {
+int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
+}
+
+extern "C" int sv_gemm_set_workgroups_per_cu(int32_t n) {
+  const int prev = g_gemm_wg_per_cu;
+  g_gemm_wg_per_cu = n < 0 ? 0 : (n > 2 ? 2 : n);
+  return prev;
+}
+
 extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
@@ -335,10 +345,12 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
                            d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
     int rc;
     if (impl == 6) rc = launch_gemm6(d, s);
+    else if (impl == 7) rc = launch_gemm7(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);
     else if (impl == 3) rc = launch_gemm3(d, s);
-    else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, "32x4");
+    else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, g_gemm_wg_per_cu ? "32x3" : "32x4");
     else if (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048)) rc = launch_gemm3(d, s);
+    else if (g_gemm_wg_per_cu) rc = launch_gemm3(d, s);  // v2's 144 KiB would not share a CU
     else rc = launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }

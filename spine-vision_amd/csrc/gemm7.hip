@@ -1,12 +1,13 @@
-// MFMA GEMM v3 (bf16 operands, f32 accumulate): 256x128 output tile per 512-thread workgroup
-// (8 waves in 4(M) x 2(N), 64x64 per wave = 4x4 v_mfma_f32_16x16x32_bf16 fragments), LDS ring of S
-// stages of BK k, filled by LDS-DMA (global_load_lds_dwordx4), persistent over the tiles.
+// MFMA GEMM v7 (bf16 operands, f32 accumulate): the v3 tile (256x128 per 512-thread workgroup,
+// 8 waves of 64x64 = 4x4 v_mfma_f32_16x16x32_bf16 fragments, BK 32) with REGISTER-STAGED operand
+// loads instead of LDS-DMA: every wave fetches its 3 KiB share of tile kt+3 with global_load_dwordx4
+// into VGPRs while tile kt is multiplied, and writes tile kt+1 into the LDS double buffer with
+// ds_write_b128.  An LDS-DMA piece costs its wave 60-185 issue cycles beside MFMAs
+// (MI355X_MICROARCH.md, cycle constants), a global_load + ds_write_b128 pair a fraction of that.
 //
-//   * configurations (SV_GEMM3_CFG): BK 32 x 3 stages = 72 KiB (two workgroups per CU: one's
-//     epilogue runs beside the other's MFMAs; default), BK 32 x 4 / BK 64 x 2 (96 KiB) and BK 64 x 3
-//     (144 KiB) at one workgroup per CU;
-//   * counted `s_waitcnt vmcnt` keeps the S-2 younger tiles in flight, one s_barrier per tile;
-//   * LDS-DMA writes lane-linearly, so bank conflicts are avoided by XOR-swizzling the SOURCE:
+//   * two tiles in flight in registers (2 x 12 VGPRs), LDS 2 x 24 KiB, one s_barrier per tile;
+//   * OCC 4: 128 VGPRs, two workgroups per CU; OCC 2: one workgroup per CU;
+//   * the LDS image is written lane-linearly, so bank conflicts are avoided by XOR-swizzling the SOURCE:
 //       k-major [rows][BK]: LDS chunk = k-chunk ^ (row & 7) (BK 64) / ^ 2((row>>3)&1) (BK 32)
 //         -> conflict-free ds_read_b128 fragment reads;
 //       m-major [BK][rows]: LDS chunk = m-chunk ^ (2(r&3) ^ 8((r>>3)&1))
@@ -22,12 +23,10 @@
 #include <string.h>
 
 namespace sv {
-extern int g_gemm_wg_per_cu;
-namespace g3 {
+namespace g7 {
 
 constexpr int BM = 256, BN = 128, THREADS = 512, NW = 8;
 
-typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 template <int BKT>
@@ -37,41 +36,42 @@ __device__ __forceinline__ int kswz(int row) {
 }
 __device__ __forceinline__ int mswz(int r) { return ((r & 3) << 1) ^ (((r >> 3) & 1) << 3); }
 
-template <int BKT, int S>
+template <int BKT, int S = 2>
 struct Cfg {
   static constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int A_PER_WAVE = A_BYTES / 1024 / NW, B_PER_WAVE = B_BYTES / 1024 / NW;
-  static constexpr int LOADS = A_PER_WAVE + B_PER_WAVE;  // LDS-DMA instructions per wave per stage
-  static constexpr size_t LDS = (size_t)S * STAGE_BYTES;
-  static constexpr bool TWO_PER_CU = LDS <= 80 * 1024;
+  static constexpr int LOADS = A_PER_WAVE + B_PER_WAVE;  // global_load_dwordx4 per wave per tile
+  static constexpr size_t LDS = (size_t)S * STAGE_BYTES > 36 * 1024 ? (size_t)S * STAGE_BYTES : 36 * 1024;
 };
 
-template <bool KMAJ, int ROWS, int BKT, int PER_WAVE>
-__device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ X, int64_t ld, int row0, int k0, int R,
-                                           char* lds_tile, int wid) {
+// Global -> register half of a tile load: the lane's 16 B of 1-KiB LDS piece `piece`, read from the
+// XOR-swizzled SOURCE address so the linear LDS image it lands in is the bank-conflict-free layout
+// the fragment reads expect (the v2/v3 LDS-DMA layout).
+template <bool KMAJ, int ROWS, int BKT>
+__device__ __forceinline__ uint4 fetch_piece(const uint16_t* __restrict__ X, int64_t ld, int row0, int k0, int R,
+                                             int piece) {
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < PER_WAVE; ++j) {
-    const int piece = wid + NW * j;
-    const int byte = piece * 1024 + lane * 16;
-    const uint16_t* src;
-    if constexpr (KMAJ) {
-      constexpr int RB = BKT * 2;
-      const int row = byte / RB, ch = (byte % RB) >> 4;
-      const int gc = ch ^ kswz<BKT>(row);
-      int grow = row0 + row;
-      if (grow >= R) grow = 0;  // clamped; the result row is never stored
-      src = X + (size_t)grow * ld + k0 + gc * 8;
-    } else {
-      constexpr int RB = ROWS * 2;
-      const int krow = byte / RB, ch = (byte % RB) >> 4;
-      const int gc = ch ^ mswz(krow);
-      int gcol = row0 + gc * 8;
-      if (gcol >= R) gcol = 0;
-      src = X + (size_t)(k0 + krow) * ld + gcol;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+  const int byte = piece * 1024 + lane * 16;
+  const uint16_t* src;
+  if constexpr (KMAJ) {
+    constexpr int RB = BKT * 2;
+    const int row = byte / RB, ch = (byte % RB) >> 4;
+    const int gc = ch ^ kswz<BKT>(row);
+    int grow = row0 + row;
+    if (grow >= R) grow = 0;  // clamped; the result row is never stored
+    src = X + (size_t)grow * ld + k0 + gc * 8;
+  } else {
+    constexpr int RB = ROWS * 2;
+    const int krow = byte / RB, ch = (byte % RB) >> 4;
+    const int gc = ch ^ mswz(krow);
+    int gcol = row0 + gc * 8;
+    if (gcol >= R) gcol = 0;
+    src = X + (size_t)(k0 + krow) * ld + gcol;
   }
+  return *reinterpret_cast<const uint4*>(src);
+}
+__device__ __forceinline__ void store_piece(char* lds_tile, const uint4& r, int piece) {
+  *reinterpret_cast<uint4*>(lds_tile + piece * 1024 + (threadIdx.x & 63) * 16) = r;
 }
 
 // MFMA fragment: lane l holds X[row = base + (l&15)][k = 32*kk + 8*(l>>4) + j], j = 0..7
@@ -147,12 +147,11 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC>
+template <bool AK, bool BKM, int EPI, int BKT, int OCC>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
-gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
+gemm7_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
              int tilesM, int tilesN, int nsplit, int stagger, EpiArgs e, float* __restrict__ colsum) {
-  using C = Cfg<BKT, S>;
-  static_assert(S >= 2 && (S - 2) * C::LOADS <= 63, "ring / vmcnt");
+  using C = Cfg<BKT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = tilesM * tilesN, total = nwg * nsplit;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 1, wn = wid & 1;
@@ -181,28 +180,26 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto issue = [&](int kt) {
-      char* st = smem + (kt % S) * C::STAGE_BYTES;
-      const int k0 = kbeg + kt * BKT;
-      issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
-      issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
-    };
-
-    __syncthreads();  // the previous tile's epilogue slabs overlap the ring
-#pragma unroll
-    for (int p = 0; p < S - 1; ++p)
-      if (p < nk) issue(p);
-    for (int kt = 0; kt < nk; ++kt) {
-      // tile kt must have landed; the min(S-2, nk-1-kt) younger tiles may stay in flight
-      const int younger = nk - 1 - kt < S - 2 ? nk - 1 - kt : S - 2;
-      if (S > 3 && younger >= 2) vm_wait<(S > 3 ? 2 * C::LOADS : 0)>();
-      else if (S > 2 && younger >= 1) vm_wait<(S > 2 ? C::LOADS : 0)>();
-      else vm_wait<0>();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (kt + S - 1 < nk) issue(kt + S - 1);  // into the slot of tile kt-1, which every wave has finished
-      const char* ai = smem + (kt % S) * C::STAGE_BYTES;
+    // staging sets: tile t lives in set t & 1; 2 A + 1 B uint4 per lane each (BK 32), kept as
+    // scalars so they stay in VGPRs
+    static_assert(C::A_PER_WAVE == 2 && C::B_PER_WAVE == 1, "staging written for BK 32");
+    uint4 x0a, x0b, x0c, x1a, x1b, x1c;
+#define SV7_GLOAD(kt, ra, rb, rc)                                                         \
+    {                                                                                     \
+      const int k0_ = kbeg + (kt) * BKT;                                                  \
+      ra = fetch_piece<AK, BM, BKT>(A, lda, m0, k0_, e.M, wid);                           \
+      rb = fetch_piece<AK, BM, BKT>(A, lda, m0, k0_, e.M, wid + NW);                      \
+      rc = fetch_piece<BKM, BN, BKT>(B, ldb, n0, k0_, e.N, wid);                          \
+    }
+#define SV7_SWRITE(kt, ra, rb, rc)                                                        \
+    {                                                                                     \
+      char* st_ = smem + ((kt) & 1) * C::STAGE_BYTES;                                     \
+      store_piece(st_, ra, wid);                                                          \
+      store_piece(st_, rb, wid + NW);                                                     \
+      store_piece(st_ + C::A_BYTES, rc, wid);                                             \
+    }
+    auto compute = [&](int kt) __attribute__((always_inline)) {
+      const char* ai = smem + (kt & 1) * C::STAGE_BYTES;
       const char* bi = ai + C::A_BYTES;
       if (do_cs) {
         if constexpr (AK) {
@@ -224,7 +221,39 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+    };
+    // one pipeline step: tile kt+1 (staged two steps ago) goes to LDS, tile kt+3 is fetched into the
+    // freed set, tile kt is multiplied.  (ra, rb, rc) = set (kt+1) & 1.
+#define SV7_STEP(kt, ra, rb, rc)                                                               \
+    {                                                                                          \
+      if ((kt) + 2 < nk) vm_wait<C::LOADS>(); /* tile kt+1 arrived, kt+2 may stay in flight */ \
+      else vm_wait<0>();                                                                       \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* my part of tile kt is in LDS */    \
+      __builtin_amdgcn_s_barrier();                      /* everyone's; slot (kt+1)&1 free */  \
+      asm volatile("" ::: "memory");                                                           \
+      if ((kt) + 1 < nk) SV7_SWRITE((kt) + 1, ra, rb, rc);                                     \
+      if ((kt) + 3 < nk) SV7_GLOAD((kt) + 3, ra, rb, rc);                                      \
+      compute(kt);                                                                             \
     }
+
+    __syncthreads();  // the previous tile's epilogue slabs overlap the LDS buffers
+    if (nk > 0) SV7_GLOAD(0, x0a, x0b, x0c);
+    if (nk > 1) SV7_GLOAD(1, x1a, x1b, x1c);
+    if (nk > 0) {
+      if (nk > 1) vm_wait<C::LOADS>();
+      else vm_wait<0>();
+      SV7_SWRITE(0, x0a, x0b, x0c);
+      if (nk > 2) SV7_GLOAD(2, x0a, x0b, x0c);
+    }
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {  // two steps per trip: the staging set stays compile-time
+      SV7_STEP(kt, x1a, x1b, x1c);
+      SV7_STEP(kt + 1, x0a, x0b, x0c);
+    }
+    if (kt < nk) SV7_STEP(kt, x1a, x1b, x1c);
+#undef SV7_STEP
+#undef SV7_SWRITE
+#undef SV7_GLOAD
     vm_wait<0>();
     __syncthreads();
     if constexpr (!AK) {
@@ -243,90 +272,65 @@ static int num_cus() {
   static int n = 0;
   if (!n) {
     int dev = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
   }
   return n;
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S>
+template <bool AK, bool BKM, int EPI, int BKT, int OCC>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
-  using C = Cfg<BKT, S>;
-  // the kernels are specialised for the operand dtype each epilogue carries in the bf16 model
+  using C = Cfg<BKT>;
   if ((EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) && d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
   if (EPI == SV_EPI_BIAS_GAMMA_RES && d->aux_dtype != SV_F32) return SV_ERR_UNSUPPORTED;
-  constexpr int OCC = C::TWO_PER_CU ? 4 : 2;
   const int kper = ceil_div(ceil_div(d->K, split), BKT) * BKT;
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-    attr_set = true;
-  }
-  // SV_GEMM3_PERSIST=1: persistent over the resident slots (measured no faster); default one workgroup
-  // per tile, which also lets kernels of the side stream take CUs as tiles retire
-  static const int persist = getenv("SV_GEMM3_PERSIST") ? atoi(getenv("SV_GEMM3_PERSIST")) : 0;
-  static const int stag_env = getenv("SV_GEMM3_STAGGER") ? atoi(getenv("SV_GEMM3_STAGGER")) : -1;
   const int total = tilesM * tilesN * split;
-  int grid = total, stagger = 0;
-  if (g_gemm_wg_per_cu > 0) {  // co-residency with a concurrent GEMM (sv_gemm_set_workgroups_per_cu)
-    const int slots = g_gemm_wg_per_cu * num_cus();
-    grid = total > slots ? slots : total;
-  } else if (persist) {
-    const int slots = (C::TWO_PER_CU ? 2 : 1) * num_cus();
-    if (total > slots) {
-      grid = slots;
-      if (C::TWO_PER_CU) stagger = (stag_env >= 0 ? stag_env : 384) * (kper / 32);  // ~half a main loop
-    }
-  }
-  gemm3_kernel<AK, BKM, EPI, BKT, S, OCC><<<grid, THREADS, C::LDS, s>>>(
+  const int slots = (OCC == 4 ? 2 : 1) * num_cus();
+  const int grid = total > slots ? slots : total;
+  static const int stag_env = getenv("SV_GEMM3_STAGGER") ? atoi(getenv("SV_GEMM3_STAGGER")) : -1;
+  const int stagger = (OCC == 4 && total > slots) ? (stag_env >= 0 ? stag_env : 384) * (kper / 32) : 0;
+  gemm7_kernel<AK, BKM, EPI, BKT, OCC><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
       tilesM, tilesN, split, stagger, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
-  return check_launch("sv_gemm(v3)");
+  return check_launch("sv_gemm(v7)");
 }
 
-// one kernel per epilogue kind: each carries only its own epilogue's registers
-template <bool AK, bool BKM, int BKT, int S>
+template <bool AK, bool BKM, int OCC>
 static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
   switch (d->epilogue) {
-    case SV_EPI_STORE: return launch<AK, BKM, SV_EPI_STORE, BKT, S>(d, split, s);
-    case SV_EPI_BIAS_GELU2: return launch<AK, BKM, SV_EPI_BIAS_GELU2, BKT, S>(d, split, s);
-    case SV_EPI_BIAS_GAMMA_RES: return launch<AK, BKM, SV_EPI_BIAS_GAMMA_RES, BKT, S>(d, split, s);
-    case SV_EPI_GELU_GRAD: return launch<AK, BKM, SV_EPI_GELU_GRAD, BKT, S>(d, split, s);
-    case SV_EPI_SLAB: return launch<AK, BKM, SV_EPI_SLAB, BKT, S>(d, split, s);
-    case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, BKT, S>(d, split, s);
-    case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, BKT, S>(d, split, s);
+    case SV_EPI_STORE: return launch<AK, BKM, SV_EPI_STORE, 32, OCC>(d, split, s);
+    case SV_EPI_BIAS_GELU2: return launch<AK, BKM, SV_EPI_BIAS_GELU2, 32, OCC>(d, split, s);
+    case SV_EPI_BIAS_GAMMA_RES: return launch<AK, BKM, SV_EPI_BIAS_GAMMA_RES, 32, OCC>(d, split, s);
+    case SV_EPI_GELU_GRAD: return launch<AK, BKM, SV_EPI_GELU_GRAD, 32, OCC>(d, split, s);
+    case SV_EPI_SLAB: return launch<AK, BKM, SV_EPI_SLAB, 32, OCC>(d, split, s);
+    case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, 32, OCC>(d, split, s);
+    case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, 32, OCC>(d, split, s);
     default: return SV_ERR_UNSUPPORTED;
   }
 }
 
-template <int BKT, int S>
-static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
-  if (d->K % BKT != 0 || d->K < BKT) return SV_ERR_UNSUPPORTED;
-  if (d->a_kmajor && d->b_kmajor) return launch_epi<true, true, BKT, S>(d, split, s);
-  if (d->a_kmajor && !d->b_kmajor) return launch_epi<true, false, BKT, S>(d, split, s);
-  if (!d->a_kmajor && d->b_kmajor) return launch_epi<false, true, BKT, S>(d, split, s);
-  return launch_epi<false, false, BKT, S>(d, split, s);
+template <int OCC>
+static int launch_occ(const sv_gemm_desc* d, int split, hipStream_t s) {
+  if (d->K % 32 != 0 || d->K < 32) return SV_ERR_UNSUPPORTED;
+  if (d->a_kmajor && d->b_kmajor) return launch_epi<true, true, OCC>(d, split, s);
+  if (d->a_kmajor && !d->b_kmajor) return launch_epi<true, false, OCC>(d, split, s);
+  if (!d->a_kmajor && d->b_kmajor) return launch_epi<false, true, OCC>(d, split, s);
+  return launch_epi<false, false, OCC>(d, split, s);
 }
 
-}  // namespace g3
+}  // namespace g7
 
-int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg) {
-  using namespace g3;
+int launch_gemm7(const sv_gemm_desc* d, hipStream_t s, int occ) {
+  using namespace g7;
   if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->a_scale_k)
     return SV_ERR_UNSUPPORTED;
   const int split = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
-  // BKxSTAGES: 32x3 (default: two workgroups per CU), 32x4, 64x2, 64x3; SV_GEMM3_CFG overrides
-  static const char* env = getenv("SV_GEMM3_CFG");
-  if (env) cfg = env;
-  if (!cfg) cfg = "32x3";
-  if (!strcmp(cfg, "32x4")) return launch_cfg<32, 4>(d, split, s);
-  if (!strcmp(cfg, "64x2")) return launch_cfg<64, 2>(d, split, s);
-  if (!strcmp(cfg, "64x3")) return launch_cfg<64, 3>(d, split, s);
-  return launch_cfg<32, 3>(d, split, s);
+  static const int occ_env = getenv("SV_GEMM7_OCC") ? atoi(getenv("SV_GEMM7_OCC")) : 0;
+  if (occ_env) occ = occ_env;
+  return occ == 2 ? launch_occ<2>(d, split, s) : launch_occ<4>(d, split, s);
 }
 
 }  // namespace sv

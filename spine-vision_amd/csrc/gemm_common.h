@@ -294,6 +294,8 @@ __device__ __forceinline__ void wave_tile_epilogue_wide(const f32x4 (&acc)[FM][F
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
 // v3 entry (gemm3.hip): same contract with K % BK == 0; cfg = "BKxSTAGES" (nullptr: 32x3)
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg = nullptr);
+// v7 entry (gemm7.hip, register-staged operand loads): occ 4 = two workgroups per CU, 2 = one
+int launch_gemm7(const sv_gemm_desc* d, hipStream_t s, int occ = 2);
 // v6 entry (gemm6.hip, 256x256 tile, one 4-wave workgroup per CU): same contract as v2
 int launch_gemm6(const sv_gemm_desc* d, hipStream_t s);
 
