@@ -184,8 +184,9 @@ int sv_layerscale_wgrad_finish(const float* G, const float* cs, const float* W2,
 
 /* fc2 weight-gradient finish fused with its split-K reduction (replaces sv_reduce_partials_pair +
  * sv_layerscale_wgrad_finish): slab[P][C][K4] and cs_part[P][C] are the SV_EPI_SLAB outputs of the
- * wgrad GEMM d_out^T * GELU(h); same accumulation semantics as sv_layerscale_wgrad_finish.  ws: f32
- * workspace of sv_layerscale_wgrad_reduce_ws(C, K4) elements.  K4 % 64 == 0.                       */
+ * wgrad GEMM d_out^T * GELU(h); same accumulation semantics as sv_layerscale_wgrad_finish.  One
+ * workgroup per row; ws is unused (sv_layerscale_wgrad_reduce_ws returns 0, ws may be NULL).
+ * K4 % 4 == 0.                                                                                       */
 int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4);
 int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t P, const float* W2,
                                const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2,

@@ -72,47 +72,68 @@ struct RedSeg {
   float* out;
 };
 
+// Two independent column reductions in one launch: workgroup `blk` < blocks_a reduces COLS = 4 * C4
+// consecutive columns of segment a over its P partial rows, the rest segment b.  256 threads =
+// C4 float4 column groups x (256 / C4) partial-row groups, folded through LDS in a fixed order.  The
+// launcher picks C4 so that even short outputs (LayerNorm dw/db: 2 x C columns over ~1000 partial
+// rows) spread over enough workgroups.
+template <int C4>
 __global__ void __launch_bounds__(kThreads) reduce_pair_kernel(RedSeg a, RedSeg b, int64_t blocks_a, int P,
                                                                float alpha, int accumulate) {
-  __shared__ float4 red[16][16];
+  constexpr int PG = kThreads / C4;
+  __shared__ float4 red[PG][C4];
   const bool sb = blockIdx.x >= blocks_a;
   const RedSeg sg = sb ? b : a;
   const int64_t blk = sb ? blockIdx.x - blocks_a : blockIdx.x;
-  const int c4 = threadIdx.x & 15, pg = threadIdx.x >> 4;
-  const int64_t col = blk * 64 + c4 * 4;
+  const int c4 = threadIdx.x % C4, pg = threadIdx.x / C4;
+  const int64_t col = blk * (4 * C4) + c4 * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col + 4 <= sg.n) {
     int p = pg;
-    for (; p + 48 < P; p += 64) {
+    for (; p + 3 * PG < P; p += 4 * PG) {
       float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sg.part + (size_t)(p + 16 * u) * sg.n + col);
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sg.part + (size_t)(p + PG * u) * sg.n + col);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
-    for (; p < P; p += 16) {
+    for (; p < P; p += PG) {
       const float4 v = *reinterpret_cast<const float4*>(sg.part + (size_t)p * sg.n + col);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
   } else if (col < sg.n) {  // ragged tail (n % 4 != 0)
     float t[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int p = pg; p < P; p += 16)
+    for (int p = pg; p < P; p += PG)
       for (int j = 0; j < 4 && col + j < sg.n; ++j) t[j] += sg.part[(size_t)p * sg.n + col + j];
     acc = make_float4(t[0], t[1], t[2], t[3]);
   }
   red[pg][c4] = acc;
   __syncthreads();
-  if (threadIdx.x < 16 && col < sg.n) {
-    float4 s = red[0][c4];
-#pragma unroll
-    for (int g = 1; g < 16; ++g) {
-      const float4 v = red[g][c4];
+  // fold the PG partial groups: C4 * 16 threads each sum PG/16 groups, then 16 -> 1 in one wave
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int F = PG >= 16 ? 16 : PG;
+  if (threadIdx.x < C4 * F) {
+    const int cc = threadIdx.x % C4, f = threadIdx.x / C4;
+    for (int g = f; g < PG; g += F) {
+      const float4 v = red[g][cc];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    const float r[4] = {s.x * alpha, s.y * alpha, s.z * alpha, s.w * alpha};
-    for (int j = 0; j < 4 && col + j < sg.n; ++j) sg.out[col + j] = accumulate ? sg.out[col + j] + r[j] : r[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < C4 * F) red[threadIdx.x / C4][threadIdx.x % C4] = s;
+  __syncthreads();
+  const int64_t c0 = blk * (4 * C4);
+  if (threadIdx.x < C4) {
+    float4 t = red[0][threadIdx.x];
+    for (int g = 1; g < F; ++g) {
+      const float4 v = red[g][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const int64_t cl = c0 + threadIdx.x * 4;
+    const float r[4] = {t.x * alpha, t.y * alpha, t.z * alpha, t.w * alpha};
+    for (int j = 0; j < 4 && cl + j < sg.n; ++j) sg.out[cl + j] = accumulate ? sg.out[cl + j] + r[j] : r[j];
   }
 }
 
@@ -155,84 +176,53 @@ __global__ void __launch_bounds__(kThreads) layerscale_finish_kernel(
 
 
 // fc2 wgrad split-K reduction fused with the layer-scale finish (replaces reduce_pair + finish):
-// workgroup `blk` < blocks_a sums the P slabs of 64 consecutive columns of one row c of G (K4 % 64
-// == 0), writes dW2 += gamma_c G and a partial row dot sum(W2 G) -> dot_part[blk]; the remaining
-// workgroups reduce the P colsum partials into cs_out.  layerscale_final folds the dots.
+// one workgroup per row c of G = sum_p slab[p][c][:]: thread t owns the float4 column groups
+// t, t + 256, ...; dW2[c] += gamma_c G[c], the row dot sum(W2[c] G[c]) and the colsum
+// cs[c] = sum_p cs_part[p][c] are block sums (fixed order), so one kernel finishes dgamma / db2 too.
 __global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float* __restrict__ slab,
                                                                      const float* __restrict__ cs_part, int P,
                                                                      const float* __restrict__ W2,
                                                                      const float* __restrict__ gamma,
-                                                                     float* __restrict__ dW2,
-                                                                     float* __restrict__ dot_part,
-                                                                     float* __restrict__ cs_out, int64_t nA, int K4,
-                                                                     int C, int64_t blocks_a) {
-  __shared__ float4 red[16][16];
-  const int c4 = threadIdx.x & 15, pg = threadIdx.x >> 4;
-  const bool seg_b = blockIdx.x >= blocks_a;
-  const int64_t blk = seg_b ? blockIdx.x - blocks_a : blockIdx.x;
-  const int64_t col = blk * 64 + c4 * 4;
-  const int64_t n = seg_b ? C : nA;
-  const float* part = seg_b ? cs_part : slab;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col + 4 <= n) {
-    int p = pg;
-    for (; p + 48 < P; p += 64) {
-      float4 v[4];
+                                                                     const float* __restrict__ b2,
+                                                                     float* __restrict__ dW2, float* __restrict__ dgamma,
+                                                                     float* __restrict__ db2, int C, int K4) {
+  __shared__ float red[kThreads / 64];
+  const int c = blockIdx.x;
+  const int ng = K4 / 4;
+  const size_t rowoff = (size_t)c * K4, pstride = (size_t)C * K4;
+  const float gc = gamma[c];
+  float dot = 0.f;
+  for (int gi = threadIdx.x; gi < ng; gi += kThreads) {
+    const size_t off = rowoff + (size_t)gi * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int p = 0;
+    for (; p + 8 <= P; p += 8) {
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (size_t)(p + 16 * u) * n + col);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (size_t)(p + u) * pstride + off);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
-    for (; p < P; p += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * n + col);
+    for (; p < P; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (size_t)p * pstride + off);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-  } else if (col < n) {
-    float t[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int p = pg; p < P; p += 16)
-      for (int j = 0; j < 4 && col + j < n; ++j) t[j] += part[(size_t)p * n + col + j];
-    acc = make_float4(t[0], t[1], t[2], t[3]);
+    const float4 w = *reinterpret_cast<const float4*>(W2 + off);
+    float4 o = *reinterpret_cast<const float4*>(dW2 + off);
+    o.x += gc * acc.x; o.y += gc * acc.y; o.z += gc * acc.z; o.w += gc * acc.w;
+    *reinterpret_cast<float4*>(dW2 + off) = o;
+    dot += w.x * acc.x + w.y * acc.y + w.z * acc.z + w.w * acc.w;
   }
-  red[pg][c4] = acc;
-  __syncthreads();
-  if (threadIdx.x >= 16) return;
-  float4 s = red[0][c4];
-#pragma unroll
-  for (int g = 1; g < 16; ++g) {
-    const float4 v = red[g][c4];
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  float cs = 0.f;
+  for (int p = threadIdx.x; p < P; p += kThreads) cs += cs_part[(size_t)p * C + c];
+  dot = block_sum(dot, red);
+  cs = block_sum(cs, red);
+  if (threadIdx.x == 0) {
+    dgamma[c] += dot + b2[c] * cs;
+    db2[c] += gc * cs;
   }
-  if (seg_b) {
-    const float r[4] = {s.x, s.y, s.z, s.w};
-    for (int j = 0; j < 4 && col + j < n; ++j) cs_out[col + j] = r[j];
-    return;
-  }
-  const int c = (int)(col / K4);
-  const float gc = gamma[c];
-  const float4 w = *reinterpret_cast<const float4*>(W2 + col);
-  float4 o = *reinterpret_cast<const float4*>(dW2 + col);
-  o.x += gc * s.x; o.y += gc * s.y; o.z += gc * s.z; o.w += gc * s.w;
-  *reinterpret_cast<float4*>(dW2 + col) = o;
-  float d = w.x * s.x + w.y * s.y + w.z * s.z + w.w * s.w;
-#pragma unroll
-  for (int o2 = 8; o2 > 0; o2 >>= 1) d += __shfl_xor(d, o2, 16);
-  if (c4 == 0) dot_part[blk] = d;
-}
-
-__global__ void __launch_bounds__(kThreads) layerscale_final_kernel(const float* __restrict__ dot_part,
-                                                                    const float* __restrict__ cs,
-                                                                    const float* __restrict__ gamma,
-                                                                    const float* __restrict__ b2,
-                                                                    float* __restrict__ dgamma, float* __restrict__ db2,
-                                                                    int C, int nb) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int j = 0; j < nb; ++j) s += dot_part[(size_t)c * nb + j];
-  dgamma[c] += s + b2[c] * cs[c];
-  db2[c] += gamma[c] * cs[c];
 }
 
 constexpr int kSqBlocks = 1024;
@@ -342,10 +332,20 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
   SV_REQUIRE(!n_b || (part_b && out_b), "sv_reduce_partials_pair: bad second segment");
   if (n_a % 4 == 0) SV_REQUIRE((((uintptr_t)part_a) & 15) == 0, "sv_reduce_partials_pair: part_a must be 16-B aligned");
   if (n_b % 4 == 0 && n_b) SV_REQUIRE((((uintptr_t)part_b) & 15) == 0, "sv_reduce_partials_pair: part_b must be 16-B aligned");
-  const int64_t ba = (n_a + 63) / 64, bb = (n_b + 63) / 64;
-  if (ba + bb == 0) return SV_OK;
   RedSeg a{part_a, n_a, out_a}, b{part_b, n_b, out_b};
-  reduce_pair_kernel<<<(unsigned)(ba + bb), kThreads, 0, (hipStream_t)stream>>>(a, b, ba, P, alpha, accumulate);
+  hipStream_t s = (hipStream_t)stream;
+  // widest column block that still gives >= 512 workgroups (or 4 columns per workgroup)
+  int cols = 64;
+  while (cols > 4 && (n_a + cols - 1) / cols + (n_b + cols - 1) / cols < 512) cols >>= 1;
+  const int64_t ba = (n_a + cols - 1) / cols, bb = (n_b + cols - 1) / cols;
+  if (ba + bb == 0) return SV_OK;
+  switch (cols) {
+    case 64: reduce_pair_kernel<16><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+    case 32: reduce_pair_kernel<8><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+    case 16: reduce_pair_kernel<4><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+    case 8: reduce_pair_kernel<2><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+    default: reduce_pair_kernel<1><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+  }
   return check_launch("sv_reduce_partials_pair");
 }
 
@@ -397,25 +397,23 @@ int sv_layerscale_wgrad_finish(const float* G, const float* cs, const float* W2,
   return check_launch("sv_layerscale_wgrad_finish");
 }
 
-int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4) { return C * (K4 / 64) + C; }
+int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4) {
+  (void)C;
+  (void)K4;
+  return 0;  // no workspace: one workgroup per row finishes everything
+}
 
 int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t P, const float* W2,
                                const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2,
                                float* ws, int32_t C, int32_t K4, sv_stream_t stream) {
-  SV_REQUIRE(slab && cs_part && W2 && gamma && b2 && dW2 && dgamma && db2 && ws && P >= 1,
+  (void)ws;
+  SV_REQUIRE(slab && cs_part && W2 && gamma && b2 && dW2 && dgamma && db2 && P >= 1,
              "sv_layerscale_wgrad_reduce: bad arguments");
-  SV_REQUIRE(K4 % 64 == 0 && C > 0, "sv_layerscale_wgrad_reduce: K4=%d must be a multiple of 64", K4);
-  SV_REQUIRE((((uintptr_t)slab | (uintptr_t)cs_part | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
+  SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_reduce: K4=%d must be a multiple of 4", K4);
+  SV_REQUIRE((((uintptr_t)slab | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
              "sv_layerscale_wgrad_reduce: buffers must be 16-B aligned");
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t nA = (int64_t)C * K4;
-  const int64_t ba = nA / 64, bb = (C + 63) / 64;
-  float* dot_part = ws;
-  float* cs = ws + (size_t)C * (K4 / 64);
-  layerscale_reduce_kernel<<<(unsigned)(ba + bb), kThreads, 0, s>>>(slab, cs_part, P, W2, gamma, dW2, dot_part, cs,
-                                                                  nA, K4, C, ba);
-  layerscale_final_kernel<<<ceil_div(C, kThreads), kThreads, 0, s>>>(dot_part, cs, gamma, b2, dgamma, db2, C,
-                                                                   K4 / 64);
+  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(slab, cs_part, P, W2, gamma, b2, dW2, dgamma,
+                                                                   db2, C, K4);
   return check_launch("sv_layerscale_wgrad_reduce");
 }
 

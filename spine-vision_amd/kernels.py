@@ -179,8 +179,9 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
 def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf16=True):
     """fc2 weight / bias / layer-scale gradients of out = x + gamma * (a W2^T + b2) from d_out:
     dW2 += gamma (.) d^T a, dgamma += rowdot(W2, d^T a) + b2 (.) colsum(d), db2 += gamma (.) colsum(d).
-    The wgrad GEMM writes split-K slabs (+ colsum partials); ONE fused pass reduces them and applies
-    the layer-scale finish (sv_layerscale_wgrad_reduce) -- G = d^T a is never materialised."""
+    The wgrad GEMM writes split-K slabs (+ colsum partials); ONE fused pass (a workgroup per row)
+    reduces them and applies the layer-scale finish (sv_layerscale_wgrad_reduce) -- G = d^T a is
+    never materialised."""
     M, C = dsrc2d.shape
     K4 = a2d.shape[1]
     tiles = -(-C // 128) * -(-K4 // 128)
@@ -189,9 +190,8 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
     gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
-    ws = torch.empty(value("sv_layerscale_wgrad_reduce_ws", C, K4), device=dsrc2d.device, dtype=torch.float32)
     call("sv_layerscale_wgrad_reduce", ptr(slab), ptr(cs), split, ptr(w2), ptr(gamma), ptr(b2), ptr(dw2),
-         ptr(dgamma), ptr(db2), ptr(ws), C, K4)
+         ptr(dgamma), ptr(db2), None, C, K4)
 
 
 # ----------------------------------------------------------------------------------------------
