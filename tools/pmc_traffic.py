@@ -4,7 +4,10 @@ gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts exactly 
 wide (16 B/lane) coalesced streaming read -- the LDS-DMA loads of the GEMM are such reads -- so it is
 doubled; WRITE_SIZE is exact for 16-B-per-lane stores (the GEMM epilogue's stores).
 
-    python tools/pmc_traffic.py <out_dir> <kernel substring> <key> [profiles/traffic.json]
+    python tools/pmc_traffic.py <out_dir> <kernel substrings, '|'-separated> <key> [profiles/traffic.json]
+
+A kernel CLASS (the forward GEMMs: fc1 on v3, fc2 on v2, downsample on v3) is matched by several
+substrings; the per-launch figure is the mean over every matched launch, like bench.py's probe.
 """
 import csv
 import json
@@ -12,6 +15,7 @@ import os
 import sys
 
 out, pat, key = sys.argv[1], sys.argv[2], sys.argv[3]
+pats = pat.split("|")
 dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/traffic.json"
 
 
@@ -19,7 +23,7 @@ def per_launch(counter):
     path = os.path.join(out, f"pmc_{counter}", "run_counter_collection.csv")
     vals = {}
     for r in csv.DictReader(open(path)):
-        if pat in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if any(p_ in r["Kernel_Name"] for p_ in pats) and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(vals.values()) / max(len(vals), 1), len(vals)
 
