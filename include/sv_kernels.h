@@ -100,7 +100,8 @@ int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float
                      int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C, float eps,
                      sv_stream_t stream);
 int sv_layernorm_bwd_nparts(int64_t rows, int32_t C);
-/* dy/x/dx dtype combinations: (f32,f32,f32), (f32,bf16,f32), (bf16,bf16,f32), (bf16,bf16,bf16).     */
+/* dy/x/dx dtype combinations: (f32,f32,f32), (f32,bf16,f32), (f32,bf16,bf16), (bf16,bf16,f32),
+ * (bf16,bf16,bf16).                                                                                */
 int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_dtype, const float* mean,
                      const float* rstd, const float* w, void* dx, int32_t dx_dtype, int32_t accumulate,
                      float* dw_part, float* db_part, int64_t rows, int32_t C, sv_stream_t stream);
@@ -137,6 +138,24 @@ int sv_stem_patchify_ln_bwd(const float* img, const float* w, const float* b, co
                             const float* mean, const float* rstd, const float* dy, float* dw_part,
                             float* db_part, float* dlnw_part, float* dlnb_part, int32_t B, int32_t H,
                             int32_t W, int32_t C, sv_stream_t stream);
+
+/* ---- ConvNeXt stem on MFMA (bf16 mode) + the batch input transform on the GPU -------------------
+ * The stem conv as one sv_gemm: patches [B*(H/4)*(W/4)][64] bf16 (k = ci*16 + kh*4 + kw, the
+ * flattened timm stem.0.weight [C,3,4,4]; k 48..63 zero) x wpack [C][64] bf16 (zero padded).
+ * img_kind SV_IMG_F32_NCHW: the reference batch["image"] [B,3,H,W] f32 (already normalised);
+ * SV_IMG_U8_GRAY: the decoded uint8 grayscale batch [B,H,W]; the reference transform
+ * (training/datasets/localization.py:196-233, 254: convert("RGB") -> ToTensor -> Normalize) is
+ * applied in flight as (u / 255 - mean[c]) / std[c] in f32.  norm_mean / norm_std: HOST float[3]
+ * (ignored for SV_IMG_F32_NCHW, may be NULL).                                                      */
+typedef enum { SV_IMG_F32_NCHW = 0, SV_IMG_U8_GRAY = 1 } sv_image_kind;
+int sv_stem_patchify(const void* img, int32_t img_kind, const float* norm_mean, const float* norm_std,
+                     uint16_t* patches, int32_t B, int32_t H, int32_t W, sv_stream_t stream);
+int sv_stem_weight_pack(const float* w, uint16_t* wpack, int32_t C, sv_stream_t stream);
+/* The same transform as a standalone op (row f1 of the scope table: the collator's ToTensor +
+ * Normalize on the device): img uint8 [B,H,W] -> out f32 [B,3,H,W], bitwise equal to torchvision's
+ * CPU result on the replicated RGB image.  H*W % 4 == 0; mean/std HOST float[3].                   */
+int sv_normalize_u8_gray(const uint8_t* img, const float* norm_mean, const float* norm_std, float* out,
+                         int32_t B, int32_t H, int32_t W, sv_stream_t stream);
 
 /* ---- ConvNeXt stage downsample: LayerNorm2d + 2x2/s2 patch gather (GEMM A operand) ------------
  * x [B,H,W,C] f32 -> patches [B*(H/2)*(W/2)][C*4] with k = c*4 + kh*2 + kw (= timm conv weight

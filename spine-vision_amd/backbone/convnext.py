@@ -170,7 +170,12 @@ class ConvNeXtHip(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             raise RuntimeError("ConvNeXtHip runs on the MI355X kernel library only (got a CPU tensor)")
-        x = x.float().contiguous()
+        if x.dtype == torch.uint8:
+            # decoded grayscale batch [B,H,W] (row f1): the reference transform runs on the device --
+            # inside the stem gather (bf16) or as the standalone normalise kernel (fp32 parity mode)
+            x = x.contiguous() if self.compute_bf16 else K.normalize_u8_gray(x.contiguous())
+        else:
+            x = x.float().contiguous()
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         if need_grad:
             anchor = torch.zeros((), device=x.device, requires_grad=True)
@@ -188,9 +193,22 @@ class ConvNeXtHip(nn.Module):
         tape = _Tape(img=img) if save else None
         cache: dict = tape.wcache if save else {}
         stem_conv, stem_ln = self.stem[0], self.stem[1]
-        x, s_mean, s_rstd = K.stem_fwd(img, stem_conv.weight, stem_conv.bias, stem_ln.weight, stem_ln.bias)
-        if save:
-            tape.stem = (s_mean, s_rstd)
+        if bf:
+            # stem conv on MFMA: 4x4 patch rows (bf16, K padded to 64) x packed weight, then LayerNorm2d
+            B, H0, W0 = img.shape[0], img.shape[-2], img.shape[-1]
+            C0 = stem_conv.weight.shape[0]
+            patches = K.stem_patchify(img)
+            z0 = torch.empty(patches.shape[0], C0, device=img.device, dtype=act)
+            K.linear_fwd(patches, K.stem_weight_pack(stem_conv.weight.detach()), out=z0, bias=stem_conv.bias,
+                         compute_bf16=True)
+            x2d, s_mean, s_rstd = K.layernorm_fwd(z0, stem_ln.weight, stem_ln.bias, out_dtype=torch.float32)
+            x = x2d.view(B, H0 // 4, W0 // 4, C0)
+            if save:
+                tape.stem = (patches, z0, s_mean, s_rstd)
+        else:
+            x, s_mean, s_rstd = K.stem_fwd(img, stem_conv.weight, stem_conv.bias, stem_ln.weight, stem_ln.bias)
+            if save:
+                tape.stem = (s_mean, s_rstd)
         for st in self.stages:
             ds_saved = None
             if not isinstance(st.downsample, nn.Identity):
@@ -337,10 +355,20 @@ class ConvNeXtHip(nn.Module):
                 d, db = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight),
                                          dlnb=g(ln.bias), with_bf16=bf)
                 self._ready([ln.weight, ln.bias, conv.weight, conv.bias])
-        s_mean, s_rstd = tape.stem
         conv, ln = self.stem[0], self.stem[1]
-        K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
-                   db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
+        if bf:
+            # LayerNorm2d backward (f32 gradient stream, bf16 saved conv output) -> bf16 dz, then the
+            # weight/bias gradient as one split-K wgrad GEMM over the saved patch rows (first 48 columns)
+            patches, z0, s_mean, s_rstd = tape.stem
+            C0 = conv.weight.shape[0]
+            dz0 = K.layernorm_bwd(d.view(-1, C0), z0, s_mean, s_rstd, ln.weight, dw=g(ln.weight), db=g(ln.bias),
+                                  out_dtype=torch.bfloat16)
+            K.linear_wgrad(dz0, patches, out=g(conv.weight).view(C0, 48), accumulate=True, bias_out=g(conv.bias),
+                           compute_bf16=True, cols=48)
+        else:
+            s_mean, s_rstd = tape.stem
+            K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
+                       db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
         nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient

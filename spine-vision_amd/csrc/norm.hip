@@ -811,6 +811,7 @@ int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_
                             rows, C))
     if (dy_dtype == SV_F32 && x_dtype == SV_F32 && dx_dtype == SV_F32) { LNBV(float, float, float); }
     else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_F32) { LNBV(float, uint16_t, float); }
+    else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) { LNBV(float, uint16_t, uint16_t); }
     else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_F32) { LNBV(uint16_t, uint16_t, float); }
     else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) { LNBV(uint16_t, uint16_t, uint16_t); }
     else return set_error(SV_ERR_UNSUPPORTED, "sv_layernorm_bwd: dtype combination (dy %d, x %d, dx %d) unsupported",
@@ -827,6 +828,8 @@ int sv_layernorm_bwd(const void* dy, int32_t dy_dtype, const void* x, int32_t x_
     LNB(float, float, float);
   } else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_F32) {
     LNB(float, uint16_t, float);
+  } else if (dy_dtype == SV_F32 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) {
+    LNB(float, uint16_t, uint16_t);
   } else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_F32) {
     LNB(uint16_t, uint16_t, float);
   } else if (dy_dtype == SV_BF16 && x_dtype == SV_BF16 && dx_dtype == SV_BF16) {

@@ -147,17 +147,19 @@ def _wgrad_split(tiles: int, K: int) -> int:
 
 
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
-                 compute_bf16=True) -> torch.Tensor:
+                 compute_bf16=True, cols=None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
     writes -- or, with ``accumulate``, adds -- into ``out``).  With ``bias_out`` the column sums of
-    dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum)."""
+    dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum).  ``cols``: use only the
+    first ``cols`` columns of x2d (the stem's 48 of its 64-wide padded patch rows)."""
     M, N = dy2d.shape
-    K = x2d.shape[1]
+    ldx = x2d.shape[1]
+    K = ldx if cols is None else cols
     tiles = -(-N // 128) * -(-K // 128)
     split = _wgrad_split(tiles, M)
     slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
-    gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, epilogue=nv.SV_EPI_SLAB,
+    gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
     if out is None:
         if split == 1 and not accumulate:
@@ -315,6 +317,57 @@ def stem_bwd(img, w, b, lnw, mean, rstd, dy, *, dw, db, dlnw, dlnb):
          ptr(pv[0]), ptr(pv[1]), ptr(pv[2]), B, H, W, C)
     reduce_pair(pw, dw, pv[0], db, P)
     reduce_pair(pv[1], dlnw, pv[2], dlnb, P)
+
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)  # torchvision Normalize constants of the reference transform
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _host3(v) -> ctypes.Array:
+    return (ctypes.c_float * 3)(*[float(x) for x in v])
+
+
+def stem_patchify(img, *, mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.Tensor:
+    """Stem patch rows for the MFMA stem conv: bf16 [B*(H/4)*(W/4), 64] (k = ci*16 + kh*4 + kw, 48..63
+    zero).  img: the normalised f32 batch [B,3,H,W] or a uint8 grayscale batch [B,H,W] (the reference
+    transform ToTensor + gray->RGB + Normalize(mean, std) is then applied in the gather)."""
+    if img.dtype == torch.uint8:
+        _check(img.dim() == 3 and img.is_contiguous(), "stem_patchify: uint8 input must be contiguous [B,H,W]")
+        B, H, W = img.shape
+        kind = nv.SV_IMG_U8_GRAY
+    else:
+        _check(img.dim() == 4 and img.shape[1] == 3 and img.dtype == torch.float32 and img.is_contiguous(),
+               "stem_patchify: expects contiguous f32 [B,3,H,W]")
+        B, _, H, W = img.shape
+        kind = nv.SV_IMG_F32_NCHW
+    _check(H % 4 == 0 and W % 4 == 0, "stem_patchify: H, W must be multiples of 4")
+    patches = torch.empty(B * (H // 4) * (W // 4), 64, device=img.device, dtype=torch.bfloat16)
+    call("sv_stem_patchify", ptr(img), kind, _host3(mean), _host3(std), ptr(patches), B, H, W)
+    return patches
+
+
+def stem_weight_pack(w) -> torch.Tensor:
+    """timm stem.0.weight [C,3,4,4] f32 -> bf16 [C,64] (k 48..63 zero), the B operand of the stem GEMM."""
+    C = w.shape[0]
+    _check(w.numel() == C * 48 and w.dtype == torch.float32 and w.is_contiguous(), "stem_weight_pack: bad weight")
+    out = torch.empty(C, 64, device=w.device, dtype=torch.bfloat16)
+    call("sv_stem_weight_pack", ptr(w), ptr(out), C)
+    return out
+
+
+def normalize_u8_gray(img_u8, *, mean=IMAGENET_MEAN, std=IMAGENET_STD, out=None) -> torch.Tensor:
+    """Device form of the reference transform tail (localization.py:196-233, 254): uint8 grayscale
+    [B,H,W] -> convert("RGB") -> ToTensor (/255) -> Normalize(mean, std) -> f32 [B,3,H,W]."""
+    _check(img_u8.dtype == torch.uint8 and img_u8.dim() == 3 and img_u8.is_contiguous(),
+           "normalize_u8_gray: expects contiguous uint8 [B,H,W]")
+    B, H, W = img_u8.shape
+    _check((H * W) % 4 == 0, "normalize_u8_gray: H*W must be a multiple of 4")
+    if out is None:
+        out = torch.empty(B, 3, H, W, device=img_u8.device, dtype=torch.float32)
+    _check(out.shape == (B, 3, H, W) and out.dtype == torch.float32 and out.is_contiguous(),
+           "normalize_u8_gray: bad out")
+    call("sv_normalize_u8_gray", ptr(img_u8), _host3(mean), _host3(std), ptr(out), B, H, W)
+    return out
 
 
 def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):

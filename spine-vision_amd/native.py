@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("SV_LIB_PATH") or os.path.join(_HERE, "libsv_kernels.s
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 
 SV_F32, SV_BF16 = 0, 1
+SV_IMG_F32_NCHW, SV_IMG_U8_GRAY = 0, 1
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
  SV_EPI_MUL_AUX) = range(7)
 
@@ -69,6 +70,9 @@ _SIGS = {
     "sv_stem_patchify_ln_fwd": [_p, _p, _p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_bwd_nparts": [_i32, _i32, _i32, _i32],
     "sv_stem_patchify_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
+    "sv_stem_patchify": [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _p],
+    "sv_stem_weight_pack": [_p, _p, _i32, _p],
+    "sv_normalize_u8_gray": [_p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_downsample_ln_patch2_fwd": [_p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_downsample_ln_patch2_bwd_nparts": [_i32, _i32, _i32, _i32],
     "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],

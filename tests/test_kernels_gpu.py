@@ -232,6 +232,61 @@ def test_stem(dev, C):
         assert rel(got, ref) < 1e-5
 
 
+def _ref_patches(img):
+    """[B,3,H,W] -> [B*(H/4)*(W/4), 64] rows, k = ci*16 + kh*4 + kw (48..63 zero), as f32."""
+    B, _, H, W = img.shape
+    p = img.view(B, 3, H // 4, 4, W // 4, 4).permute(0, 2, 4, 1, 3, 5).reshape(-1, 48)
+    return torch.cat([p, torch.zeros(p.shape[0], 16)], 1)
+
+
+def test_stem_patchify_and_weight_pack(dev):
+    g = torch.Generator().manual_seed(11)
+    B, H, W, C = 3, 32, 40, 128
+    img = torch.randn(B, 3, H, W, generator=g)
+    got = K.stem_patchify(img.to(dev)).cpu()
+    assert torch.equal(got, _ref_patches(img).to(torch.bfloat16))  # bitwise: same RNE rounding
+    w = torch.randn(C, 3, 4, 4, generator=g)
+    wp = K.stem_weight_pack(w.to(dev)).cpu()
+    assert torch.equal(wp[:, :48], w.view(C, 48).to(torch.bfloat16)) and not wp[:, 48:].any()
+
+
+def test_normalize_u8_gray_bitwise(dev):
+    """Device transform == the reference's CPU transform (Image.convert("RGB") -> ToTensor -> Normalize,
+    localization.py:196-233, 254) bit for bit, and the u8 stem gather == the gather of that tensor."""
+    from spine_vision_amd.training.datasets.localization import normalize_u8
+
+    g = torch.Generator().manual_seed(5)
+    B, H, W = 2, 64, 48
+    u8 = torch.randint(0, 256, (B, H, W), generator=g, dtype=torch.uint8)
+    u8[0, 0, :4] = torch.tensor([0, 1, 254, 255], dtype=torch.uint8)
+    ref = torch.stack([normalize_u8(u8[i]) for i in range(B)])
+    got = K.normalize_u8_gray(u8.to(dev)).cpu()
+    assert torch.equal(got, ref)
+    assert torch.equal(K.stem_patchify(u8.to(dev)).cpu(), K.stem_patchify(ref.to(dev)).cpu())
+
+
+def test_stem_mfma_path(dev):
+    """bf16 stem = patch gather + v3 GEMM (K 64) + LayerNorm; weight grad = split-K wgrad over 48 of
+    the 64 patch columns.  Against torch fp32 conv + LN on the same bf16-rounded operands."""
+    g = torch.Generator().manual_seed(3)
+    B, H, W, C = 2, 64, 64, 128
+    img = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(C, 3, 4, 4, generator=g) * 0.2
+    b = torch.randn(C, generator=g) * 0.1
+    patches = K.stem_patchify(img.to(dev))
+    z = torch.empty(patches.shape[0], C, device=dev, dtype=torch.bfloat16)
+    K.linear_fwd(patches, K.stem_weight_pack(w.to(dev)), out=z, bias=b.to(dev), compute_bf16=True)
+    zr = F.conv2d(bf(img), bf(w), b, stride=4).permute(0, 2, 3, 1).reshape(-1, C)
+    assert rel(z, zr) < 4e-3
+    dz = torch.randn(patches.shape[0], C, generator=g).to(torch.bfloat16)
+    dw = torch.zeros(C, 48, device=dev)
+    db = torch.zeros(C, device=dev)
+    K.linear_wgrad(dz.to(dev), patches, out=dw, accumulate=True, bias_out=db, compute_bf16=True, cols=48)
+    ref_w = dz.float().t() @ _ref_patches(bf(img))[:, :48]
+    assert rel(dw, ref_w) < 2e-3
+    assert rel(db, dz.float().sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("C", [128, 256])
 def test_downsample(dev, C):
     g = torch.Generator().manual_seed(C + 1)
@@ -326,11 +381,14 @@ def test_adamw_and_clip(dev):
 
 # ------------------------------------------------- bf16 gradient paths (bf16 mode: dy, dz in bf16)
 @pytest.mark.parametrize("C", [128, 512])
-def test_layernorm_bwd_bf16_io(dev, C):
+@pytest.mark.parametrize("dy_f32", [False, True])
+def test_layernorm_bwd_bf16_io(dev, C, dy_f32):
     g = torch.Generator().manual_seed(C + 1)
     x = (torch.randn(333, C, generator=g) * 2 + 0.5).to(torch.bfloat16)
     w = torch.rand(C, generator=g) + 0.5
-    dy = torch.randn(333, C, generator=g).to(torch.bfloat16)
+    dy = torch.randn(333, C, generator=g)
+    if not dy_f32:  # (f32, bf16, bf16) is the stem's combination: f32 gradient stream, bf16 saved input
+        dy = dy.to(torch.bfloat16)
     xr = x.double().requires_grad_(True)
     wr = w.double().requires_grad_(True)
     yr = F.layer_norm(xr, (C,), wr, None, 1e-6)
