@@ -36,8 +36,9 @@ class LocalizationDataset(Dataset):
     def __init__(self, data_path: Path, split: Literal["train", "val", "test", "all"] = "all", val_ratio: float = 0.15,
                  test_ratio: float = 0.05, series_types: list[str] | None = None, sources: list[str] | None = None,
                  image_size: tuple[int, int] = (256, 256), augment: bool = True, normalize: bool = True,
-                 seed: int = 42) -> None:
+                 seed: int = 42, device_transform: bool = False) -> None:
         self.data_path = Path(data_path)
+        self.device_transform = device_transform
         self.split = split
         self.image_size = tuple(image_size)
         self.augment = augment and split == "train"
@@ -80,7 +81,10 @@ class LocalizationDataset(Dataset):
         rel = self.image_list[i]
         rec = self.image_records[rel]
         u8 = self._load(rel)
-        image = normalize_u8(u8) if self.normalize else u8.float().div(255).unsqueeze(0).expand(3, -1, -1)
+        if self.device_transform:  # uint8 [H,W]; normalised on the GPU (kernels.normalize_u8_gray / stem)
+            image = u8
+        else:
+            image = normalize_u8(u8) if self.normalize else u8.float().div(255).unsqueeze(0).expand(3, -1, -1)
         coords = torch.zeros(NUM_LEVELS, 2)
         mask = torch.zeros(NUM_LEVELS)
         for lvl, (x, y) in rec["coords"].items():
@@ -105,8 +109,10 @@ class SyntheticLocalizationDataset(Dataset):
     """Seeded synthetic samples with the BASELINE input spec: uint8 grayscale U{0..255} -> RGB ->
     /255 -> ImageNet normalise; coords U(0.05, 0.95); ~10% of levels masked."""
 
-    def __init__(self, n: int, image_size: tuple[int, int] = (512, 512), seed: int = 42) -> None:
+    def __init__(self, n: int, image_size: tuple[int, int] = (512, 512), seed: int = 42,
+                 device_transform: bool = False) -> None:
         self.n, self.image_size, self.seed = n, tuple(image_size), seed
+        self.device_transform = device_transform
 
     def __len__(self) -> int:
         return self.n
@@ -116,7 +122,7 @@ class SyntheticLocalizationDataset(Dataset):
         u8 = torch.randint(0, 256, self.image_size, generator=g, dtype=torch.uint8)
         coords = torch.rand(NUM_LEVELS, 2, generator=g) * 0.9 + 0.05
         mask = (torch.rand(NUM_LEVELS, generator=g) >= 0.1).float()
-        return {"image": normalize_u8(u8), "coords": coords, "mask": mask, "series_type_idx": 1,
+        return {"image": u8 if self.device_transform else normalize_u8(u8), "coords": coords, "mask": mask, "series_type_idx": 1,
                 "metadata": {"image_path": f"synthetic_{i}.png", "source": "synthetic", "series_type": "sag_t2"}}
 
     def get_stats(self) -> dict[str, Any]:

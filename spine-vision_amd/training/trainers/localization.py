@@ -53,11 +53,13 @@ class LocalizationTrainer(BaseTrainer):
         if train_dataset is None:
             train_dataset = LocalizationDataset(Path(config.data_path), split="train", val_ratio=config.val_split,
                                                 series_types=config.series_types, sources=config.sources,
-                                                image_size=config.image_size, augment=config.augment)
+                                                image_size=config.image_size, augment=config.augment,
+                                                device_transform=config.device_transform)
         if val_dataset is None:
             val_dataset = LocalizationDataset(Path(config.data_path), split="val", val_ratio=config.val_split,
                                               series_types=config.series_types, sources=config.sources,
-                                              image_size=config.image_size, augment=False)
+                                              image_size=config.image_size, augment=False,
+                                              device_transform=config.device_transform)
         super().__init__(config, model, train_dataset, val_dataset)
         self.metrics = LocalizationMetrics(pck_thresholds=config.pck_thresholds,
                                            level_names=list(IDX_TO_LEVEL.values()))
@@ -129,7 +131,8 @@ class LocalizationTrainer(BaseTrainer):
             c = self.config
             test_dataset = LocalizationDataset(Path(c.data_path), split="test", val_ratio=c.val_split,
                                                series_types=c.series_types, sources=c.sources,
-                                               image_size=c.image_size, augment=False)
+                                               image_size=c.image_size, augment=False,
+                                               device_transform=c.device_transform)
         saved = self.val_loader
         self.val_loader = self._create_dataloader(test_dataset, shuffle=False)
         try:

@@ -146,3 +146,19 @@ def test_sharding_matches_accelerate(world, n, bs, drop):
         m = min(len(ours), len(ref))
         assert ours[:m] == ref[:m]
         assert len(ours) == len(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
+
+
+def test_device_transform_dataset_contract():
+    """Row f1 host side: with device_transform the dataset yields the decoded uint8 image and the
+    collator stacks [B,H,W] uint8; normalising it gives exactly the host-transform sample."""
+    from spine_vision_amd.training.datasets import LocalizationCollator, SyntheticLocalizationDataset
+    from spine_vision_amd.training.datasets.localization import normalize_u8
+
+    a = SyntheticLocalizationDataset(3, (32, 32), seed=9, device_transform=True)
+    b = SyntheticLocalizationDataset(3, (32, 32), seed=9)
+    for i in range(3):
+        assert a[i]["image"].dtype == torch.uint8
+        assert torch.equal(normalize_u8(a[i]["image"]), b[i]["image"])
+        assert torch.equal(a[i]["coords"], b[i]["coords"]) and torch.equal(a[i]["mask"], b[i]["mask"])
+    batch = LocalizationCollator()([a[i] for i in range(3)])
+    assert batch["image"].shape == (3, 32, 32) and batch["image"].dtype == torch.uint8

@@ -27,6 +27,35 @@ def test_localization_trainer_gpu(dev, tmp_path, precision):
     assert len(ck["optimizer_state_dict"]["state"]) == len(list(tr.model.parameters()))
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_device_transform_matches_host_transform(dev, precision):
+    """Row f1: uint8 batches normalised on the device (inside the stem gather in bf16, by
+    sv_normalize_u8_gray in fp32) give the SAME training step as the reference's host transform:
+    identical stem input bits, so identical loss, gradients and updated weights."""
+    from oracle import weights as ow
+    from spine_vision_amd.training import StepEngine
+    from spine_vision_amd.training.datasets import LocalizationCollator
+
+    ds_u8 = SyntheticLocalizationDataset(4, (64, 64), seed=3, device_transform=True)
+    ds_f = SyntheticLocalizationDataset(4, (64, 64), seed=3)
+    col = LocalizationCollator()
+    b_u8 = col([ds_u8[i] for i in range(4)])
+    b_f = col([ds_f[i] for i in range(4)])
+    assert b_u8["image"].dtype == torch.uint8 and b_u8["image"].shape == (4, 64, 64)
+    out = []
+    for batch in (b_u8, b_f):
+        m = CoordinateRegressor("convnext_base", pretrained=False, dropout=0.0, precision=precision)
+        ow.fill_module(m)
+        m = m.to(dev).train()
+        eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+        loss = eng.step_localization(batch["image"].to(dev), batch["coords"].to(dev), batch["mask"].to(dev))
+        out.append((float(loss), float(eng.last_grad_norm), m.backbone.stem[0].weight.detach().cpu(),
+                    m.head[5].weight.detach().cpu()))
+    (l0, n0, w0, h0), (l1, n1, w1, h1) = out
+    assert l0 == l1 and n0 == n1
+    assert torch.equal(w0, w1) and torch.equal(h0, h1)
+
+
 @pytest.mark.parametrize("backbone,precision", [("resnet18", "bf16"), ("resnet50", "fp32")])
 def test_classification_trainer_gpu(dev, tmp_path, backbone, precision):
     from spine_vision_amd.training import ClassificationConfig, ClassificationTrainer
