@@ -294,6 +294,7 @@ using namespace sv;
 
 namespace sv {
 int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
+int g_store_wt = getenv("SV_STORE_WT") ? atoi(getenv("SV_STORE_WT")) : 0;
 }
 
 extern "C" int sv_gemm_set_workgroups_per_cu(int32_t n) {

@@ -241,6 +241,7 @@ static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
+  e.wt = g_store_wt;
   constexpr size_t lds = Cfg<BN>::LDS;
   static bool attr_set = false;
   if (!attr_set) {

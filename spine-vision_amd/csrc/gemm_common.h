@@ -21,7 +21,18 @@ struct EpiArgs {
   const float* bias;
   const float* gamma;
   const void* aux; int aux_dtype; int64_t ld_aux;
+  int wt = 0;  // 1: epilogue stores write-through (sc1), see st16_wt
 };
+
+// Write-through 16-B store (global_store_dwordx4 ... sc1): the line leaves the XCD's L2 with the store
+// and is not left dirty, so the kernel-end L2 write-back (the dependent-launch boundary grows by
+// dirty bytes / ~6 TB/s, MI355X_MICROARCH.md "boundary") has nothing to flush.  Issued as inline
+// asm: hipcc has no sc1 store builtin for flat/global pointers.  vmcnt still counts it.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_wt(void* p, uint4 v) {
+  const u32x4_t d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+}
 
 __device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
   return dt == SV_F32 ? ld4(reinterpret_cast<const float*>(p), i) : ld4(reinterpret_cast<const uint16_t*>(p), i);
@@ -82,6 +93,17 @@ __device__ __forceinline__ void st8_any(void* p, int dt, size_t i, float4 a, flo
   } else {
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p) + i) =
         make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
+  }
+}
+__device__ __forceinline__ void st8_out(void* p, int dt, size_t i, float4 a, float4 b, int wt) {
+  if (!wt) return st8_any(p, dt, i, a, b);
+  if (dt == SV_F32) {
+    float* f = reinterpret_cast<float*>(p) + i;
+    st16_wt(f, make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w)));
+    st16_wt(f + 4, make_uint4(__float_as_uint(b.x), __float_as_uint(b.y), __float_as_uint(b.z), __float_as_uint(b.w)));
+  } else {
+    st16_wt(reinterpret_cast<uint16_t*>(p) + i,
+            make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w)));
   }
 }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -216,8 +238,11 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       float4 vb = make_float4(sp[4], sp[5], sp[6], sp[7]);
       if (slab_out) {
         float* C = reinterpret_cast<float*>(e.C) + (size_t)split * e.M * e.N + (size_t)m * e.N + n;
-        *reinterpret_cast<float4*>(C) = va;
-        if (okn4) *reinterpret_cast<float4*>(C + 4) = vb;
+        if (okn4) {
+          st8_out(C, SV_F32, 0, va, vb, e.wt);
+        } else {
+          *reinterpret_cast<float4*>(C) = va;
+        }
         continue;
       }
       va = add4(va, b0);
@@ -243,13 +268,13 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         ob = ggrad4(vb, xb[si][h]);
       }
       const size_t ci = (size_t)m * e.ldc + n;
-      if (okn4) st8_any(e.C, e.c_dtype, ci, oa, ob);
+      if (okn4) st8_out(e.C, e.c_dtype, ci, oa, ob, e.wt);
       else st4_any(e.C, e.c_dtype, ci, oa);
       if (e.epi == SV_EPI_BIAS_GELU2) {
-        if (okn4) st8_any(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb));
+        if (okn4) st8_out(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb), e.wt);
         else st4_any(e.C2, e.c2_dtype, ci, gelu4(va));
       } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
-        if (okn4) st8_any(e.C2, e.c2_dtype, ci, va, vb);
+        if (okn4) st8_out(e.C2, e.c2_dtype, ci, va, vb, e.wt);
         else st4_any(e.C2, e.c2_dtype, ci, va);
       }
     }
@@ -289,6 +314,9 @@ __device__ __forceinline__ void wave_tile_epilogue_wide(const f32x4 (&acc)[FM][F
     if constexpr (FN >= 8) wave_group_epilogue<FM, PRE, FN, 4>(acc, 4, slab, mb + 64, nb + 64, e, split);
   }
 }
+
+// SV_STORE_WT=1: write-through (sc1) epilogue stores in the v2/v3 GEMMs (gemm.hip reads the env once)
+extern int g_store_wt;
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
