@@ -228,6 +228,8 @@ def main():
                 "resident in HBM; random-init weights")
     else:
         metric = METRIC
+        if (args.backbone, args.image_size, args.batch) != ("convnext_base", 512, 32):
+            metric = f"images/sec training, {args.backbone} {args.image_size}x{args.image_size} loc, bs{args.batch}"
         workload = f"CoordinateRegressor({args.backbone}) localization train step fwd+bwd+allreduce+clip+AdamW"
         data = "synthetic uint8 512x512 grayscale->RGB, ImageNet-normalised, resident in HBM; random-init weights"
     if cls:

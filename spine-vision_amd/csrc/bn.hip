@@ -5,7 +5,7 @@
 // (timm/models/resnet.py, built at spine_vision/training/models/backbone.py:166) and their autograd
 // backward.  All kernels are HBM-bound streaming passes: one thread owns 4 consecutive channels
 // (16-B f32 / 8-B bf16 accesses), channel statistics are reduced per block into deterministic
-// partials [nparts][2][C] and finished by a one-thread-per-channel pass (no atomics, bit-stable).
+// partials [nparts][2][C] and finished by a 16-wave fold per 64 channels (no atomics, bit-stable).
 // Batch statistics use shifted sums (shift = the channel's value in row 0) so mean^2 >> var does
 // not cancel catastrophically in f32.
 #include <math.h>
@@ -93,16 +93,52 @@ __global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict_
   reduce_write(s1, s2, tpr, rp, c, C, part);
 }
 
-__global__ void stats_finish_kernel(const void* __restrict__ y, int ydt, const float* __restrict__ part, int P,
-                                    int64_t rows, int C, float eps, float momentum, float* __restrict__ mean,
-                                    float* __restrict__ rstd, float* __restrict__ rmean, float* __restrict__ rvar) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int p = 0; p < P; ++p) {
-    s1 += part[(size_t)p * 2 * C + c];
-    s2 += part[(size_t)p * 2 * C + C + c];
+// Sum of the per-block partials [P][2][C] for 64 channels per workgroup: the 16 waves of the
+// workgroup take every 16th partial (lane = channel, 256-B coalesced loads, 4 independent accumulator
+// pairs in flight), then the wave sums are folded through LDS in a fixed order (bit-stable).  The old
+// one-thread-per-channel loop walked all P partials serially (156 us per BatchNorm at P = 1024).
+constexpr int kFinWaves = 16;
+__device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int P, int C, float& s1, float& s2) {
+  __shared__ float red[2][kFinWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int p = w;
+    for (; p + 3 * kFinWaves < P; p += 4 * kFinWaves) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* q = part + (size_t)(p + u * kFinWaves) * 2 * C + c;
+        a1[u] += q[0];
+        a2[u] += q[C];
+      }
+    }
+    for (; p < P; p += kFinWaves) {
+      a1[0] += part[(size_t)p * 2 * C + c];
+      a2[0] += part[(size_t)p * 2 * C + C + c];
+    }
   }
+  red[0][w][lane] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+  red[1][w][lane] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  __syncthreads();
+  if (w != 0 || c >= C) return false;
+  s1 = 0.f;
+  s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < kFinWaves; ++i) {
+    s1 += red[0][i][lane];
+    s2 += red[1][i][lane];
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
+    const void* __restrict__ y, int ydt, const float* __restrict__ part, int P, int64_t rows, int C, float eps,
+    float momentum, float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rmean,
+    float* __restrict__ rvar) {
+  float s1, s2;
+  if (!fold_partials(part, P, C, s1, s2)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float k = ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
   const float n = (float)rows;
   const float m1 = s1 / n;
@@ -196,15 +232,13 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
   reduce_write(s1, s2, tpr, rp, c, C, part);
 }
 
-__global__ void bwd_finish_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ sums,
-                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int p = 0; p < P; ++p) {
-    s1 += part[(size_t)p * 2 * C + c];
-    s2 += part[(size_t)p * 2 * C + C + c];
-  }
+__global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float* __restrict__ part, int P, int C,
+                                                                     float* __restrict__ sums,
+                                                                     float* __restrict__ dgamma,
+                                                                     float* __restrict__ dbeta) {
+  float s1, s2;
+  if (!fold_partials(part, P, C, s1, s2)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   sums[c] = s1;
   sums[C + c] = s2;
   if (dgamma) dgamma[c] += s2;
@@ -385,7 +419,7 @@ extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* p
                                   float* running_var, sv_stream_t stream) {
   SV_REQUIRE(y && part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
              "sv_bn_stats_finish: bad arguments");
-  stats_finish_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
+  stats_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
                                                                         momentum, mean, rstd, running_mean, running_var);
   return check_launch("sv_bn_stats_finish");
 }
@@ -431,7 +465,7 @@ extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void*
 extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
                                 sv_stream_t stream) {
   SV_REQUIRE(part && sums && nparts > 0 && C > 0, "sv_bn_bwd_finish: bad arguments");
-  bwd_finish_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
+  bwd_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
   return check_launch("sv_bn_bwd_finish");
 }
 

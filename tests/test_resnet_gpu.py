@@ -168,29 +168,38 @@ def _pair(name, precision, dev):
 
 @pytest.mark.parametrize("name", ["resnet18", "resnet50"])
 def test_resnet_fp32_forward_backward(dev, name):
+    """fp32 parity mode at 64x64, B=4.  layer4's train-mode BN normalises over 16 values per channel, so
+    the parameter gradients are ill-conditioned: the CPU fp32 oracle itself is up to 3.4% (resnet50)
+    away from float64.  Each HIP gradient is therefore checked against the oracle run in float64, within
+    max(1e-3, 3x the fp32 oracle's own error) -- the bound of test_classification_step_matches_oracle."""
+    import copy
+
     ref, hip = _pair(name, "fp32", dev)
     ref.train()
     hip.train()
+    r64 = copy.deepcopy(ref).double().train()
     img, _ = ow.classification_batch(4, 64, 64)
     f_ref = ref(img)
     f_hip = hip(img.to(dev))
+    f64 = r64(img.double())
     assert rel(f_hip, f_ref) < 1e-4
     dfeat = torch.from_numpy(ow.uniform("dfeat", f_ref.numel(), -1, 1).reshape(f_ref.shape))
     f_ref.backward(dfeat)
     f_hip.backward(dfeat.to(dev))
-    worst = 0.0
+    f64.backward(dfeat.double())
     hp = dict(hip.named_parameters())
+    p64 = dict(r64.named_parameters())
     for n, p in ref.named_parameters():
-        r = rel(hp[n].grad, p.grad)
-        worst = max(worst, r)
-        assert r < 1e-3, f"{n}: rel {r}"
+        g64 = p64[n].grad
+        e_hip = rel(hp[n].grad.double(), g64)
+        e_ora = rel(p.grad.double(), g64)
+        assert e_hip < max(1e-3, 3.0 * e_ora), f"{n}: hip {e_hip} vs fp32 oracle {e_ora}"
     hb = dict(hip.named_buffers())
     for n, b in ref.named_buffers():
         if b.is_floating_point():
             assert rel(hb[n], b) < 1e-5, n
         else:
             assert int(hb[n]) == int(b), n
-    print(f"{name}: worst grad rel {worst:.2e}")
 
 
 @pytest.mark.parametrize("name", ["resnet18", "resnet50"])
