@@ -275,9 +275,10 @@ int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int3
  * (unbiased variance, torch semantics) when they are non-NULL.                                    */
 int sv_bn_nparts(int64_t rows, int32_t C);
 int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream);
+/* num_batches_tracked (int64, nullable): incremented by one on the device (BatchNorm2d.num_batches_tracked). */
 int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows, int32_t C,
                        float eps, float momentum, float* mean, float* rstd, float* running_mean,
-                       float* running_var, sv_stream_t stream);
+                       float* running_var, int64_t* num_batches_tracked, sv_stream_t stream);
 /* eval mode: mean = running_mean, rstd = 1/sqrt(running_var + eps).                               */
 int sv_bn_eval_params(const float* running_mean, const float* running_var, float eps, float* mean, float* rstd,
                       int32_t C, sv_stream_t stream);

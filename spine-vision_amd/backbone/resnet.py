@@ -160,8 +160,7 @@ class ResNetHip(nn.Module):
         if self.training:
             momentum = 0.1 if bn.momentum is None else bn.momentum
             mean, rstd = K.bn_stats(y2d, eps=bn.eps, momentum=momentum, running_mean=bn.running_mean,
-                                    running_var=bn.running_var)
-            bn.num_batches_tracked.add_(1)
+                                    running_var=bn.running_var, num_batches_tracked=bn.num_batches_tracked)
             return mean, rstd
         return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
 

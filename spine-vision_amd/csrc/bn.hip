@@ -135,7 +135,8 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, in
 __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
     const void* __restrict__ y, int ydt, const float* __restrict__ part, int P, int64_t rows, int C, float eps,
     float momentum, float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rmean,
-    float* __restrict__ rvar) {
+    float* __restrict__ rvar, int64_t* __restrict__ nbt) {
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   float s1, s2;
   if (!fold_partials(part, P, C, s1, s2)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -416,11 +417,12 @@ extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t
 
 extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows,
                                   int32_t C, float eps, float momentum, float* mean, float* rstd, float* running_mean,
-                                  float* running_var, sv_stream_t stream) {
+                                  float* running_var, int64_t* num_batches_tracked, sv_stream_t stream) {
   SV_REQUIRE(y && part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
              "sv_bn_stats_finish: bad arguments");
   stats_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
-                                                                        momentum, mean, rstd, running_mean, running_var);
+                                                                        momentum, mean, rstd, running_mean, running_var,
+                                                                        num_batches_tracked);
   return check_launch("sv_bn_stats_finish");
 }
 

@@ -493,11 +493,24 @@ def _conv_check_x(x: torch.Tensor, s: nv.ConvShape, dtype: torch.dtype, who: str
            f"{who}: x must be contiguous {dtype} [B,H,W,Cs]={(s.B, s.H, s.W, s.Cs)}, got {tuple(x.shape)} {x.dtype}")
 
 
+def _pointwise(s: nv.ConvShape, dtype: torch.dtype) -> bool:
+    """1x1 / stride 1 / no padding over unpadded channels in bf16: in NHWC the conv IS a GEMM over
+    [B*H*W, C] rows, so it runs on the LDS-DMA MFMA GEMM (sv_gemm v3) instead of the implicit-GEMM
+    conv kernel (ResNet-50 bottleneck conv1 / conv3: ~half of its conv FLOPs)."""
+    return (s.KH == 1 and s.KW == 1 and s.stride == 1 and s.pad == 0 and s.Cs == s.Cin and dtype == torch.bfloat16
+            and s.Cs % 32 == 0 and s.Cout % 32 == 0)
+
+
 def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype) -> torch.Tensor:
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
+    if _pointwise(s, wp.dtype):
+        M = s.B * s.H * s.W
+        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
+             ldb=s.Cs, C=y.view(M, s.Cout), compute_bf16=True)
+        return y
     call("sv_conv_fwd", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s))
     return y
 
@@ -512,6 +525,17 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
         _check(not accumulate, "conv_bwd_data: accumulate needs dx")
         dx = torch.empty(s.B, s.H, s.W, s.Cs, device=dy.device, dtype=dx_dtype)
     _check(dx.is_contiguous() and tuple(dx.shape) == (s.B, s.H, s.W, s.Cs), "conv_bwd_data: dx shape")
+    if _pointwise(s, wp.dtype) and (not accumulate or dx.dtype == torch.float32):
+        M = s.B * s.H * s.W
+        if accumulate:  # dx += dy W: the layer-scale/residual epilogue with gamma = 1, residual = dx (in place)
+            ones = torch.ones(s.Cs, device=dy.device, dtype=torch.float32)
+            gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
+                 lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, gamma=ones,
+                 aux=dx.view(M, s.Cs), compute_bf16=True)
+        else:
+            gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
+                 lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), compute_bf16=True)
+        return dx
     call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s))
     return dx
 
@@ -523,6 +547,11 @@ def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: t
     _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout), "conv_bwd_weight: dy shape")
     _check(dw.dtype == torch.float32 and dw.is_contiguous() and tuple(dw.shape) == (s.Cout, s.Cin, s.KH, s.KW),
            "conv_bwd_weight: dw must be f32 [Cout,Cin,k,k]")
+    if _pointwise(s, dy.dtype):
+        M = s.B * s.H * s.W
+        linear_wgrad(dy.view(M, s.Cout), x.view(M, s.Cs), out=dw.view(s.Cout, s.Cs), accumulate=accumulate,
+                     compute_bf16=True)
+        return dw
     nwork = value("sv_conv_bwd_weight_work_floats", ctypes.byref(s))
     work = torch.empty(nwork, device=dy.device, dtype=torch.float32)
     call("sv_conv_bwd_weight", ptr(dy), ptr(x), ptr(work), ptr(dw), int(accumulate), dt(dy), ctypes.byref(s))
@@ -541,8 +570,10 @@ def _bn_c_ok(C: int) -> bool:
     return C >= 4 and C % 4 == 0 and (C // 4 <= 256 or (C // 4) % 256 == 0)
 
 
-def bn_stats(y2d: torch.Tensor, *, eps: float = EPS_BN, momentum: float = 0.1, running_mean=None, running_var=None):
-    """Train-mode batch statistics of y [rows, C] -> (mean, rstd) f32; running stats updated in place."""
+def bn_stats(y2d: torch.Tensor, *, eps: float = EPS_BN, momentum: float = 0.1, running_mean=None, running_var=None,
+             num_batches_tracked=None):
+    """Train-mode batch statistics of y [rows, C] -> (mean, rstd) f32; running stats (and the int64
+    num_batches_tracked counter) updated in place on the device."""
     rows, C = y2d.shape
     _check(_bn_c_ok(C) and y2d.is_contiguous() and rows > 0, f"bn_stats: unsupported C={C}")
     P = value("sv_bn_nparts", rows, C)
@@ -551,7 +582,7 @@ def bn_stats(y2d: torch.Tensor, *, eps: float = EPS_BN, momentum: float = 0.1, r
     mean = torch.empty(C, device=y2d.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
     call("sv_bn_stats_finish", ptr(y2d), dt(y2d), ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
-         ptr(rstd), ptr(running_mean), ptr(running_var))
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked))
     return mean, rstd
 
 

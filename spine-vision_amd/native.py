@@ -100,7 +100,7 @@ _SIGS = {
     "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_bn_nparts": [_i64, _i32],
     "sv_bn_stats": [_p, _i32, _i64, _i32, _p, _p],
-    "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p],
+    "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p],
     "sv_bn_eval_params": [_p, _p, _f32, _p, _p, _i32, _p],
     "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
