@@ -344,8 +344,17 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     //   v2 (BK 64, 3 stages): long-K residual epilogue (fc2 fwd).
     const bool heavy_epi = d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
                            d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
+    // v8 (256x256, one workgroup per CU) where it measured faster and the chip holds >= one full wave
+    // of its tiles: the fc1 forward (GELU dual epilogue) and the long-K forward GEMMs (fc2 residual,
+    // K >= 2048); never beside the side-stream GEMMs (128 KiB of LDS leaves no room for a co-resident
+    // workgroup).  tools/gemm_bench.py, gpurun_out g8a.
+    const long tiles8 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
+    const bool v8_shape = tiles8 >= 256 && (d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
+                                            ((d->epilogue == SV_EPI_BIAS_GAMMA_RES) && d->K >= 2048));
     int rc;
-    if (impl == 6) rc = launch_gemm6(d, s);
+    if (impl == 0 && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);
+    else if (impl == 8) rc = launch_gemm8(d, s);
+    else if (impl == 6) rc = launch_gemm6(d, s);
     else if (impl == 7) rc = launch_gemm7(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);
     else if (impl == 3) rc = launch_gemm3(d, s);

@@ -324,6 +324,8 @@ int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg = nullptr);
 // v7 entry (gemm7.hip, register-staged operand loads): occ 4 = two workgroups per CU, 2 = one
 int launch_gemm7(const sv_gemm_desc* d, hipStream_t s, int occ = 2);
+// v8 entry (gemm8.hip, 256x256 tile, 8 waves, one workgroup per CU): same contract as v3
+int launch_gemm8(const sv_gemm_desc* d, hipStream_t s);
 // v6 entry (gemm6.hip, 256x256 tile, one 4-wave workgroup per CU): same contract as v2
 int launch_gemm6(const sv_gemm_desc* d, hipStream_t s);
 
