@@ -450,3 +450,36 @@ def test_layerscale_wgrad_fused(dev, M, C, compute_bf16):
     assert rel(dw2, ref_w) < tol
     assert rel(dgam, ref_g) < tol
     assert rel(db2, ref_b) < tol
+
+
+@pytest.mark.parametrize("case", ["dual", "residual"])
+def test_gemm_v8_dispatch_shapes(dev, case):
+    """Shapes large enough (>= 256 tiles of 256x256) that sv_gemm dispatches the v8 kernel by default:
+    the fc1 GELU-dual epilogue and the long-K (>= 2048) residual epilogue.  Checked on 512 sampled rows
+    against a torch fp32 reference on the same bf16 operands."""
+    g = torch.Generator().manual_seed(8 if case == "dual" else 9)
+    if case == "dual":
+        M, N, Kd = 16384, 4096, 256
+    else:
+        M, N, Kd = 65536, 256, 2048
+    A = (torch.randn(M, Kd, generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    rows = torch.randperm(M, generator=g)[:512]
+    ref = A[rows].float() @ W.float().t() + b
+    Ad, Wd = A.to(dev), W.to(dev)
+    if case == "dual":
+        gh = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        a = torch.empty_like(gh)
+        K.linear_fwd(Ad, Wd, out=gh, out2=a, bias=b.to(dev), epilogue=nv.SV_EPI_BIAS_GELU_DUAL)
+        hr = ref.clone().requires_grad_(True)
+        F.gelu(hr).sum().backward()
+        assert rel(a[rows.to(dev)], F.gelu(ref)) < 1e-2
+        assert rel(gh[rows.to(dev)], hr.grad) < 1e-2
+    else:
+        gam = torch.rand(N, generator=g) * 0.25 + 0.05
+        x = torch.randn(M, N, generator=g)
+        out = torch.empty(M, N, device=dev)
+        K.linear_fwd(Ad, Wd, out=out, bias=b.to(dev), gamma=gam.to(dev), residual=x.to(dev),
+                     epilogue=nv.SV_EPI_BIAS_GAMMA_RES)
+        assert rel(out[rows.to(dev)], x[rows] + gam * ref) < 1e-5 + 2e-3
