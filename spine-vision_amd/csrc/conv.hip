@@ -23,6 +23,8 @@
 #include "gemm_common.h"
 #include "mfma_v1.h"
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 namespace sv {
@@ -486,6 +488,44 @@ static int wgrad_split(const sv_conv_shape* s) {
   return split < 1 ? 1 : split;
 }
 
+// the v3 LDS-DMA GEMM with gathered operands (gemm3.hip, CONV modes) for bf16 convolutions whose
+// channel count is a power of two >= 32 (every 32-deep k-step inside one tap)
+static ConvG make_convg(int SH, int SW, int SC, int GH, int GW, int si) {
+  ConvG g{};
+  g.SH = SH;
+  g.SW = SW;
+  g.lsc = ilog2(SC);
+  g.GH = GH;
+  g.GW = GW;
+  g.si = si;
+  conv_fastdiv((uint32_t)GW, g.gw_mul, g.gw_shift);
+  conv_fastdiv((uint32_t)(GH * GW), g.ghw_mul, g.ghw_shift);
+  return g;
+}
+static sv_gemm_desc conv_desc(const void* A, const void* B, int M, int N, int K, int b_kmajor, int64_t ldb, void* C,
+                              int c_dtype) {
+  sv_gemm_desc d{};
+  d.M = M;
+  d.N = N;
+  d.K = K;
+  d.A = A;
+  d.a_dtype = SV_BF16;
+  d.a_kmajor = 1;
+  d.lda = K;
+  d.B = B;
+  d.b_dtype = SV_BF16;
+  d.b_kmajor = b_kmajor;
+  d.ldb = ldb;
+  d.epilogue = SV_EPI_STORE;
+  d.C = C;
+  d.c_dtype = c_dtype;
+  d.ldc = N;
+  d.split_k = 1;
+  d.compute = SV_BF16;
+  return d;
+}
+static const bool g_conv_gemm = getenv("SV_CONV_GEMM") ? atoi(getenv("SV_CONV_GEMM")) != 0 : true;
+
 }  // namespace conv
 }  // namespace sv
 
@@ -548,6 +588,16 @@ extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dty
   a.C = y;
   a.c_dtype = y_dtype;
   a.kper = ceil_div(a.K, BKT) * BKT;
+  if (g_conv_gemm && dtype == SV_BF16 && s->Cs >= 32 && pow2(s->Cs) && a.K % 32 == 0) {
+    ConvG g = make_convg(s->H, s->W, s->Cs, OH, OW, s->stride);
+    for (int j = 0; j < a.ntaps; ++j) {
+      g.tdy[j] = a.tdy[j];
+      g.tdx[j] = a.tdx[j];
+    }
+    const sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype);
+    const int rc = launch_gemm3_conv(&d, g, 1, (hipStream_t)stream);
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+  }
   return launch_dt<FPROP>(a, dtype, 1, (hipStream_t)stream);
 }
 
@@ -559,6 +609,30 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
   SV_REQUIRE(pow2(s->Cout), "sv_conv_bwd_data: Cout=%d must be a power of two", s->Cout);
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
   const int st = s->stride;
+  const int T_ = s->KH * s->KW;
+  if (g_conv_gemm && dtype == SV_BF16 && st == 1 && s->Cout >= 32 && (s->Cs % 8) == 0 &&
+      (!accumulate || dx_dtype == SV_F32) && ((int64_t)T_ * s->Cout) % 32 == 0) {
+    // stride 1: one gather conv over dy (taps pad - kh, pad - kw) against the weight's rows
+    ConvG g = make_convg(OH, OW, s->Cout, s->H, s->W, 1);
+    g.lcout = ilog2(s->Cout);
+    g.Tw = T_;
+    g.Cs = s->Cs;
+    for (int kh = 0; kh < s->KH; ++kh)
+      for (int kw = 0; kw < s->KW; ++kw) {
+        g.tdy[kh * s->KW + kw] = (int8_t)(s->pad - kh);
+        g.tdx[kh * s->KW + kw] = (int8_t)(s->pad - kw);
+        g.twt[kh * s->KW + kw] = (uint8_t)(kh * s->KW + kw);
+      }
+    sv_gemm_desc d = conv_desc(dy, wp, s->B * s->H * s->W, s->Cs, T_ * s->Cout, 0, (int64_t)T_ * s->Cs, dx, dx_dtype);
+    if (accumulate) {  // dx += conv^T(dy): residual epilogue with gamma = 1 reading dx in place
+      d.epilogue = SV_EPI_BIAS_GAMMA_RES;
+      d.aux = dx;
+      d.aux_dtype = SV_F32;
+      d.ld_aux = s->Cs;
+    }
+    const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+  }
   for (int py = 0; py < st; ++py)
     for (int px = 0; px < st; ++px) {
       Args a{};

@@ -74,6 +74,34 @@ __device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ X, int64
   }
 }
 
+// implicit-GEMM A operand (CONV 1/2): 16-B chunks of gathered pixels; out-of-image taps and rows
+// past M read this zero page, so the MFMA consumer never branches
+__device__ __attribute__((aligned(64))) uint16_t g_conv_zero[64];
+
+template <int BKT, int PER_WAVE>
+__device__ __forceinline__ void issue_gather(const uint16_t* __restrict__ X, const ConvG& g, const int (&gb)[PER_WAVE],
+                                             const int (&gy)[PER_WAVE], const int (&gx)[PER_WAVE], int ty, int tx,
+                                             int cb, char* lds_tile, int wid) {
+  const int lane = threadIdx.x & 63;
+  constexpr int RB = BKT * 2;
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int piece = wid + NW * j;
+    const int byte = piece * 1024 + lane * 16;
+    const int row = byte / RB, ch = (byte % RB) >> 4;
+    const int gc = ch ^ kswz<BKT>(row);
+    const int iy = gy[j] + ty, ix = gx[j] + tx;
+    const uint16_t* src = g_conv_zero;
+    if (gb[j] >= 0 && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW)
+      src = X + ((((size_t)(gb[j] + iy) * g.SW + ix) << g.lsc) + cb + gc * 8);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ uint32_t cg_div(uint32_t n, uint32_t mul, uint32_t shift) {
+  return (uint32_t)(((uint64_t)__umulhi(n, mul) + n) >> shift);
+}
+
 // MFMA fragment: lane l holds X[row = base + (l&15)][k = 32*kk + 8*(l>>4) + j], j = 0..7
 template <bool KMAJ, int ROWS, int BKT>
 __device__ __forceinline__ bf16x8 frag(const char* __restrict__ img, int base, int kk) {
@@ -147,10 +175,10 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC>
+template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC, int CONV = 0>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
-             int tilesM, int tilesN, int nsplit, int stagger, EpiArgs e, float* __restrict__ colsum) {
+             int tilesM, int tilesN, int nsplit, int stagger, EpiArgs e, float* __restrict__ colsum, ConvG cg) {
   using C = Cfg<BKT, S>;
   static_assert(S >= 2 && (S - 2) * C::LOADS <= 63, "ring / vmcnt");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -181,11 +209,43 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // implicit-GEMM rows: the pixel of each of this lane's A rows, decoded once per tile
+    int gb[C::A_PER_WAVE], gy[C::A_PER_WAVE], gx[C::A_PER_WAVE];
+    if constexpr (CONV > 0) {
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < C::A_PER_WAVE; ++j) {
+        const int row = ((wid + NW * j) * 1024 + lane * 16) / (BKT * 2);
+        const int m = m0 + row;
+        gb[j] = -1;
+        gy[j] = gx[j] = 0;
+        if (m < e.M) {
+          const uint32_t b = cg_div((uint32_t)m, cg.ghw_mul, cg.ghw_shift);
+          const uint32_t rem = (uint32_t)m - b * (uint32_t)(cg.GH * cg.GW);
+          const uint32_t oy = cg_div(rem, cg.gw_mul, cg.gw_shift);
+          const uint32_t ox = rem - oy * (uint32_t)cg.GW;
+          gb[j] = (int)b * cg.SH;
+          gy[j] = (int)oy * cg.si;
+          gx[j] = (int)ox * cg.si;
+        }
+      }
+    }
     auto issue = [&](int kt) {
       char* st = smem + (kt % S) * C::STAGE_BYTES;
       const int k0 = kbeg + kt * BKT;
-      issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
-      issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
+      if constexpr (CONV == 0) {
+        issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
+        issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
+      } else {
+        const int jt = k0 >> cg.lsc, cb = k0 & ((1 << cg.lsc) - 1);  // wave-uniform tap / channel base
+        issue_gather<BKT, C::A_PER_WAVE>(A, cg, gb, gy, gx, cg.tdy[jt], cg.tdx[jt], cb, st, wid);
+        if constexpr (CONV == 1) {
+          issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
+        } else {  // dgrad: k = j*Cout + co -> weight rows (co*Tw + twt[j])*Cs, i.e. rows co of stride Tw*Cs
+          issue_tile<false, BN, BKT, C::B_PER_WAVE>(B + (size_t)cg.twt[jt] * cg.Cs, (int64_t)cg.Tw * cg.Cs, n0, cb,
+                                                    e.N, st + C::A_BYTES, wid);
+        }
+      }
     };
 
     __syncthreads();  // the previous tile's epilogue slabs overlap the ring
@@ -249,8 +309,8 @@ static int num_cus() {
   return n;
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S>
-static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
+template <bool AK, bool BKM, int EPI, int BKT, int S, int CONV = 0>
+static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* cg = nullptr) {
   using C = Cfg<BKT, S>;
   // the kernels are specialised for the operand dtype each epilogue carries in the bf16 model
   if ((EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) && d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
@@ -263,7 +323,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   e.wt = g_store_wt;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr_set = true;
   }
@@ -283,9 +343,10 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
       if (C::TWO_PER_CU) stagger = (stag_env >= 0 ? stag_env : 384) * (kper / 32);  // ~half a main loop
     }
   }
-  gemm3_kernel<AK, BKM, EPI, BKT, S, OCC><<<grid, THREADS, C::LDS, s>>>(
+  gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
-      tilesM, tilesN, split, stagger, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
+      tilesM, tilesN, split, stagger, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,
+      cg ? *cg : ConvG{});
   return check_launch("sv_gemm(v3)");
 }
 
@@ -314,6 +375,17 @@ static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
 }
 
 }  // namespace g3
+
+int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
+  using namespace g3;
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || g.lsc < 5)
+    return SV_ERR_UNSUPPORTED;
+  if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, 3, 2>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
+    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, 3, 2>(d, 1, s, &g);
+  return SV_ERR_UNSUPPORTED;
+}
 
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg) {
   using namespace g3;

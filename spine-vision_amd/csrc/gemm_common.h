@@ -150,8 +150,12 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
     if (okn4) b1 = *reinterpret_cast<const float4*>(e.bias + n + 4);
   }
   if (okn && e.epi == SV_EPI_BIAS_GAMMA_RES) {
-    g0 = *reinterpret_cast<const float4*>(e.gamma + n);
-    if (okn4) g1 = *reinterpret_cast<const float4*>(e.gamma + n + 4);
+    if (e.gamma) {
+      g0 = *reinterpret_cast<const float4*>(e.gamma + n);
+      if (okn4) g1 = *reinterpret_cast<const float4*>(e.gamma + n + 4);
+    } else {  // gamma == NULL: C = aux + acc (in-place accumulate when aux == C)
+      g0 = g1 = make_float4(1.f, 1.f, 1.f, 1.f);
+    }
   }
   constexpr int NP = PRE == 1 ? 4 : 1;
   float4 xa[NP][2], xb[NP][2];
@@ -314,6 +318,32 @@ __device__ __forceinline__ void wave_tile_epilogue_wide(const f32x4 (&acc)[FM][F
     if constexpr (FN >= 8) wave_group_epilogue<FM, PRE, FN, 4>(acc, 4, slab, mb + 64, nb + 64, e, split);
   }
 }
+
+// Implicit-GEMM convolution geometry for the v3 kernel's gathered operands (ResNet, conv.hip):
+//   CONV 1 (fprop):  A(m = (b,oy,ox), k = j*SC + c) = x[b, oy*si + tdy[j], ox*si + tdx[j], c] (0 outside),
+//                    B = packed weight [Cout][T*SC] (K-major, plain);
+//   CONV 2 (dgrad, stride 1): A = dy gathered the same way (SC = Cout, taps pad - kh / pad - kw),
+//                    B(k = j*Cout + co, n = c) = wp[(co*Tw + twt[j])*Cs + c] (M-major rows).
+// SC is a power of two >= 32, so every 32-deep k-step lies inside one tap: the tap is wave-uniform.
+constexpr int CONV_MAX_TAPS = 64;
+struct ConvG {
+  int SH, SW, lsc;      // gather source [batch][SH][SW][1 << lsc]
+  int GH, GW, si;       // output pixel grid and source step per output pixel
+  uint32_t gw_mul, gw_shift, ghw_mul, ghw_shift;  // n / GW and n / (GH*GW) as multiply-shift
+  int lcout, Tw, Cs;    // dgrad: B rows
+  int8_t tdy[CONV_MAX_TAPS], tdx[CONV_MAX_TAPS];
+  uint8_t twt[CONV_MAX_TAPS];
+};
+// d = n / D for n < 2^31: (umulhi(n, mul) + n) >> shift
+inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
+  uint32_t l = 0;
+  while ((1ull << l) < D) ++l;
+  shift = l;
+  mul = (uint32_t)((((1ull << l) - D) << 32) / D + 1);
+}
+// fprop (mode 1) / stride-1 dgrad (mode 2) through the v3 kernel; d describes the GEMM view
+// (M = pixels, N = Cout or Cs, K = taps * channels), epilogue STORE or BIAS_GAMMA_RES (accumulate)
+int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s);
 
 // SV_STORE_WT=1: write-through (sc1) epilogue stores in the v2/v3 GEMMs (gemm.hip reads the env once)
 extern int g_store_wt;
