@@ -679,9 +679,22 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
   return SV_OK;
 }
 
+// split-K depth of the v3 gather wgrad: ~512 workgroups over its 256x128 tiles, >= 512 pixels per slice
+static int wgrad_split3(const sv_conv_shape* s) {
+  const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  const int64_t K = (int64_t)s->B * OH * OW;
+  const int tiles = ceil_div(s->Cout, 256) * ceil_div((int64_t)s->KH * s->KW * s->Cs, 128);
+  int64_t split = ceil_div(512, tiles);
+  const int64_t maxs = K / 512 > 0 ? K / 512 : 1;
+  if (split > maxs) split = maxs;
+  if (split > 256) split = 256;
+  return split < 1 ? 1 : (int)split;
+}
+
 extern "C" int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s) {
   if (!s) return -1;
-  return (int64_t)wgrad_split(s) * s->Cout * s->KH * s->KW * s->Cs;
+  const int sp = wgrad_split(s) > wgrad_split3(s) ? wgrad_split(s) : wgrad_split3(s);
+  return (int64_t)sp * s->Cout * s->KH * s->KW * s->Cs;
 }
 
 extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate,
@@ -689,6 +702,32 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_weight")) return rc;
   SV_REQUIRE(dy && x && work && dw, "sv_conv_bwd_weight: null pointer");
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
+  const int T_ = s->KH * s->KW;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t npix = (int64_t)s->B * OH * OW;
+  if (g_conv_gemm && dtype == SV_BF16 && s->Cs >= 8 && pow2(s->Cs) && npix % 32 == 0 && s->Cout % 8 == 0) {
+    // v3 gather wgrad: A = dy (M-major: [pixel][Cout]), B = gathered x rows, split-K f32 slabs
+    const int sp = wgrad_split3(s);
+    ConvG g = make_convg(s->H, s->W, s->Cs, OH, OW, s->stride);
+    for (int kh = 0; kh < s->KH; ++kh)
+      for (int kw = 0; kw < s->KW; ++kw) {
+        g.tdy[kh * s->KW + kw] = (int8_t)(kh - s->pad);
+        g.tdx[kh * s->KW + kw] = (int8_t)(kw - s->pad);
+      }
+    sv_gemm_desc d = conv_desc(dy, x, s->Cout, T_ * s->Cs, (int)npix, 0, T_ * s->Cs, work, SV_F32);
+    d.a_kmajor = 0;
+    d.lda = s->Cout;
+    d.epilogue = SV_EPI_SLAB;
+    d.split_k = sp;
+    const int rc = launch_gemm3_conv(&d, g, 3, st);
+    if (rc == SV_OK) {
+      const int64_t n = (int64_t)s->Cout * s->Cin * T_;
+      wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, sp, s->Cout, s->Cin, T_, s->Cs, dw,
+                                                                    accumulate);
+      return check_launch("sv_conv_bwd_weight(finish)");
+    }
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+  }
   const int split = wgrad_split(s);
   Args a{};
   a.A = dy;
@@ -712,9 +751,7 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
   a.C = work;
   a.c_dtype = SV_F32;
   a.kper = ceil_div(ceil_div(a.K, split), BKT) * BKT;
-  hipStream_t st = (hipStream_t)stream;
   if (int rc = launch_dt<WGRAD>(a, dtype, split, st)) return rc;
-  const int T_ = s->KH * s->KW;
   const int64_t n = (int64_t)s->Cout * s->Cin * T_;
   wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, split, s->Cout, s->Cin, T_, s->Cs, dw, accumulate);
   return check_launch("sv_conv_bwd_weight(finish)");

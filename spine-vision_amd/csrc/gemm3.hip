@@ -102,6 +102,34 @@ __device__ __forceinline__ uint32_t cg_div(uint32_t n, uint32_t mul, uint32_t sh
   return (uint32_t)(((uint64_t)__umulhi(n, mul) + n) >> shift);
 }
 
+// implicit-GEMM B operand of the weight gradient (CONV 3): B(k = pixel, n = t*SC + c) =
+// x[b, oy*si + tdy[t], ox*si + tdx[t], c], M-major image [BK][BN].  A lane's k-row and 8-column chunk
+// are fixed for the whole tile (so its tap / channel offset is precomputed: bc, by, bx); per k-step
+// only the pixel k0 + krow is decoded.
+template <int BKT, int PER_WAVE>
+__device__ __forceinline__ void issue_gather_n(const uint16_t* __restrict__ X, const ConvG& g, int K, int k0,
+                                               const int (&bk)[PER_WAVE], const int (&bc)[PER_WAVE],
+                                               const int (&by)[PER_WAVE], const int (&bx)[PER_WAVE],
+                                               char* lds_tile, int wid) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int piece = wid + NW * j;
+    const int pix = k0 + bk[j];
+    const uint16_t* src = g_conv_zero;
+    if (bc[j] >= 0 && pix < K) {
+      const uint32_t b = cg_div((uint32_t)pix, g.ghw_mul, g.ghw_shift);
+      const uint32_t rem = (uint32_t)pix - b * (uint32_t)(g.GH * g.GW);
+      const uint32_t oy = cg_div(rem, g.gw_mul, g.gw_shift);
+      const uint32_t ox = rem - oy * (uint32_t)g.GW;
+      const int iy = (int)oy * g.si + by[j], ix = (int)ox * g.si + bx[j];
+      if ((unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW)
+        src = X + (((((size_t)b * g.SH + iy) * g.SW + ix) << g.lsc) + bc[j]);
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
 // MFMA fragment: lane l holds X[row = base + (l&15)][k = 32*kk + 8*(l>>4) + j], j = 0..7
 template <bool KMAJ, int ROWS, int BKT>
 __device__ __forceinline__ bf16x8 frag(const char* __restrict__ img, int base, int kk) {
@@ -230,10 +258,29 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
         }
       }
     }
+    // weight-gradient gather (CONV 3): this lane's B k-row and (tap, channel) per DMA piece
+    int bk[C::B_PER_WAVE], bc[C::B_PER_WAVE], by[C::B_PER_WAVE], bx[C::B_PER_WAVE];
+    if constexpr (CONV == 3) {
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < C::B_PER_WAVE; ++j) {
+        const int byte = (wid + NW * j) * 1024 + lane * 16;
+        const int krow = byte / (BN * 2), ch = (byte % (BN * 2)) >> 4;
+        const int n = n0 + (ch ^ mswz(krow)) * 8;
+        const int t = n >> cg.lsc;
+        bk[j] = krow;
+        bc[j] = n < e.N ? n & ((1 << cg.lsc) - 1) : -1;
+        by[j] = n < e.N ? cg.tdy[t] : 0;
+        bx[j] = n < e.N ? cg.tdx[t] : 0;
+      }
+    }
     auto issue = [&](int kt) {
       char* st = smem + (kt % S) * C::STAGE_BYTES;
       const int k0 = kbeg + kt * BKT;
-      if constexpr (CONV == 0) {
+      if constexpr (CONV == 3) {
+        issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
+        issue_gather_n<BKT, C::B_PER_WAVE>(B, cg, K, k0, bk, bc, by, bx, st + C::A_BYTES, wid);
+      } else if constexpr (CONV == 0) {
         issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
         issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
       } else {
@@ -378,12 +425,14 @@ static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
 
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
-  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || g.lsc < 5)
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && g.lsc < 5))
     return SV_ERR_UNSUPPORTED;
   if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, 3, 2>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
     return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, 3, 2>(d, 1, s, &g);
+  if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
+    return launch<false, false, SV_EPI_SLAB, 32, 4, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   return SV_ERR_UNSUPPORTED;
 }
 
