@@ -1,0 +1,104 @@
+"""GPU: the data-parallel step end to end (StepEngine with distributed=True: rank-0 parameter broadcast,
+bucketed gradient all-reduce launched from the backbone's per-block grad_ready_hook on the comm stream,
+finish() joining it before clip + AdamW) with two ranks on the box's one GPU over gloo (RCCL needs one
+GPU per rank; the bucket/stream logic is backend-agnostic).
+
+Two ranks on B images each must reproduce a single process on the 2B-image batch: the reference's DDP
+semantics -- mean loss per rank, gradients averaged over ranks.  fp32 parity mode,
+all-valid masks (so every rank's masked mean has the same denominator)."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, S = 2, 64
+
+
+def _batch():
+    from oracle import weights as ow
+
+    img, coords, mask = ow.localization_batch(2 * B, S, S)
+    return img, coords, torch.ones_like(mask)
+
+
+def _model(dev):
+    from oracle import weights as ow
+    from spine_vision_amd.training import CoordinateRegressor
+
+    m = CoordinateRegressor("convnext_base", pretrained=False, dropout=0.0, precision="fp32")
+    ow.fill_module(m)
+    return m.to(dev).train()
+
+
+def _rank(rank, world, port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    import torch.distributed as dist
+
+    from spine_vision_amd.training import StepEngine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    m = _model(dev)
+    if rank == 1:  # the broadcast must overwrite a diverged replica
+        with torch.no_grad():
+            m.head[5].bias.add_(1.0)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=16.0)
+    img, coords, mask = _batch()
+    sl = slice(rank * B, (rank + 1) * B)
+    loss = eng.step_localization(img[sl].to(dev), coords[sl].to(dev), mask[sl].to(dev))
+    torch.cuda.synchronize()
+    out[rank] = (float(loss), float(eng.last_grad_norm), eng.arena.grad_flat.cpu().clone(),
+                 eng.arena.param_flat.cpu().clone(), len(eng.bucketer.buckets))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_step_matches_single_process(dev):
+    from spine_vision_amd.training import StepEngine
+
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    (l0, n0, g0, p0, nb), (l1, n1, g1, p1, _) = out[0], out[1]
+    assert nb > 1, "expected several gradient buckets"
+    # every rank holds the all-reduced gradient and the same updated parameters
+    assert torch.equal(g0, g1) and n0 == n1
+    assert torch.equal(p0, p1)
+    # == one process over the whole batch
+    m = _model(dev)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=False)
+    img, coords, mask = _batch()
+    l_ref = float(eng.step_localization(img.to(dev), coords.to(dev), mask.to(dev)))
+    g_ref = eng.arena.grad_flat.cpu()
+    assert float((g0 - g_ref).norm() / g_ref.norm()) < 1e-4
+    assert abs(n0 - float(eng.last_grad_norm)) / float(eng.last_grad_norm) < 1e-4
+    assert abs(0.5 * (l0 + l1) - l_ref) / l_ref < 1e-5
+    dp = (p0 - eng.arena.param_flat.cpu()).abs().max()
+    assert float(dp) <= 2e-4 * 1.001  # first AdamW step: each element moves by ~lr*sign(g)
