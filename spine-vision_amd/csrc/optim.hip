@@ -133,7 +133,16 @@ __global__ void __launch_bounds__(kThreads) reduce_pair_kernel(RedSeg a, RedSeg 
     }
     const int64_t cl = c0 + threadIdx.x * 4;
     const float r[4] = {t.x * alpha, t.y * alpha, t.z * alpha, t.w * alpha};
-    for (int j = 0; j < 4 && cl + j < sg.n; ++j) sg.out[cl + j] = accumulate ? sg.out[cl + j] + r[j] : r[j];
+    if (cl + 4 <= sg.n && ((reinterpret_cast<uintptr_t>(sg.out + cl) & 15) == 0)) {
+      float4 o = make_float4(r[0], r[1], r[2], r[3]);
+      if (accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(sg.out + cl);
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *reinterpret_cast<float4*>(sg.out + cl) = o;
+    } else {
+      for (int j = 0; j < 4 && cl + j < sg.n; ++j) sg.out[cl + j] = accumulate ? sg.out[cl + j] + r[j] : r[j];
+    }
   }
 }
 
@@ -334,12 +343,15 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
   if (n_b % 4 == 0 && n_b) SV_REQUIRE((((uintptr_t)part_b) & 15) == 0, "sv_reduce_partials_pair: part_b must be 16-B aligned");
   RedSeg a{part_a, n_a, out_a}, b{part_b, n_b, out_b};
   hipStream_t s = (hipStream_t)stream;
-  // widest column block that still gives >= 512 workgroups (or 4 columns per workgroup)
-  int cols = 64;
+  // widest column block that still gives >= 512 workgroups (or 4 columns per workgroup); with few
+  // partial rows (split-K slabs: P = 2..8) up to 256 columns, so that no partial-row group idles
+  int cols = P <= 4 ? 256 : (P <= 8 ? 128 : 64);
   while (cols > 4 && (n_a + cols - 1) / cols + (n_b + cols - 1) / cols < 512) cols >>= 1;
   const int64_t ba = (n_a + cols - 1) / cols, bb = (n_b + cols - 1) / cols;
   if (ba + bb == 0) return SV_OK;
   switch (cols) {
+    case 256: reduce_pair_kernel<64><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
+    case 128: reduce_pair_kernel<32><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
     case 64: reduce_pair_kernel<16><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
     case 32: reduce_pair_kernel<8><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
     case 16: reduce_pair_kernel<4><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
