@@ -131,10 +131,10 @@ __global__ void __launch_bounds__(kLnThreads) ln_bwd_kernel(const TDY* __restric
 
 
 // ------------------------------------------------------------------------------------------
-// Vectorised LayerNorm for C = 8 * LPR * NV with LPR in {16, 32, 64}: every lane owns NV runs of
+// Vectorised LayerNorm for C = 8 * LPR * NV with LPR in {8, 16, 32, 64}: every lane owns NV runs of
 // 8 consecutive channels (one 16-B bf16 / two 16-B f32 accesses per run), a row is spread over LPR
-// lanes, a wave covers 64/LPR rows at once.  ConvNeXt-base's C = 128/256/512/1024 all fit; the
-// per-lane-channel kernels above serve the other widths (e.g. ConvNeXt-large's 192/384/768/1536).
+// lanes, a wave covers 64/LPR rows at once.  ConvNeXt-base's C = 128/256/512/1024 and ConvNeXt-large's
+// 192/384/768/1536 all fit; the per-lane-channel kernels above serve the other widths.
 template <typename T>
 __device__ __forceinline__ void ld8v(const T* __restrict__ p, float (&v)[8]) {
   if constexpr (sizeof(T) == 4) {
@@ -326,13 +326,15 @@ __global__ void __launch_bounds__(kLnThreads) ln_bwd_vec_kernel(const TDY* __res
   }
 }
 
-// fast-path geometry: C = 8 * LPR * NV, LPR in {16,32,64}, NV in {1,2,4}; returns LPR*16+NV or 0
+// fast-path geometry: C = 8 * LPR * NV; returns LPR*16+NV or 0.  ConvNeXt-base 128..1024 (NV 1, 2, 4)
+// and ConvNeXt-large 192/384/768/1536 (NV 3 over LPR 8/16/32/64 lanes)
 static int ln_vec_kind(int C) {
   if (C % 8) return 0;
   const int u = C / 8;
   if (u == 16 || u == 32 || u == 64) return u * 16 + 1;
   if (u == 128) return 64 * 16 + 2;
   if (u == 256) return 64 * 16 + 4;
+  if (u % 3 == 0 && (u / 3 == 8 || u / 3 == 16 || u / 3 == 32 || u / 3 == 64)) return (u / 3) * 16 + 3;
   return 0;
 }
 #define SV_LNVEC_SWITCH(KIND, ...)                                           \
@@ -342,15 +344,19 @@ static int ln_vec_kind(int C) {
     case 64 * 16 + 1: { constexpr int LPR = 64, NV = 1; __VA_ARGS__; } break; \
     case 64 * 16 + 2: { constexpr int LPR = 64, NV = 2; __VA_ARGS__; } break; \
     case 64 * 16 + 4: { constexpr int LPR = 64, NV = 4; __VA_ARGS__; } break; \
+    case 8 * 16 + 3: { constexpr int LPR = 8, NV = 3; __VA_ARGS__; } break;   \
+    case 16 * 16 + 3: { constexpr int LPR = 16, NV = 3; __VA_ARGS__; } break; \
+    case 32 * 16 + 3: { constexpr int LPR = 32, NV = 3; __VA_ARGS__; } break; \
+    case 64 * 16 + 3: { constexpr int LPR = 64, NV = 3; __VA_ARGS__; } break; \
     default: break;                                                          \
   }
 static int ln_vec_fwd_grid(int64_t rows, int C) {
-  const int rpw = 64 / (C / 8 < 64 ? C / 8 : 64);
+  const int rpw = 64 / (ln_vec_kind(C) / 16);
   const int64_t waves = (rows + rpw - 1) / rpw;
   return (int)((waves + kLnThreads / 64 - 1) / (kLnThreads / 64));
 }
 static int ln_vec_bwd_grid(int64_t rows, int C) {
-  const int rpw = 64 / (C / 8 < 64 ? C / 8 : 64);
+  const int rpw = 64 / (ln_vec_kind(C) / 16);
   const int64_t groups = (rows + rpw - 1) / rpw;
   // ~8 row groups per wave: enough loop trip for the prefetch, partials stay small
   int64_t g = (groups + 8 * (kLnThreads / 64) - 1) / (8 * (kLnThreads / 64));

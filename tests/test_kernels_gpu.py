@@ -149,8 +149,8 @@ def test_reduce_partials_deep(dev):
 
 
 # ---------------------------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("C,rows", [(128, 333), (128, 9001), (192, 333), (256, 333), (512, 333), (512, 9001),
-                                    (1024, 333), (2048, 77)])
+@pytest.mark.parametrize("C,rows", [(128, 333), (128, 9001), (192, 333), (192, 9001), (256, 333), (384, 1001),
+                                    (512, 333), (512, 9001), (768, 1001), (1024, 333), (1536, 555), (2048, 77)])
 def test_layernorm_fwd_bwd(dev, C, rows):
     g = torch.Generator().manual_seed(C + rows)
     x = torch.randn(rows, C, generator=g) * 2 + 0.5
@@ -380,7 +380,7 @@ def test_adamw_and_clip(dev):
 
 
 # ------------------------------------------------- bf16 gradient paths (bf16 mode: dy, dz in bf16)
-@pytest.mark.parametrize("C", [128, 512])
+@pytest.mark.parametrize("C", [128, 512, 768])
 @pytest.mark.parametrize("dy_f32", [False, True])
 def test_layernorm_bwd_bf16_io(dev, C, dy_f32):
     g = torch.Generator().manual_seed(C + 1)
