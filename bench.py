@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--probe", default="fwd", choices=sorted(PROBE_KEYS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inference", action="store_true",
+                    help="secondary line (row f2): the validation / predict forward (eval mode, no tape) instead "
+                         "of the training step")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU sample budget")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -179,6 +182,16 @@ def main():
         def run_step():
             return engine.step_localization(img, coords, mask)
 
+    if args.inference:  # row f2: trainers' _validate_epoch / predict forward, no autograd tape
+        model.eval()
+        train_step = run_step
+
+        def run_step():
+            with torch.no_grad():
+                out = model(img)
+            return out.float().mean() if not isinstance(out, dict) else sum(v.float().mean() for v in out.values())
+
+        del train_step
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()
@@ -221,7 +234,13 @@ def main():
     value = world * args.batch * args.steps / elapsed
     gflop = STEP_GFLOP.get((args.backbone, args.image_size))
     step_tflops = gflop * args.batch / (ms * 1e-3) / 1e3 if gflop else None
-    if cls:
+    if args.inference:
+        metric = f"images/sec inference (eval forward), {args.backbone} {args.image_size}x{args.image_size}, bs{args.batch}"
+        workload = f"{'Classifier' if cls else 'CoordinateRegressor'}({args.backbone}) eval forward (validation / predict)"
+        data = "synthetic, resident in HBM; random-init weights"
+        gflop = STEP_GFLOP.get((args.backbone, args.image_size))
+        step_tflops = (gflop / 3.0) * args.batch / (ms * 1e-3) / 1e3 if gflop else None  # fwd = 1/3 of fwd+bwd
+    elif cls:
         metric = f"images/sec training, {args.backbone} {args.image_size}x{args.image_size} 3-head cls, bs{args.batch}"
         workload = f"Classifier({args.backbone}, pfirrmann+modic+herniation) train step fwd+bwd+allreduce+clip+AdamW"
         data = (f"synthetic uint8 {args.image_size}x{args.image_size} [T2,T1,T2] crops, ImageNet-normalised, "
