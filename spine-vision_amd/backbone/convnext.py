@@ -337,8 +337,13 @@ class ConvNeXtHip(nn.Module):
                     # every gradient of the block is final on this stream now (the LN ones were made on
                     # the main stream before the wait above): the bucketer's event covers them all
                     self._ready(blk_params)
-                if side is not None:
-                    main.wait_event(ev_w2)  # fc2 wgrad has read db before the depthwise backward rewrites it
+                if side is not None and bf:
+                    # the bf16 copy of the gradient stream goes to a fresh buffer: the side stream's fc2
+                    # wgrad may still be reading the previous one (record_stream above keeps it alive), so
+                    # the main stream does not wait for the side stream here
+                    db = torch.empty_like(db)
+                elif side is not None:
+                    main.wait_event(ev_w2)  # fp32: the fc2 wgrad reads d itself, which is updated in place
                 K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
             if ds_saved is not None:
                 x_prev, patches, d_mean, d_rstd = ds_saved
