@@ -65,7 +65,9 @@ typedef enum {
                              /* the bias gradient of a wgrad GEMM (A = dY^T) without another pass.   */
   SV_EPI_BIAS_GELU_DUAL = 5, /* h = acc + bias[n]: C = GELU_erf'(h), C2 = GELU_erf(h)  (fc1 forward: */
                              /* the backward then needs no erf, only SV_EPI_MUL_AUX)                 */
-  SV_EPI_MUL_AUX = 6         /* C = acc * aux[m,n]                       (fc2 dgrad through GELU)    */
+  SV_EPI_MUL_AUX = 6,        /* C = acc * aux[m,n]                       (fc2 dgrad through GELU)    */
+  SV_EPI_BIAS_GELU = 7       /* C = GELU_erf(acc + bias[n])   (fc1 of the tape-free eval forward:   */
+                             /* one output, no GELU' for a backward that will not run)             */
 } sv_epilogue;
 
 typedef struct {

@@ -230,11 +230,17 @@ class ConvNeXtHip(nn.Module):
                                                     blk.norm.bias, act_dtype=act)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 w2 = self._w(blk.mlp.fc2.weight, cache)
-                # fc1 epilogue: a = GELU(h) (fc2 operand) and gh = GELU'(h) (for the backward), one erf
-                gh = torch.empty(M, 4 * C, device=x.device, dtype=act)
+                # fc1 epilogue: a = GELU(h) (fc2 operand) and gh = GELU'(h) (for the backward), one erf;
+                # the tape-free forward (eval / predict) writes a only
                 a = torch.empty(M, 4 * C, device=x.device, dtype=act)
-                K.linear_fwd(y, w1, out=gh, out2=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU_DUAL,
-                             compute_bf16=bf)
+                if save:
+                    gh = torch.empty(M, 4 * C, device=x.device, dtype=act)
+                    K.linear_fwd(y, w1, out=gh, out2=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU_DUAL,
+                                 compute_bf16=bf)
+                else:
+                    gh = None
+                    K.linear_fwd(y, w1, out=a, bias=blk.mlp.fc1.bias, epilogue=nv.SV_EPI_BIAS_GELU,
+                                 compute_bf16=bf)
                 xo = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
                 K.linear_fwd(a, w2, out=xo.view(M, C), bias=blk.mlp.fc2.bias, gamma=blk.gamma,
                              residual=x.view(M, C), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, compute_bf16=bf)

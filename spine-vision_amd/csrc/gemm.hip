@@ -307,7 +307,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
-  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_MUL_AUX, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_BIAS_GELU, "sv_gemm: bad epilogue %d", d->epilogue);
   if (d->M == 0 || d->N == 0) return SV_OK;
   const bool bf = d->compute == SV_BF16;
   SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
@@ -343,13 +343,14 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     //   v3 32x4 (one workgroup per CU, two tiles in flight): the split-K wgrads (-10..25% vs v2);
     //   v2 (BK 64, 3 stages): long-K residual epilogue (fc2 fwd).
     const bool heavy_epi = d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
-                           d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX;
+                           d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX ||
+                           d->epilogue == SV_EPI_BIAS_GELU;
     // v8 (256x256, one workgroup per CU) where it measured faster and the chip holds >= one full wave
     // of its tiles: the fc1 forward (GELU dual epilogue) and the long-K forward GEMMs (fc2 residual,
     // K >= 2048); never beside the side-stream GEMMs (128 KiB of LDS leaves no room for a co-resident
     // workgroup).  tools/gemm_bench.py, gpurun_out g8a.
     const long tiles8 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
-    const bool v8_shape = tiles8 >= 256 && (d->epilogue == SV_EPI_BIAS_GELU_DUAL ||
+    const bool v8_shape = tiles8 >= 256 && (d->epilogue == SV_EPI_BIAS_GELU_DUAL || d->epilogue == SV_EPI_BIAS_GELU ||
                                             ((d->epilogue == SV_EPI_BIAS_GAMMA_RES) && d->K >= 2048));
     int rc;
     if (impl == 0 && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);

@@ -408,6 +408,7 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
     case SV_EPI_SLAB: return launch<AK, BKM, SV_EPI_SLAB, BKT, S>(d, split, s);
     case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, BKT, S>(d, split, s);
     case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, BKT, S>(d, split, s);
+    case SV_EPI_BIAS_GELU: return launch<AK, BKM, SV_EPI_BIAS_GELU, BKT, S>(d, split, s);
     default: return SV_ERR_UNSUPPORTED;
   }
 }

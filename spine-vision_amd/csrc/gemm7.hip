@@ -308,6 +308,7 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
     case SV_EPI_SLAB: return launch<AK, BKM, SV_EPI_SLAB, 32, OCC>(d, split, s);
     case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, 32, OCC>(d, split, s);
     case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, 32, OCC>(d, split, s);
+    case SV_EPI_BIAS_GELU: return launch<AK, BKM, SV_EPI_BIAS_GELU, 32, OCC>(d, split, s);
     default: return SV_ERR_UNSUPPORTED;
   }
 }

@@ -59,6 +59,8 @@ __device__ __forceinline__ void epi4(const EpiArgs& e, int m, int n, float4 v, i
   } else if (e.epi == SV_EPI_BIAS_GELU2) {
     st4_any(e.C, e.c_dtype, ci, v);
     st4_any(e.C2, e.c2_dtype, ci, make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)));
+  } else if (e.epi == SV_EPI_BIAS_GELU) {
+    st4_any(e.C, e.c_dtype, ci, make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)));
   } else if (e.epi == SV_EPI_BIAS_GAMMA_RES) {
     const float4 g = *reinterpret_cast<const float4*>(e.gamma + n);
     const float4 r = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
@@ -261,6 +263,9 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         gelu_dual4(vb, gb, ob);
         va = ga;  // C2 gets GELU, C gets GELU'
         vb = gb;
+      } else if (e.epi == SV_EPI_BIAS_GELU) {
+        oa = gelu4(va);
+        ob = gelu4(vb);
       } else if (e.epi == SV_EPI_MUL_AUX) {
         oa = mul4(va, xa[si][h]);
         ob = mul4(vb, xb[si][h]);

@@ -93,6 +93,12 @@ def test_gemm_epilogues(dev, compute_bf16):
     F.gelu(hr).sum().backward()
     assert rel(a2, F.gelu(h_ref)) < tol
     assert rel(gh, hr.grad) < tol
+    # fc1 + GELU, one output (eval forward): the same GELU(h) as the dual epilogue's C2, bit for bit
+    a3 = torch.empty_like(h)
+    K.linear_fwd(y.to(act).to(dev), w1.to(act).to(dev), out=a3, bias=b1.to(dev), epilogue=nv.SV_EPI_BIAS_GELU,
+                 compute_bf16=compute_bf16)
+    assert rel(a3, F.gelu(h_ref)) < tol
+    assert torch.equal(a3, a2)
     # fc2 + gamma + residual
     out = torch.empty(M, Cc, device=dev)
     K.linear_fwd(a, w2.to(act).to(dev), out=out, bias=b2.to(dev), gamma=gam.to(dev), residual=x.to(dev),
@@ -452,13 +458,13 @@ def test_layerscale_wgrad_fused(dev, M, C, compute_bf16):
     assert rel(db2, ref_b) < tol
 
 
-@pytest.mark.parametrize("case", ["dual", "residual"])
+@pytest.mark.parametrize("case", ["dual", "gelu", "residual"])
 def test_gemm_v8_dispatch_shapes(dev, case):
     """Shapes large enough (>= 256 tiles of 256x256) that sv_gemm dispatches the v8 kernel by default:
     the fc1 GELU-dual epilogue and the long-K (>= 2048) residual epilogue.  Checked on 512 sampled rows
     against a torch fp32 reference on the same bf16 operands."""
     g = torch.Generator().manual_seed(8 if case == "dual" else 9)
-    if case == "dual":
+    if case in ("dual", "gelu"):
         M, N, Kd = 16384, 4096, 256
     else:
         M, N, Kd = 65536, 256, 2048
@@ -476,6 +482,10 @@ def test_gemm_v8_dispatch_shapes(dev, case):
         F.gelu(hr).sum().backward()
         assert rel(a[rows.to(dev)], F.gelu(ref)) < 1e-2
         assert rel(gh[rows.to(dev)], hr.grad) < 1e-2
+    elif case == "gelu":
+        a = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.linear_fwd(Ad, Wd, out=a, bias=b.to(dev), epilogue=nv.SV_EPI_BIAS_GELU)
+        assert rel(a[rows.to(dev)], F.gelu(ref)) < 1e-2
     else:
         gam = torch.rand(N, generator=g) * 0.25 + 0.05
         x = torch.randn(M, N, generator=g)
