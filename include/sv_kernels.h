@@ -268,6 +268,14 @@ int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype,
 int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s);
 int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate, int32_t dtype,
                        const sv_conv_shape* s, sv_stream_t stream);
+/* Row f1, classification side: the collated uint8 HWC crops [B][H][W][3] -- the output of the
+ * reference's construct_3channel ([T2,T1,T2], or one plane replicated; spine_vision/training/
+ * datasets/classification.py:40-68) before ToTensor/Normalize (:247-278) -- straight into the ResNet
+ * stem's NHWC operand [B][H][W][Cs] (dtype): out[c] = (u8/255 - mean[c]) / std[c] for c < 3,
+ * channels >= 3 zero.  f32 values are bitwise torchvision's CPU ToTensor+Normalize; bf16 their RNE
+ * rounding.  B*H*W % 4 == 0, img 4-byte aligned, Cs in {4, 8}; mean/std HOST float[3].           */
+int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mean, const float* norm_std, void* out,
+                            int32_t dtype, int32_t B, int32_t H, int32_t W, int32_t Cs, sv_stream_t stream);
 /* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
 int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                      int32_t Cs, sv_stream_t stream);

@@ -144,7 +144,9 @@ class ResNetHip(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             raise RuntimeError("ResNetHip runs on the MI355X kernel library only (got a CPU tensor)")
-        x = x.float().contiguous()
+        # uint8 [B,H,W,3] crops (row f1, ClassificationConfig.device_transform): ToTensor + Normalize run
+        # on the device inside the stem's NHWC conversion; otherwise the normalised f32 NCHW batch
+        x = x.contiguous() if x.dtype == torch.uint8 else x.float().contiguous()
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         if need_grad:
             anchor = torch.zeros((), device=x.device, requires_grad=True)
@@ -175,7 +177,10 @@ class ResNetHip(nn.Module):
     def _forward_impl(self, img: torch.Tensor, save: bool):
         act = self.act_dtype
         cs0 = 8 if self.compute_bf16 else 4
-        x0 = K.image_to_nhwc(img, cs0, act)
+        if img.dtype == torch.uint8:
+            x0 = K.image_u8_hwc_to_nhwc(img, cs0, act)
+        else:
+            x0 = K.image_to_nhwc(img, cs0, act)
         y0, wp0, s0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3)
         B, H, W, C = y0.shape
         m0, r0 = self._bn(self.bn1, y0.view(-1, C))

@@ -426,6 +426,37 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restric
   st(out, (size_t)i, v);
 }
 
+// uint8 HWC crops -> normalised NHWC stem operand: one thread per 4 pixels (12 input bytes as three
+// aligned dwords, 4 x Cs output channels as 16-B stores).  Same arithmetic as torchvision's CPU
+// ToTensor (x / 255) then Normalize ((x - mean) / std), in f32.
+template <typename T, int CS>
+__global__ void __launch_bounds__(256) image_u8_hwc_kernel(const uint8_t* __restrict__ img, float m0, float m1,
+                                                           float m2, float s0, float s1, float s2,
+                                                           T* __restrict__ out, int64_t n4) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n4) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(img) + t * 3;
+  const uint32_t w[3] = {src[0], src[1], src[2]};
+  const float ms[3] = {m0, m1, m2}, ss[3] = {s0, s1, s2};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float v[CS];
+#pragma unroll
+    for (int c = 0; c < CS; ++c) {
+      if (c < 3) {
+        const int byte = 3 * p + c;
+        const uint32_t u = (w[byte >> 2] >> (8 * (byte & 3))) & 0xffu;
+        v[c] = ((float)u / 255.0f - ms[c]) / ss[c];
+      } else {
+        v[c] = 0.f;
+      }
+    }
+    const size_t o = (size_t)(t * 4 + p) * CS;
+#pragma unroll
+    for (int c = 0; c < CS; c += 4) st4(out, o + c, make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]));
+  }
+}
+
 // dw[co][c][t] (+)= sum_s slab[s][co][t*Cs + c]   (c < Cin)
 __global__ void wgrad_finish_kernel(const float* __restrict__ slab, int split, int Cout, int Cin, int T_, int Cs,
                                     float* __restrict__ dw, int accumulate) {
@@ -558,6 +589,33 @@ extern "C" int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int3
   else
     image_to_nhwc_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>(img, (float*)out, C, H, W, Cs, n);
   return check_launch("sv_image_to_nhwc");
+}
+
+extern "C" int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mean, const float* norm_std,
+                                       void* out, int32_t dtype, int32_t B, int32_t H, int32_t W, int32_t Cs,
+                                       sv_stream_t stream) {
+  SV_REQUIRE(img && norm_mean && norm_std && out, "sv_image_u8_hwc_to_nhwc: null pointer");
+  SV_REQUIRE(B > 0 && H > 0 && W > 0, "sv_image_u8_hwc_to_nhwc: bad shape");
+  const int64_t npix = (int64_t)B * H * W;
+  SV_REQUIRE(npix % 4 == 0, "sv_image_u8_hwc_to_nhwc: B*H*W must be a multiple of 4");
+  SV_REQUIRE(Cs == 4 || Cs == 8, "sv_image_u8_hwc_to_nhwc: Cs must be 4 or 8 (got %d)", Cs);
+  SV_REQUIRE(dtype == SV_BF16 || dtype == SV_F32, "sv_image_u8_hwc_to_nhwc: bad dtype");
+  SV_REQUIRE(((uintptr_t)img & 3) == 0, "sv_image_u8_hwc_to_nhwc: img must be 4-byte aligned");
+  SV_REQUIRE(((uintptr_t)out & (dtype == SV_BF16 ? 7 : 15)) == 0, "sv_image_u8_hwc_to_nhwc: misaligned out");
+  const int64_t n4 = npix / 4;
+  const int blocks = (int)((n4 + 255) / 256);
+  const float* m = norm_mean;
+  const float* sd = norm_std;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SV_BF16 && Cs == 8)
+    image_u8_hwc_kernel<uint16_t, 8><<<blocks, 256, 0, st>>>(img, m[0], m[1], m[2], sd[0], sd[1], sd[2], (uint16_t*)out, n4);
+  else if (dtype == SV_BF16)
+    image_u8_hwc_kernel<uint16_t, 4><<<blocks, 256, 0, st>>>(img, m[0], m[1], m[2], sd[0], sd[1], sd[2], (uint16_t*)out, n4);
+  else if (Cs == 8)
+    image_u8_hwc_kernel<float, 8><<<blocks, 256, 0, st>>>(img, m[0], m[1], m[2], sd[0], sd[1], sd[2], (float*)out, n4);
+  else
+    image_u8_hwc_kernel<float, 4><<<blocks, 256, 0, st>>>(img, m[0], m[1], m[2], sd[0], sd[1], sd[2], (float*)out, n4);
+  return check_launch("sv_image_u8_hwc_to_nhwc");
 }
 
 extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,

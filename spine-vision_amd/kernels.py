@@ -558,6 +558,20 @@ def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: t
     return dw
 
 
+def image_u8_hwc_to_nhwc(img_u8: torch.Tensor, Cs: int, dtype: torch.dtype, *, mean=IMAGENET_MEAN,
+                         std=IMAGENET_STD) -> torch.Tensor:
+    """Device form of the classification transform tail (row f1): collated uint8 crops [B,H,W,3]
+    (reference construct_3channel, training/datasets/classification.py:40-68) -> ToTensor -> Normalize
+    -> the ResNet stem operand NHWC [B,H,W,Cs] (channels >= 3 zero)."""
+    _check(img_u8.dtype == torch.uint8 and img_u8.dim() == 4 and img_u8.shape[-1] == 3 and img_u8.is_contiguous(),
+           "image_u8_hwc_to_nhwc: expects contiguous uint8 [B,H,W,3]")
+    B, H, W, _ = img_u8.shape
+    _check((B * H * W) % 4 == 0, "image_u8_hwc_to_nhwc: B*H*W must be a multiple of 4")
+    out = torch.empty(B, H, W, Cs, device=img_u8.device, dtype=dtype)
+    call("sv_image_u8_hwc_to_nhwc", ptr(img_u8), _host3(mean), _host3(std), ptr(out), dt(out), B, H, W, Cs)
+    return out
+
+
 def image_to_nhwc(img: torch.Tensor, Cs: int, dtype: torch.dtype) -> torch.Tensor:
     B, C, H, W = img.shape
     _check(img.dtype == torch.float32 and img.is_contiguous() and Cs >= C, "image_to_nhwc: need contiguous f32 NCHW")

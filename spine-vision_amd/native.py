@@ -98,6 +98,7 @@ _SIGS = {
     "sv_conv_bwd_weight_work_floats": [_CS],
     "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],
     "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_image_u8_hwc_to_nhwc": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_bn_nparts": [_i64, _i32],
     "sv_bn_stats": [_p, _i32, _i64, _i32, _p, _p],
     "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p],

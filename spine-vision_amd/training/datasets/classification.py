@@ -13,6 +13,18 @@ from ...core.tasks import get_task
 from .localization import normalize_u8
 
 
+def construct_3channel(t2: torch.Tensor | None, t1: torch.Tensor | None) -> torch.Tensor:
+    """uint8 [H,W] planes -> [H,W,3]: [T2,T1,T2] with both, else the one plane replicated
+    (reference training/datasets/classification.py:40-68)."""
+    if t2 is not None and t1 is not None:
+        return torch.stack([t2, t1, t2], dim=-1)
+    if t2 is not None:
+        return torch.stack([t2, t2, t2], dim=-1)
+    if t1 is not None:
+        return torch.stack([t1, t1, t1], dim=-1)
+    raise ValueError("At least one of t2_crop or t1_crop must be provided")
+
+
 class DynamicTargets:
     """Per-task target tensors with .to(device) / .to_dict() / attribute access."""
 
@@ -55,11 +67,14 @@ class ClassificationCollator:
 class SyntheticClassificationDataset(Dataset):
     """Seeded synthetic IVD crops: channels [T2, T1, T2] from two uint8 planes -> /255 -> ImageNet
     normalise; labels pfirrmann U{0..4}, modic U{0..3}, herniation Bernoulli(0.3).  ``records``
-    mirrors the reference's record dicts so create_weighted_sampler works unchanged."""
+    mirrors the reference's record dicts so create_weighted_sampler works unchanged.
+    ``device_transform``: yield the uint8 [H,W,3] crop of construct_3channel instead (the ResNet
+    backbone normalises it on the GPU, row f1)."""
 
     def __init__(self, n: int, output_size: tuple[int, int] = (256, 256), seed: int = 42,
-                 target_labels: list[str] | None = None) -> None:
+                 target_labels: list[str] | None = None, device_transform: bool = False) -> None:
         self.n, self.output_size, self.seed = n, tuple(output_size), seed
+        self.device_transform = device_transform
         self.target_labels = target_labels or ["pfirrmann", "modic", "herniation"]
         g = torch.Generator().manual_seed(seed)
         self.records = [
@@ -75,7 +90,7 @@ class SyntheticClassificationDataset(Dataset):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
         t2 = torch.randint(0, 256, self.output_size, generator=g, dtype=torch.uint8)
         t1 = torch.randint(0, 256, self.output_size, generator=g, dtype=torch.uint8)
-        img = normalize_u8(torch.stack([t2, t1, t2]))
+        img = construct_3channel(t2, t1) if self.device_transform else normalize_u8(torch.stack([t2, t1, t2]))
         r = self.records[i]
         values = {"pfirrmann": r["pfirrmann"] - 1, "modic": r["modic"], "herniation": float(r["herniation"])}
         return {"image": img, "targets": {k: values[k] for k in self.target_labels}, "level_idx": i % 5,

@@ -91,12 +91,14 @@ class TrainingConfig(BaseConfig):
     """Backbone compute precision: bf16 MFMA (throughput; the reference's fp16 autocast analogue) or
     exact f32 MFMA (parity with the reference CPU path).  ``mixed_precision=False`` forces fp32."""
     bucket_mb: float = 64.0
-    device_transform: bool = False
-    """Localization input pipeline (row f1): datasets yield the decoded uint8 grayscale image and the
-    reference transform tail (RGB replicate -> ToTensor -> Normalize) runs on the GPU, inside the
-    ConvNeXt stem's patch gather (bf16) or as ``sv_normalize_u8_gray`` (fp32) -- 12x fewer host->device
-    bytes per image and no per-sample float work in the DataLoader workers."""
     """Gradient all-reduce bucket size (MB) for multi-GPU runs."""
+    device_transform: bool = False
+    """Input pipeline (row f1): datasets yield decoded uint8 images and the reference transform tail
+    (ToTensor -> Normalize) runs on the GPU.  Localization: uint8 grayscale [H,W], RGB-replicated and
+    normalised inside the ConvNeXt stem's patch gather (bf16) or by ``sv_normalize_u8_gray`` (fp32) --
+    12x fewer host->device bytes.  Classification: the uint8 [H,W,3] crop of construct_3channel
+    ([T2,T1,T2] or one plane replicated), normalised inside the ResNet stem's NHWC conversion
+    (``sv_image_u8_hwc_to_nhwc``) -- 4x fewer bytes.  No per-sample float work in the workers."""
 
     model_config = {"arbitrary_types_allowed": True}
 

@@ -271,6 +271,29 @@ def test_normalize_u8_gray_bitwise(dev):
     assert torch.equal(K.stem_patchify(u8.to(dev)).cpu(), K.stem_patchify(ref.to(dev)).cpu())
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_image_u8_hwc_to_nhwc_bitwise(dev, dtype):
+    """Classification device transform: uint8 [B,H,W,3] crops ([T2,T1,T2]) -> ToTensor -> Normalize ->
+    NHWC stem operand, bit for bit the host transform (f32) or its RNE bf16 rounding, pad channels 0."""
+    from spine_vision_amd.training.datasets.classification import construct_3channel
+    from spine_vision_amd.training.datasets.localization import normalize_u8
+
+    g = torch.Generator().manual_seed(6)
+    B, H, W = 3, 32, 20
+    t2 = torch.randint(0, 256, (B, H, W), generator=g, dtype=torch.uint8)
+    t1 = torch.randint(0, 256, (B, H, W), generator=g, dtype=torch.uint8)
+    t2[0, 0, :4] = torch.tensor([0, 1, 254, 255], dtype=torch.uint8)
+    u8 = torch.stack([construct_3channel(t2[i], t1[i]) for i in range(B)])
+    ref = torch.stack([normalize_u8(torch.stack([t2[i], t1[i], t2[i]])) for i in range(B)]).permute(0, 2, 3, 1)
+    Cs = 8 if dtype == torch.bfloat16 else 4
+    got = K.image_u8_hwc_to_nhwc(u8.to(dev), Cs, dtype).cpu()
+    assert got.shape == (B, H, W, Cs)
+    assert torch.equal(got[..., :3], ref.to(dtype)) and not got[..., 3:].any()
+    # the f32 NCHW route of the same batch gives the same stem operand
+    nchw = ref.permute(0, 3, 1, 2).contiguous()
+    assert torch.equal(got, K.image_to_nhwc(nchw.to(dev), Cs, dtype).cpu())
+
+
 def test_stem_mfma_path(dev):
     """bf16 stem = patch gather + v3 GEMM (K 64) + LayerNorm; weight grad = split-K wgrad over 48 of
     the 64 patch columns.  Against torch fp32 conv + LN on the same bf16-rounded operands."""

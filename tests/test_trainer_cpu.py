@@ -162,3 +162,30 @@ def test_device_transform_dataset_contract():
         assert torch.equal(a[i]["coords"], b[i]["coords"]) and torch.equal(a[i]["mask"], b[i]["mask"])
     batch = LocalizationCollator()([a[i] for i in range(3)])
     assert batch["image"].shape == (3, 32, 32) and batch["image"].dtype == torch.uint8
+
+
+def test_classification_device_transform_dataset_contract():
+    """Row f1 host side, classification: construct_3channel follows the reference channel layout
+    ([T2,T1,T2], else one plane replicated, classification.py:40-68); with device_transform the dataset
+    yields that uint8 [H,W,3] crop and normalising it channel-first gives exactly the host sample."""
+    from spine_vision_amd.training.datasets import ClassificationCollator
+    from spine_vision_amd.training.datasets.classification import construct_3channel
+    from spine_vision_amd.training.datasets.localization import normalize_u8
+
+    t2 = torch.randint(0, 256, (4, 5), dtype=torch.uint8)
+    t1 = torch.randint(0, 256, (4, 5), dtype=torch.uint8)
+    both = construct_3channel(t2, t1)
+    assert both.shape == (4, 5, 3)
+    assert torch.equal(both[..., 0], t2) and torch.equal(both[..., 1], t1) and torch.equal(both[..., 2], t2)
+    assert torch.equal(construct_3channel(t2, None), t2.unsqueeze(-1).expand(4, 5, 3))
+    assert torch.equal(construct_3channel(None, t1), t1.unsqueeze(-1).expand(4, 5, 3))
+    with pytest.raises(ValueError):
+        construct_3channel(None, None)
+    a = SyntheticClassificationDataset(3, (16, 16), seed=9, device_transform=True)
+    b = SyntheticClassificationDataset(3, (16, 16), seed=9)
+    for i in range(3):
+        assert a[i]["image"].dtype == torch.uint8 and a[i]["image"].shape == (16, 16, 3)
+        assert torch.equal(normalize_u8(a[i]["image"].permute(2, 0, 1)), b[i]["image"])
+        assert a[i]["targets"] == b[i]["targets"]
+    batch = ClassificationCollator()([a[i] for i in range(3)])
+    assert batch["image"].shape == (3, 16, 16, 3) and batch["image"].dtype == torch.uint8

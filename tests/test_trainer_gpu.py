@@ -4,7 +4,7 @@ flat fused AdamW, device-side clip; two epochs on synthetic 64x64 data, checkpoi
 import pytest
 import torch
 
-from spine_vision_amd.training import CoordinateRegressor, LocalizationConfig, LocalizationTrainer
+from spine_vision_amd.training import Classifier, CoordinateRegressor, LocalizationConfig, LocalizationTrainer
 from spine_vision_amd.training.datasets import SyntheticLocalizationDataset
 
 pytestmark = pytest.mark.gpu
@@ -54,6 +54,37 @@ def test_device_transform_matches_host_transform(dev, precision):
     (l0, n0, w0, h0), (l1, n1, w1, h1) = out
     assert l0 == l1 and n0 == n1
     assert torch.equal(w0, w1) and torch.equal(h0, h1)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_classification_device_transform_matches_host_transform(dev, precision):
+    """Row f1, classification: uint8 [H,W,3] crops normalised inside the ResNet stem's NHWC conversion
+    give the SAME training step as the host ToTensor/Normalize batch (identical loss, grad norm, weights)."""
+    from oracle import weights as ow
+    from spine_vision_amd.training import StepEngine
+    from spine_vision_amd.training.datasets import ClassificationCollator, SyntheticClassificationDataset
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    ds_u8 = SyntheticClassificationDataset(4, (64, 64), seed=3, device_transform=True)
+    ds_f = SyntheticClassificationDataset(4, (64, 64), seed=3)
+    col = ClassificationCollator()
+    b_u8 = col([ds_u8[i] for i in range(4)])
+    b_f = col([ds_f[i] for i in range(4)])
+    assert b_u8["image"].dtype == torch.uint8 and b_u8["image"].shape == (4, 64, 64, 3)
+    out = []
+    for batch in (b_u8, b_f):
+        tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
+        m = Classifier("resnet18", tasks=tasks, pretrained=False, dropout=0.0, precision=precision)
+        ow.fill_module(m)
+        m = m.to(dev).train()
+        eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+        tg = {k: v.to(dev) for k, v in batch["targets"].to_dict().items()}
+        loss = eng.step_classification(batch["image"].to(dev), tg)
+        out.append((float(loss), float(eng.last_grad_norm), m.backbone.conv1.weight.detach().cpu(),
+                    m.backbone.bn1.running_mean.detach().cpu()))
+    (l0, n0, w0, r0), (l1, n1, w1, r1) = out
+    assert l0 == l1 and n0 == n1
+    assert torch.equal(w0, w1) and torch.equal(r0, r1)
 
 
 @pytest.mark.parametrize("backbone,precision", [("resnet18", "bf16"), ("resnet50", "fp32")])
