@@ -82,6 +82,8 @@ class _Tape:
     pool: tuple = ()
     out_shape: tuple = ()
     wcache: dict = field(default_factory=dict)  # bf16 weight casts shared by forward and backward
+    w2g: dict = field(default_factory=dict)  # bf16 (fc2 weight x gamma) per block, for the fc2 dgrad
+    w2g_ready: object = None  # event on the side stream after the last w2g
 
 
 class _ConvNeXtFn(torch.autograd.Function):
@@ -193,6 +195,19 @@ class ConvNeXtHip(nn.Module):
         tape = _Tape(img=img) if save else None
         cache: dict = tape.wcache if save else {}
         stem_conv, stem_ln = self.stem[0], self.stem[1]
+        if save and bf and self.overlap_wgrad:
+            # the fc2 dgrad operand bf16(W2 * gamma) of every block, made on the (otherwise idle during
+            # the forward) side stream beside the forward; the backward waits on one event
+            main = torch.cuda.current_stream()
+            side = self._side_stream(main.device)
+            side.wait_event(main.record_event())
+            with torch.cuda.stream(side):
+                for st in self.stages:
+                    for blk in st.blocks:
+                        w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+                        w2g.record_stream(main)
+                        tape.w2g[id(blk)] = w2g
+            tape.w2g_ready = side.record_event()
         if bf:
             # stem conv on MFMA: 4x4 patch rows (bf16, K padded to 64) x packed weight, then LayerNorm2d
             B, H0, W0 = img.shape[0], img.shape[-2], img.shape[-1]
@@ -285,6 +300,8 @@ class ConvNeXtHip(nn.Module):
         # d: f32 gradient stream (residual accumulation); db: its bf16 copy, the GEMM operand (bf16 mode)
         d, db = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight),
                               dlnb=g(hn.bias), with_bf16=bf)
+        if tape.w2g_ready is not None:
+            main.wait_event(tape.w2g_ready)
         self._ready([hn.weight, hn.bias])
         for st, (ds_saved, blocks_saved) in zip(reversed(list(self.stages)), reversed(tape.stages)):
             for blk, saved in zip(reversed(list(st.blocks)), reversed(blocks_saved)):
@@ -311,7 +328,9 @@ class ConvNeXtHip(nn.Module):
                 # GELU'(h) was stored by the forward epilogue
                 dh = torch.empty(M, 4 * C, device=d.device, dtype=act)
                 if bf:
-                    w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+                    w2g = tape.w2g.pop(id(blk), None)
+                    if w2g is None:
+                        w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
                     K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
                 else:
                     K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_MUL_AUX,
@@ -329,8 +348,10 @@ class ConvNeXtHip(nn.Module):
                 dy = torch.empty(M, C, device=d.device, dtype=act)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
                 # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
-                dz = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
-                                     db=g(blk.norm.bias), out_dtype=act)
+                # the LN weight/bias partials are folded on the side stream (off the data-gradient chain)
+                dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight,
+                                                dw=g(blk.norm.weight), db=g(blk.norm.bias), out_dtype=act,
+                                                defer_reduce=True)
                 dz4 = dz.view(B, H, W, C)
                 blk_params = [blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
                               blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma]
@@ -339,9 +360,10 @@ class ConvNeXtHip(nn.Module):
                     for t_ in (dz, x):
                         t_.record_stream(side)
                 with torch.cuda.stream(side) if side is not None else _nullctx():
+                    ln_finish()
                     K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
-                    # every gradient of the block is final on this stream now (the LN ones were made on
-                    # the main stream before the wait above): the bucketer's event covers them all
+                    # every gradient of the block is final on this stream now: the bucketer's event
+                    # covers them all
                     self._ready(blk_params)
                 if side is not None and bf:
                     # the bf16 copy of the gradient stream goes to a fresh buffer: the side stream's fc2

@@ -243,7 +243,12 @@ def layernorm_fwd(x2d, w, b, *, out_dtype, eps=EPS_LN):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=False, out_dtype=torch.float32):
+def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=False, out_dtype=torch.float32,
+                  defer_reduce=False):
+    """dx (+)= LayerNorm backward; dw/db (+)= the weight/bias gradient through per-block partials.
+    ``defer_reduce``: return ``(dx, finish)`` instead, ``finish()`` folding the partials into dw/db on
+    whatever stream is current when it is called (the ConvNeXt backward runs it on the weight-gradient
+    side stream, off the data-gradient chain)."""
     rows, C = x2d.shape
     _check(tuple(dy2d.shape) == (rows, C) and dy2d.is_contiguous(), "layernorm_bwd: dy must be contiguous [rows,C]")
     if dx is None:
@@ -252,6 +257,11 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
     pw = torch.empty(2, P * C, device=x2d.device, dtype=torch.float32)
     call("sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx), dt(dx),
          int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
+    if defer_reduce:
+        def finish():
+            pw.record_stream(torch.cuda.current_stream())
+            reduce_pair(pw[0], dw, pw[1], db, P)
+        return dx, finish
     if dw is not None and db is not None:
         reduce_pair(pw[0], dw, pw[1], db, P)
     elif dw is not None:
