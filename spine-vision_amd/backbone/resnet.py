@@ -114,7 +114,14 @@ class ResNetHip(nn.Module):
             setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
         self.num_features = inplanes
         self.grad_ready_hook: Callable[[list], None] | None = None
+        self._shadow: dict[int, torch.Tensor] | None = None
         self._init_weights()
+
+    def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
+        """Install bf16 views kept fresh by the flat optimizer (id(param) -> bf16 tensor).  A 1x1 conv
+        whose channels need no padding (Cs == Cin) reads its shadow directly: [Cout][Cin][1][1] is
+        already the packed [Cout][1][Cs] layout, so no per-step pack launch."""
+        self._shadow = shadow
 
     # timm ResNet.init_weights: kaiming_normal_(fan_out, relu) for convs, BN weight 1 / bias 0, and
     # zero_init_last=True: the last BN of every block starts at weight 0
@@ -170,7 +177,11 @@ class ResNetHip(nn.Module):
         """conv(x) -> (y, packed weight, shape); y in the activation dtype."""
         B, H, W, Cs = x4d.shape
         s = K.conv_shape(B, H, W, Cs, conv.weight.shape[0], k, stride, pad, Cin)
-        wp = K.conv_weight_pack(conv.weight.detach(), Cs, self.act_dtype)
+        sh = self._shadow
+        if k == 1 and self.compute_bf16 and sh is not None and id(conv.weight) in sh and Cs == conv.weight.shape[1]:
+            wp = sh[id(conv.weight)].view(conv.weight.shape[0], 1, Cs)
+        else:
+            wp = K.conv_weight_pack(conv.weight.detach(), Cs, self.act_dtype)
         return K.conv_fwd(x4d, wp, s, self.act_dtype), wp, s
 
     @torch.no_grad()

@@ -525,6 +525,18 @@ def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torc
     return y
 
 
+_ONES: dict = {}
+
+
+def _ones(n: int, device: torch.device) -> torch.Tensor:
+    """Cached f32 ones[n] per device (the gamma of an in-place accumulate epilogue): no fill launch per call."""
+    key = (n, device)
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(n, device=device, dtype=torch.float32)
+    return t
+
+
 def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: torch.Tensor | None = None,
                   accumulate: bool = False, dx_dtype: torch.dtype = torch.float32) -> torch.Tensor:
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
@@ -538,7 +550,7 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
     if _pointwise(s, wp.dtype) and (not accumulate or dx.dtype == torch.float32):
         M = s.B * s.H * s.W
         if accumulate:  # dx += dy W: the layer-scale/residual epilogue with gamma = 1, residual = dx (in place)
-            ones = torch.ones(s.Cs, device=dy.device, dtype=torch.float32)
+            ones = _ones(s.Cs, dy.device)
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
                  lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, gamma=ones,
                  aux=dx.view(M, s.Cs), compute_bf16=True)
