@@ -66,8 +66,12 @@ typedef enum {
   SV_EPI_BIAS_GELU_DUAL = 5, /* h = acc + bias[n]: C = GELU_erf'(h), C2 = GELU_erf(h)  (fc1 forward: */
                              /* the backward then needs no erf, only SV_EPI_MUL_AUX)                 */
   SV_EPI_MUL_AUX = 6,        /* C = acc * aux[m,n]                       (fc2 dgrad through GELU)    */
-  SV_EPI_BIAS_GELU = 7       /* C = GELU_erf(acc + bias[n])   (fc1 of the tape-free eval forward:   */
+  SV_EPI_BIAS_GELU = 7,      /* C = GELU_erf(acc + bias[n])   (fc1 of the tape-free eval forward:   */
                              /* one output, no GELU' for a backward that will not run)             */
+  SV_EPI_STORE_STATS = 8     /* C = acc (+ bias[n]) and the train-mode BatchNorm statistics of C:  */
+                             /* C2 (f32) [ceil(M/64)][2][N] = per 64-row group, column sum and sum */
+                             /* of squares of the values as stored (rounded to c_dtype); bf16 only, */
+                             /* N % 8 == 0, v3 kernels (a shape they cannot take is an error)      */
 } sv_epilogue;
 
 typedef struct {
@@ -276,6 +280,12 @@ int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, in
  * rounding.  B*H*W % 4 == 0, img 4-byte aligned, Cs in {4, 8}; mean/std HOST float[3].           */
 int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mean, const float* norm_std, void* out,
                             int32_t dtype, int32_t B, int32_t H, int32_t W, int32_t Cs, sv_stream_t stream);
+/* sv_conv_fwd + the BatchNorm statistics of y from the GEMM epilogue (SV_EPI_STORE_STATS): stats =
+ * f32 [ceil(M/64)][2][Cout] unshifted partials, M = B*OH*OW, folded by sv_bn_stats_finish(y = NULL).
+ * Only the bf16 gathered-operand path (Cs >= 32, power of two, Cout % 8 == 0) carries it: other
+ * shapes return SV_ERR_UNSUPPORTED (use sv_conv_fwd + sv_bn_stats).                                */
+int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
+                      float* stats, sv_stream_t stream);
 /* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
 int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                      int32_t Cs, sv_stream_t stream);
@@ -285,7 +295,8 @@ int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int3
  * (unbiased variance, torch semantics) when they are non-NULL.                                    */
 int sv_bn_nparts(int64_t rows, int32_t C);
 int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream);
-/* num_batches_tracked (int64, nullable): incremented by one on the device (BatchNorm2d.num_batches_tracked). */
+/* num_batches_tracked (int64, nullable): incremented by one on the device (BatchNorm2d.num_batches_tracked).
+ * y == NULL: `part` holds UNSHIFTED sums (the SV_EPI_STORE_STATS / sv_conv_fwd_stats partials).   */
 int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows, int32_t C,
                        float eps, float momentum, float* mean, float* rstd, float* running_mean,
                        float* running_var, int64_t* num_batches_tracked, sv_stream_t stream);

@@ -164,17 +164,23 @@ class ResNetHip(nn.Module):
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
         return self.forward(x)
 
-    def _bn(self, bn: nn.BatchNorm2d, y2d: torch.Tensor):
-        """(mean, rstd) of a BatchNorm: batch statistics (+ running update) in train mode."""
+    def _bn(self, bn: nn.BatchNorm2d, y2d: torch.Tensor, part: torch.Tensor | None = None):
+        """(mean, rstd) of a BatchNorm: batch statistics (+ running update) in train mode.  ``part``: the
+        statistics partials the conv's GEMM epilogue already produced (no read pass over y)."""
         if self.training:
             momentum = 0.1 if bn.momentum is None else bn.momentum
+            if part is not None:
+                return K.bn_stats_from_partials(part, y2d.shape[0], eps=bn.eps, momentum=momentum,
+                                                running_mean=bn.running_mean, running_var=bn.running_var,
+                                                num_batches_tracked=bn.num_batches_tracked)
             mean, rstd = K.bn_stats(y2d, eps=bn.eps, momentum=momentum, running_mean=bn.running_mean,
                                     running_var=bn.running_var, num_batches_tracked=bn.num_batches_tracked)
             return mean, rstd
         return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
 
     def _conv(self, x4d, conv, k, stride, pad, Cin=None):
-        """conv(x) -> (y, packed weight, shape); y in the activation dtype."""
+        """conv(x) -> (y, packed weight, shape, BN-statistics partials or None); y in the activation dtype.
+        In train mode (bf16) the conv GEMM's epilogue also emits the following BatchNorm's statistics."""
         B, H, W, Cs = x4d.shape
         s = K.conv_shape(B, H, W, Cs, conv.weight.shape[0], k, stride, pad, Cin)
         sh = self._shadow
@@ -182,7 +188,10 @@ class ResNetHip(nn.Module):
             wp = sh[id(conv.weight)].view(conv.weight.shape[0], 1, Cs)
         else:
             wp = K.conv_weight_pack(conv.weight.detach(), Cs, self.act_dtype)
-        return K.conv_fwd(x4d, wp, s, self.act_dtype), wp, s
+        if self.training and self.compute_bf16:
+            y, part = K.conv_fwd_bn_stats(x4d, wp, s, self.act_dtype)
+            return y, wp, s, part
+        return K.conv_fwd(x4d, wp, s, self.act_dtype), wp, s, None
 
     @torch.no_grad()
     def _forward_impl(self, img: torch.Tensor, save: bool):
@@ -192,9 +201,9 @@ class ResNetHip(nn.Module):
             x0 = K.image_u8_hwc_to_nhwc(img, cs0, act)
         else:
             x0 = K.image_to_nhwc(img, cs0, act)
-        y0, wp0, s0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3)
+        y0, wp0, s0, p0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3)
         B, H, W, C = y0.shape
-        m0, r0 = self._bn(self.bn1, y0.view(-1, C))
+        m0, r0 = self._bn(self.bn1, y0.view(-1, C), p0)
         a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act).view(B, H, W, C)
         x, idx = K.maxpool_fwd(a0)
         tape = _Tape() if save else None
@@ -206,9 +215,9 @@ class ResNetHip(nn.Module):
             saved = []
             convs = blk.convs()
             for ci, (conv, bn, k, st, pad, relu) in enumerate(convs):
-                y, wp, s = self._conv(cur, conv, k, st, pad)
+                y, wp, s, part = self._conv(cur, conv, k, st, pad)
                 Bq, Hq, Wq, Cq = y.shape
-                mean, rstd = self._bn(bn, y.view(-1, Cq))
+                mean, rstd = self._bn(bn, y.view(-1, Cq), part)
                 last = ci == len(convs) - 1
                 if not last:
                     a = K.bn_act(y.view(-1, Cq), mean, rstd, bn.weight, bn.bias, relu=True, out_dtype=act)
@@ -224,8 +233,8 @@ class ResNetHip(nn.Module):
             ds_saved = None
             if blk.downsample is not None:
                 dconv, dbn = blk.downsample[0], blk.downsample[1]
-                yd, wpd, sd = self._conv(x_in, dconv, 1, blk.stride, 0)
-                md, rd = self._bn(dbn, yd.view(-1, Cq))
+                yd, wpd, sd, pd = self._conv(x_in, dconv, 1, blk.stride, 0)
+                md, rd = self._bn(dbn, yd.view(-1, Cq), pd)
                 out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias, res=yd.view(-1, Cq),
                                res_bn=(md, rd, dbn.weight, dbn.bias), relu=True, out_dtype=act)
                 ds_saved = (yd, md, rd, wpd, sd)

@@ -140,7 +140,9 @@ __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
   float s1, s2;
   if (!fold_partials(part, P, C, s1, s2)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float k = ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
+  // shift k: row 0 of y (sv_bn_stats partials); y == NULL: unshifted partials (SV_EPI_STORE_STATS)
+  const float k = y == nullptr ? 0.f
+                  : ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
   const float n = (float)rows;
   const float m1 = s1 / n;
   const float var = fmaxf(s2 / n - m1 * m1, 0.f);
@@ -418,7 +420,7 @@ extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t
 extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows,
                                   int32_t C, float eps, float momentum, float* mean, float* rstd, float* running_mean,
                                   float* running_var, int64_t* num_batches_tracked, sv_stream_t stream) {
-  SV_REQUIRE(y && part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
+  SV_REQUIRE(part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
              "sv_bn_stats_finish: bad arguments");
   stats_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
                                                                         momentum, mean, rstd, running_mean, running_var,

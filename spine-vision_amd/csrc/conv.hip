@@ -618,8 +618,8 @@ extern "C" int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mea
   return check_launch("sv_image_u8_hwc_to_nhwc");
 }
 
-extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                           const sv_conv_shape* s, sv_stream_t stream) {
+static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
+                         const sv_conv_shape* s, float* stats, sv_stream_t stream) {
   if (int rc = check_shape(s, dtype, "sv_conv_fwd")) return rc;
   SV_REQUIRE(x && wp && y, "sv_conv_fwd: null pointer");
   SV_REQUIRE(y_dtype == SV_BF16 || y_dtype == SV_F32, "sv_conv_fwd: bad y dtype");
@@ -652,11 +652,29 @@ extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dty
       g.tdy[j] = a.tdy[j];
       g.tdx[j] = a.tdx[j];
     }
-    const sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype);
+    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype);
+    if (stats) {
+      SV_REQUIRE(a.N % 8 == 0 && ((uintptr_t)stats & 15) == 0, "sv_conv_fwd_stats: Cout %% 8 / stats alignment");
+      d.epilogue = SV_EPI_STORE_STATS;
+      d.C2 = stats;
+      d.c2_dtype = SV_F32;
+    }
     const int rc = launch_gemm3_conv(&d, g, 1, (hipStream_t)stream);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
+  SV_REQUIRE(!stats, "sv_conv_fwd_stats: shape not on the gathered bf16 GEMM path (use sv_conv_fwd + sv_bn_stats)");
   return launch_dt<FPROP>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
+                           const sv_conv_shape* s, sv_stream_t stream) {
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, nullptr, stream);
+}
+
+extern "C" int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
+                                 const sv_conv_shape* s, float* stats, sv_stream_t stream) {
+  SV_REQUIRE(stats, "sv_conv_fwd_stats: null stats");
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream);
 }
 
 extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,

@@ -307,7 +307,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
-  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_BIAS_GELU, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_STORE_STATS, "sv_gemm: bad epilogue %d", d->epilogue);
   if (d->M == 0 || d->N == 0) return SV_OK;
   const bool bf = d->compute == SV_BF16;
   SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
@@ -328,6 +328,8 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (d->epilogue == SV_EPI_BIAS_GELU2 || d->epilogue == SV_EPI_BIAS_GELU_DUAL)
     SV_REQUIRE(d->C2 && al16(d->C2), "sv_gemm: GELU epilogue needs an aligned C2");
   if (d->epilogue == SV_EPI_BIAS_GAMMA_RES) SV_REQUIRE(d->gamma && d->aux, "sv_gemm: gamma/residual missing");
+  if (d->epilogue == SV_EPI_STORE_STATS)
+    SV_REQUIRE(bf && d->C2 && al16(d->C2) && d->N % 8 == 0, "sv_gemm: STORE_STATS needs bf16, an aligned C2, N %% 8 == 0");
   if (d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX) SV_REQUIRE(d->aux, "sv_gemm: aux missing");
   if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
@@ -336,6 +338,11 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
   static const bool force_v1 = getenv("SV_GEMM_V1") != nullptr;
   static const int impl = getenv("SV_GEMM_IMPL") ? atoi(getenv("SV_GEMM_IMPL")) : 0;
+  if (d->epilogue == SV_EPI_STORE_STATS) {  // only the v3 kernels carry the statistics epilogue
+    const int rc = launch_gemm3(d, s);
+    SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_STATS needs K %% 32 == 0 and bf16 operands");
+    return rc;
+  }
   if (!force_v1) {
     // Measured per ConvNeXt shape (tools/gemm_bench.py, profiles/r1s2_gemm_cfg.txt):
     //   v3 32x3 (two workgroups per CU, one's epilogue beside the other's MFMAs): VALU-heavy and

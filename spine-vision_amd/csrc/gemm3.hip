@@ -409,6 +409,7 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
     case SV_EPI_BIAS_GELU_DUAL: return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, BKT, S>(d, split, s);
     case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, BKT, S>(d, split, s);
     case SV_EPI_BIAS_GELU: return launch<AK, BKM, SV_EPI_BIAS_GELU, BKT, S>(d, split, s);
+    case SV_EPI_STORE_STATS: return launch<AK, BKM, SV_EPI_STORE_STATS, BKT, S>(d, split, s);
     default: return SV_ERR_UNSUPPORTED;
   }
 }
@@ -429,6 +430,8 @@ int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream
   if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && g.lsc < 5))
     return SV_ERR_UNSUPPORTED;
   if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
+  if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
+    return launch<true, true, SV_EPI_STORE_STATS, 32, 3, 1>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, 3, 2>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
     return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, 3, 2>(d, 1, s, &g);

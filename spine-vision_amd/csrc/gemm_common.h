@@ -146,6 +146,13 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
   const bool okn4 = n + 4 < e.N;
   const bool slab_out = e.epi == SV_EPI_SLAB;
   const bool need_aux = e.epi == SV_EPI_BIAS_GAMMA_RES || e.epi == SV_EPI_GELU_GRAD || e.epi == SV_EPI_MUL_AUX;
+  // SV_EPI_STORE_STATS (compile-time kernels only): per-lane column sums of the stored values
+  constexpr bool kStats = EPI == SV_EPI_STORE_STATS;
+  float cs1[8], cs2[8];
+  if constexpr (kStats) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs1[j] = cs2[j] = 0.f;
+  }
   float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, g0 = b0, g1 = b0;
   if (okn && e.bias && !slab_out && e.epi != SV_EPI_GELU_GRAD && e.epi != SV_EPI_MUL_AUX) {
     b0 = *reinterpret_cast<const float4*>(e.bias + n);
@@ -254,7 +261,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       va = add4(va, b0);
       vb = add4(vb, b1);
       float4 oa, ob;
-      if (e.epi == SV_EPI_STORE || e.epi == SV_EPI_BIAS_GELU2) {
+      if (e.epi == SV_EPI_STORE || e.epi == SV_EPI_BIAS_GELU2 || e.epi == SV_EPI_STORE_STATS) {
         oa = va;
         ob = vb;
       } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
@@ -279,6 +286,15 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       const size_t ci = (size_t)m * e.ldc + n;
       if (okn4) st8_out(e.C, e.c_dtype, ci, oa, ob, e.wt);
       else st4_any(e.C, e.c_dtype, ci, oa);
+      if constexpr (kStats) {  // N % 8 == 0: all 8 columns valid
+        const float o8[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float q = e.c_dtype == SV_BF16 ? __uint_as_float((uint32_t)f2bf(o8[j]) << 16) : o8[j];
+          cs1[j] += q;
+          cs2[j] = fmaf(q, q, cs2[j]);
+        }
+      }
       if (e.epi == SV_EPI_BIAS_GELU2) {
         if (okn4) st8_out(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb), e.wt);
         else st4_any(e.C2, e.c2_dtype, ci, gelu4(va));
@@ -290,6 +306,25 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  if constexpr (kStats) {
+    // lanes l, l+8, ..., l+56 hold the same 8 columns over the group's 64 rows: fold them (fixed
+    // order, bit-stable), then lanes 0..7 write the group's partial row [mb/64][2][N] (one writer each)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1) {
+        cs1[j] += __shfl_xor(cs1[j], off);
+        cs2[j] += __shfl_xor(cs2[j], off);
+      }
+    }
+    if (l < 8 && okn && mb < e.M) {  // groups wholly past M have no partial row
+      float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N + n;
+      *reinterpret_cast<float4*>(P) = make_float4(cs1[0], cs1[1], cs1[2], cs1[3]);
+      *reinterpret_cast<float4*>(P + 4) = make_float4(cs1[4], cs1[5], cs1[6], cs1[7]);
+      *reinterpret_cast<float4*>(P + e.N) = make_float4(cs2[0], cs2[1], cs2[2], cs2[3]);
+      *reinterpret_cast<float4*>(P + e.N + 4) = make_float4(cs2[4], cs2[5], cs2[6], cs2[7]);
+    }
   }
 }
 

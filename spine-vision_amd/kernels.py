@@ -9,6 +9,7 @@ missing library or a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -535,6 +536,48 @@ def _ones(n: int, device: torch.device) -> torch.Tensor:
     if t is None:
         t = _ONES[key] = torch.ones(n, device=device, dtype=torch.float32)
     return t
+
+
+_CONV_GEMM = os.environ.get("SV_CONV_GEMM", "1") not in ("0", "")
+
+
+def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype):
+    """conv_fwd plus the train-mode BatchNorm statistics of y straight from the GEMM epilogue
+    (SV_EPI_STORE_STATS: no separate read pass over y) -> (y, partials [ceil(M/64)][2][Cout] f32), or
+    (y, None) when the conv runs on a path without that epilogue (then use bn_stats(y))."""
+    if wp.dtype != torch.bfloat16 or out_dtype != torch.bfloat16 or s.Cout % 8:
+        return conv_fwd(x, wp, s, out_dtype), None
+    OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
+    M = s.B * OH * OW
+    if _pointwise(s, wp.dtype):
+        if s.Cs % 32:
+            return conv_fwd(x, wp, s, out_dtype), None
+        _conv_check_x(x, s, wp.dtype, "conv_fwd")
+        y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
+        part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
+        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
+             ldb=s.Cs, C=y.view(M, s.Cout), C2=part, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True)
+        return y, part
+    if not (_CONV_GEMM and s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0):
+        return conv_fwd(x, wp, s, out_dtype), None
+    _conv_check_x(x, s, wp.dtype, "conv_fwd")
+    _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
+    y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
+    part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
+    call("sv_conv_fwd_stats", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part))
+    return y, part
+
+
+def bn_stats_from_partials(part: torch.Tensor, rows: int, *, eps: float = EPS_BN, momentum: float = 0.1,
+                           running_mean=None, running_var=None, num_batches_tracked=None):
+    """(mean, rstd) from conv_fwd_bn_stats' unshifted partials; running stats updated like bn_stats."""
+    P, two, C = part.shape
+    _check(two == 2 and part.dtype == torch.float32 and part.is_contiguous(), "bn_stats_from_partials: bad partials")
+    mean = torch.empty(C, device=part.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    call("sv_bn_stats_finish", None, SV_F32, ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked))
+    return mean, rstd
 
 
 def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: torch.Tensor | None = None,

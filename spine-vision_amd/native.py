@@ -21,7 +21,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 SV_F32, SV_BF16 = 0, 1
 SV_IMG_F32_NCHW, SV_IMG_U8_GRAY = 0, 1
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
- SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU) = range(8)
+ SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS) = range(9)
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -94,6 +94,7 @@ _SIGS = {
     # ResNet
     "sv_conv_weight_pack": [_p, _p, _i32, _CS, _p],
     "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _p],
+    "sv_conv_fwd_stats": [_p, _p, _p, _i32, _i32, _CS, _p, _p],
     "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],
     "sv_conv_bwd_weight_work_floats": [_CS],
     "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],

@@ -85,6 +85,38 @@ def test_conv_fwd_dgrad_wgrad(dev, case, precision):
         assert rel(base - 1.0, dx) < 1e-6
 
 
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 128, 1, 1), (1, 9, 9, 64, 64, 3, 1), (2, 14, 10, 64, 256, 3, 1),
+                                  (2, 16, 16, 256, 512, 1, 2), (3, 7, 5, 128, 64, 3, 2)])
+def test_conv_fwd_bn_stats_epilogue(dev, case):
+    """SV_EPI_STORE_STATS: the conv GEMM's epilogue emits the BatchNorm statistics of its stored bf16
+    output.  Same y as conv_fwd (bitwise), and mean / rstd / running stats as bn_stats over that y
+    (f32 rounding only).  Cases: pointwise GEMM, gathered 3x3 / stride 2, M not a multiple of 64
+    (81 rows: a partial row group) and M below one 256-row tile."""
+    B, H, W, Cs, Cout, k, st = case
+    pad = k // 2
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(B, H, W, Cs, generator=g) + 0.5).to(torch.bfloat16).to(dev)
+    w = torch.randn(Cout, Cs, k, k, generator=g) * 0.1
+    s = K.conv_shape(B, H, W, Cs, Cout, k, st, pad)
+    wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
+    y_ref = K.conv_fwd(x, wp, s, torch.bfloat16)
+    y, part = K.conv_fwd_bn_stats(x, wp, s, torch.bfloat16)
+    assert part is not None
+    assert torch.equal(y, y_ref)
+    rows = y.numel() // Cout
+    assert part.shape == ((rows + 63) // 64, 2, Cout)
+    rm0 = torch.rand(Cout, generator=g).to(dev)
+    rv0 = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    rm1, rv1, rm2, rv2 = rm0.clone(), rv0.clone(), rm0.clone(), rv0.clone()
+    m1, r1 = K.bn_stats(y.view(rows, Cout), running_mean=rm1, running_var=rv1)
+    m2, r2 = K.bn_stats_from_partials(part, rows, running_mean=rm2, running_var=rv2)
+    yd = y.view(rows, Cout).double().cpu()
+    assert rel(m2, yd.mean(0)) < 1e-5
+    assert rel(r2, 1.0 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-4
+    assert rel(m2, m1) < 1e-5 and rel(r2, r1) < 1e-4
+    assert rel(rm2, rm1) < 1e-5 and rel(rv2, rv1) < 1e-4
+
+
 @pytest.mark.parametrize("C", [64, 256, 2048])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_batchnorm_train_fwd_bwd(dev, C, precision):
