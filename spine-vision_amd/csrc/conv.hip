@@ -458,19 +458,21 @@ __global__ void __launch_bounds__(256) image_u8_hwc_kernel(const uint8_t* __rest
 }
 
 // dw[co][c][t] (+)= sum_s slab[s][co][t*Cs + c]   (c < Cin)
+// One thread per slab element, in slab order [Cout][T][Cs] (c fastest): the split x reads -- the bulk
+// of the traffic -- are coalesced; only the single write per element is strided (by T, torch layout).
 __global__ void wgrad_finish_kernel(const float* __restrict__ slab, int split, int Cout, int Cin, int T_, int Cs,
                                     float* __restrict__ dw, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over dw [Cout][Cin][T]
-  const int64_t n = (int64_t)Cout * Cin * T_;
-  if (i >= n) return;
-  const int t = (int)(i % T_);
-  const int c = (int)((i / T_) % Cin);
-  const int co = (int)(i / ((int64_t)T_ * Cin));
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over slab [Cout][T][Cs]
   const int64_t MN = (int64_t)Cout * T_ * Cs;
-  const int64_t off = (int64_t)co * T_ * Cs + (int64_t)t * Cs + c;
+  if (i >= MN) return;
+  const int c = (int)(i % Cs);
+  if (c >= Cin) return;  // padded channels
+  const int t = (int)((i / Cs) % T_);
+  const int co = (int)(i / ((int64_t)Cs * T_));
   float s = 0.f;
-  for (int p = 0; p < split; ++p) s += slab[p * MN + off];
-  dw[i] = accumulate ? dw[i] + s : s;
+  for (int p = 0; p < split; ++p) s += slab[p * MN + i];
+  const int64_t o = ((int64_t)co * Cin + c) * T_ + t;
+  dw[o] = accumulate ? dw[o] + s : s;
 }
 
 // ---- host helpers -----------------------------------------------------------------------------
@@ -797,7 +799,7 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
     d.split_k = sp;
     const int rc = launch_gemm3_conv(&d, g, 3, st);
     if (rc == SV_OK) {
-      const int64_t n = (int64_t)s->Cout * s->Cin * T_;
+      const int64_t n = (int64_t)s->Cout * T_ * s->Cs;
       wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, sp, s->Cout, s->Cin, T_, s->Cs, dw,
                                                                     accumulate);
       return check_launch("sv_conv_bwd_weight(finish)");
@@ -828,7 +830,7 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
   a.c_dtype = SV_F32;
   a.kper = ceil_div(ceil_div(a.K, split), BKT) * BKT;
   if (int rc = launch_dt<WGRAD>(a, dtype, split, st)) return rc;
-  const int64_t n = (int64_t)s->Cout * s->Cin * T_;
+  const int64_t n = (int64_t)s->Cout * T_ * s->Cs;
   wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, split, s->Cout, s->Cin, T_, s->Cs, dw, accumulate);
   return check_launch("sv_conv_bwd_weight(finish)");
 }
