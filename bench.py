@@ -305,6 +305,7 @@ def main():
         },
         "roofline": roof,
         "loss": round(final_loss, 6),
+        "hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)

@@ -12,6 +12,8 @@ caller), so the host can run ahead and enqueue the next step while the GPU works
 
 from __future__ import annotations
 
+import os
+from collections import deque
 from typing import Any, Callable
 
 import torch
@@ -21,6 +23,33 @@ from .. import kernels as K
 from .comm import BufferSync, GradBucketer, broadcast_parameters
 from .flat import FlatArena
 from .optim import FlatAdamW
+
+
+class InflightLimiter:
+    """Bounds how many enqueued training steps the host may run ahead of the GPU.
+
+    Tensors handed to the weight-gradient side stream (``record_stream``) and the all-reduce stream
+    can only be reused by the caching allocator once the GPU has passed them.  A host that runs
+    unboundedly ahead therefore keeps every in-flight step's activations allocated.  Measured on
+    ConvNeXt-base bs32: 124 GB reserved; ConvNeXt-large bs64 filled the 288 GB and fell into
+    allocator free-and-retry at 165 img/s.  After each step an event is recorded, and the host waits
+    for the step ``max_inflight`` steps back.  The GPU still always has a full step queued.
+    """
+
+    def __init__(self, max_inflight: int | None = None) -> None:
+        if max_inflight is None:  # SV_MAX_INFLIGHT: 0 = unbounded
+            max_inflight = int(os.environ.get("SV_MAX_INFLIGHT", "2"))
+        self.max_inflight = int(max_inflight)
+        self._events: deque = deque()
+
+    def step_done(self) -> None:
+        if self.max_inflight <= 0 or not torch.cuda.is_initialized():
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        self._events.append(ev)
+        while len(self._events) > self.max_inflight:
+            self._events.popleft().synchronize()
 
 
 class StepEngine:
@@ -43,6 +72,7 @@ class StepEngine:
             self.bucketer.attach(model)
             self.buffer_sync = BufferSync(model)
         self.last_grad_norm: torch.Tensor | None = None
+        self.limiter = InflightLimiter() if self.device.type == "cuda" else None
 
     def step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
         """Run one optimisation step; returns the (device) loss tensor."""
@@ -59,6 +89,8 @@ class StepEngine:
             self.last_grad_norm = nc[0:1]
             scale = nc[1:2]
         self.optimizer.step(grad_scale=scale)
+        if self.limiter is not None:
+            self.limiter.step_done()
         return loss.detach()
 
     # convenience wrappers for the two reference trainers' batch layouts

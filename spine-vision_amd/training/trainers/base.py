@@ -36,6 +36,7 @@ from torch.utils.data import DataLoader, Dataset, Sampler
 
 from .. import optim as flat_optim
 from ..comm import BufferSync, GradBucketer, broadcast_parameters
+from ..engine import InflightLimiter
 from ..flat import FlatArena
 
 logger = logging.getLogger("spine_vision_amd")
@@ -198,6 +199,8 @@ class BaseTrainer:
         self.scheduler = self._create_scheduler()
         self.bucketer = None
         self.buffer_sync = None
+        # bounded host lookahead (engine.InflightLimiter): side-stream tensors of queued steps stay pinned
+        self._limiter = InflightLimiter() if self.device.type == "cuda" else None
         if self.world > 1:
             self.buffer_sync = BufferSync(self.model)
             if isinstance(self.optimizer, flat_optim.FlatAdamW):
@@ -308,6 +311,8 @@ class BaseTrainer:
 
                 scale = K.grad_clip_coef(opt.arena.grad_flat, self.config.grad_clip)[1:2]
             opt.step(grad_scale=scale)
+            if self._limiter is not None:
+                self._limiter.step_done()
         else:
             params = [p for p in self.model.parameters() if p.grad is not None]
             if self.world > 1:
