@@ -201,9 +201,15 @@ def main():
 
     bf = args.precision == "bf16"
     probe = K.GemmProbe(PROBE_KEYS[args.probe] + (bf,))
-    K.PROBE = None if cls else probe  # the classification line reports the whole-step rate, no probe
+    # The probe's HIP events bracket every launch of the class in the LAST timed step: each timing event
+    # is a release packet that writes back L2, and probing all K steps cost 2.3% of the step
+    # (tools/gpu_probe_ab.sh).  The classification line reports the whole-step rate and takes no probe;
+    # SV_BENCH_PROBE=0 leaves the roofline fields empty and SV_BENCH_PROBE=all probes every step.
+    probe_mode = os.environ.get("SV_BENCH_PROBE", "1")
+    use_probe = not cls and probe_mode != "0"
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        K.PROBE = probe if use_probe and (probe_mode == "all" or i == args.steps - 1) else None
         loss = run_step()
     torch.cuda.synchronize()
     if world > 1:
