@@ -124,6 +124,10 @@ class ConvNeXtHip(nn.Module):
         # weight-gradient kernels on a side stream beside the data-gradient chain (SV_SIDE_STREAM=0: off)
         self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
         self.side_wg_per_cu = int(os.environ.get("SV_SIDE_WG_PER_CU", "1"))
+        # bf16 backward: ONE main->side hand-off per block (after the LayerNorm backward) instead of three,
+        # and the side stream's operands kept alive in a list until the streams join instead of
+        # record_stream -- every cross-stream event / allocator event is a release packet (L2 write-back)
+        self.lean_sync = os.environ.get("SV_LEAN_SYNC", "1") != "0"
         self._side: dict = {}
         self._init_weights()
 
@@ -297,6 +301,8 @@ class ConvNeXtHip(nn.Module):
         side = self._side_stream(main.device) if self.overlap_wgrad else None
         # block GEMMs of the two streams: one persistent workgroup per CU each, so they share every CU
         prev_res = nv.value("sv_gemm_set_workgroups_per_cu", self.side_wg_per_cu if side is not None else 0)
+        lean = side is not None and bf and self.lean_sync
+        keep: list = []  # lean mode: side-stream operands, released once main has joined the side stream
         # d: f32 gradient stream (residual accumulation); db: its bf16 copy, the GEMM operand (bf16 mode)
         d, db = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight),
                               dlnb=g(hn.bias), with_bf16=bf)
@@ -311,6 +317,9 @@ class ConvNeXtHip(nn.Module):
                 d2 = d.view(M, C)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 dsrc = db.view(M, C) if bf else d2
+                if lean:
+                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, keep)
+                    continue
                 # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
                 # stream beside the data-gradient chain of the main stream: the wgrads are MFMA-bound
                 # with small outputs, the dgrads epilogue/HBM-bound, so the two overlap on the chip
@@ -405,7 +414,46 @@ class ConvNeXtHip(nn.Module):
         nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
+            keep.clear()  # safe: later main-stream allocations are ordered after the join
         self._ready([conv.weight, conv.bias, ln.weight, ln.bias])
+
+
+    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, keep):
+        """bf16 block backward with one main->side hand-off.  Main: fc2 dgrad (x GELU'), fc1 dgrad,
+        LayerNorm backward, depthwise backward-data.  Side, after the LayerNorm backward: fc2 wgrad
+        (+ gamma, bias), fc1 wgrad (+ bias), the LayerNorm weight/bias fold and the depthwise wgrad of
+        the block, beside the main stream's next block.  Returns the new (d, db)."""
+        g = self._grad
+        x, z, y, mean, rstd, gh, a = saved
+        B, H, W, C = x.shape
+        M = B * H * W
+        w1 = self._w(blk.mlp.fc1.weight, cache)
+        w2g = tape.w2g.pop(id(blk), None)
+        if w2g is None:
+            w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+        dh = torch.empty(M, 4 * C, device=d.device, dtype=torch.bfloat16)
+        K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
+        dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
+        K.linear_dgrad(dh, w1, out=dy, compute_bf16=True)
+        dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                        db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
+        dz4 = dz.view(B, H, W, C)
+        side.wait_event(main.record_event())
+        keep.extend((dsrc, dh, dz, ln_finish))
+        with torch.cuda.stream(side):
+            K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
+                               dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
+                               compute_bf16=True)
+            K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
+                           compute_bf16=True)
+            ln_finish(record=False)
+            K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+            self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias, blk.mlp.fc1.weight,
+                         blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
+        # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
+        db = torch.empty_like(db)
+        K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
+        return d, db
 
 
 def create_convnext(name: str, precision: str = "bf16") -> ConvNeXtHip:

@@ -259,8 +259,9 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
     call("sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx), dt(dx),
          int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
     if defer_reduce:
-        def finish():
-            pw.record_stream(torch.cuda.current_stream())
+        def finish(record: bool = True):
+            if record:  # the caller may instead keep pw alive until the streams have joined
+                pw.record_stream(torch.cuda.current_stream())
             reduce_pair(pw[0], dw, pw[1], db, P)
         return dx, finish
     if dw is not None and db is not None:
