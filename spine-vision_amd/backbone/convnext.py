@@ -202,15 +202,17 @@ class ConvNeXtHip(nn.Module):
         if save and bf and self.overlap_wgrad:
             # the fc2 dgrad operand bf16(W2 * gamma) of every block, made on the (otherwise idle during
             # the forward) side stream beside the forward; the backward waits on one event
+            # (allocated on the main stream, which frees them after waiting on w2g_ready: no
+            # record_stream, whose allocator event is one more release packet per tensor)
             main = torch.cuda.current_stream()
             side = self._side_stream(main.device)
+            blocks = [blk for st in self.stages for blk in st.blocks]
+            for blk in blocks:
+                tape.w2g[id(blk)] = torch.empty(blk.mlp.fc2.weight.shape, device=img.device, dtype=torch.bfloat16)
             side.wait_event(main.record_event())
             with torch.cuda.stream(side):
-                for st in self.stages:
-                    for blk in st.blocks:
-                        w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
-                        w2g.record_stream(main)
-                        tape.w2g[id(blk)] = w2g
+                for blk in blocks:
+                    K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach(), out=tape.w2g[id(blk)])
             tape.w2g_ready = side.record_event()
         if bf:
             # stem conv on MFMA: 4x4 patch rows (bf16, K padded to 64) x packed weight, then LayerNorm2d
@@ -272,6 +274,11 @@ class ConvNeXtHip(nn.Module):
         if save:
             tape.pool = (pooled, p_mean, p_rstd)
             tape.out_shape = tuple(x.shape)
+            if tape.w2g_ready is not None:
+                # the main stream owns the w2g buffers: join the side stream's writes before any path
+                # (backward, or a tape dropped without one) can free them (long finished by now)
+                torch.cuda.current_stream().wait_event(tape.w2g_ready)
+                tape.w2g_ready = None
         return feat, tape
 
     # -- backward ----------------------------------------------------------------------------------

@@ -431,11 +431,13 @@ def pool_ln_bwd(dfeat, pooled, mean, rstd, lnw, shape, *, dlnw, dlnb, with_bf16=
 
 # ----------------------------------------------------------------------------------------------
 # optimizer pieces
-def scale_rows_bf16(W: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+def scale_rows_bf16(W: torch.Tensor, scale: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """bf16(W * scale[:, None]) for a 2-D f32 weight (fc2 weight with the layer scale folded in)."""
     rows, cols = W.shape
     _check(W.dtype == torch.float32 and W.is_contiguous() and scale.numel() == rows, "scale_rows_bf16: bad args")
-    out = torch.empty(rows, cols, device=W.device, dtype=torch.bfloat16)
+    if out is None:
+        out = torch.empty(rows, cols, device=W.device, dtype=torch.bfloat16)
+    _check(out.shape == (rows, cols) and out.dtype == torch.bfloat16 and out.is_contiguous(), "scale_rows_bf16: bad out")
     call("sv_scale_rows_bf16", ptr(W), ptr(scale), ptr(out), rows, cols)
     return out
 
