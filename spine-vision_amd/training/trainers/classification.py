@@ -67,6 +67,11 @@ class ClassificationTrainer(BaseTrainer):
             raise NotImplementedError(
                 "ClassificationDataset crop extraction is outside the MI355X training path; pass train_dataset/"
                 "val_dataset (e.g. training.datasets.SyntheticClassificationDataset or your own crops)")
+        if config.device_transform:
+            # row f1: datasets that support it yield the uint8 [H,W,3] crop (normalised on the device)
+            for ds in (train_dataset, val_dataset):
+                if hasattr(ds, "device_transform"):
+                    ds.device_transform = True
         target_labels = config.target_labels or list(AVAILABLE_TASK_NAMES)
         self._sampler_obj = None
         if config.use_weighted_sampling and hasattr(train_dataset, "records"):

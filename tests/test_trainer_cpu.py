@@ -189,3 +189,21 @@ def test_classification_device_transform_dataset_contract():
         assert a[i]["targets"] == b[i]["targets"]
     batch = ClassificationCollator()([a[i] for i in range(3)])
     assert batch["image"].shape == (3, 16, 16, 3) and batch["image"].dtype == torch.uint8
+
+
+def test_classification_config_device_transform_reaches_datasets(tmp_path):
+    """ClassificationConfig(device_transform=True) switches datasets that support it to the uint8 crop."""
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    class CpuCls(ClassificationTrainer):
+        def _create_optimizer(self):
+            return torch.optim.AdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-5)
+
+    labels = ["pfirrmann", "modic", "herniation"]
+    tr_ds = SyntheticClassificationDataset(4, (16, 16), seed=1, target_labels=labels)
+    va_ds = SyntheticClassificationDataset(2, (16, 16), seed=2, target_labels=labels)
+    cfg = ClassificationConfig(output_path=tmp_path, batch_size=2, num_epochs=1, num_workers=0, pin_memory=False,
+                               target_labels=labels, output_size=(16, 16), pretrained=False, device_transform=True)
+    CpuCls(cfg, model=TinyCls(_create_tasks_for_training(labels)), train_dataset=tr_ds, val_dataset=va_ds)
+    assert tr_ds.device_transform and va_ds.device_transform
+    assert tr_ds[0]["image"].dtype == torch.uint8 and tr_ds[0]["image"].shape == (16, 16, 3)
