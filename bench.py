@@ -4,12 +4,20 @@
 images normalised like the reference's transforms, inputs already resident in HBM.
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py)
 
-Rank 0 prints ONE JSON line.  ``roofline`` times every launch of one GEMM class (the dominant
-kernel) with HIP events on its own stream inside the timed region; ``cpu_baseline``
-times the fp32 CPU restatement of the same step (oracle/, TEST INFRASTRUCTURE) on the host cores
-over a bounded sample, rank 0 at N=1 only.
+N > 1: when launched without torch.distributed.run (no WORLD_SIZE in the environment) bench.py starts
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1`` on itself as a CHILD
+process before touching the GPU, and exits with its code; launched by torch.distributed.run it is one
+rank (RANK / LOCAL_RANK / WORLD_SIZE from the environment; rank 0 checks WORLD_SIZE == --gpus).
+
+Rank 0 prints ONE JSON line.  ``roofline`` is the dominant GEMM class of the step (the one with the
+most device time): every launch of each probed class is timed with HIP events on its launching
+stream in the last timed step; ``roofline.kernels`` carries every probed class (split-K weight
+gradients, the fc2 data gradient, the forward GEMMs) and ``step_mfma_frac`` the whole-step model-FLOP
+rate against the bf16 MFMA peak (the north-star quantity).  ``comm`` (N > 1) carries the RCCL
+all-reduce bus bandwidth and the fraction of it hidden under the backward.  ``cpu_baseline`` times
+the fp32 CPU restatement of the same step (oracle/, TEST INFRASTRUCTURE) on the host cores over a
+bounded sample, rank 0 at N=1 only.
 """
 
 from __future__ import annotations
@@ -17,6 +25,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,12 +42,18 @@ METRIC = "images/sec training, ConvNeXt-base 512x512 loc, bs32, at 1/2/4/8 MI355
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_F32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (guide: ~8 TB/s)
-PROBE_KEYS = {"fwd": (True, True), "dgrad": (True, False), "wgrad": (False, False)}
+SV_EPI_SLAB, SV_EPI_MUL_AUX = 4, 6  # include/sv_kernels.h (checked against native at run time)
+# probed GEMM classes: (a_kmajor, b_kmajor[, epilogue])
+PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, SV_EPI_MUL_AUX),
+              "fwd": (True, True)}
+PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsample, stem; side stream)",
+               "fc2_dgrad": "fc2 data gradient dh = (dY (W2 gamma)) * GELU'(h) (critical path)",
+               "fwd": "forward GEMMs: fc1 (+GELU), fc2 (+gamma, residual), stem, downsample"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, or 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="localization", choices=["localization", "classification"],
@@ -47,7 +63,9 @@ def parse():
     ap.add_argument("--image-size", type=int, default=None, help="default 512 (localization) / 256 (classification)")
     ap.add_argument("--backbone", default=None, help="default convnext_base / resnet50")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--probe", default="fwd", choices=sorted(PROBE_KEYS))
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher / all-reduce plumbing check on CPU (gloo, a small torch model): no GPU, no "
+                         "measurement -- used by tests/test_bench_launcher.py")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inference", action="store_true",
                     help="secondary line (row f2): the validation / predict forward (eval mode, no tape) instead "
@@ -104,9 +122,9 @@ def cpu_baseline(args):
     from oracle import heads as oh
     from oracle import step as ostep
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
-    B = 4
+    B = args.batch  # the same batch as the GPU line
     if args.workload == "classification":
         from oracle import resnet as orn
 
@@ -146,20 +164,178 @@ def cpu_baseline(args):
     }
 
 
+def host_threads() -> int:
+    """Host threads for the CPU baseline: the CPUs this process may run on, capped by the cgroup CPU
+    quota when there is one (a GPU box's share of a large host: affinity shows every CPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline_config0():
+    """configs[0] (plumbing): ResNet18 256x256 classification, bs4, 2 epochs over 32 synthetic crops, fp32
+    CPU restatement of the step (oracle/, baseline only)."""
+    from oracle import heads as oh
+    from oracle import resnet as orn
+    from oracle import step as ostep
+
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    model = oh.Classifier(orn.create("resnet18"), 512, dropout=0.3)
+    opt = ostep.make_optimizer(model)
+    model.train()
+    crops = [synthetic_cls_batch(4, 256, 256, "cpu", 100 + i) for i in range(8)]
+    t0 = time.perf_counter()
+    for _epoch in range(2):
+        for img, targets in crops:
+            ostep.train_step_classification(model, opt, img, targets)
+    el = time.perf_counter() - t0
+    return {"value": round(64 / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": "configs[0]: ResNet18 256x256 bs4, 2 epochs x 8 steps (32 synthetic crops), fp32 oracle/ "
+                      "restatement, end to end"}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """N ranks of this script under torch.distributed.run, started as a child process BEFORE any GPU
+    call in this process (never an exec); returns the child's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def selftest(args, world: int, rank: int) -> None:
+    """--selftest: the multi-rank plumbing of this script on CPU (gloo) -- launcher, rank env, the flat
+    bucketed all-reduce and the max-over-ranks timing -- on a small torch model.  Not a measurement."""
+    import torch.nn as nn
+
+    pkg = __graft_entry__.load_package()  # noqa: F841
+    from spine_vision_amd.training.comm import GradBucketer, broadcast_parameters
+    from spine_vision_amd.training.flat import FlatArena
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.manual_seed(rank)
+    model = nn.Sequential(nn.Linear(64, 256), nn.GELU(), nn.Linear(256, 64))
+    arena = FlatArena(model, "cpu", with_shadow=False)
+    buck = None
+    if world > 1:
+        broadcast_parameters(arena, model)
+        buck = GradBucketer(arena, bucket_mb=16 * 1024 * 4 / 2**20)
+        buck.attach(model)
+    x = torch.randn(args.batch, 64, generator=torch.Generator().manual_seed(1234 + rank))
+    for _ in range(args.warmup):
+        arena.zero_grad()
+        model(x).pow(2).mean().backward()
+        if buck is not None:
+            buck.finish()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        arena.zero_grad()
+        model(x).pow(2).mean().backward()
+        if buck is not None:
+            buck.finish()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    g = arena.grad_flat.clone()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+        allg = [torch.empty_like(g) for _ in range(world)]
+        dist.all_gather(allg, g)
+        same = all(torch.equal(allg[0], a) for a in allg)
+    else:
+        same = True
+    if rank == 0:
+        print(json.dumps({"metric": "selftest (launcher / all-reduce plumbing, CPU gloo; not a measurement)",
+                          "value": round(world * args.batch * args.steps / el, 3), "unit": "samples/sec",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "selftest", "parallelism": f"dp{world}",
+                                     "buckets": len(buck.buckets) if buck else 0},
+                          "grads_identical_across_ranks": same}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: dict) -> dict:
+    """Roofline of one probed GEMM class: algorithmic FLOPs / bytes per launch against the mean launch
+    duration from HIP events; the binding roof is the larger of FLOPs/peak and bytes/HBM peak."""
+    n = max(probe.launches, 1)
+    avg_ms = probe.elapsed_ms() / n
+    flops, nbytes = probe.flops / n, probe.bytes / n
+    tflops = flops / (avg_ms * 1e-3) / 1e12 if probe.launches else 0.0
+    gbs = nbytes / (avg_ms * 1e-3) / 1e9 if probe.launches else 0.0
+    hbm_bound = nbytes / (PEAK_HBM_GBS * 1e9) > flops / (peak * 1e12)
+    tr = traffic.get(f"{name}_bytes_per_launch")
+    return {
+        "kernel": PROBE_NAMES[name],
+        "bound": "hbm" if hbm_bound else "mfma",
+        "achieved": round(gbs, 1) if hbm_bound else round(tflops, 2),
+        "peak": PEAK_HBM_GBS if hbm_bound else peak,
+        "unit": "GB/s" if hbm_bound else "TFLOP/s",
+        "frac": round(gbs / PEAK_HBM_GBS if hbm_bound else tflops / peak, 4),
+        "traffic": tr,
+        "traffic_ratio": round(tr / nbytes, 3) if tr and nbytes else None,
+        "launches_per_step": round(probe.launches / max(steps_probed, 1), 1),
+        "ms_per_step": round(avg_ms * probe.launches / max(steps_probed, 1), 3),
+        "avg_launch_us": round(avg_ms * 1e3, 2),
+        "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
+        "algorithmic_bytes_per_launch": int(nbytes),
+        "mfma_tflops": round(tflops, 2),
+        "mfma_frac": round(tflops / peak, 4),
+        "hbm_gbs": round(gbs, 1),
+        "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+    }
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args))  # before any GPU call in this process
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.selftest:
+        return selftest(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
     device = torch.device("cuda", local)
 
-    pkg = __graft_entry__.load_package()
+    pkg = __graft_entry__.load_package()  # noqa: F841
     from spine_vision_amd import kernels as K
+    from spine_vision_amd import native as nv
     from spine_vision_amd.training import Classifier, CoordinateRegressor, StepEngine
 
+    assert (nv.SV_EPI_SLAB, nv.SV_EPI_MUL_AUX) == (SV_EPI_SLAB, SV_EPI_MUL_AUX)
     torch.manual_seed(42)
     cls = args.workload == "classification"
     if cls:
@@ -184,57 +360,58 @@ def main():
 
     if args.inference:  # row f2: trainers' _validate_epoch / predict forward, no autograd tape
         model.eval()
-        train_step = run_step
 
-        def run_step():
+        def run_step():  # noqa: F811
             with torch.no_grad():
                 out = model(img)
             return out.float().mean() if not isinstance(out, dict) else sum(v.float().mean() for v in out.values())
 
-        del train_step
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(device)
+    retries0 = torch.cuda.memory_stats(device).get("num_alloc_retries", 0)
 
     bf = args.precision == "bf16"
-    probe = K.GemmProbe(PROBE_KEYS[args.probe] + (bf,))
-    # The probe's HIP events bracket every launch of the class in the LAST timed step: each timing event
-    # is a release packet that writes back L2, and probing all K steps cost 2.3% of the step
+    probes = {k: K.GemmProbe(v[:2] + (bf,) + v[2:], k) for k, v in PROBE_KEYS.items()}
+    # The probes' HIP events bracket every launch of their classes in the LAST timed step: each timing
+    # event is a release packet that writes back L2, and probing all K steps cost 2.3% of the step
     # (tools/gpu_probe_ab.sh).  The classification line reports the whole-step rate and takes no probe;
-    # SV_BENCH_PROBE=0 leaves the roofline fields empty and SV_BENCH_PROBE=all probes every step.
+    # SV_BENCH_PROBE=0 leaves the per-kernel fields empty and SV_BENCH_PROBE=all probes every step.
     probe_mode = os.environ.get("SV_BENCH_PROBE", "1")
-    use_probe = not cls and probe_mode != "0"
+    use_probe = not cls and not args.inference and probe_mode != "0"
+    bucketer = engine.bucketer
     t0 = time.perf_counter()
     for i in range(args.steps):
-        K.PROBE = probe if use_probe and (probe_mode == "all" or i == args.steps - 1) else None
+        last = i == args.steps - 1
+        K.PROBES = list(probes.values()) if use_probe and (probe_mode == "all" or last) else []
+        if bucketer is not None:
+            bucketer.timing = last
         loss = run_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    K.PROBE = None
+    K.PROBES = []
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
     assert final_loss == final_loss, "loss is NaN"
+    mstats = torch.cuda.memory_stats(device)
 
-    probe_ms = probe.elapsed_ms()
-    avg_launch_ms = probe_ms / max(probe.launches, 1)
-    flops_per_launch = probe.flops / max(probe.launches, 1)
-    achieved = flops_per_launch / (avg_launch_ms * 1e-3) / 1e12 if probe.launches else 0.0
     peak = PEAK_BF16_TFLOPS if bf else PEAK_F32_MFMA_TFLOPS
-    traffic = None
+    traffic = {}
     if os.path.exists(args.traffic_file):
         try:
-            traffic = json.load(open(args.traffic_file)).get(f"{args.probe}_bytes_per_launch")
+            traffic = json.load(open(args.traffic_file))
         except Exception:
-            traffic = None
+            traffic = {}
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
@@ -244,7 +421,6 @@ def main():
         metric = f"images/sec inference (eval forward), {args.backbone} {args.image_size}x{args.image_size}, bs{args.batch}"
         workload = f"{'Classifier' if cls else 'CoordinateRegressor'}({args.backbone}) eval forward (validation / predict)"
         data = "synthetic, resident in HBM; random-init weights"
-        gflop = STEP_GFLOP.get((args.backbone, args.image_size))
         step_tflops = (gflop / 3.0) * args.batch / (ms * 1e-3) / 1e3 if gflop else None  # fwd = 1/3 of fwd+bwd
     elif cls:
         metric = f"images/sec training, {args.backbone} {args.image_size}x{args.image_size} 3-head cls, bs{args.batch}"
@@ -257,38 +433,22 @@ def main():
             metric = f"images/sec training, {args.backbone} {args.image_size}x{args.image_size} loc, bs{args.batch}"
         workload = f"CoordinateRegressor({args.backbone}) localization train step fwd+bwd+allreduce+clip+AdamW"
         data = "synthetic uint8 512x512 grayscale->RGB, ImageNet-normalised, resident in HBM; random-init weights"
-    if cls:
-        # the conv kernels are not GEMM-probed: report the whole-step model FLOP rate against the peak
-        roof = {"bound": "mfma", "kernel": "whole training step (implicit-GEMM conv + BN), model FLOPs",
-                "achieved": round(step_tflops, 2) if step_tflops else None, "peak": peak, "unit": "TFLOP/s",
-                "frac": round(step_tflops / peak, 4) if step_tflops else None, "traffic": None}
+    step_frac = round(step_tflops / peak, 4) if step_tflops else None
+    if use_probe:
+        nprobed = args.steps if probe_mode == "all" else 1
+        kern = {k: kernel_roofline(k, p_, nprobed, peak, traffic) for k, p_ in probes.items() if p_.launches}
+        dominant = max(kern, key=lambda k: kern[k]["ms_per_step"])
+        roof = dict(kern[dominant])
+        roof["kernel"] = f"{dominant}: {roof['kernel']} (dominant GEMM class by device time)"
+        roof["step_tflops_per_gpu"] = round(step_tflops, 1) if step_tflops else None
+        roof["step_mfma_frac"] = step_frac
+        roof["kernels"] = kern
     else:
-        # which roof binds the probed kernel class: its algorithmic FLOPs at the MFMA peak, or its
-        # algorithmic bytes (A, B read once; C, C2, residual/aux once) at the HBM peak
-        bytes_per_launch = probe.bytes / max(probe.launches, 1)
-        t_mfma = flops_per_launch / (peak * 1e12)
-        t_hbm = bytes_per_launch / (PEAK_HBM_GBS * 1e9)
-        gbs = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if probe.launches else 0.0
-        hbm_bound = t_hbm > t_mfma
-        roof = {
-            "bound": "hbm" if hbm_bound else "mfma",
-            "kernel": f"gemm {args.probe} class ({'bf16' if bf else 'f32'} MFMA): fc1/fc2/downsample",
-            "achieved": round(gbs, 1) if hbm_bound else round(achieved, 2),
-            "peak": PEAK_HBM_GBS if hbm_bound else peak,
-            "unit": "GB/s" if hbm_bound else "TFLOP/s",
-            "frac": round((gbs / PEAK_HBM_GBS) if hbm_bound else (achieved / peak), 4),
-            "traffic": traffic,
-            "launches_timed": probe.launches,
-            "avg_launch_us": round(avg_launch_ms * 1e3, 2),
-            "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
-            "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "mfma_tflops": round(achieved, 2),
-            "mfma_frac": round(achieved / peak, 4),
-            "hbm_gbs": round(gbs, 1),
-            "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
-            "step_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
-            "step_mfma_frac": round(step_tflops / peak, 4) if step_tflops else None,
-        }
+        # no per-kernel probe: report the whole-step model FLOP rate against the peak
+        roof = {"bound": "mfma", "kernel": "whole training step, model FLOPs" if not args.inference
+                else "whole eval forward, model FLOPs",
+                "achieved": round(step_tflops, 2) if step_tflops else None, "peak": peak, "unit": "TFLOP/s",
+                "frac": step_frac, "traffic": None, "step_mfma_frac": step_frac}
     result = {
         "metric": metric,
         "value": round(value, 3),
@@ -312,9 +472,28 @@ def main():
         "roofline": roof,
         "loss": round(final_loss, 6),
         "hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
+        "hbm_peak_allocated_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 1),
+        "num_alloc_retries": int(mstats.get("num_alloc_retries", 0) - retries0),
     }
+    if bucketer is not None:
+        comm = bucketer.timing_stats()
+        # the whole gradient buffer once more, alone, for the bus bandwidth of one large all-reduce
+        g = engine.arena.grad_flat
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dist.barrier()
+        e0.record()
+        for _ in range(3):
+            dist.all_reduce(g)
+        e1.record()
+        torch.cuda.synchronize()
+        t_ar = e0.elapsed_time(e1) / 3 * 1e-3
+        comm["allreduce_full_mb"] = round(g.numel() * 4 / 2**20, 1)
+        comm["allreduce_full_busbw_gbs"] = round(2.0 * (world - 1) / world * g.numel() * 4 / t_ar / 1e9, 1)
+        result["comm"] = comm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
+        if not cls and not args.inference:
+            result["cpu_baseline_configs0"] = cpu_baseline_config0()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

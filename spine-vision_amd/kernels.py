@@ -20,21 +20,31 @@ EPS_LN = 1e-6
 
 
 class GemmProbe:
-    """Times every launch of one GEMM layout class with HIP events on the launching stream
-    (bench.py's live roofline measurement).  key = (a_kmajor, b_kmajor, compute_bf16)."""
+    """Times every launch of one GEMM class with HIP events on the launching stream (bench.py's live
+    roofline measurement).  key = (a_kmajor, b_kmajor, compute_bf16) or, to single out one epilogue
+    kind, (a_kmajor, b_kmajor, compute_bf16, epilogue).  ``bytes`` counts the ALGORITHMIC HBM bytes
+    of the launch: operands read once (A, B, the epilogue operand) and the REQUIRED outputs written
+    once -- for a split-K weight gradient that is the N x K f32 gradient, not the self-chosen slabs."""
 
-    def __init__(self, key: tuple[bool, bool, bool]) -> None:
+    def __init__(self, key: tuple, name: str = "") -> None:
         self.key = key
+        self.name = name
         self.events: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self.flops = 0.0
-        self.bytes = 0.0  # algorithmic HBM bytes: A, B read once; C (+C2, aux) once
+        self.bytes = 0.0
         self.launches = 0
+
+    def matches(self, a_kmajor: bool, b_kmajor: bool, bf: bool, epilogue: int) -> bool:
+        k = (bool(a_kmajor), bool(b_kmajor), bool(bf))
+        return self.key[:3] == k and (len(self.key) < 4 or self.key[3] == epilogue)
 
     def elapsed_ms(self) -> float:
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in self.events)
 
 
+PROBES: list[GemmProbe] = []
+# single-probe alias kept for older tools (tools/*.py set K.PROBE)
 PROBE: GemmProbe | None = None
 
 
@@ -100,22 +110,31 @@ def gemm(
         d.aux, d.aux_dtype, d.ld_aux = ptr(aux), dt(aux), ld_aux if ld_aux is not None else N
     d.split_k = split_k
     d.compute = _cdt(compute_bf16)
-    probe = PROBE
-    if probe is not None and probe.key == (bool(a_kmajor), bool(b_kmajor), bool(compute_bf16)):
+    probes = [p_ for p_ in (PROBES + ([PROBE] if PROBE is not None else [])) if p_.matches(a_kmajor, b_kmajor,
+                                                                                      compute_bf16, epilogue)]
+    if probes:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         call("sv_gemm", ctypes.byref(d))
         ev1.record()
-        probe.events.append((ev0, ev1))
-        probe.flops += 2.0 * M * N * K
         nbytes = M * K * A.element_size() + N * K * B.element_size()
-        nbytes += (split_k if epilogue == nv.SV_EPI_SLAB else 1) * M * N * C.element_size()
-        if C2 is not None:
-            nbytes += (split_k * M if epilogue == nv.SV_EPI_SLAB else M * N) * C2.element_size()
+        if epilogue == nv.SV_EPI_SLAB:
+            nbytes += M * N * 4  # the weight gradient itself (the split-K slabs are a design choice)
+            if C2 is not None:
+                nbytes += M * 4  # its bias gradient (column sums)
+        elif epilogue == nv.SV_EPI_BIAS_GELU_DUAL:
+            nbytes += M * N * C2.element_size()  # GELU(h) is required; the GELU'(h) store is a design choice
+        else:
+            nbytes += M * N * C.element_size()
+            if C2 is not None:
+                nbytes += M * N * C2.element_size()
         if aux is not None:
             nbytes += M * N * aux.element_size()
-        probe.bytes += nbytes
-        probe.launches += 1
+        for p_ in probes:
+            p_.events.append((ev0, ev1))
+            p_.flops += 2.0 * M * N * K
+            p_.bytes += nbytes
+            p_.launches += 1
     else:
         call("sv_gemm", ctypes.byref(d))
     return C

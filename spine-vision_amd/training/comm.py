@@ -55,6 +55,11 @@ class GradBucketer:
         self.use_streams = arena.grad_flat.is_cuda
         self.comm_stream = torch.cuda.Stream(priority=-1) if self.use_streams else None
         self._hooks = []
+        # timing (bench.py): HIP events around every bucket's all-reduce on the comm stream, and around
+        # the compute stream's join (the exposed, un-overlapped part of the exchange)
+        self.timing = False
+        self._bucket_ev: list = []
+        self._join_ev = None
         self.reset()
 
     def reset(self) -> None:
@@ -93,10 +98,24 @@ class GradBucketer:
             ev.record(torch.cuda.current_stream())
             self.comm_stream.wait_event(ev)
             with torch.cuda.stream(self.comm_stream):
+                e0 = None
+                if self.timing:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
                 w = dist.all_reduce(view, op=op, group=self.group, async_op=True)
+                # the comm stream waits on RCCL's internal stream (no host block), so later buckets,
+                # the timing event and the compute stream's join are all ordered after this reduce
+                w.wait()
+                if op == dist.ReduceOp.SUM and self.world > 1:
+                    view.div_(self.world)
+                if e0 is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    self._bucket_ev.append((e0, e1, view.numel() * view.element_size()))
+            self.works.append((None, view, op))
         else:
             w = dist.all_reduce(view, op=op, group=self.group, async_op=True)
-        self.works.append((w, view, op))
+            self.works.append((w, view, op))
         self.launched[b] = True
 
     def finish(self) -> None:
@@ -105,12 +124,53 @@ class GradBucketer:
             if not self.launched[b]:
                 self._launch(b)
         for w, view, op in self.works:
+            if w is None:
+                continue
             w.wait()
             if op == dist.ReduceOp.SUM and self.world > 1:
                 view.div_(self.world)
         if self.use_streams:
-            torch.cuda.current_stream().wait_stream(self.comm_stream)
+            cur = torch.cuda.current_stream()
+            pre = None
+            if self.timing:
+                pre = torch.cuda.Event(enable_timing=True)
+                pre.record(cur)
+            cur.wait_stream(self.comm_stream)
+            if pre is not None:
+                post = torch.cuda.Event(enable_timing=True)
+                post.record(cur)
+                self._join_ev = (pre, post)
         self.reset()
+
+    def timing_stats(self) -> dict:
+        """All-reduce bus bandwidth and overlap of the timed steps (call after a synchronize).
+
+        busbw = 2 (n-1)/n x bytes / time per bucket (the ring all-reduce convention);
+        comm_overlap_frac = 1 - exposed / total, where exposed is the time the compute stream waited
+        for the exchange after its own backward work was done (last step)."""
+        if not self._bucket_ev:
+            return {}
+        torch.cuda.synchronize()
+        n = self.world
+        tot_ms = sum(a.elapsed_time(b) for a, b, _ in self._bucket_ev)
+        tot_bytes = sum(nb for _, _, nb in self._bucket_ev)
+        busbw = [2.0 * (n - 1) / n * nb / (a.elapsed_time(b) * 1e-3) / 1e9 for a, b, nb in self._bucket_ev]
+        exposed = self._join_ev[0].elapsed_time(self._join_ev[1]) if self._join_ev else None
+        nsteps = max(1, len(self._bucket_ev) // max(1, len(self.buckets)))
+        return {
+            "buckets": len(self.buckets),
+            "bucket_mb": round(tot_bytes / len(self._bucket_ev) / 2**20, 1),
+            "allreduce_ms_per_step": round(tot_ms / nsteps, 3),
+            "allreduce_busbw_gbs": round(2.0 * (n - 1) / n * tot_bytes / (tot_ms * 1e-3) / 1e9, 1),
+            "allreduce_busbw_gbs_max_bucket": round(max(busbw), 1),
+            "exposed_ms_last_step": round(exposed, 3) if exposed is not None else None,
+            "comm_overlap_frac": (round(max(0.0, 1.0 - exposed / (tot_ms / nsteps)), 4)
+                                  if exposed is not None and tot_ms > 0 else None),
+        }
+
+    def clear_timing(self) -> None:
+        self._bucket_ev.clear()
+        self._join_ev = None
 
 
 class BufferSync:

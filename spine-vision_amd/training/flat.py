@@ -57,6 +57,12 @@ class FlatArena:
             for p, o in zip(self.params, self.offsets):
                 self.shadow[id(p)] = self.shadow_flat[o : o + p.numel()].view_as(p)
             self.refresh_shadow()
+            # a load_state_dict through the model (or through the backbone alone, e.g. loading
+            # best_model.pt before evaluate/predict) rewrites the f32 masters in place: re-derive the
+            # bf16 shadow the GEMMs read, or they would mix stale bf16 weights with fresh f32 ones
+            hooked = [model] + [m for m in model.modules() if hasattr(m, "set_weight_shadow") and m is not model]
+            for m in hooked:
+                m.register_load_state_dict_post_hook(lambda _m, _keys: self.refresh_shadow())
             for m in model.modules():
                 if hasattr(m, "set_weight_shadow"):
                     m.set_weight_shadow(self.shadow)

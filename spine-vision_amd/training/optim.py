@@ -14,7 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import kernels as K
-from .flat import FlatArena
+from .flat import FlatArena, _align
 
 
 class FlatAdamW(torch.optim.Optimizer):
@@ -26,7 +26,11 @@ class FlatAdamW(torch.optim.Optimizer):
         self.arena = arena
         self.exp_avg = torch.zeros_like(arena.param_flat)
         self.exp_avg_sq = torch.zeros_like(arena.param_flat)
-        self._step = 0
+        # torch.optim.AdamW keeps one step count PER PARAMETER, starting when the parameter first
+        # takes a step.  A backbone frozen for ``freeze_backbone_epochs`` (the reference's
+        # localization.py:383-389 hook) therefore starts its bias correction at step 1 after the
+        # unfreeze, not at the head's count.  Runs of the flat buffer are cut where the counts differ.
+        self._steps = [0] * len(arena.params)
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: torch.Tensor | None = None):
@@ -37,15 +41,35 @@ class FlatAdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         group = self.param_groups[0]
-        self._step += 1
         a = self.arena
         shadow = a.shadow_flat
-        for s, e in a.trainable_runs():
+        for s, e, st in self._runs():
             K.adamw_flat(a.param_flat[s:e], a.grad_flat[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e],
                          shadow[s:e] if shadow is not None else None, lr=group["lr"], beta1=group["betas"][0],
                          beta2=group["betas"][1], eps=group["eps"], weight_decay=group["weight_decay"],
-                         step=self._step, grad_scale=grad_scale)
+                         step=st, grad_scale=grad_scale)
         return loss
+
+    def _runs(self) -> list[tuple[int, int, int]]:
+        """Advance the step count of every trainable parameter and return the maximal contiguous
+        [start, end) ranges of trainable parameters that share a (new) step count."""
+        a = self.arena
+        runs: list[list[int]] = []
+        for i, (p, o) in enumerate(zip(a.params, a.offsets)):
+            if not p.requires_grad:
+                continue
+            self._steps[i] += 1
+            e = o + _align(p.numel())
+            if runs and runs[-1][1] == o and runs[-1][2] == self._steps[i]:
+                runs[-1][1] = e
+            else:
+                runs.append([o, e, self._steps[i]])
+        return [tuple(r) for r in runs]
+
+    @property
+    def _step(self) -> int:
+        """Largest per-parameter step count (the count of an optimizer that never froze anything)."""
+        return max(self._steps) if self._steps else 0
 
     def zero_grad(self, set_to_none: bool = True) -> None:  # grads live in the arena: always zero
         self.arena.zero_grad()
@@ -56,9 +80,11 @@ class FlatAdamW(torch.optim.Optimizer):
         a = self.arena
         state = {}
         for i, (p, o) in enumerate(zip(a.params, a.offsets)):
+            if self._steps[i] == 0:  # torch writes no state for a parameter that never stepped
+                continue
             n = p.numel()
             state[i] = {
-                "step": torch.tensor(float(self._step)),
+                "step": torch.tensor(float(self._steps[i])),
                 "exp_avg": self.exp_avg[o : o + n].view_as(p).clone(),
                 "exp_avg_sq": self.exp_avg_sq[o : o + n].view_as(p).clone(),
             }
@@ -73,15 +99,15 @@ class FlatAdamW(torch.optim.Optimizer):
                     g[k] = v
         a = self.arena
         st = state_dict.get("state", {})
-        steps = []
         with torch.no_grad():
             for i, (p, o) in enumerate(zip(a.params, a.offsets)):
                 s = st.get(i)
-                if not s:
-                    continue
                 n = p.numel()
+                if not s:
+                    self._steps[i] = 0
+                    self.exp_avg[o : o + n].zero_()
+                    self.exp_avg_sq[o : o + n].zero_()
+                    continue
                 self.exp_avg[o : o + n].copy_(s["exp_avg"].reshape(-1).to(self.exp_avg.device))
                 self.exp_avg_sq[o : o + n].copy_(s["exp_avg_sq"].reshape(-1).to(self.exp_avg.device))
-                steps.append(int(float(s["step"])))
-        if steps:
-            self._step = max(steps)
+                self._steps[i] = int(float(s["step"]))

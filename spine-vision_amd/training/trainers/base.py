@@ -155,8 +155,13 @@ class EpochResult:
 
 
 class ShardedBatchSampler(Sampler):
-    """accelerate BatchSamplerShard (split_batches=False, even_batches=True): batches of the
-    underlying sampler dealt round-robin to ranks; the epoch is cut to a multiple of world size."""
+    """accelerate's BatchSamplerShard (split_batches=False, even_batches=True -- the default that
+    ``accelerator.prepare`` builds for the reference's train and val loaders, base.py:253-263):
+    batches of the underlying sampler are dealt round-robin to the ranks.  With ``drop_last`` an
+    incomplete final group is cut; without it (validation) the last group is completed by cycling
+    indices from the start of the epoch, so every rank yields the same number of FULL batches and the
+    per-batch all-gather of ``_validate_epoch`` always sees equal shapes (the duplicated samples are
+    then part of the gathered metrics, exactly as with the reference's ``accelerator.gather``)."""
 
     def __init__(self, sampler, batch_size: int, drop_last: bool, rank: int, world: int) -> None:
         self.sampler, self.batch_size, self.drop_last = sampler, batch_size, drop_last
@@ -173,17 +178,47 @@ class ShardedBatchSampler(Sampler):
             yield b
 
     def __iter__(self):
-        group = []
-        for b in self._batches():
-            group.append(b)
-            if len(group) == self.world:
-                yield group[self.rank]
-                group = []
+        bs, world, rank = self.batch_size, self.world, self.rank
+        head: list = []  # indices of the first `world` batches: the padding source
+        pending = None
+        idx, last = -1, []
+        for idx, b in enumerate(self._batches()):
+            if not self.drop_last and idx < world:
+                head += b
+            if idx % world == rank:
+                pending = b
+            if idx % world == world - 1 and len(b) == bs:
+                yield pending
+                pending = None
+            last = b
+        if self.drop_last or not head:
+            return
+        if pending is not None and len(pending) == bs:
+            yield pending
+        while len(head) < world * bs:  # fewer samples than one full group
+            head = head + head
+        batch = list(last)
+        if len(batch) == bs:  # the last batch was full and went out with its group
+            batch, idx = [], idx + 1
+        pos = 0
+        while idx % world != 0 or batch:
+            take = bs - len(batch)
+            batch = batch + head[pos : pos + take]
+            if idx % world == rank:
+                yield batch
+            pos += take
+            batch, idx = [], idx + 1
+
+    def num_batches(self) -> int:
+        """Batches per epoch of the UNSHARDED loader (what the reference's scheduler counts)."""
+        n = len(self.sampler)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __len__(self) -> int:
-        n = len(self.sampler)
-        nb = n // self.batch_size if self.drop_last else -(-n // self.batch_size)
-        return nb // self.world
+        nb = self.num_batches()
+        if nb % self.world == 0 or self.drop_last:
+            return nb // self.world
+        return nb // self.world + 1
 
 
 class BaseTrainer:
@@ -275,7 +310,11 @@ class BaseTrainer:
         c = self.config
         if c.scheduler_type == "none":
             return None
-        total = len(self.train_loader) * c.num_epochs
+        # the reference builds the scheduler BEFORE accelerator.prepare shards the loader (base.py:243-266),
+        # so T_max counts the unsharded batches; _scheduler_step then steps it world times per epoch
+        bsamp = getattr(self.train_loader, "batch_sampler", None)
+        per_epoch = bsamp.num_batches() if isinstance(bsamp, ShardedBatchSampler) else len(self.train_loader)
+        total = per_epoch * c.num_epochs
         if c.scheduler_type == "cosine":
             return torch.optim.lr_scheduler.CosineAnnealingLR(self.optimizer, T_max=total, eta_min=c.learning_rate * 0.01)
         if c.scheduler_type == "step":

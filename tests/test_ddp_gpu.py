@@ -102,3 +102,57 @@ def test_two_rank_step_matches_single_process(dev):
     assert abs(0.5 * (l0 + l1) - l_ref) / l_ref < 1e-5
     dp = (p0 - eng.arena.param_flat.cpu()).abs().max()
     assert float(dp) <= 2e-4 * 1.001  # first AdamW step: each element moves by ~lr*sign(g)
+
+
+def _rccl_rank(port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    import torch.distributed as dist
+
+    from spine_vision_amd.training import StepEngine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    m = _model(dev)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=16.0)
+    eng.bucketer.timing = True
+    img, coords, mask = _batch()
+    loss = eng.step_localization(img.to(dev), coords.to(dev), mask.to(dev))
+    torch.cuda.synchronize()
+    stats = eng.bucketer.timing_stats()
+    out["r"] = (dist.get_backend(), float(loss), eng.arena.grad_flat.cpu().clone(), eng.arena.param_flat.cpu().clone(),
+                len(eng.bucketer.buckets), stats)
+    dist.destroy_process_group()
+
+
+def test_rccl_bucketer_world1_matches_single_process(dev):
+    """The RCCL ("nccl") branch of GradBucketer -- ReduceOp.AVG issued on the high-priority comm stream,
+    the comm stream joined to RCCL's stream per bucket, the compute stream joined before clip/AdamW --
+    executed at world 1 (the box has one GPU): gradients and the AdamW update equal the non-distributed
+    step bit for bit, and the timing hooks report every bucket."""
+    from spine_vision_amd.training import StepEngine
+
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    p = ctx.Process(target=_rccl_rank, args=(_free_port(), out))
+    p.start()
+    p.join(timeout=300)
+    assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    backend, loss, g, prm, nb, stats = out["r"]
+    assert backend == "nccl" and nb > 1
+    m = _model(dev)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=False)
+    img, coords, mask = _batch()
+    l_ref = float(eng.step_localization(img.to(dev), coords.to(dev), mask.to(dev)))
+    assert loss == l_ref
+    assert torch.equal(g, eng.arena.grad_flat.cpu())
+    assert torch.equal(prm, eng.arena.param_flat.cpu())
+    assert stats["buckets"] == nb and stats["allreduce_ms_per_step"] > 0

@@ -134,18 +134,36 @@ def test_classification_trainer_plumbing(tmp_path):
     assert "macro_f1" in res.history
 
 
-@pytest.mark.parametrize("world,n,bs,drop", [(2, 37, 4, True), (2, 37, 4, False), (4, 64, 8, True), (3, 10, 3, False)])
+@pytest.mark.parametrize("world,n,bs,drop", [(2, 37, 4, True), (2, 37, 4, False), (4, 64, 8, True), (3, 10, 3, False),
+                                           (2, 100, 32, False), (4, 5, 2, False), (3, 12, 4, False), (2, 36, 4, False)])
 def test_sharding_matches_accelerate(world, n, bs, drop):
+    """Every rank's batches equal accelerate's BatchSamplerShard with its prepare() default
+    even_batches=True (validation: the last group padded by cycling from the epoch's start)."""
     from accelerate.data_loader import BatchSamplerShard
     from torch.utils.data import BatchSampler, SequentialSampler
 
+    lens = set()
     for r in range(world):
         ours = list(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
         ref = list(BatchSamplerShard(BatchSampler(SequentialSampler(range(n)), bs, drop), num_processes=world,
-                                     process_index=r, split_batches=False, even_batches=False))
-        m = min(len(ours), len(ref))
-        assert ours[:m] == ref[:m]
+                                     process_index=r, split_batches=False, even_batches=True))
+        assert ours == ref, (r, ours, ref)
         assert len(ours) == len(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
+        if not drop:
+            assert all(len(b) == bs for b in ours)  # equal shapes for the per-batch all-gather
+        lens.add(len(ours))
+    assert len(lens) == 1
+
+
+def test_cosine_tmax_counts_unsharded_batches():
+    """The reference creates the scheduler before accelerator.prepare shards the loader
+    (base.py:243-266): T_max = unsharded batches x epochs at any world size."""
+    from torch.utils.data import SequentialSampler
+
+    for world in (1, 2, 4):
+        bs = ShardedBatchSampler(SequentialSampler(range(37)), 4, True, 0, world)
+        assert bs.num_batches() == 9
+        assert len(bs) == 9 // world
 
 
 def test_device_transform_dataset_contract():
