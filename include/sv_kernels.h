@@ -163,6 +163,17 @@ int sv_stem_weight_pack(const float* w, uint16_t* wpack, int32_t C, sv_stream_t 
 int sv_normalize_u8_gray(const uint8_t* img, const float* norm_mean, const float* norm_std, float* out,
                          int32_t B, int32_t H, int32_t W, sv_stream_t stream);
 
+/* ---- train-time augmentation of decoded uint8 images (row f1) ----------------------------------
+ * Replaces the PIL/torchvision tail of the reference's train transforms after Resize
+ * (training/datasets/localization.py:202-216: RandomHorizontalFlip(0.5), RandomAffine(10, (0.05,
+ * 0.05), (0.95, 1.05)), ColorJitter(0.2, 0.2); classification.py:276-289: RandomAffine +
+ * ColorJitter) with the SAME pixel arithmetic as Pillow's NEAREST affine and ImageEnhance blends.
+ * in/out uint8 [B][H][W][C] (C = 1 grayscale plane or 3 interleaved RGB; must not alias);
+ * params double [B][10] = {flip, inverse affine a0..a5, brightness, contrast, order (0 = brightness
+ * first)} drawn on the host as torchvision draws them; row_sums int32 [B*H] workspace.             */
+int sv_augment_u8(const uint8_t* in, uint8_t* out, int32_t B, int32_t H, int32_t W, int32_t C, const double* params,
+                  int32_t* row_sums, sv_stream_t stream);
+
 /* ---- ConvNeXt stage downsample: LayerNorm2d + 2x2/s2 patch gather (GEMM A operand) ------------
  * x [B,H,W,C] f32 -> patches [B*(H/2)*(W/2)][C*4] with k = c*4 + kh*2 + kw (= timm conv weight
  * [2C,C,2,2] flattened), so the Conv2d(k2,s2) is one sv_gemm with b_kmajor=1 on the weight.        */

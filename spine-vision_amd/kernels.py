@@ -401,6 +401,27 @@ def normalize_u8_gray(img_u8, *, mean=IMAGENET_MEAN, std=IMAGENET_STD, out=None)
     return out
 
 
+def augment_u8(img_u8: torch.Tensor, params: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Train-time flip / affine / colour jitter of decoded uint8 images on the device (row f1):
+    ``img_u8`` [B,H,W] (grayscale) or [B,H,W,3] (RGB), ``params`` float64 [B,10] from
+    ``training.datasets.augment.sample_params`` (torchvision's draws).  Bitwise equal to the PIL
+    operations torchvision applies on the host (sv_augment_u8)."""
+    _check(img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.dim() in (3, 4),
+           "augment_u8: expects contiguous uint8 [B,H,W] or [B,H,W,3]")
+    B, H, W = img_u8.shape[:3]
+    C = 1 if img_u8.dim() == 3 else img_u8.shape[3]
+    _check(C in (1, 3), "augment_u8: 1 or 3 channels")
+    params = params.to(device=img_u8.device, dtype=torch.float64).contiguous()
+    _check(tuple(params.shape) == (B, 10), "augment_u8: params must be [B,10]")
+    if out is None:
+        out = torch.empty_like(img_u8)
+    _check(out.shape == img_u8.shape and out.dtype == torch.uint8 and out.is_contiguous()
+           and out.data_ptr() != img_u8.data_ptr(), "augment_u8: bad out")
+    rows = torch.empty(B * H, device=img_u8.device, dtype=torch.int32)
+    call("sv_augment_u8", ptr(img_u8), ptr(out), B, H, W, C, ptr(params), ptr(rows))
+    return out
+
+
 def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):
     B, H, W, C = x4d.shape
     _check(H % 2 == 0 and W % 2 == 0, "downsample: H, W must be even")

@@ -8,8 +8,10 @@ normalise); LocalizationDataset reads the reference's annotations.csv + PNG layo
 reference's patient-stratified train/val/test split (row f4).
 """
 
+from .augment import apply_pil, sample_params
 from .classification import (
     ClassificationCollator,
+    ClassificationDataset,
     DynamicTargets,
     SyntheticClassificationDataset,
     create_weighted_sampler,
@@ -28,7 +30,7 @@ from .localization import (
 )
 
 __all__ = [
-    "ClassificationCollator", "DynamicTargets", "IDX_TO_LEVEL", "LocalizationCollator", "LocalizationDataset",
+    "ClassificationCollator", "ClassificationDataset", "DynamicTargets", "apply_pil", "sample_params", "IDX_TO_LEVEL", "LocalizationCollator", "LocalizationDataset",
     "NUM_LEVELS", "SyntheticClassificationDataset", "SyntheticLocalizationDataset", "create_weighted_sampler",
     "get_patient_multilabel_matrix", "get_patient_single_label", "split_patients",
 ]

@@ -30,15 +30,23 @@ def normalize_u8(img_u8: torch.Tensor) -> torch.Tensor:
 
 class LocalizationDataset(Dataset):
     """annotations.csv (image_path, level, relative_x, relative_y, series_type, source) + images.
-    Per sample: image [3,H,W] (Resize -> ToTensor -> Normalize), coords [5,2], mask [5],
-    series_type_idx, metadata -- the reference's record layout and patient-free image split."""
+    Per sample: image [3,H,W] (convert("RGB") -> Resize -> [HFlip, RandomAffine, ColorJitter when
+    augmenting] -> ToTensor -> Normalize), coords [5,2], mask [5], series_type_idx, metadata -- the
+    reference's record layout, transform chain (localization.py:196-233, 254) and image split.
+
+    ``device_transform``: yield the resized uint8 plane [H,W] (and, when augmenting, the sample's
+    augmentation parameters under "augment", drawn like torchvision); the trainer runs the flip /
+    affine / jitter (``kernels.augment_u8``) and ToTensor -> Normalize on the GPU.  MRI PNGs are
+    grayscale; an image whose RGB channels differ raises in this mode (use the host transform).
+    ``augment_coords``: move the keypoints with the flip / affine (the reference does not)."""
 
     def __init__(self, data_path: Path, split: Literal["train", "val", "test", "all"] = "all", val_ratio: float = 0.15,
                  test_ratio: float = 0.05, series_types: list[str] | None = None, sources: list[str] | None = None,
                  image_size: tuple[int, int] = (256, 256), augment: bool = True, normalize: bool = True,
-                 seed: int = 42, device_transform: bool = False) -> None:
+                 seed: int = 42, device_transform: bool = False, augment_coords: bool = False) -> None:
         self.data_path = Path(data_path)
         self.device_transform = device_transform
+        self.augment_coords = augment_coords
         self.split = split
         self.image_size = tuple(image_size)
         self.augment = augment and split == "train"
@@ -70,28 +78,43 @@ class LocalizationDataset(Dataset):
     def __len__(self) -> int:
         return len(self.image_list)
 
-    def _load(self, rel: str) -> torch.Tensor:
+    def _load(self, rel: str):
+        """convert("RGB") -> Resize (torchvision Resize on PIL = Image.resize((w, h), BILINEAR))."""
         from PIL import Image
 
-        im = Image.open(self.data_path / rel).convert("L").resize((self.image_size[1], self.image_size[0]),
-                                                                  Image.BILINEAR)
-        return torch.from_numpy(np.asarray(im, dtype=np.uint8).copy())
+        return Image.open(self.data_path / rel).convert("RGB").resize((self.image_size[1], self.image_size[0]),
+                                                                      Image.BILINEAR)
 
     def __getitem__(self, i: int) -> dict[str, Any]:
+        from .augment import apply_pil, sample_params, transform_coords
+
         rel = self.image_list[i]
         rec = self.image_records[rel]
-        u8 = self._load(rel)
-        if self.device_transform:  # uint8 [H,W]; normalised on the GPU (kernels.normalize_u8_gray / stem)
-            image = u8
+        im = self._load(rel)
+        params = sample_params(self.image_size[0], self.image_size[1], flip=True) if self.augment else None
+        out: dict[str, Any] = {}
+        if self.device_transform:  # uint8 [H,W]; augmented + normalised on the GPU
+            rgb = np.asarray(im, dtype=np.uint8)
+            if not (np.array_equal(rgb[..., 0], rgb[..., 1]) and np.array_equal(rgb[..., 0], rgb[..., 2])):
+                raise ValueError(f"{rel}: device_transform expects grayscale images (RGB channels differ)")
+            image = torch.from_numpy(rgb[..., 0].copy())
+            if params is not None:
+                out["augment"] = params
         else:
-            image = normalize_u8(u8) if self.normalize else u8.float().div(255).unsqueeze(0).expand(3, -1, -1)
+            if params is not None:
+                im = apply_pil(im, params)
+            x = torch.from_numpy(np.asarray(im, dtype=np.uint8).copy()).permute(2, 0, 1)
+            image = normalize_u8(x) if self.normalize else x.float().div(255)
         coords = torch.zeros(NUM_LEVELS, 2)
         mask = torch.zeros(NUM_LEVELS)
-        for lvl, (x, y) in rec["coords"].items():
-            coords[lvl, 0], coords[lvl, 1], mask[lvl] = x, y, 1.0
-        return {"image": image, "coords": coords, "mask": mask,
-                "series_type_idx": SERIES_TYPE_TO_IDX.get(rec["series_type"], 0),
-                "metadata": {"image_path": rel, "source": rec["source"], "series_type": rec["series_type"]}}
+        for lvl, (x_, y_) in rec["coords"].items():
+            coords[lvl, 0], coords[lvl, 1], mask[lvl] = x_, y_, 1.0
+        if params is not None and self.augment_coords:
+            coords = transform_coords(coords, params, self.image_size[0], self.image_size[1]) * mask[:, None]
+        out.update({"image": image, "coords": coords, "mask": mask,
+                    "series_type_idx": SERIES_TYPE_TO_IDX.get(rec["series_type"], 0),
+                    "metadata": {"image_path": rel, "source": rec["source"], "series_type": rec["series_type"]}})
+        return out
 
     def get_stats(self) -> dict[str, Any]:
         lc: dict[int, int] = defaultdict(int)
@@ -107,12 +130,15 @@ class LocalizationDataset(Dataset):
 
 class SyntheticLocalizationDataset(Dataset):
     """Seeded synthetic samples with the BASELINE input spec: uint8 grayscale U{0..255} -> RGB ->
-    /255 -> ImageNet normalise; coords U(0.05, 0.95); ~10% of levels masked."""
+    /255 -> ImageNet normalise; coords U(0.05, 0.95); ~10% of levels masked.  ``augment``: the
+    reference's train augmentation, host (PIL) or device (``device_transform``) path as in
+    LocalizationDataset."""
 
     def __init__(self, n: int, image_size: tuple[int, int] = (512, 512), seed: int = 42,
-                 device_transform: bool = False) -> None:
+                 device_transform: bool = False, augment: bool = False) -> None:
         self.n, self.image_size, self.seed = n, tuple(image_size), seed
         self.device_transform = device_transform
+        self.augment = augment
 
     def __len__(self) -> int:
         return self.n
@@ -122,19 +148,37 @@ class SyntheticLocalizationDataset(Dataset):
         u8 = torch.randint(0, 256, self.image_size, generator=g, dtype=torch.uint8)
         coords = torch.rand(NUM_LEVELS, 2, generator=g) * 0.9 + 0.05
         mask = (torch.rand(NUM_LEVELS, generator=g) >= 0.1).float()
-        return {"image": u8 if self.device_transform else normalize_u8(u8), "coords": coords, "mask": mask, "series_type_idx": 1,
-                "metadata": {"image_path": f"synthetic_{i}.png", "source": "synthetic", "series_type": "sag_t2"}}
+        out: dict[str, Any] = {}
+        if self.augment:
+            from .augment import apply_pil, sample_params
+
+            params = sample_params(self.image_size[0], self.image_size[1], flip=True)
+            if self.device_transform:
+                out["augment"] = params
+            else:
+                from PIL import Image
+
+                u8 = torch.from_numpy(np.asarray(apply_pil(Image.fromarray(u8.numpy(), "L"), params)).copy())
+        out.update({"image": u8 if self.device_transform else normalize_u8(u8), "coords": coords, "mask": mask,
+                    "series_type_idx": 1,
+                    "metadata": {"image_path": f"synthetic_{i}.png", "source": "synthetic", "series_type": "sag_t2"}})
+        return out
 
     def get_stats(self) -> dict[str, Any]:
         return {"num_images": self.n, "source": "synthetic"}
 
 
 class LocalizationCollator:
+    """training/datasets/localization.py:315-337 of the reference (+ "augment" [B,10] when present)."""
+
     def __call__(self, samples: list[dict[str, Any]]) -> dict[str, Any]:
-        return {
+        out = {
             "image": torch.stack([s["image"] for s in samples]),
             "coords": torch.stack([s["coords"] for s in samples]),
             "mask": torch.stack([s["mask"] for s in samples]),
             "series_type_idx": torch.tensor([s["series_type_idx"] for s in samples], dtype=torch.long),
             "metadata": [s["metadata"] for s in samples],
         }
+        if "augment" in samples[0]:  # device_transform: per-sample augmentation parameters [B,10]
+            out["augment"] = torch.stack([s["augment"] for s in samples])
+        return out

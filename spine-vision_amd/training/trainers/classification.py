@@ -8,12 +8,14 @@ checkpoint metric.  Rank-local validation metrics (the reference does not gather
 
 from __future__ import annotations
 
+from pathlib import Path
+
 from typing import Any
 
 import torch
 
 from ...core.tasks import AVAILABLE_TASK_NAMES, TaskConfig, get_task
-from ..datasets.classification import ClassificationCollator, create_weighted_sampler
+from ..datasets.classification import ClassificationCollator, ClassificationDataset, create_weighted_sampler
 from ..metrics import ClassifierMetrics
 from ..models.generic import Classifier
 from .base import BaseTrainer, TrainingConfig, logger
@@ -39,7 +41,7 @@ def _create_tasks_for_training(target_labels: list[str] | None = None, label_smo
 
 class ClassificationConfig(TrainingConfig):
     task: str = "classification"
-    data_path: Any = "data/processed/classification"
+    data_path: Path = Path("data/processed/classification")
     backbone: str = "resnet18"
     pretrained: bool = True
     dropout: float = 0.3
@@ -63,10 +65,14 @@ class ClassificationConfig(TrainingConfig):
 class ClassificationTrainer(BaseTrainer):
     def __init__(self, config: ClassificationConfig, model: Classifier | None = None, train_dataset=None,
                  val_dataset=None) -> None:
-        if train_dataset is None or val_dataset is None:
-            raise NotImplementedError(
-                "ClassificationDataset crop extraction is outside the MI355X training path; pass train_dataset/"
-                "val_dataset (e.g. training.datasets.SyntheticClassificationDataset or your own crops)")
+        common = dict(val_ratio=config.val_split, levels=config.levels, series_types=config.series_types,
+                      target_labels=config.target_labels, output_size=config.output_size,
+                      device_transform=config.device_transform)
+        if train_dataset is None:
+            train_dataset = ClassificationDataset(Path(config.data_path), split="train", augment=config.augment,
+                                                  **common)
+        if val_dataset is None:
+            val_dataset = ClassificationDataset(Path(config.data_path), split="val", augment=False, **common)
         if config.device_transform:
             # row f1: datasets that support it yield the uint8 [H,W,3] crop (normalised on the device)
             for ds in (train_dataset, val_dataset):
@@ -106,6 +112,10 @@ class ClassificationTrainer(BaseTrainer):
 
     def _train_step(self, batch: dict[str, Any]) -> torch.Tensor:
         image = batch["image"].to(self.device, non_blocking=True)
+        if "augment" in batch:  # device_transform: affine / jitter of the uint8 crops on the GPU
+            from ... import kernels as K
+
+            image = K.augment_u8(image, batch["augment"].to(self.device, non_blocking=True))
         targets = batch["targets"].to(self.device).to_dict()
         return self._optimize(lambda: self.model.get_loss(self.model(image), targets))
 

@@ -37,6 +37,9 @@ class LocalizationConfig(TrainingConfig):
     sources: list[str] | None = None
     image_size: tuple[int, int] = (512, 512)
     augment: bool = True
+    augment_coords: bool = False
+    """MI355X build addition: move the keypoints with the train-time flip / affine.  The reference
+    augments the image only (its coords come from the CSV), so False keeps its behaviour."""
     pck_thresholds: list[float] = [0.02, 0.05, 0.10]
     visualize_predictions: bool = True
     num_visualization_samples: int = 16
@@ -54,7 +57,8 @@ class LocalizationTrainer(BaseTrainer):
             train_dataset = LocalizationDataset(Path(config.data_path), split="train", val_ratio=config.val_split,
                                                 series_types=config.series_types, sources=config.sources,
                                                 image_size=config.image_size, augment=config.augment,
-                                                device_transform=config.device_transform)
+                                                device_transform=config.device_transform,
+                                                augment_coords=config.augment_coords)
         if val_dataset is None:
             val_dataset = LocalizationDataset(Path(config.data_path), split="val", val_ratio=config.val_split,
                                               series_types=config.series_types, sources=config.sources,
@@ -74,6 +78,10 @@ class LocalizationTrainer(BaseTrainer):
     def _train_step(self, batch: dict[str, Any]) -> torch.Tensor:
         dev = self.device
         image = batch["image"].to(dev, non_blocking=True)
+        if "augment" in batch:  # device_transform: flip / affine / jitter of the uint8 batch on the GPU
+            from ... import kernels as K
+
+            image = K.augment_u8(image, batch["augment"].to(dev, non_blocking=True))
         coords = batch["coords"].to(dev, non_blocking=True)
         mask = batch["mask"].to(dev, non_blocking=True)
         return self._optimize(lambda: self.model.get_loss(self.model(image), coords, mask=mask))

@@ -1,0 +1,218 @@
+"""CPU: the train-time augmentation (row f1).
+
+* The pixel arithmetic the device kernel (csrc/augment.hip) implements is restated here in numpy and
+  checked bit for bit against Pillow itself -- the library torchvision calls for the reference's
+  RandomHorizontalFlip / RandomAffine(NEAREST, fill 0) / ColorJitter on PIL images: 16.16 fixed-point
+  affine (double walk when the matrix is diagonal), float32 un-fused blends with truncation, the
+  contrast mean int(mean(L) + 0.5) with Pillow's L = (R*19595 + G*38470 + B*7471 + 0x8000) >> 16.
+* The datasets: augmentation on/off by split, the device-transform contract (uint8 + parameters),
+  ClassificationDataset over an on-disk crop dataset (CSV pairing, patient split, transforms) and
+  ClassificationTrainer built from ``data_path`` alone.
+"""
+
+import csv
+import math
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image, ImageEnhance
+
+from spine_vision_amd.training.datasets.augment import apply_pil, inverse_affine_matrix, sample_params
+
+
+def _coord(v):
+    return -1 if v < 0.0 else int(v)
+
+
+def _fix(v):
+    return int(math.floor(v * 65536.0 + 0.5))
+
+
+def _affine_np(img, a):
+    H, W = img.shape[:2]
+    out = np.zeros_like(img)
+    if a[1] == 0.0 and a[3] == 0.0:  # ImagingScaleAffine: incremental double walk
+        xo0, yo = a[2] + a[0] * 0.5, a[5] + a[4] * 0.5
+        xin = []
+        for _ in range(W):
+            xin.append(_coord(xo0))
+            xo0 += a[0]
+        for y in range(H):
+            yi = _coord(yo)
+            if 0 <= yi < H:
+                for x in range(W):
+                    if 0 <= xin[x] < W:
+                        out[y, x] = img[yi, xin[x]]
+            yo += a[4]
+        return out
+    f = [_fix(v) for v in a]
+    xo = _fix(a[2] + a[0] * 0.5 + a[1] * 0.5)  # Pillow affine_fixed: half-pixel offsets folded before FIX
+    yo = _fix(a[5] + a[3] * 0.5 + a[4] * 0.5)
+    ys, xs = np.mgrid[0:H, 0:W]
+    xi = (xo + ys * f[1] + xs * f[0]) >> 16
+    yi = (yo + ys * f[4] + xs * f[3]) >> 16
+    ok = (xi >= 0) & (xi < W) & (yi >= 0) & (yi < H)
+    out[ok] = img[yi[ok], xi[ok]]
+    return out
+
+
+def _blend_np(deg, img, alpha):
+    al = np.float32(alpha)
+    t = np.float32(deg) + (al * (img.astype(np.int32) - np.int32(deg)).astype(np.float32)).astype(np.float32)
+    t = t.astype(np.float32)
+    if 0 <= alpha <= 1.0:
+        return t.astype(np.uint8)
+    return np.clip(t, 0, 255).astype(np.uint8)
+
+
+def _apply_np(arr, p):
+    p = p.tolist()
+    if p[0]:
+        arr = arr[:, ::-1].copy()
+    arr = _affine_np(arr, p[1:7])
+    for op in ((0, 1) if p[9] == 0.0 else (1, 0)):
+        if op == 0:
+            arr = _blend_np(0, arr, p[7])
+        else:
+            L = arr.astype(np.int64) if arr.ndim == 2 else (
+                (arr[..., 0].astype(np.int64) * 19595 + arr[..., 1].astype(np.int64) * 38470
+                 + arr[..., 2].astype(np.int64) * 7471 + 0x8000) >> 16)
+            arr = _blend_np(int(float(L.sum()) / L.size + 0.5), arr, p[8])
+    return arr
+
+
+@pytest.mark.parametrize("mode", ["L", "RGB"])
+def test_device_arithmetic_restatement_matches_pillow(mode):
+    rng = np.random.default_rng(3)
+    torch.manual_seed(0)
+    for trial in range(40):
+        H, W = int(rng.integers(16, 80)), int(rng.integers(16, 80))
+        arr = rng.integers(0, 256, (H, W) if mode == "L" else (H, W, 3), dtype=np.uint8)
+        p = sample_params(H, W, flip=True)
+        if trial % 5 == 0:  # the diagonal (scale-only) Pillow path
+            p[1:7] = torch.tensor(inverse_affine_matrix([W * 0.5, H * 0.5], 0.0, (1, -2), 1.03), dtype=torch.float64)
+        if trial % 3 == 0:
+            p[7] = 1.2  # brightness > 1: the clipping branch
+        ref = np.asarray(apply_pil(Image.fromarray(arr, mode), p))
+        got = _apply_np(arr, p)
+        assert np.array_equal(ref, got), (trial, int((ref != got).sum()))
+
+
+def test_sample_params_ranges_and_reproducibility():
+    torch.manual_seed(11)
+    a = torch.stack([sample_params(512, 512, flip=True) for _ in range(200)])
+    torch.manual_seed(11)
+    b = torch.stack([sample_params(512, 512, flip=True) for _ in range(200)])
+    assert torch.equal(a, b)
+    assert set(a[:, 0].tolist()) == {0.0, 1.0}
+    assert ((a[:, 7] >= 0.8) & (a[:, 7] <= 1.2)).all() and ((a[:, 8] >= 0.8) & (a[:, 8] <= 1.2)).all()
+    assert set(a[:, 9].tolist()) == {0.0, 1.0}
+    # inverse-affine scale within 1/1.05 .. 1/0.95 and rotation within 10 degrees
+    det = a[:, 1] * a[:, 5] - a[:, 2] * a[:, 4]
+    assert ((det >= 1 / 1.05 ** 2 - 1e-9) & (det <= 1 / 0.95 ** 2 + 1e-9)).all()
+    no_flip = sample_params(64, 64, flip=False)
+    assert no_flip[0] == 0.0
+
+
+def _write_crop_dataset(root, n_patients=12):
+    (root / "images").mkdir(parents=True)
+    rng = np.random.default_rng(0)
+    rows = []
+    for p in range(n_patients):
+        for lvl in (4, 5):
+            labels = {"pfirrmann_grade": 1 + (p % 2) * 2, "modic": p % 2, "disc_herniation": p % 2,
+                      "disc_narrowing": 0, "disc_bulging": 0, "spondylolisthesis": 0, "up_endplate": 0,
+                      "low_endplate": 0}
+            for st in ("sag_t1", "sag_t2"):
+                name = f"images/phenikaa_{p}_{st}_L{lvl}.png"
+                Image.fromarray(rng.integers(0, 256, (40, 36), dtype=np.uint8), "L").save(root / name)
+                rows.append({"image_path": name, "patient_id": str(p), "ivd_level": lvl, "series_type": st,
+                             "source": "phenikaa", **labels})
+    with open(root / "annotations.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+
+
+def test_classification_dataset_from_disk(tmp_path):
+    from spine_vision_amd.training.datasets import ClassificationCollator, ClassificationDataset
+
+    _write_crop_dataset(tmp_path)
+    kw = dict(target_labels=["pfirrmann", "modic", "herniation"], output_size=(32, 32), val_ratio=0.2, test_ratio=0.2)
+    tr = ClassificationDataset(tmp_path, split="train", **kw)
+    va = ClassificationDataset(tmp_path, split="val", augment=True, **kw)
+    te = ClassificationDataset(tmp_path, split="test", **kw)
+    assert tr.augment and not va.augment  # augmentation is train-only, as in the reference
+    pats = [set(r["patient_key"] for r in d.records) for d in (tr, va, te)]
+    assert not (pats[0] & pats[1]) and not (pats[0] & pats[2]) and not (pats[1] & pats[2])
+    assert len(tr) + len(va) + len(te) == 24  # 12 patients x 2 levels, T1+T2 paired into one record
+    s = tr[0]
+    assert s["image"].shape == (3, 32, 32) and s["image"].dtype == torch.float32
+    assert set(s["targets"]) == {"pfirrmann", "modic", "herniation"} and isinstance(s["targets"]["herniation"], list)
+    b = ClassificationCollator()([tr[i] for i in range(3)])
+    assert b["targets"].herniation.shape == (3, 1) and b["targets"].pfirrmann.dtype == torch.int64
+    dev = ClassificationDataset(tmp_path, split="train", device_transform=True, **kw)
+    sd = dev[0]
+    assert sd["image"].shape == (32, 32, 3) and sd["image"].dtype == torch.uint8 and sd["augment"].shape == (10,)
+    only_t2 = ClassificationDataset(tmp_path, split="all", series_types=["sag_t2"], **kw)
+    assert len(only_t2) == 24  # (like the reference, the filter only requires T2; a present T1 is still paired)
+    assert tr.get_stats()["num_samples"] == len(tr)
+    assert set(tr.compute_class_weights()) == {"pfirrmann", "modic", "herniation"}
+
+
+def test_classification_trainer_from_data_path(tmp_path):
+    from test_trainer_cpu import TinyCls
+
+    from spine_vision_amd.training.trainers import ClassificationConfig, ClassificationTrainer
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    class CpuCls(ClassificationTrainer):
+        def _create_optimizer(self):
+            return torch.optim.AdamW(self.model.parameters(), lr=1e-4)
+
+    _write_crop_dataset(tmp_path / "data")
+    labels = ["pfirrmann", "modic", "herniation"]
+    cfg = ClassificationConfig(data_path=tmp_path / "data", output_path=tmp_path / "out", batch_size=2, num_epochs=1,
+                               num_workers=0, pin_memory=False, target_labels=labels, output_size=(32, 32),
+                               pretrained=False, val_split=0.2)
+    tr = CpuCls(cfg, model=TinyCls(_create_tasks_for_training(labels)))
+    assert len(tr.train_dataset) > 0 and len(tr.val_dataset) > 0
+    res = tr.train()
+    assert res.final_train_loss == res.final_train_loss
+
+
+def test_localization_dataset_augment_paths(tmp_path):
+    from spine_vision_amd.training.datasets import LocalizationCollator, LocalizationDataset
+
+    (tmp_path / "img").mkdir()
+    rows = []
+    rng = np.random.default_rng(1)
+    for i in range(6):
+        name = f"img/s{i}.png"
+        Image.fromarray(rng.integers(0, 256, (50, 40), dtype=np.uint8), "L").save(tmp_path / name)
+        for lvl, lname in enumerate(("L1/L2", "L2/L3", "L3/L4", "L4/L5", "L5/S1")):
+            rows.append({"image_path": name, "level": lname, "relative_x": 0.3 + 0.05 * lvl, "relative_y": 0.2 + 0.1 * lvl,
+                         "series_type": "sag_t2", "source": "rsna"})
+    with open(tmp_path / "annotations.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    kw = dict(image_size=(32, 32), val_ratio=0.0, test_ratio=0.0)
+    torch.manual_seed(5)
+    host = LocalizationDataset(tmp_path, split="train", **kw)
+    a = host[0]
+    torch.manual_seed(5)
+    dev = LocalizationDataset(tmp_path, split="train", device_transform=True, **kw)
+    d = dev[0]
+    assert a["image"].shape == (3, 32, 32) and d["image"].shape == (32, 32) and d["image"].dtype == torch.uint8
+    # same RNG draws -> the host image is exactly the PIL augmentation of the device path's input
+    from spine_vision_amd.training.datasets.localization import normalize_u8
+
+    ref = apply_pil(Image.fromarray(d["image"].numpy(), "L").convert("RGB"), d["augment"])
+    assert torch.equal(normalize_u8(torch.from_numpy(np.asarray(ref).copy()).permute(2, 0, 1)), a["image"])
+    assert torch.equal(a["coords"], d["coords"])  # the reference moves no keypoint
+    moved = LocalizationDataset(tmp_path, split="train", augment_coords=True, **kw)[0]
+    assert moved["coords"].shape == (5, 2)
+    b = LocalizationCollator()([dev[i] for i in range(2)])
+    assert b["augment"].shape == (2, 10) and b["image"].shape == (2, 32, 32)
