@@ -95,6 +95,11 @@ int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
  * that GEMMs issued concurrently on two streams (data gradients + weight gradients) are co-resident
  * on every CU instead of the first one filling the chip.  Returns the previous value.               */
 int sv_gemm_set_workgroups_per_cu(int32_t n);
+/* Kernel family for the bf16 GEMMs launched after this call (host-side, process-wide, initially 0):
+ * 0 = the measured per-shape dispatch, 2 / 3 / 8 = force that family where its contract holds
+ * (tests/test_gemm_family_gpu.py compares the families bit for bit; tools/gemm_bench.py times them).
+ * Returns the previous value.                                                                      */
+int sv_gemm_set_impl(int32_t impl);
 
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.

@@ -123,7 +123,7 @@ class ConvNeXtHip(nn.Module):
         self._shadow: dict[int, torch.Tensor] | None = None  # id(param) -> bf16 shadow view
         # weight-gradient kernels on a side stream beside the data-gradient chain (SV_SIDE_STREAM=0: off)
         self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
-        self.side_wg_per_cu = int(os.environ.get("SV_SIDE_WG_PER_CU", "1"))
+        self.side_wg_per_cu = 1  # the data-gradient GEMMs keep one workgroup per CU free for the side stream
         # bf16 backward: ONE main->side hand-off per block (after the LayerNorm backward) instead of three,
         # and the side stream's operands kept alive in a list until the streams join instead of
         # record_stream -- every cross-stream event / allocator event is a release packet (L2 write-back)

@@ -557,7 +557,6 @@ static sv_gemm_desc conv_desc(const void* A, const void* B, int M, int N, int K,
   d.compute = SV_BF16;
   return d;
 }
-static const bool g_conv_gemm = getenv("SV_CONV_GEMM") ? atoi(getenv("SV_CONV_GEMM")) != 0 : true;
 
 }  // namespace conv
 }  // namespace sv
@@ -648,7 +647,7 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
   a.C = y;
   a.c_dtype = y_dtype;
   a.kper = ceil_div(a.K, BKT) * BKT;
-  if (g_conv_gemm && dtype == SV_BF16 && s->Cs >= 32 && pow2(s->Cs) && a.K % 32 == 0) {
+  if (dtype == SV_BF16 && s->Cs >= 32 && pow2(s->Cs) && a.K % 32 == 0) {
     ConvG g = make_convg(s->H, s->W, s->Cs, OH, OW, s->stride);
     for (int j = 0; j < a.ntaps; ++j) {
       g.tdy[j] = a.tdy[j];
@@ -688,7 +687,7 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
   const int st = s->stride;
   const int T_ = s->KH * s->KW;
-  if (g_conv_gemm && dtype == SV_BF16 && st == 1 && s->Cout >= 32 && (s->Cs % 8) == 0 &&
+  if (dtype == SV_BF16 && st == 1 && s->Cout >= 32 && (s->Cs % 8) == 0 &&
       (!accumulate || dx_dtype == SV_F32) && ((int64_t)T_ * s->Cout) % 32 == 0) {
     // stride 1: one gather conv over dy (taps pad - kh, pad - kw) against the weight's rows
     ConvG g = make_convg(OH, OW, s->Cout, s->H, s->W, 1);
@@ -783,7 +782,7 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
   const int T_ = s->KH * s->KW;
   hipStream_t st = (hipStream_t)stream;
   const int64_t npix = (int64_t)s->B * OH * OW;
-  if (g_conv_gemm && dtype == SV_BF16 && s->Cs >= 8 && pow2(s->Cs) && npix % 32 == 0 && s->Cout % 8 == 0) {
+  if (dtype == SV_BF16 && s->Cs >= 8 && pow2(s->Cs) && npix % 32 == 0 && s->Cout % 8 == 0) {
     // v3 gather wgrad: A = dy (M-major: [pixel][Cout]), B = gathered x rows, split-K f32 slabs
     const int sp = wgrad_split3(s);
     ConvG g = make_convg(s->H, s->W, s->Cs, OH, OW, s->stride);

@@ -1,14 +1,14 @@
 // Depthwise 7x7 convolution (pad 3, stride 1) on NHWC activations -- ConvNeXtBlock.conv_dw
 // (timm convnext.py; HF equivalent transformers/models/convnext/modeling_convnext.py:130,144).
 //
-// Layout/tiling (gfx950): one WAVE owns a 16-row x 8-column output strip of one image for one
+// Layout/tiling (gfx950): one WAVE owns a 16-row x 4-column output strip of one image for one
 // 64-channel group (lane == channel, so every global access of a wave is 64 consecutive channels:
-// 256 B f32 / 128 B bf16, fully coalesced).  The wave streams the 22 input rows of its strip
-// through registers once, top to bottom: each 14-wide input row feeds the 7 output rows it touches
-// (7 x 8 x 7 FMAs per 14 loads), with a rolling set of 7 output-row accumulators -- an output row
-// is stored as soon as its 7th input row has been consumed.  No LDS and no barriers: the 3.6x halo
-// re-read of an 8x8 tile becomes 2.4x row re-reads that the CU's L1 / the XCD's L2 absorb, and the
-// HBM traffic is one read of the input and one write of the output.
+// 256 B f32 / 128 B bf16, fully coalesced).  The wave streams the 22 input rows of its strip once,
+// top to bottom, through a wave-private LDS ring filled by LDS-DMA: each 10-wide input row feeds the
+// 7 output rows it touches, with a rolling set of 7 output-row accumulators -- an output row is
+// stored as soon as its 7th input row has been consumed.  No barriers: the halo re-reads are row
+// re-reads that the CU's L1 / the XCD's L2 absorb, and the HBM traffic is one read of the input and
+// one write of the output.
 //
 // The op is HBM-bound (49 FMA per 4-8 bytes moved).
 //
@@ -43,186 +43,8 @@ __device__ __forceinline__ void dw_tile(const DwGeo& g, int tile, int& b, int& h
   w0 = tw * g.tw;
 }
 
-// one (TW+6)-wide input row (zero outside the image) of channel c
-template <int TC, typename TIN>
-__device__ __forceinline__ void load_row(float (&in)[TC], const TIN* __restrict__ x, const DwGeo& g, int b, int h,
-                                         int w0, int c) {
-  const bool okh = h >= 0 && h < g.H;
-  const size_t base = (((size_t)b * g.H + (okh ? h : 0)) * g.W) * g.C + c;
-#pragma unroll
-  for (int j = 0; j < TC; ++j) {
-    const int w = w0 - 3 + j;
-    in[j] = (okh && w >= 0 && w < g.W) ? ld(x, base + (size_t)w * g.C) : 0.f;
-  }
-}
-
-// z (or dx) for one 16x8 strip x 64 channels per wave.  FLIP: use w[48 - tap] (backward-data).
-template <int TW, typename TIN, typename TOUT, bool FLIP, bool ACCUM>
-__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_kernel(const TIN* __restrict__ x,
-                                                             const float* __restrict__ wdw,
-                                                             const float* __restrict__ bdw,
-                                                             TOUT* __restrict__ out,
-                                                             uint16_t* __restrict__ out_bf16, DwGeo g) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * (kDwThreads / 64) + (threadIdx.x >> 6);
-  const int ncg = g.C / 64;
-  if (gw >= g.ntiles * ncg) return;  // whole wave; the kernel has no barriers
-  const int tile = gw % g.ntiles, c = (gw / g.ntiles) * 64 + lane;
-  int b, h0, w0;
-  dw_tile(g, tile, b, h0, w0);
-  float wk[49];
-#pragma unroll
-  for (int i = 0; i < 49; ++i) wk[i] = wdw[(size_t)c * 49 + (FLIP ? 48 - i : i)];
-  const float bias = bdw ? bdw[c] : 0.f;
-  constexpr int TC = TW + 6;
-  float acc[7][TW];
-#pragma unroll
-  for (int r = 0; r < 7; ++r)
-#pragma unroll
-    for (int o = 0; o < TW; ++o) acc[r][o] = bias;
-  float in[TC], nxt[TC];
-  float pcur[TW], pnew[TW];  // ACCUM: the old values of the next output row, loaded one row early
-#pragma unroll
-  for (int o = 0; o < TW; ++o) pcur[o] = pnew[o] = 0.f;
-  load_row(nxt, x, g, b, h0 - 3, w0, c);
-  // input rows in blocks of 7: inside a block, the accumulator slot of output row ir - kh is the
-  // compile-time (u - kh) mod 7 (ib is a multiple of 7); sched_barrier keeps each row's loads one
-  // row ahead instead of letting the scheduler hoist all 308 of them
-#pragma nounroll
-  for (int ib = 0; ib < TR; ib += 7) {
-#pragma unroll
-    for (int u = 0; u < 7; ++u) {
-      const int ir = ib + u;
-      if (ir >= TR) break;
-#pragma unroll
-      for (int j = 0; j < TC; ++j) in[j] = nxt[j];
-      if (ir + 1 < TR) load_row(nxt, x, g, b, h0 - 3 + ir + 1, w0, c);  // next row in flight
-      if (ACCUM && ir >= 5 && ir - 5 < TH) {
-        const int h = h0 + ir - 5;
-#pragma unroll
-        for (int o = 0; o < TW; ++o) {
-          const int w = w0 + o;
-          pnew[o] = (h < g.H && w < g.W) ? ld(out, (((size_t)b * g.H + h) * g.W + w) * g.C + c) : 0.f;
-        }
-      }
-#pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        const int orow = ir - kh;
-        if (orow < 0 || orow >= TH) continue;
-        const int sl = (u - kh + 7) % 7;
-#pragma unroll
-        for (int o = 0; o < TW; ++o)
-#pragma unroll
-          for (int kw = 0; kw < 7; ++kw) acc[sl][o] = fmaf(wk[kh * 7 + kw], in[o + kw], acc[sl][o]);
-      }
-      if (ir >= 6) {
-        const int orow = ir - 6;  // its 7th (last) input row was just consumed
-        const int sl = (u + 1) % 7;  // == (u - 6) mod 7
-        const int h = h0 + orow;
-        if (h < g.H) {
-#pragma unroll
-          for (int o = 0; o < TW; ++o) {
-            const int w = w0 + o;
-            if (w < g.W) {
-              const size_t i = (((size_t)b * g.H + h) * g.W + w) * g.C + c;
-              const float v = ACCUM ? pcur[o] + acc[sl][o] : acc[sl][o];
-              st(out, i, v);
-              if (out_bf16) out_bf16[i] = f2bf(v);
-            }
-          }
-        }
-#pragma unroll
-        for (int o = 0; o < TW; ++o) acc[sl][o] = bias;  // reused by output row orow + 7
-      }
-      if (ACCUM) {
-#pragma unroll
-        for (int o = 0; o < TW; ++o) pcur[o] = pnew[o];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-// backward-weight partials.  grid = (nparts, C/64); wave v of workgroup p visits strips
-// 4p + v, 4p + v + 4 nparts, ...; the 4 waves are combined through LDS into part p.
-template <int TW, typename TDZ, typename TIN>
-__global__ void __launch_bounds__(kDwThreads) __attribute__((amdgpu_waves_per_eu(3))) dwconv7_wgrad_kernel(const TDZ* __restrict__ dz,
-                                                                   const TIN* __restrict__ x,
-                                                                   float* __restrict__ dw_part,
-                                                                   float* __restrict__ db_part, DwGeo g) {
-  __shared__ float red[4 * 49 * 64 + 4 * 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c0 = blockIdx.y * 64, c = c0 + lane;
-  float acc[49];
-#pragma unroll
-  for (int i = 0; i < 49; ++i) acc[i] = 0.f;
-  float dbacc = 0.f;
-  for (int tile = blockIdx.x * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
-    int b, h0, w0;
-    dw_tile(g, tile, b, h0, w0);
-    constexpr int TC = TW + 6;
-    float dzb[7][TW];
-    float in[TC], nxt[TC];
-    load_row(nxt, x, g, b, h0 - 3, w0, c);
-#pragma nounroll
-    for (int ib = 0; ib < TR; ib += 7) {
-#pragma unroll
-      for (int u = 0; u < 7; ++u) {
-        const int ir = ib + u;
-        if (ir >= TR) break;
-#pragma unroll
-        for (int j = 0; j < TC; ++j) in[j] = nxt[j];
-        if (ir + 1 < TR) load_row(nxt, x, g, b, h0 - 3 + ir + 1, w0, c);
-        if (ir < TH) {  // output-gradient row ir enters the rolling set (slot u)
-          const int h = h0 + ir;
-#pragma unroll
-          for (int o = 0; o < TW; ++o) {
-            const int w = w0 + o;
-            const float v = (h < g.H && w < g.W) ? ld(dz, (((size_t)b * g.H + h) * g.W + w) * g.C + c) : 0.f;
-            dzb[u][o] = v;
-            dbacc += v;
-          }
-        }
-#pragma unroll
-        for (int kh = 0; kh < 7; ++kh) {
-          const int orow = ir - kh;
-          if (orow < 0 || orow >= TH) continue;
-          const int sl = (u - kh + 7) % 7;
-#pragma unroll
-          for (int kw = 0; kw < 7; ++kw) {
-            float s = acc[kh * 7 + kw];
-#pragma unroll
-            for (int o = 0; o < TW; ++o) s = fmaf(dzb[sl][o], in[o + kw], s);
-            acc[kh * 7 + kw] = s;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-  // deterministic combine of the 4 waves through LDS: red[wave][tap][64]
-#pragma unroll
-  for (int i = 0; i < 49; ++i) red[(wv * 49 + i) * 64 + lane] = acc[i];
-  float* redb = red + 4 * 49 * 64;
-  redb[wv * 64 + lane] = dbacc;
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 49; i += kDwThreads) {
-    const int ch = i / 49, tap = i - ch * 49;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s += red[(k * 49 + tap) * 64 + ch];
-    dw_part[(size_t)blockIdx.x * g.C * 49 + (size_t)(c0 + ch) * 49 + tap] = s;
-  }
-  if (threadIdx.x < 64) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s += redb[k * 64 + threadIdx.x];
-    db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = s;
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// Ring variants (default): the same per-wave strip streaming, but the input rows arrive through a
+// Ring kernels: per-wave strip streaming (above); the input rows arrive through a
 // wave-private LDS ring filled by LDS-DMA (global_load_lds, one 64-lane column per instruction)
 // PF-1 rows ahead of the row being consumed; the prefetch costs no VGPRs.  Everything except the
 // channel is wave-uniform, so the strip geometry lives in SGPRs (readfirstlane'd wave id) and every
@@ -486,39 +308,13 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
   if (threadIdx.x < 64) db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = redb[threadIdx.x];
 }
 
-// implementation switch (A/B): SV_DW_IMPL=0 -> register-prefetch kernels; default ring, SV_DW_PF
-// = ring depth (2..4)
-static int dw_impl() {
-  static const int v = getenv("SV_DW_IMPL") ? atoi(getenv("SV_DW_IMPL")) : 1;
-  return v;
-}
-static int dw_pf() {
-  static const int v = getenv("SV_DW_PF") ? atoi(getenv("SV_DW_PF")) : 4;
-  return v < 2 ? 2 : (v > 4 ? 4 : v);
-}
-// wgrad ring depth: its ring holds x AND dz rows (14 columns), so depth 2 keeps 4 workgroups per CU
-// (measured: 2 >= 3, 4 on the S1/S3 shapes)
-static int dw_wgrad_pf() {
-  static const int v = getenv("SV_DW_WGRAD_PF") ? atoi(getenv("SV_DW_WGRAD_PF")) : 2;
-  return v < 2 ? 2 : (v > 4 ? 4 : v);
-}
-
-// strip width: 4 columns keeps a lane within 3 waves/SIMD (143 VGPRs); SV_DW_TW=8 trades occupancy for
-// fewer horizontal halo reads
-static int dw_tw() {
-  static const int tw = getenv("SV_DW_TW") && atoi(getenv("SV_DW_TW")) == 8 ? 8 : 4;
-  return tw;
-}
-
-static DwGeo dw_geo_tw(int B, int H, int W, int C, int tw) {
-  DwGeo g{B, H, W, C, tw, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
-  g.ntiles = B * g.tilesW * g.tilesH;
-  return g;
-}
+// ring depths: PF 4 rows for fwd / bwd-data; the wgrad ring holds x AND dz rows (14 columns), so depth 2
+// keeps 4 workgroups per CU (measured: 2 >= 3, 4 on the S1/S3 shapes).  Strip width 4 keeps a lane
+// within 3 waves/SIMD; the register-prefetch (no ring) kernels and 8-wide strips measured slower (round 1).
+constexpr int DW_PF = 4, DW_WGRAD_PF = 2, DW_TW = 4;
 
 static DwGeo dw_geo(int B, int H, int W, int C) {
-  const int tw = dw_tw();
-  DwGeo g{B, H, W, C, tw, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
+  DwGeo g{B, H, W, C, DW_TW, (W + DW_TW - 1) / DW_TW, (H + TH - 1) / TH, 0};
   g.ntiles = B * g.tilesW * g.tilesH;
   return g;
 }
@@ -539,39 +335,17 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_ln_fwd: C=%d must be a multiple of 64", C);
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (dw_impl() == 1) {
-    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
-    const int grid = dw_blocks(g);
-    const int pf = dw_pf();
-#define RLAUNCH(PFV, TI, TO)                                                                              \
-  dwconv7_ring_kernel<PFV, 4, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<PFV, 4, TI>(), s>>>(   \
-      (const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
-#define RLAUNCH_PF(TI, TO) \
-  if (pf == 4) RLAUNCH(4, TI, TO); else if (pf == 3) RLAUNCH(3, TI, TO); else RLAUNCH(2, TI, TO)
-    if (x_dtype == SV_F32 && z_dtype == SV_F32) { RLAUNCH_PF(float, float); }
-    else if (x_dtype == SV_F32 && z_dtype == SV_BF16) { RLAUNCH_PF(float, uint16_t); }
-    else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) { RLAUNCH_PF(uint16_t, uint16_t); }
-    else if (x_dtype == SV_BF16 && z_dtype == SV_F32) { RLAUNCH_PF(uint16_t, float); }
-    else return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_ln_fwd: bad dtype");
-#undef RLAUNCH_PF
-#undef RLAUNCH
-    int rc = check_launch("sv_dwconv7_ln_fwd(dwconv)");
-    if (rc) return rc;
-    return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
-  }
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
-#define LAUNCH(TI, TO)                                                                                      \
-  if (g.tw == 8)                                                                                           \
-    dwconv7_kernel<8, TI, TO, false, false><<<grid, kDwThreads, 0, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, g); \
-  else                                                                                                     \
-    dwconv7_kernel<4, TI, TO, false, false><<<grid, kDwThreads, 0, s>>>((const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
-  if (x_dtype == SV_F32 && z_dtype == SV_F32) LAUNCH(float, float);
-  else if (x_dtype == SV_F32 && z_dtype == SV_BF16) LAUNCH(float, uint16_t);
-  else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) LAUNCH(uint16_t, uint16_t);
-  else if (x_dtype == SV_BF16 && z_dtype == SV_F32) LAUNCH(uint16_t, float);
+#define RLAUNCH(TI, TO)                                                                                         \
+  dwconv7_ring_kernel<DW_PF, DW_TW, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<DW_PF, DW_TW, TI>(), s>>>( \
+      (const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
+  if (x_dtype == SV_F32 && z_dtype == SV_F32) RLAUNCH(float, float);
+  else if (x_dtype == SV_F32 && z_dtype == SV_BF16) RLAUNCH(float, uint16_t);
+  else if (x_dtype == SV_BF16 && z_dtype == SV_BF16) RLAUNCH(uint16_t, uint16_t);
+  else if (x_dtype == SV_BF16 && z_dtype == SV_F32) RLAUNCH(uint16_t, float);
   else return set_error(SV_ERR_INVALID_ARG, "sv_dwconv7_ln_fwd: bad dtype");
-#undef LAUNCH
+#undef RLAUNCH
   int rc = check_launch("sv_dwconv7_ln_fwd(dwconv)");
   if (rc) return rc;
   return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
@@ -585,42 +359,22 @@ int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, floa
   SV_REQUIRE(dz_dtype == SV_F32 || dz_dtype == SV_BF16, "sv_dwconv7_bwd_data: bad dz dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (dw_impl() == 1) {
-    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
-    const int grid = dw_blocks(g);
-    const int pf = dw_pf();
-#define RBWD(PFV, TD, ACC)                                                                                    \
-  dwconv7_ring_kernel<PFV, 4, TD, float, true, ACC><<<grid, kDwThreads, dw_ring_lds<PFV, 4, TD>(), s>>>(       \
-      (const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
-#define RBWD_PF(TD, ACC) \
-  if (pf == 4) RBWD(4, TD, ACC); else if (pf == 3) RBWD(3, TD, ACC); else RBWD(2, TD, ACC)
-    if (dz_dtype == SV_F32) {
-      if (accumulate) { RBWD_PF(float, true); } else { RBWD_PF(float, false); }
-    } else {
-      if (accumulate) { RBWD_PF(uint16_t, true); } else { RBWD_PF(uint16_t, false); }
-    }
-#undef RBWD_PF
-#undef RBWD
-    return check_launch("sv_dwconv7_bwd_data");
-  }
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
-#define BWD(TWV, TD, ACC) \
-  dwconv7_kernel<TWV, TD, float, true, ACC><<<grid, kDwThreads, 0, s>>>((const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
-#define BWD_TW(TD, ACC) \
-  if (g.tw == 8) BWD(8, TD, ACC); else BWD(4, TD, ACC)
+#define RBWD(TD, ACC)                                                                                             \
+  dwconv7_ring_kernel<DW_PF, DW_TW, TD, float, true, ACC><<<grid, kDwThreads, dw_ring_lds<DW_PF, DW_TW, TD>(), s>>>( \
+      (const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
   if (dz_dtype == SV_F32) {
-    if (accumulate) { BWD_TW(float, true); } else { BWD_TW(float, false); }
+    if (accumulate) RBWD(float, true); else RBWD(float, false);
   } else {
-    if (accumulate) { BWD_TW(uint16_t, true); } else { BWD_TW(uint16_t, false); }
+    if (accumulate) RBWD(uint16_t, true); else RBWD(uint16_t, false);
   }
-#undef BWD_TW
-#undef BWD
+#undef RBWD
   return check_launch("sv_dwconv7_bwd_data");
 }
 
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
-  const DwGeo g = dw_impl() == 1 ? dw_geo_tw(B, H, W, C, 4) : dw_geo(B, H, W, C);
+  const DwGeo g = dw_geo(B, H, W, C);
   const int ncg = C / 64 > 0 ? C / 64 : 1;
   int np = 512 / ncg;  // ~2048 waves over all channel groups
   if (np < 1) np = 1;
@@ -637,40 +391,20 @@ int sv_dwconv7_bwd_weight(const void* dz, int32_t dz_dtype, const void* x, int32
              "sv_dwconv7_bwd_weight: bad dtype");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (dw_impl() == 1) {
-    const DwGeo g = dw_geo_tw(B, H, W, C, 4);
-    const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
-    const int pf = dw_wgrad_pf();
-    constexpr size_t red_bytes = (49 * 64 + 64) * sizeof(float);
-#define RWG(PFV, TD, TX)                                                                                      \
-  {                                                                                                           \
-    const size_t lds = dw_wgrad_ring_lds<PFV, 4, TD, TX>() > red_bytes ? dw_wgrad_ring_lds<PFV, 4, TD, TX>()  \
-                                                                       : red_bytes;                          \
-    dwconv7_wgrad_ring_kernel<PFV, 4, TD, TX><<<grid, kDwThreads, lds, s>>>((const TD*)dz, (const TX*)x, dw_part, \
-                                                                            db_part, g);                     \
-  }
-#define RWG_PF(TD, TX) \
-  if (pf == 4) RWG(4, TD, TX) else if (pf == 3) RWG(3, TD, TX) else RWG(2, TD, TX)
-    if (dz_dtype == SV_F32 && x_dtype == SV_F32) { RWG_PF(float, float); }
-    else if (dz_dtype == SV_F32) { RWG_PF(float, uint16_t); }
-    else if (x_dtype == SV_F32) { RWG_PF(uint16_t, float); }
-    else { RWG_PF(uint16_t, uint16_t); }
-#undef RWG_PF
-#undef RWG
-    return check_launch("sv_dwconv7_bwd_weight");
-  }
   const DwGeo g = dw_geo(B, H, W, C);
   const dim3 grid(sv_dwconv7_bwd_weight_nparts(B, H, W, C), C / 64);
-#define WG(TWV, TD, TX) \
-  dwconv7_wgrad_kernel<TWV, TD, TX><<<grid, kDwThreads, 0, s>>>((const TD*)dz, (const TX*)x, dw_part, db_part, g)
-#define WG_TW(TD, TX) \
-  if (g.tw == 8) WG(8, TD, TX); else WG(4, TD, TX)
-  if (dz_dtype == SV_F32 && x_dtype == SV_F32) { WG_TW(float, float); }
-  else if (dz_dtype == SV_F32) { WG_TW(float, uint16_t); }
-  else if (x_dtype == SV_F32) { WG_TW(uint16_t, float); }
-  else { WG_TW(uint16_t, uint16_t); }
-#undef WG_TW
-#undef WG
+  constexpr size_t red_bytes = (49 * 64 + 64) * sizeof(float);
+#define RWG(TD, TX)                                                                                            \
+  {                                                                                                            \
+    constexpr size_t ring = dw_wgrad_ring_lds<DW_WGRAD_PF, DW_TW, TD, TX>();                                   \
+    dwconv7_wgrad_ring_kernel<DW_WGRAD_PF, DW_TW, TD, TX><<<grid, kDwThreads, ring > red_bytes ? ring : red_bytes, s>>>( \
+        (const TD*)dz, (const TX*)x, dw_part, db_part, g);                                                     \
+  }
+  if (dz_dtype == SV_F32 && x_dtype == SV_F32) RWG(float, float)
+  else if (dz_dtype == SV_F32) RWG(float, uint16_t)
+  else if (x_dtype == SV_F32) RWG(uint16_t, float)
+  else RWG(uint16_t, uint16_t)
+#undef RWG
   return check_launch("sv_dwconv7_bwd_weight");
 }
 

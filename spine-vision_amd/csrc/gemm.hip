@@ -294,7 +294,14 @@ using namespace sv;
 
 namespace sv {
 int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
-int g_store_wt = getenv("SV_STORE_WT") ? atoi(getenv("SV_STORE_WT")) : 0;
+}
+
+static int g_gemm_impl = 0;  // sv_gemm_set_impl: 0 = measured per-shape dispatch, 2/3/8 = force a family
+
+extern "C" int sv_gemm_set_impl(int32_t impl) {
+  const int prev = g_gemm_impl;
+  g_gemm_impl = impl;
+  return prev;
 }
 
 extern "C" int sv_gemm_set_workgroups_per_cu(int32_t n) {
@@ -336,14 +343,13 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!bf) return launch_layout<false, float, float>(d, s);
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
-  static const bool force_v1 = getenv("SV_GEMM_V1") != nullptr;
-  static const int impl = getenv("SV_GEMM_IMPL") ? atoi(getenv("SV_GEMM_IMPL")) : 0;
+  const int impl = g_gemm_impl;
   if (d->epilogue == SV_EPI_STORE_STATS) {  // only the v3 kernels carry the statistics epilogue
     const int rc = launch_gemm3(d, s);
     SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_STATS needs K %% 32 == 0 and bf16 operands");
     return rc;
   }
-  if (!force_v1) {
+  {
     // Measured per ConvNeXt shape (tools/gemm_bench.py, profiles/r1s2_gemm_cfg.txt):
     //   v3 32x3 (two workgroups per CU, one's epilogue beside the other's MFMAs): VALU-heavy and
     //     operand-reading epilogues and plain stores with K <= 2048 (fc1 fwd, fc2 dgrad, fc1 dgrad);
@@ -362,8 +368,6 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     int rc;
     if (impl == 0 && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);
     else if (impl == 8) rc = launch_gemm8(d, s);
-    else if (impl == 6) rc = launch_gemm6(d, s);
-    else if (impl == 7) rc = launch_gemm7(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);
     else if (impl == 3) rc = launch_gemm3(d, s);
     else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, g_gemm_wg_per_cu ? "32x3" : "32x4");

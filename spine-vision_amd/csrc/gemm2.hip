@@ -241,7 +241,6 @@ static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  e.wt = g_store_wt;
   constexpr size_t lds = Cfg<BN>::LDS;
   static bool attr_set = false;
   if (!attr_set) {
@@ -258,15 +257,9 @@ static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
 
 template <bool AK, bool BKM>
 static int launch_bn(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
-  // 256-wide tiles (SV_GEMM_BN=256) halve the L2->LDS bytes per FLOP
-  static const int force = getenv("SV_GEMM_BN") ? atoi(getenv("SV_GEMM_BN")) : 0;
-  const long tiles256 = (long)ceil_div(d->M, BM) * ceil_div(d->N, 256) * split;
-  // measured slower than 128-wide tiles on every ConvNeXt shape (2-stage ring exposes the DMA
-  // latency at one workgroup per CU): opt-in only
-  bool wide = false;
-  (void)tiles256;
-  if (force == 256) wide = d->N >= 256;
-  return wide ? launch<AK, BKM, 256>(d, split, kper, s) : launch<AK, BKM, 128>(d, split, kper, s);
+  // 256-wide tiles (half the L2->LDS bytes per FLOP) measured slower than 128-wide on every ConvNeXt
+  // shape (the 2-stage ring exposes the DMA latency at one workgroup per CU), round 1
+  return launch<AK, BKM, 128>(d, split, kper, s);
 }
 
 }  // namespace g2

@@ -2,17 +2,17 @@
 // (8 waves in 4(M) x 2(N), 64x64 per wave = 4x4 v_mfma_f32_16x16x32_bf16 fragments), LDS ring of S
 // stages of BK k, filled by LDS-DMA (global_load_lds_dwordx4), persistent over the tiles.
 //
-//   * configurations (SV_GEMM3_CFG): BK 32 x 3 stages = 72 KiB (two workgroups per CU: one's
-//     epilogue runs beside the other's MFMAs; default), BK 32 x 4 / BK 64 x 2 (96 KiB) and BK 64 x 3
-//     (144 KiB) at one workgroup per CU;
+//   * configurations: BK 32 x 3 stages = 72 KiB (two workgroups per CU: one's epilogue runs beside
+//     the other's MFMAs; default) and BK 32 x 4 = 96 KiB (one workgroup per CU, the split-K wgrads).
+//     BK 64 x 2/3, a persistent grid and a staggered second workgroup measured no faster (round 1);
 //   * counted `s_waitcnt vmcnt` keeps the S-2 younger tiles in flight, one s_barrier per tile;
 //   * LDS-DMA writes lane-linearly, so bank conflicts are avoided by XOR-swizzling the SOURCE:
 //       k-major [rows][BK]: LDS chunk = k-chunk ^ (row & 7) (BK 64) / ^ 2((row>>3)&1) (BK 32)
 //         -> conflict-free ds_read_b128 fragment reads;
 //       m-major [BK][rows]: LDS chunk = m-chunk ^ (2(r&3) ^ 8((r>>3)&1))
 //         -> conflict-free ds_read_b64_tr_b16 (no transposed copies in HBM);
-//   * persistent: gridDim.x = slots (two per CU at 72 KiB), tile t = blockIdx.x + k gridDim.x in an
-//     XCD-aware order; the second workgroup of each CU starts `stagger` cycles late;
+//   * one workgroup per tile (the grid is capped at the co-resident slots only under
+//     sv_gemm_set_workgroups_per_cu), tile t = blockIdx.x + k gridDim.x in an XCD-aware order;
 //   * one kernel per epilogue kind; bf16 epilogue operands (GELU'(h)) are fetched one slab ahead so
 //     their wait never drains the stores issued before them.
 #include "common.h"
@@ -206,15 +206,12 @@ __device__ __forceinline__ void vm_wait() {
 template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC, int CONV = 0>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
-             int tilesM, int tilesN, int nsplit, int stagger, EpiArgs e, float* __restrict__ colsum, ConvG cg) {
+             int tilesM, int tilesN, int nsplit, EpiArgs e, float* __restrict__ colsum, ConvG cg) {
   using C = Cfg<BKT, S>;
   static_assert(S >= 2 && (S - 2) * C::LOADS <= 63, "ring / vmcnt");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = tilesM * tilesN, total = nwg * nsplit;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 1, wn = wid & 1;
-  if (stagger > 0 && blockIdx.x >= gridDim.x / 2) {
-    for (int c = 0; c < stagger; c += 2048) __builtin_amdgcn_s_sleep(32);
-  }
   for (int t = blockIdx.x; t < total; t += gridDim.x) {
     // XCD-aware order: tiles t = x (mod 8) run on XCD x, each XCD walks a contiguous tile range so
     // concurrently resident tiles share A row panels in that XCD's L2
@@ -367,32 +364,22 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  e.wt = g_store_wt;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr_set = true;
   }
-  // SV_GEMM3_PERSIST=1: persistent over the resident slots (measured no faster); default one workgroup
-  // per tile, which also lets kernels of the side stream take CUs as tiles retire
-  static const int persist = getenv("SV_GEMM3_PERSIST") ? atoi(getenv("SV_GEMM3_PERSIST")) : 0;
-  static const int stag_env = getenv("SV_GEMM3_STAGGER") ? atoi(getenv("SV_GEMM3_STAGGER")) : -1;
+  // one workgroup per tile, which lets kernels of the side stream take CUs as tiles retire
   const int total = tilesM * tilesN * split;
-  int grid = total, stagger = 0;
+  int grid = total;
   if (g_gemm_wg_per_cu > 0) {  // co-residency with a concurrent GEMM (sv_gemm_set_workgroups_per_cu)
     const int slots = g_gemm_wg_per_cu * num_cus();
     grid = total > slots ? slots : total;
-  } else if (persist) {
-    const int slots = (C::TWO_PER_CU ? 2 : 1) * num_cus();
-    if (total > slots) {
-      grid = slots;
-      if (C::TWO_PER_CU) stagger = (stag_env >= 0 ? stag_env : 384) * (kper / 32);  // ~half a main loop
-    }
   }
   gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
-      tilesM, tilesN, split, stagger, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,
+      tilesM, tilesN, split, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,
       cg ? *cg : ConvG{});
   return check_launch("sv_gemm(v3)");
 }
@@ -445,13 +432,8 @@ int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg) {
   if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->a_scale_k)
     return SV_ERR_UNSUPPORTED;
   const int split = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
-  // BKxSTAGES: 32x3 (default: two workgroups per CU), 32x4, 64x2, 64x3; SV_GEMM3_CFG overrides
-  static const char* env = getenv("SV_GEMM3_CFG");
-  if (env) cfg = env;
-  if (!cfg) cfg = "32x3";
-  if (!strcmp(cfg, "32x4")) return launch_cfg<32, 4>(d, split, s);
-  if (!strcmp(cfg, "64x2")) return launch_cfg<64, 2>(d, split, s);
-  if (!strcmp(cfg, "64x3")) return launch_cfg<64, 3>(d, split, s);
+  // BKxSTAGES: 32x3 (default: two workgroups per CU) or 32x4
+  if (cfg && !strcmp(cfg, "32x4")) return launch_cfg<32, 4>(d, split, s);
   return launch_cfg<32, 3>(d, split, s);
 }
 

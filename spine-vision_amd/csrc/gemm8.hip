@@ -243,7 +243,6 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  e.wt = g_store_wt;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<AK, BKM, EPI, BKT, S, OCC>),

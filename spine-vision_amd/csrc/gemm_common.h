@@ -21,18 +21,7 @@ struct EpiArgs {
   const float* bias;
   const float* gamma;
   const void* aux; int aux_dtype; int64_t ld_aux;
-  int wt = 0;  // 1: epilogue stores write-through (sc1), see st16_wt
 };
-
-// Write-through 16-B store (global_store_dwordx4 ... sc1): the line leaves the XCD's L2 with the store
-// and is not left dirty, so the kernel-end L2 write-back (the dependent-launch boundary grows by
-// dirty bytes / ~6 TB/s, MI355X_MICROARCH.md "boundary") has nothing to flush.  Issued as inline
-// asm: hipcc has no sc1 store builtin for flat/global pointers.  vmcnt still counts it.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st16_wt(void* p, uint4 v) {
-  const u32x4_t d = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
-}
 
 __device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
   return dt == SV_F32 ? ld4(reinterpret_cast<const float*>(p), i) : ld4(reinterpret_cast<const uint16_t*>(p), i);
@@ -95,17 +84,6 @@ __device__ __forceinline__ void st8_any(void* p, int dt, size_t i, float4 a, flo
   } else {
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p) + i) =
         make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
-  }
-}
-__device__ __forceinline__ void st8_out(void* p, int dt, size_t i, float4 a, float4 b, int wt) {
-  if (!wt) return st8_any(p, dt, i, a, b);
-  if (dt == SV_F32) {
-    float* f = reinterpret_cast<float*>(p) + i;
-    st16_wt(f, make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w)));
-    st16_wt(f + 4, make_uint4(__float_as_uint(b.x), __float_as_uint(b.y), __float_as_uint(b.z), __float_as_uint(b.w)));
-  } else {
-    st16_wt(reinterpret_cast<uint16_t*>(p) + i,
-            make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w)));
   }
 }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -252,7 +230,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       if (slab_out) {
         float* C = reinterpret_cast<float*>(e.C) + (size_t)split * e.M * e.N + (size_t)m * e.N + n;
         if (okn4) {
-          st8_out(C, SV_F32, 0, va, vb, e.wt);
+          st8_any(C, SV_F32, 0, va, vb);
         } else {
           *reinterpret_cast<float4*>(C) = va;
         }
@@ -284,7 +262,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         ob = ggrad4(vb, xb[si][h]);
       }
       const size_t ci = (size_t)m * e.ldc + n;
-      if (okn4) st8_out(e.C, e.c_dtype, ci, oa, ob, e.wt);
+      if (okn4) st8_any(e.C, e.c_dtype, ci, oa, ob);
       else st4_any(e.C, e.c_dtype, ci, oa);
       if constexpr (kStats) {  // N % 8 == 0: all 8 columns valid
         const float o8[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
@@ -296,10 +274,10 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         }
       }
       if (e.epi == SV_EPI_BIAS_GELU2) {
-        if (okn4) st8_out(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb), e.wt);
+        if (okn4) st8_any(e.C2, e.c2_dtype, ci, gelu4(va), gelu4(vb));
         else st4_any(e.C2, e.c2_dtype, ci, gelu4(va));
       } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
-        if (okn4) st8_out(e.C2, e.c2_dtype, ci, va, vb, e.wt);
+        if (okn4) st8_any(e.C2, e.c2_dtype, ci, va, vb);
         else st4_any(e.C2, e.c2_dtype, ci, va);
       }
     }
@@ -385,18 +363,11 @@ inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
 // (M = pixels, N = Cout or Cs, K = taps * channels), epilogue STORE or BIAS_GAMMA_RES (accumulate)
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s);
 
-// SV_STORE_WT=1: write-through (sc1) epilogue stores in the v2/v3 GEMMs (gemm.hip reads the env once)
-extern int g_store_wt;
-
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
 int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
 // v3 entry (gemm3.hip): same contract with K % BK == 0; cfg = "BKxSTAGES" (nullptr: 32x3)
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg = nullptr);
-// v7 entry (gemm7.hip, register-staged operand loads): occ 4 = two workgroups per CU, 2 = one
-int launch_gemm7(const sv_gemm_desc* d, hipStream_t s, int occ = 2);
 // v8 entry (gemm8.hip, 256x256 tile, 8 waves, one workgroup per CU): same contract as v3
 int launch_gemm8(const sv_gemm_desc* d, hipStream_t s);
-// v6 entry (gemm6.hip, 256x256 tile, one 4-wave workgroup per CU): same contract as v2
-int launch_gemm6(const sv_gemm_desc* d, hipStream_t s);
 
 }  // namespace sv

@@ -9,7 +9,6 @@ missing library or a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -157,7 +156,7 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
                 a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16)
 
 
-_WGRAD_TARGET = int(__import__("os").environ.get("SV_WGRAD_TARGET", "512"))
+_WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
 
 
 def _wgrad_split(tiles: int, K: int) -> int:
@@ -581,9 +580,6 @@ def _ones(n: int, device: torch.device) -> torch.Tensor:
     return t
 
 
-_CONV_GEMM = os.environ.get("SV_CONV_GEMM", "1") not in ("0", "")
-
-
 def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype):
     """conv_fwd plus the train-mode BatchNorm statistics of y straight from the GEMM epilogue
     (SV_EPI_STORE_STATS: no separate read pass over y) -> (y, partials [ceil(M/64)][2][Cout] f32), or
@@ -601,7 +597,7 @@ def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dt
         gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
              ldb=s.Cs, C=y.view(M, s.Cout), C2=part, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True)
         return y, part
-    if not (_CONV_GEMM and s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0):
+    if not (s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0):
         return conv_fwd(x, wp, s, out_dtype), None
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")

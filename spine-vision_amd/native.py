@@ -60,6 +60,7 @@ _SIGS = {
     "sv_build_target": [],
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
     "sv_gemm_set_workgroups_per_cu": [_i32],
+    "sv_gemm_set_impl": [_i32],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
     "sv_layernorm_bwd_nparts": [_i64, _i32],
     "sv_layernorm_bwd": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _i64, _i32, _p],
@@ -119,7 +120,7 @@ _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
 _VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
-                                                                     "sv_gemm_set_workgroups_per_cu"}
+                                                                     "sv_gemm_set_workgroups_per_cu", "sv_gemm_set_impl"}
 
 _lib = None
 _lock = threading.Lock()

@@ -178,6 +178,9 @@ class ShardedBatchSampler(Sampler):
             yield b
 
     def __iter__(self):
+        if self.world == 1:  # accelerate does not shard (or pad) a single-process loader
+            yield from self._batches()
+            return
         bs, world, rank = self.batch_size, self.world, self.rank
         head: list = []  # indices of the first `world` batches: the padding source
         pending = None
@@ -216,7 +219,7 @@ class ShardedBatchSampler(Sampler):
 
     def __len__(self) -> int:
         nb = self.num_batches()
-        if nb % self.world == 0 or self.drop_last:
+        if self.world == 1 or nb % self.world == 0 or self.drop_last:
             return nb // self.world
         return nb // self.world + 1
 

@@ -143,6 +143,8 @@ def test_sharding_matches_accelerate(world, n, bs, drop):
     from torch.utils.data import BatchSampler, SequentialSampler
 
     lens = set()
+    one = list(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, 0, 1))
+    assert one == list(BatchSampler(SequentialSampler(range(n)), bs, drop))  # world 1: no sharding, no padding
     for r in range(world):
         ours = list(ShardedBatchSampler(SequentialSampler(range(n)), bs, drop, r, world))
         ref = list(BatchSamplerShard(BatchSampler(SequentialSampler(range(n)), bs, drop), num_processes=world,

@@ -1,7 +1,7 @@
 """Standalone timing of the depthwise-conv kernels at the ConvNeXt-base @512 bs32 stage shapes
-(HIP events).  Variants are selected by the SV_DW_* environment variables of the process.
+(HIP events).
 
-    SV_DW_IMPL=1 SV_DW_PF=4 python tools/dw_bench.py [--stages S1,S3] [--iters 20]
+    python tools/dw_bench.py [--stages S1,S3] [--iters 20]
 """
 
 import argparse
@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    tag = f"impl={os.environ.get('SV_DW_IMPL', '1')} pf={os.environ.get('SV_DW_PF', '4')}"
+    tag = "ring"
     B = args.batch
     for st in args.stages.split(","):
         S, C = STAGES[st]

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--stages", default="S1,S2,S3,S4")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cases", default="", help="comma-separated case-name substrings to run")
+    ap.add_argument("--impls", default="0", help="comma-separated sv_gemm_set_impl values, timed interleaved")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     for st in args.stages.split(","):
@@ -70,17 +71,24 @@ def main():
         for name, fl, fn in cases(M, C, dev):
             if args.cases and not any(c in name for c in args.cases.split(",")):
                 continue
-            for _ in range(3):
-                fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record()
-            for _ in range(args.iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) / args.iters * 1e3
-            print(f"{st} M={M:7d} C={C:5d} {name:18s} {us:8.1f} us  {fl / us / 1e6:7.1f} TFLOP/s", flush=True)
+            impls = [int(x) for x in args.impls.split(",")] if not name.startswith("torch") else [0]
+            res = {i: [] for i in impls}
+            for rnd in range(2):
+                for impl in impls:
+                    nv.value("sv_gemm_set_impl", impl)
+                    for _ in range(3):
+                        fn()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record()
+                    for _ in range(args.iters):
+                        fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    res[impl].append(e0.elapsed_time(e1) / args.iters * 1e3)
+            nv.value("sv_gemm_set_impl", 0)
+            line = " | ".join(f"impl{i} {min(v):7.1f} us {fl / min(v) / 1e6:7.1f} TF" for i, v in res.items())
+            print(f"{st} M={M:7d} C={C:5d} {name:18s} {line}", flush=True)
 
 
 if __name__ == "__main__":
