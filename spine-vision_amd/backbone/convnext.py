@@ -309,7 +309,9 @@ class ConvNeXtHip(nn.Module):
         # block GEMMs of the two streams: one persistent workgroup per CU each, so they share every CU
         prev_res = nv.value("sv_gemm_set_workgroups_per_cu", self.side_wg_per_cu if side is not None else 0)
         lean = side is not None and bf and self.lean_sync
-        keep: list = []  # lean mode: side-stream operands, released once main has joined the side stream
+        # lean mode: per block (side-stream event, the operands the side stream reads), oldest first;
+        # released in batches once the side stream has passed them (_release_side)
+        pending: list = []
         # d: f32 gradient stream (residual accumulation); db: its bf16 copy, the GEMM operand (bf16 mode)
         d, db = K.pool_ln_bwd(dfeat.float(), *tape.pool, hn.weight, tape.out_shape, dlnw=g(hn.weight),
                               dlnb=g(hn.bias), with_bf16=bf)
@@ -317,7 +319,11 @@ class ConvNeXtHip(nn.Module):
             main.wait_event(tape.w2g_ready)
         self._ready([hn.weight, hn.bias])
         for st, (ds_saved, blocks_saved) in zip(reversed(list(self.stages)), reversed(tape.stages)):
-            for blk, saved in zip(reversed(list(st.blocks)), reversed(blocks_saved)):
+            for bi in range(len(blocks_saved) - 1, -1, -1):
+                blk, saved = st.blocks[bi], blocks_saved[bi]
+                # the tape lets go of the block: its main-stream reads are stream-ordered before any
+                # later main-stream allocation, its side-stream reads stay referenced below
+                blocks_saved[bi] = None
                 x, z, y, mean, rstd, gh, a = saved
                 B, H, W, C = x.shape
                 M = B * H * W
@@ -325,7 +331,8 @@ class ConvNeXtHip(nn.Module):
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 dsrc = db.view(M, C) if bf else d2
                 if lean:
-                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, keep)
+                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending)
+                    self._release_side(main, pending)
                     continue
                 # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
                 # stream beside the data-gradient chain of the main stream: the wgrads are MFMA-bound
@@ -421,11 +428,26 @@ class ConvNeXtHip(nn.Module):
         nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
-            keep.clear()  # safe: later main-stream allocations are ordered after the join
+            pending.clear()  # safe: later main-stream allocations are ordered after the join
         self._ready([conv.weight, conv.bias, ln.weight, ln.bias])
 
 
-    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, keep):
+    # lean mode keeps at most 2 x _RELEASE_BATCH blocks of side-stream operands (dh alone is M x 4C
+    # bf16) instead of every block's until the backward ends; one main->side wait per batch
+    _RELEASE_BATCH = 4
+
+    @classmethod
+    def _release_side(cls, main, pending: list) -> None:
+        """Drop the side-stream operands of the oldest blocks: free ones whose event has completed,
+        and once 2 x _RELEASE_BATCH blocks are pending, make main wait for the side stream to pass
+        the oldest batch (cheap: the side stream runs about one block behind) and drop that batch."""
+        while pending and pending[0][0].query():
+            pending.pop(0)
+        if len(pending) >= 2 * cls._RELEASE_BATCH:
+            main.wait_event(pending[cls._RELEASE_BATCH - 1][0])
+            del pending[:cls._RELEASE_BATCH]
+
+    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, pending):
         """bf16 block backward with one main->side hand-off.  Main: fc2 dgrad (x GELU'), fc1 dgrad,
         LayerNorm backward, depthwise backward-data.  Side, after the LayerNorm backward: fc2 wgrad
         (+ gamma, bias), fc1 wgrad (+ bias), the LayerNorm weight/bias fold and the depthwise wgrad of
@@ -446,7 +468,6 @@ class ConvNeXtHip(nn.Module):
                                         db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
-        keep.extend((dsrc, dh, dz, ln_finish))
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
@@ -457,6 +478,7 @@ class ConvNeXtHip(nn.Module):
             K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
             self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias, blk.mlp.fc1.weight,
                          blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
+            pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a)))
         # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
         db = torch.empty_like(db)
         K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)

@@ -21,7 +21,8 @@ class FlatAdamW(torch.optim.Optimizer):
     def __init__(self, arena: FlatArena, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2) -> None:
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
-                        foreach=None, capturable=False, differentiable=False, fused=None)
+                        foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled_weight_decay=True)  # torch.optim.AdamW's param-group keys
         super().__init__(arena.params, defaults)
         self.arena = arena
         self.exp_avg = torch.zeros_like(arena.param_flat)
