@@ -95,11 +95,21 @@ int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
  * that GEMMs issued concurrently on two streams (data gradients + weight gradients) are co-resident
  * on every CU instead of the first one filling the chip.  Returns the previous value.               */
 int sv_gemm_set_workgroups_per_cu(int32_t n);
+/* Wave priority of the v3 GEMMs launched after this call (host-side, process-wide): 1 = their waves
+ * run at raised s_setprio, so a critical-path GEMM sharing CUs with a concurrent stream's kernels
+ * issues first; 0 (default) = normal.  Returns the previous value.                                  */
+int sv_gemm_set_priority(int32_t p);
 /* Kernel family for the bf16 GEMMs launched after this call (host-side, process-wide, initially 0):
  * 0 = the measured per-shape dispatch, 2 / 3 / 8 = force that family where its contract holds
  * (tests/test_gemm_family_gpu.py compares the families bit for bit; tools/gemm_bench.py times them).
  * Returns the previous value.                                                                      */
 int sv_gemm_set_impl(int32_t impl);
+/* Finish of a split-K GEMM (SV_EPI_SLAB): C[m, n] = (accumulate ? C[m, n] : 0) + sum_s slab[s][m][n],
+ * slices summed in order (deterministic); c_dtype f32 or bf16 (accumulate: f32 only).  stats != NULL
+ * (bf16 C): also the SV_EPI_STORE_STATS partials [ceil(M/64)][2][N] of the values as stored.
+ * N, ldc multiples of 4; slab, C, stats 16-byte aligned.                                          */
+int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, void* C, int32_t c_dtype, int64_t ldc,
+                        int32_t accumulate, float* stats, sv_stream_t stream);
 
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.
@@ -302,6 +312,15 @@ int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mean, const fl
  * shapes return SV_ERR_UNSUPPORTED (use sv_conv_fwd + sv_bn_stats).                                */
 int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
                       float* stats, sv_stream_t stream);
+/* Split-K forms for grids smaller than the chip (the deep ResNet stages: few 256x128 output tiles,
+ * long K = taps x channels): the gathered GEMM writes `split` f32 slabs [split][M][N] into `work`
+ * (split * M * N floats), then sv_gemm_slab_finish sums them into y (+ the STORE_STATS partials when
+ * stats != NULL) / into dx (+= when accumulate, f32 dx).  bf16 gathered-operand shapes only (as
+ * sv_conv_fwd_stats; dgrad: stride 1, Cout >= 32); others are an error.                             */
+int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
+                      float* stats, float* work, int32_t split, sv_stream_t stream);
+int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                           int32_t dtype, const sv_conv_shape* s, float* work, int32_t split, sv_stream_t stream);
 /* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
 int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                      int32_t Cs, sv_stream_t stream);
@@ -338,6 +357,15 @@ int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, 
 int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                     int32_t y_dtype, const float* mean, const float* rstd, const float* gamma, const float* sums,
                     void* dx, int32_t dx_dtype, float* gmask, int64_t rows, int32_t C, sv_stream_t stream);
+/* The same backward for a BN followed by its own ReLU (no residual): the mask is recomputed from y
+ * exactly as sv_bn_act_fwd computes the pre-activation, fmaf(gamma rstd, y - mean, beta) > 0, so
+ * the activation tensor is not read again (one 2-byte stream less per element in both passes).    */
+int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, int64_t rows, int32_t C,
+                         float* part, sv_stream_t stream);
+int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, const float* sums, void* dx,
+                         int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
 /* g = dout * (act > 0), f32 out (block-output ReLU of the residual join).                         */
 int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g, int64_t n,
                  sv_stream_t stream);

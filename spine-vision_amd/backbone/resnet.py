@@ -290,7 +290,8 @@ class ResNetHip(nn.Module):
             pconv, pbn, _, _, _, _ = convs[ci - 1]
             _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
             Cp = py.shape[-1]
-            dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, act=pa.view(-1, Cp),
+            # the inner BN's own ReLU: mask recomputed from y (the activation pa is not read again)
+            dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, relu_beta=pbn.bias.detach(),
                           dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act)
             params += [pbn.weight, pbn.bias]
         # dy is now the gradient at conv1's output; conv1's input is x_in
@@ -321,7 +322,7 @@ class ResNetHip(nn.Module):
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
         da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
-        dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, act=a0.view(-1, C),
+        dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
                        dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act)
         K.conv_bwd_weight(dy0.view(y0.shape), x0, s0, dw=g(self.conv1.weight), accumulate=True)
         self._ready([self.conv1.weight, self.bn1.weight, self.bn1.bias])

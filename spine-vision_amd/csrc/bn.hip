@@ -31,14 +31,64 @@ __device__ __forceinline__ void st4d(void* p, int dt, size_t i, float4 v) {
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
 __device__ __forceinline__ float4 ld4f(const float* p, int c) { return *reinterpret_cast<const float4*>(p + c); }
 
-// Block layout for per-channel reductions: tpr threads cover one row (4 channels each), rp rows in
-// parallel; grid.x = channel slices of 4*tpr channels, grid.y = row parts.
+// V consecutive channels per thread: 8 (one 16-B bf16 access, two 16-B f32 accesses) when C % 8 == 0,
+// else 4.  Per-channel parameters are read as float4s from L1/L2.
+template <int V>
+__device__ __forceinline__ void ldv(const void* p, int dt, size_t i, float (&o)[V]) {
+  if constexpr (V == 8) {
+    if (dt == SV_F32) {
+      const float* f = reinterpret_cast<const float*>(p) + i;
+      const float4 a = *reinterpret_cast<const float4*>(f), b = *reinterpret_cast<const float4*>(f + 4);
+      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+    } else {
+      const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(p) + i);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] = __uint_as_float(w[k] << 16);
+        o[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      }
+    }
+  } else {
+    const float4 a = ld4d(p, dt, i);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  }
+}
+template <int V>
+__device__ __forceinline__ void stv(void* p, int dt, size_t i, const float (&v)[V]) {
+  if constexpr (V == 8) {
+    if (dt == SV_F32) {
+      float* f = reinterpret_cast<float*>(p) + i;
+      *reinterpret_cast<float4*>(f) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(f + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p) + i) =
+          make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    }
+  } else {
+    st4d(p, dt, i, make_float4(v[0], v[1], v[2], v[3]));
+  }
+}
+template <int V>
+__device__ __forceinline__ void ldp(const float* p, int c, float (&o)[V]) {
+#pragma unroll
+  for (int k = 0; k < V; k += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p + c + k);
+    o[k] = a.x; o[k + 1] = a.y; o[k + 2] = a.z; o[k + 3] = a.w;
+  }
+}
+
+static int vec_for(int C) { return (C % 8 == 0 && ((C / 8) <= kThreads || (C / 8) % kThreads == 0)) ? 8 : 4; }
+
+// Block layout for per-channel reductions: tpr threads cover one row (V channels each), rp rows in
+// parallel; grid.x = channel slices of V*tpr channels, grid.y = row parts.
 struct RedGeo {
-  int tpr, rp, cslices;
+  int vec, tpr, rp, cslices;
 };
 static RedGeo red_geo(int C) {
-  const int cg = C / 4;
   RedGeo g;
+  g.vec = vec_for(C);
+  const int cg = C / g.vec;
   g.tpr = cg < kThreads ? cg : kThreads;
   g.rp = kThreads / g.tpr;
   g.cslices = cg / g.tpr;
@@ -54,43 +104,58 @@ static int nparts_for(int64_t rows, int C) {
   return (int)p;
 }
 
-// block-level reduce of two float4 per thread over the rp row-groups; writes part[p][0|1][c..c+3]
-__device__ __forceinline__ void reduce_write(float4 s1, float4 s2, int tpr, int rp, int c, int C, float* part) {
-  __shared__ float4 red[2][kThreads];
+// block-level reduce of two V-vectors per thread over the rp row-groups; writes part[p][0|1][c..c+V-1]
+template <int V>
+__device__ __forceinline__ void reduce_write(float (&s1)[V], float (&s2)[V], int tpr, int rp, int c, int C, float* part) {
+  __shared__ float red[2][V][kThreads];
   const int t = threadIdx.x;
-  red[0][t] = s1;
-  red[1][t] = s2;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    red[0][k][t] = s1[k];
+    red[1][k][t] = s2[k];
+  }
   __syncthreads();
   if (t < tpr) {
-    for (int r = 1; r < rp; ++r) {
-      const float4 a = red[0][r * tpr + t], b = red[1][r * tpr + t];
-      s1.x += a.x; s1.y += a.y; s1.z += a.z; s1.w += a.w;
-      s2.x += b.x; s2.y += b.y; s2.z += b.z; s2.w += b.w;
-    }
+    for (int r = 1; r < rp; ++r)
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        s1[k] += red[0][k][r * tpr + t];
+        s2[k] += red[1][k][r * tpr + t];
+      }
     float* o = part + (size_t)blockIdx.y * 2 * C;
-    *reinterpret_cast<float4*>(o + c) = s1;
-    *reinterpret_cast<float4*>(o + C + c) = s2;
+#pragma unroll
+    for (int k = 0; k < V; k += 4) {
+      *reinterpret_cast<float4*>(o + c + k) = make_float4(s1[k], s1[k + 1], s1[k + 2], s1[k + 3]);
+      *reinterpret_cast<float4*>(o + C + c + k) = make_float4(s2[k], s2[k + 1], s2[k + 2], s2[k + 3]);
+    }
   }
 }
 
 // forward statistics: shifted sums S1 = sum (y - y0), S2 = sum (y - y0)^2
+template <int V>
 __global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict__ y, int ydt, int64_t rows, int C,
                                                          int tpr, int rp, int64_t rpp, float* __restrict__ part) {
   const int t = threadIdx.x;
-  const int c = (blockIdx.x * tpr + t % tpr) * 4;
+  const int c = (blockIdx.x * tpr + t % tpr) * V;
   const int rsub = t / tpr;
-  const float4 k = ld4d(y, ydt, (size_t)c);
-  float4 s1 = f4(0.f), s2 = f4(0.f);
+  float k[V], s1[V], s2[V];
+  ldv<V>(y, ydt, (size_t)c, k);
+#pragma unroll
+  for (int q = 0; q < V; ++q) s1[q] = s2[q] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.y * rpp;
   int64_t r1 = r0 + rpp;
   if (r1 > rows) r1 = rows;
   for (int64_t r = r0 + rsub; r < r1; r += rp) {
-    const float4 v = ld4d(y, ydt, (size_t)r * C + c);
-    const float dx = v.x - k.x, dy = v.y - k.y, dz = v.z - k.z, dw = v.w - k.w;
-    s1.x += dx; s1.y += dy; s1.z += dz; s1.w += dw;
-    s2.x = fmaf(dx, dx, s2.x); s2.y = fmaf(dy, dy, s2.y); s2.z = fmaf(dz, dz, s2.z); s2.w = fmaf(dw, dw, s2.w);
+    float v[V];
+    ldv<V>(y, ydt, (size_t)r * C + c, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const float dv = v[q] - k[q];
+      s1[q] += dv;
+      s2[q] = fmaf(dv, dv, s2[q]);
+    }
   }
-  reduce_write(s1, s2, tpr, rp, c, C, part);
+  reduce_write<V>(s1, s2, tpr, rp, c, C, part);
 }
 
 // Sum of the per-block partials [P][2][C] for 64 channels per workgroup: the 16 waves of the
@@ -171,28 +236,40 @@ struct ActArgs {
   int64_t rows; int C;
 };
 
+template <int V>
 __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
-  const int64_t n4 = a.rows * a.C / 4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const size_t e = (size_t)i * 4;
+  const int64_t nv = a.rows * a.C / V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t e = (size_t)i * V;
     const int c = (int)(e % a.C);
-    const float4 v = ld4d(a.y, a.ydt, e);
-    const float4 mu = ld4f(a.mean, c), rs = ld4f(a.rstd, c), g = ld4f(a.gamma, c), b = ld4f(a.beta, c);
-    float4 o = make_float4(fmaf(g.x * rs.x, v.x - mu.x, b.x), fmaf(g.y * rs.y, v.y - mu.y, b.y),
-                           fmaf(g.z * rs.z, v.z - mu.z, b.z), fmaf(g.w * rs.w, v.w - mu.w, b.w));
+    float v[V], mu[V], rs[V], g[V], b[V], o[V];
+    ldv<V>(a.y, a.ydt, e, v);
+    ldp<V>(a.mean, c, mu);
+    ldp<V>(a.rstd, c, rs);
+    ldp<V>(a.gamma, c, g);
+    ldp<V>(a.beta, c, b);
+#pragma unroll
+    for (int q = 0; q < V; ++q) o[q] = fmaf(g[q] * rs[q], v[q] - mu[q], b[q]);
     if (a.res) {
-      float4 r = ld4d(a.res, a.rdt, e);
+      float r[V];
+      ldv<V>(a.res, a.rdt, e, r);
       if (a.rmean) {
-        const float4 rm = ld4f(a.rmean, c), rr = ld4f(a.rrstd, c), rg = ld4f(a.rgamma, c), rb = ld4f(a.rbeta, c);
-        r = make_float4(fmaf(rg.x * rr.x, r.x - rm.x, rb.x), fmaf(rg.y * rr.y, r.y - rm.y, rb.y),
-                        fmaf(rg.z * rr.z, r.z - rm.z, rb.z), fmaf(rg.w * rr.w, r.w - rm.w, rb.w));
+        float rm[V], rr[V], rg[V], rb[V];
+        ldp<V>(a.rmean, c, rm);
+        ldp<V>(a.rrstd, c, rr);
+        ldp<V>(a.rgamma, c, rg);
+        ldp<V>(a.rbeta, c, rb);
+#pragma unroll
+        for (int q = 0; q < V; ++q) r[q] = fmaf(rg[q] * rr[q], r[q] - rm[q], rb[q]);
       }
-      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+#pragma unroll
+      for (int q = 0; q < V; ++q) o[q] += r[q];
     }
     if (a.relu) {
-      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+#pragma unroll
+      for (int q = 0; q < V; ++q) o[q] = fmaxf(o[q], 0.f);
     }
-    st4d(a.out, a.odt, e, o);
+    stv<V>(a.out, a.odt, e, o);
   }
 }
 
@@ -207,32 +284,62 @@ __device__ __forceinline__ float4 masked(float4 g, const void* act, int adt, siz
   return g;
 }
 
-// backward statistics: sum g and sum g * xhat, g = dout * (act > 0)
+// g = dout * mask: mask = (act > 0), or (RELU_Y) recomputed from y as act_kernel computes the
+// pre-activation -- fmaf(gamma rstd, y - mean, beta) > 0 -- so the activation is not read again
+template <int V, bool RELU_Y>
+__device__ __forceinline__ void grad_masked(const void* dout, int ddt, const void* act, int adt, size_t e,
+                                            const float (&v)[V], const float (&mu)[V], const float (&rs)[V],
+                                            const float* gamma, const float* beta, int c, float (&g)[V]) {
+  ldv<V>(dout, ddt, e, g);
+  if constexpr (RELU_Y) {
+    float ga[V], be[V];
+    ldp<V>(gamma, c, ga);
+    ldp<V>(beta, c, be);
+#pragma unroll
+    for (int q = 0; q < V; ++q) g[q] = fmaf(ga[q] * rs[q], v[q] - mu[q], be[q]) > 0.f ? g[q] : 0.f;
+  } else {
+    if (act) {
+      float m[V];
+      ldv<V>(act, adt, e, m);
+#pragma unroll
+      for (int q = 0; q < V; ++q) g[q] = m[q] > 0.f ? g[q] : 0.f;
+    }
+  }
+}
+
+// backward statistics: sum g and sum g * xhat
+template <int V, bool RELU_Y>
 __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restrict__ dout, int ddt,
                                                              const void* __restrict__ act, int adt,
                                                              const void* __restrict__ y, int ydt,
                                                              const float* __restrict__ mean,
-                                                             const float* __restrict__ rstd, int64_t rows, int C,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int64_t rows, int C,
                                                              int tpr, int rp, int64_t rpp, float* __restrict__ part) {
   const int t = threadIdx.x;
-  const int c = (blockIdx.x * tpr + t % tpr) * 4;
+  const int c = (blockIdx.x * tpr + t % tpr) * V;
   const int rsub = t / tpr;
-  const float4 mu = ld4f(mean, c), rs = ld4f(rstd, c);
-  float4 s1 = f4(0.f), s2 = f4(0.f);
+  float mu[V], rs[V], s1[V], s2[V];
+  ldp<V>(mean, c, mu);
+  ldp<V>(rstd, c, rs);
+#pragma unroll
+  for (int q = 0; q < V; ++q) s1[q] = s2[q] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.y * rpp;
   int64_t r1 = r0 + rpp;
   if (r1 > rows) r1 = rows;
   for (int64_t r = r0 + rsub; r < r1; r += rp) {
     const size_t e = (size_t)r * C + c;
-    const float4 g = masked(ld4d(dout, ddt, e), act, adt, e);
-    const float4 v = ld4d(y, ydt, e);
-    s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
-    s2.x = fmaf(g.x, (v.x - mu.x) * rs.x, s2.x);
-    s2.y = fmaf(g.y, (v.y - mu.y) * rs.y, s2.y);
-    s2.z = fmaf(g.z, (v.z - mu.z) * rs.z, s2.z);
-    s2.w = fmaf(g.w, (v.w - mu.w) * rs.w, s2.w);
+    float v[V], g[V];
+    ldv<V>(y, ydt, e, v);
+    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s1[q] += g[q];
+      s2[q] = fmaf(g[q], (v[q] - mu[q]) * rs[q], s2[q]);
+    }
   }
-  reduce_write(s1, s2, tpr, rp, c, C, part);
+  reduce_write<V>(s1, s2, tpr, rp, c, C, part);
 }
 
 __global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float* __restrict__ part, int P, int C,
@@ -252,29 +359,32 @@ struct BwdArgs {
   const void* dout; int ddt;
   const void* act; int adt;
   const void* y; int ydt;
-  const float *mean, *rstd, *gamma, *sums;
+  const float *mean, *rstd, *gamma, *beta, *sums;
   void* dx; int xdt;
   float* gmask;
   int64_t rows; int C;
 };
 
+template <int V, bool RELU_Y>
 __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
-  const int64_t n4 = a.rows * a.C / 4;
+  const int64_t nv = a.rows * a.C / V;
   const float inv_n = 1.0f / (float)a.rows;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const size_t e = (size_t)i * 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t e = (size_t)i * V;
     const int c = (int)(e % a.C);
-    const float4 g = masked(ld4d(a.dout, a.ddt, e), a.act, a.adt, e);
-    const float4 v = ld4d(a.y, a.ydt, e);
-    const float4 mu = ld4f(a.mean, c), rs = ld4f(a.rstd, c), ga = ld4f(a.gamma, c);
-    const float4 sg = ld4f(a.sums, c), sgx = ld4f(a.sums + a.C, c);
-    float4 o;
-    o.x = ga.x * rs.x * (g.x - sg.x * inv_n - (v.x - mu.x) * rs.x * sgx.x * inv_n);
-    o.y = ga.y * rs.y * (g.y - sg.y * inv_n - (v.y - mu.y) * rs.y * sgx.y * inv_n);
-    o.z = ga.z * rs.z * (g.z - sg.z * inv_n - (v.z - mu.z) * rs.z * sgx.z * inv_n);
-    o.w = ga.w * rs.w * (g.w - sg.w * inv_n - (v.w - mu.w) * rs.w * sgx.w * inv_n);
-    st4d(a.dx, a.xdt, e, o);
-    if (a.gmask) *reinterpret_cast<float4*>(a.gmask + e) = g;
+    float v[V], mu[V], rs[V], ga[V], sg[V], sgx[V], g[V], o[V];
+    ldv<V>(a.y, a.ydt, e, v);
+    ldp<V>(a.mean, c, mu);
+    ldp<V>(a.rstd, c, rs);
+    grad_masked<V, RELU_Y>(a.dout, a.ddt, a.act, a.adt, e, v, mu, rs, a.gamma, a.beta, c, g);
+    ldp<V>(a.gamma, c, ga);
+    ldp<V>(a.sums, c, sg);
+    ldp<V>(a.sums + a.C, c, sgx);
+#pragma unroll
+    for (int q = 0; q < V; ++q)
+      o[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (v[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+    stv<V>(a.dx, a.xdt, e, o);
+    if (a.gmask) stv<V>(a.gmask, SV_F32, e, g);
   }
 }
 
@@ -413,7 +523,10 @@ extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t
   const RedGeo g = red_geo(C);
   const int P = nparts_for(rows, C);
   const int64_t rpp = (rows + P - 1) / P;
-  stats_kernel<<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(y, y_dtype, rows, C, g.tpr, g.rp, rpp, part);
+  if (g.vec == 8)
+    stats_kernel<8><<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(y, y_dtype, rows, C, g.tpr, g.rp, rpp, part);
+  else
+    stats_kernel<4><<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(y, y_dtype, rows, C, g.tpr, g.rp, rpp, part);
   return check_launch("sv_bn_stats");
 }
 
@@ -446,8 +559,31 @@ extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, 
   SV_REQUIRE(!res_mean || (res && res_rstd && res_gamma && res_beta), "sv_bn_act_fwd: incomplete residual BN");
   ActArgs a{y, y_dtype, mean, rstd, gamma, beta, res, res_dtype, res_mean, res_rstd, res_gamma, res_beta,
             relu, out, out_dtype, rows, C};
-  act_kernel<<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
+  if (vec_for(C) == 8)
+    act_kernel<8><<<grid_for(rows * C / 8), kThreads, 0, (hipStream_t)stream>>>(a);
+  else
+    act_kernel<4><<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
   return check_launch("sv_bn_act_fwd");
+}
+
+static int bwd_stats_launch(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                            int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                            const float* beta, int64_t rows, int32_t C, float* part, sv_stream_t stream) {
+  const RedGeo g = red_geo(C);
+  const int P = nparts_for(rows, C);
+  const int64_t rpp = (rows + P - 1) / P;
+  const dim3 grid(g.cslices, P);
+  hipStream_t st = (hipStream_t)stream;
+#define BWDS(VV, RY)                                                                                              \
+  bwd_stats_kernel<VV, RY><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, \
+                                                      beta, rows, C, g.tpr, g.rp, rpp, part)
+  if (beta) {
+    if (g.vec == 8) BWDS(8, true); else BWDS(4, true);
+  } else {
+    if (g.vec == 8) BWDS(8, false); else BWDS(4, false);
+  }
+#undef BWDS
+  return check_launch("sv_bn_bwd_stats");
 }
 
 extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
@@ -457,13 +593,18 @@ extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void*
   SV_REQUIRE(dout && y && mean && rstd && part && rows > 0 && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
                  (!act || dt_ok(act_dtype)),
              "sv_bn_bwd_stats: bad arguments");
-  const RedGeo g = red_geo(C);
-  const int P = nparts_for(rows, C);
-  const int64_t rpp = (rows + P - 1) / P;
-  bwd_stats_kernel<<<dim3(g.cslices, P), kThreads, 0, (hipStream_t)stream>>>(dout, dout_dtype, act, act_dtype, y,
-                                                                            y_dtype, mean, rstd, rows, C, g.tpr, g.rp,
-                                                                            rpp, part);
-  return check_launch("sv_bn_bwd_stats");
+  return bwd_stats_launch(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, nullptr, nullptr, rows, C, part,
+                          stream);
+}
+
+extern "C" int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype,
+                                    const float* mean, const float* rstd, const float* gamma, const float* beta,
+                                    int64_t rows, int32_t C, float* part, sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_relu_bwd_stats");
+  SV_REQUIRE(dout && y && mean && rstd && gamma && beta && part && rows > 0 && dt_ok(dout_dtype) && dt_ok(y_dtype),
+             "sv_bn_relu_bwd_stats: bad arguments");
+  return bwd_stats_launch(dout, dout_dtype, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, rows, C, part,
+                          stream);
 }
 
 extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
@@ -471,6 +612,20 @@ extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, fl
   SV_REQUIRE(part && sums && nparts > 0 && C > 0, "sv_bn_bwd_finish: bad arguments");
   bwd_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
   return check_launch("sv_bn_bwd_finish");
+}
+
+static int bwd_apply_launch(const BwdArgs& a, sv_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const bool v8 = vec_for(a.C) == 8;
+  const int grid = grid_for(a.rows * a.C / (v8 ? 8 : 4));
+  if (a.beta) {
+    if (v8) bwd_apply_kernel<8, true><<<grid, kThreads, 0, st>>>(a);
+    else bwd_apply_kernel<4, true><<<grid, kThreads, 0, st>>>(a);
+  } else {
+    if (v8) bwd_apply_kernel<8, false><<<grid, kThreads, 0, st>>>(a);
+    else bwd_apply_kernel<4, false><<<grid, kThreads, 0, st>>>(a);
+  }
+  return check_launch("sv_bn_bwd_apply");
 }
 
 extern "C" int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
@@ -481,9 +636,22 @@ extern "C" int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void*
   SV_REQUIRE(dout && y && mean && rstd && gamma && sums && dx && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
                  dt_ok(dx_dtype) && (!act || dt_ok(act_dtype)),
              "sv_bn_bwd_apply: bad arguments");
-  BwdArgs a{dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, sums, dx, dx_dtype, gmask, rows, C};
-  bwd_apply_kernel<<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
-  return check_launch("sv_bn_bwd_apply");
+  BwdArgs a{dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, nullptr, sums, dx, dx_dtype, gmask,
+            rows, C};
+  return bwd_apply_launch(a, stream);
+}
+
+extern "C" int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype,
+                                    const float* mean, const float* rstd, const float* gamma, const float* beta,
+                                    const float* sums, void* dx, int32_t dx_dtype, int64_t rows, int32_t C,
+                                    sv_stream_t stream) {
+  SV_REQUIRE(C % 4 == 0 && C > 0 && rows > 0, "sv_bn_relu_bwd_apply: C must be a multiple of 4");
+  SV_REQUIRE(dout && y && mean && rstd && gamma && beta && sums && dx && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
+                 dt_ok(dx_dtype),
+             "sv_bn_relu_bwd_apply: bad arguments");
+  BwdArgs a{dout, dout_dtype, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, sums, dx, dx_dtype, nullptr,
+            rows, C};
+  return bwd_apply_launch(a, stream);
 }
 
 extern "C" int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g,

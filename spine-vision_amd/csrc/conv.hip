@@ -620,7 +620,8 @@ extern "C" int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mea
 }
 
 static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                         const sv_conv_shape* s, float* stats, sv_stream_t stream) {
+                         const sv_conv_shape* s, float* stats, sv_stream_t stream, float* slab = nullptr,
+                         int split = 1) {
   if (int rc = check_shape(s, dtype, "sv_conv_fwd")) return rc;
   SV_REQUIRE(x && wp && y, "sv_conv_fwd: null pointer");
   SV_REQUIRE(y_dtype == SV_BF16 || y_dtype == SV_F32, "sv_conv_fwd: bad y dtype");
@@ -654,6 +655,15 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
       g.tdx[j] = a.tdx[j];
     }
     sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype);
+    if (slab) {
+      d.epilogue = SV_EPI_SLAB;
+      d.C = slab;
+      d.c_dtype = SV_F32;
+      d.split_k = split;
+      const int rc = launch_gemm3_conv(&d, g, 1, (hipStream_t)stream);
+      if (rc) return rc;
+      return sv_gemm_slab_finish(slab, split, a.M, a.N, y, y_dtype, a.N, 0, stats, stream);
+    }
     if (stats) {
       SV_REQUIRE(a.N % 8 == 0 && ((uintptr_t)stats & 15) == 0, "sv_conv_fwd_stats: Cout %% 8 / stats alignment");
       d.epilogue = SV_EPI_STORE_STATS;
@@ -664,6 +674,7 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   SV_REQUIRE(!stats, "sv_conv_fwd_stats: shape not on the gathered bf16 GEMM path (use sv_conv_fwd + sv_bn_stats)");
+  SV_REQUIRE(!slab, "sv_conv_fwd_split: shape not on the gathered bf16 GEMM path");
   return launch_dt<FPROP>(a, dtype, 1, (hipStream_t)stream);
 }
 
@@ -678,8 +689,14 @@ extern "C" int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t
   return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream);
 }
 
-extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                                int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
+extern "C" int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
+                                 const sv_conv_shape* s, float* stats, float* work, int32_t split, sv_stream_t stream) {
+  SV_REQUIRE(work && split >= 1, "sv_conv_fwd_split: need a workspace and split >= 1");
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream, work, split);
+}
+
+static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                              int32_t dtype, const sv_conv_shape* s, sv_stream_t stream, float* slab, int split) {
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_data")) return rc;
   SV_REQUIRE(dy && wp && dx, "sv_conv_bwd_data: null pointer");
   SV_REQUIRE(dx_dtype == SV_BF16 || dx_dtype == SV_F32, "sv_conv_bwd_data: bad dx dtype");
@@ -701,6 +718,15 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
         g.twt[kh * s->KW + kw] = (uint8_t)(kh * s->KW + kw);
       }
     sv_gemm_desc d = conv_desc(dy, wp, s->B * s->H * s->W, s->Cs, T_ * s->Cout, 0, (int64_t)T_ * s->Cs, dx, dx_dtype);
+    if (slab) {
+      d.epilogue = SV_EPI_SLAB;
+      d.C = slab;
+      d.c_dtype = SV_F32;
+      d.split_k = split;
+      const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
+      if (rc) return rc;
+      return sv_gemm_slab_finish(slab, split, d.M, d.N, dx, dx_dtype, s->Cs, accumulate, nullptr, stream);
+    }
     if (accumulate) {  // dx += conv^T(dy): residual epilogue with gamma = 1 reading dx in place
       d.epilogue = SV_EPI_BIAS_GAMMA_RES;
       d.aux = dx;
@@ -710,6 +736,7 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
     const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
+  SV_REQUIRE(!slab, "sv_conv_bwd_data_split: shape not on the gathered bf16 GEMM path (stride 1, Cout >= 32)");
   for (int py = 0; py < st; ++py)
     for (int px = 0; px < st; ++px) {
       Args a{};
@@ -754,6 +781,18 @@ extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_
       if (int rc = launch_dt<DGRAD>(a, dtype, 1, (hipStream_t)stream)) return rc;
     }
   return SV_OK;
+}
+
+extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                                int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
+  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, nullptr, 1);
+}
+
+extern "C" int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
+                                      int32_t dtype, const sv_conv_shape* s, float* work, int32_t split,
+                                      sv_stream_t stream) {
+  SV_REQUIRE(work && split >= 1, "sv_conv_bwd_data_split: need a workspace and split >= 1");
+  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, work, split);
 }
 
 // split-K depth of the v3 gather wgrad: ~512 workgroups over its 256x128 tiles, >= 512 pixels per slice

@@ -294,6 +294,7 @@ using namespace sv;
 
 namespace sv {
 int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
+int g_gemm_prio = 0;       // sv_gemm_set_priority
 }
 
 static int g_gemm_impl = 0;  // sv_gemm_set_impl: 0 = measured per-shape dispatch, 2/3/8 = force a family
@@ -301,6 +302,12 @@ static int g_gemm_impl = 0;  // sv_gemm_set_impl: 0 = measured per-shape dispatc
 extern "C" int sv_gemm_set_impl(int32_t impl) {
   const int prev = g_gemm_impl;
   g_gemm_impl = impl;
+  return prev;
+}
+
+extern "C" int sv_gemm_set_priority(int32_t p) {
+  const int prev = g_gemm_prio;
+  g_gemm_prio = p ? 1 : 0;
   return prev;
 }
 
@@ -382,4 +389,88 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (a32 && !b32) return launch_layout<true, float, uint16_t>(d, s);
   if (!a32 && b32) return launch_layout<true, uint16_t, float>(d, s);
   return launch_layout<true, float, float>(d, s);
+}
+
+// ---- split-K finish ------------------------------------------------------------------------------
+// C = (accumulate ? C : 0) + sum_s slab[s] over the f32 slabs of a split-K GEMM (SV_EPI_SLAB), slices
+// summed in order s = 0, 1, ... (deterministic), and optionally the SV_EPI_STORE_STATS partials of
+// the stored values.  Block = 256 threads over a 64-row x 64-column tile: thread (ph, q) owns columns
+// n0 + 4q .. +3 of rows m0 + ph + 16 i, i < 4 (16-B slab reads; every slab load of a thread is
+// independent, so the split slices stream in parallel); the 16 row phases are folded through LDS into
+// the 64-row group's statistics row.  Small grids are the point of split-K, so the tile is small.
+namespace sv {
+namespace {
+constexpr int SF_THREADS = 256;
+__global__ void __launch_bounds__(SF_THREADS) slab_finish_kernel(const float* __restrict__ slab, int split, int M, int N,
+                                                                 void* __restrict__ C, int c_dtype, int64_t ldc,
+                                                                 int accumulate, float* __restrict__ stats) {
+  const int q = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + q * 4, m0 = blockIdx.y * 64;
+  const size_t sstride = (size_t)M * N;
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  if (n < N) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + ph + 16 * i;
+      if (m >= M) break;
+      const float* p = slab + (size_t)m * N + n;
+      float4 v = *reinterpret_cast<const float4*>(p);
+      for (int sl = 1; sl < split; ++sl) {
+        const float4 w = *reinterpret_cast<const float4*>(p + sl * sstride);
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+      const size_t ci = (size_t)m * ldc + n;
+      if (c_dtype == SV_F32) {
+        float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + ci);
+        if (accumulate) {
+          const float4 o = *cp;
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *cp = v;
+      } else {
+        const uint2 u = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci) = u;
+        // statistics of the values as stored
+        v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                        __uint_as_float(u.y & 0xffff0000u));
+      }
+      if (stats) {
+        s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
+        s2.x = fmaf(v.x, v.x, s2.x); s2.y = fmaf(v.y, v.y, s2.y); s2.z = fmaf(v.z, v.z, s2.z); s2.w = fmaf(v.w, v.w, s2.w);
+      }
+    }
+  }
+  if (!stats) return;  // grid-uniform
+  __shared__ float4 red[2][SF_THREADS];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    for (int k = 1; k < 16; ++k) {
+      const float4 a = red[0][k * 16 + q], b = red[1][k * 16 + q];
+      s1.x += a.x; s1.y += a.y; s1.z += a.z; s1.w += a.w;
+      s2.x += b.x; s2.y += b.y; s2.z += b.z; s2.w += b.w;
+    }
+    float* o = stats + (size_t)blockIdx.y * 2 * N;
+    *reinterpret_cast<float4*>(o + n) = s1;
+    *reinterpret_cast<float4*>(o + N + n) = s2;
+  }
+}
+}  // namespace
+}  // namespace sv
+
+extern "C" int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, void* C, int32_t c_dtype,
+                                   int64_t ldc, int32_t accumulate, float* stats, sv_stream_t stream) {
+  SV_REQUIRE(slab && C, "sv_gemm_slab_finish: null pointer");
+  SV_REQUIRE(split >= 1 && M >= 0 && N >= 0 && N % 4 == 0 && ldc % 4 == 0 && ldc >= N,
+             "sv_gemm_slab_finish: bad sizes (N, ldc multiples of 4)");
+  SV_REQUIRE(c_dtype == SV_F32 || c_dtype == SV_BF16, "sv_gemm_slab_finish: bad C dtype");
+  SV_REQUIRE(!accumulate || c_dtype == SV_F32, "sv_gemm_slab_finish: accumulate needs f32 C");
+  SV_REQUIRE(!stats || c_dtype == SV_BF16, "sv_gemm_slab_finish: statistics are of bf16 outputs");
+  SV_REQUIRE(al16(slab) && al16(C) && (!stats || al16(stats)), "sv_gemm_slab_finish: operands must be 16-byte aligned");
+  if (M == 0 || N == 0) return SV_OK;
+  const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64));
+  sv::slab_finish_kernel<<<grid, sv::SF_THREADS, 0, (hipStream_t)stream>>>(slab, split, M, N, C, c_dtype, ldc,
+                                                                           accumulate, stats);
+  return check_launch("sv_gemm_slab_finish");
 }

@@ -23,6 +23,7 @@
 
 namespace sv {
 extern int g_gemm_wg_per_cu;
+extern int g_gemm_prio;
 namespace g3 {
 
 constexpr int BM = 256, BN = 128, THREADS = 512, NW = 8;
@@ -212,6 +213,8 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = tilesM * tilesN, total = nwg * nsplit;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 1, wn = wid & 1;
+  // a critical-path GEMM sharing its CUs with a concurrent stream's kernels issues first
+  if (e.prio) __builtin_amdgcn_s_setprio(2);
   for (int t = blockIdx.x; t < total; t += gridDim.x) {
     // XCD-aware order: tiles t = x (mod 8) run on XCD x, each XCD walks a contiguous tile range so
     // concurrently resident tiles share A row panels in that XCD's L2
@@ -364,6 +367,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
+  e.prio = g_gemm_prio;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>),
@@ -422,6 +426,11 @@ int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream
   if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, 3, 2>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
     return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, 3, 2>(d, 1, s, &g);
+  // split-K fprop / dgrad for grids below one workgroup per CU: f32 slabs, summed by sv_gemm_slab_finish
+  if (mode == 1 && d->epilogue == SV_EPI_SLAB)
+    return launch<true, true, SV_EPI_SLAB, 32, 3, 1>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_SLAB)
+    return launch<true, false, SV_EPI_SLAB, 32, 3, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
     return launch<false, false, SV_EPI_SLAB, 32, 4, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   return SV_ERR_UNSUPPORTED;

@@ -21,6 +21,7 @@ struct EpiArgs {
   const float* bias;
   const float* gamma;
   const void* aux; int aux_dtype; int64_t ld_aux;
+  int prio = 0;  // 1: the kernel's waves issue at raised priority (sv_gemm_set_priority)
 };
 
 __device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {

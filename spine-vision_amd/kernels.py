@@ -554,15 +554,58 @@ def _pointwise(s: nv.ConvShape, dtype: torch.dtype) -> bool:
             and s.Cs % 32 == 0 and s.Cout % 32 == 0)
 
 
+def _conv_split(M: int, N: int, K: int) -> int:
+    """split-K depth of a bf16 conv GEMM whose grid of 256x128 tiles would not give every CU a workgroup
+    (ResNet layer3/4 at 256 px: 32-128 tiles, each a long latency-bound chain of 32-deep k-steps):
+    about one workgroup per CU, >= 16 k-steps per slice, <= 32 MiB of f32 slabs (written by the GEMM,
+    read back by sv_gemm_slab_finish), at most 16 slices.  1 = no split (also for K < 1024, where the
+    slab round trip costs more than the chain it shortens)."""
+    tiles = -(-M // 256) * -(-N // 128)
+    ksteps = K // 32
+    if tiles >= 192 or ksteps < 32:
+        return 1
+    return max(1, min(-(-256 // tiles), ksteps // 16, (32 << 20) // (M * N * 4), 16))
+
+
+def _gathered(s: nv.ConvShape, dtype: torch.dtype) -> bool:
+    """the bf16 gathered-operand GEMM path of sv_conv_fwd (csrc/conv.hip conv_fwd_impl)"""
+    return dtype == torch.bfloat16 and s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0
+
+
+def _slab_finish(work: torch.Tensor, split: int, M: int, N: int, C: torch.Tensor, *, accumulate: bool = False,
+                 stats: torch.Tensor | None = None) -> None:
+    call("sv_gemm_slab_finish", ptr(work), split, M, N, ptr(C), dt(C), N, int(accumulate), ptr(stats))
+
+
+def _pointwise_fwd(x, wp, s, y, M, stats=None):
+    """1x1 conv forward as a GEMM over [M, Cs] rows; split-K + slab finish when the grid is small."""
+    split = _conv_split(M, s.Cout, s.Cs)
+    if split > 1:
+        work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
+        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
+             ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+        _slab_finish(work, split, M, s.Cout, y, stats=stats)
+    elif stats is not None:
+        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
+             ldb=s.Cs, C=y.view(M, s.Cout), C2=stats, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True)
+    else:
+        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
+             ldb=s.Cs, C=y.view(M, s.Cout), compute_bf16=True)
+
+
 def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype) -> torch.Tensor:
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
     if _pointwise(s, wp.dtype):
-        M = s.B * s.H * s.W
-        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
-             ldb=s.Cs, C=y.view(M, s.Cout), compute_bf16=True)
+        _pointwise_fwd(x, wp, s, y, s.B * s.H * s.W)
+        return y
+    M, K = s.B * OH * OW, s.KH * s.KW * s.Cs
+    split = _conv_split(M, s.Cout, K) if _gathered(s, wp.dtype) else 1
+    if split > 1:
+        work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
+        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), None, ptr(work), split)
         return y
     call("sv_conv_fwd", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s))
     return y
@@ -594,16 +637,20 @@ def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dt
         _conv_check_x(x, s, wp.dtype, "conv_fwd")
         y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
         part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
-        gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
-             ldb=s.Cs, C=y.view(M, s.Cout), C2=part, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True)
+        _pointwise_fwd(x, wp, s, y, M, stats=part)
         return y, part
-    if not (s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0):
+    if not _gathered(s, wp.dtype):
         return conv_fwd(x, wp, s, out_dtype), None
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
     part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
-    call("sv_conv_fwd_stats", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part))
+    split = _conv_split(M, s.Cout, s.KH * s.KW * s.Cs)
+    if split > 1:
+        work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
+        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), ptr(work), split)
+    else:
+        call("sv_conv_fwd_stats", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part))
     return y, part
 
 
@@ -631,7 +678,13 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
     _check(dx.is_contiguous() and tuple(dx.shape) == (s.B, s.H, s.W, s.Cs), "conv_bwd_data: dx shape")
     if _pointwise(s, wp.dtype) and (not accumulate or dx.dtype == torch.float32):
         M = s.B * s.H * s.W
-        if accumulate:  # dx += dy W: the layer-scale/residual epilogue with gamma = 1, residual = dx (in place)
+        split = _conv_split(M, s.Cs, s.Cout)
+        if split > 1:
+            work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
+            gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
+                 lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+            _slab_finish(work, split, M, s.Cs, dx, accumulate=accumulate)
+        elif accumulate:  # dx += dy W: the layer-scale/residual epilogue with gamma = 1, residual = dx (in place)
             ones = _ones(s.Cs, dy.device)
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
                  lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, gamma=ones,
@@ -640,6 +693,16 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
                  lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), compute_bf16=True)
         return dx
+    T = s.KH * s.KW
+    if (wp.dtype == torch.bfloat16 and s.stride == 1 and s.Cout >= 32 and s.Cs % 8 == 0
+            and (not accumulate or dx.dtype == torch.float32) and (T * s.Cout) % 32 == 0):
+        M = s.B * s.H * s.W
+        split = _conv_split(M, s.Cs, T * s.Cout)
+        if split > 1:
+            work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
+            call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
+                 ctypes.byref(s), ptr(work), split)
+            return dx
     call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s))
     return dx
 
@@ -727,24 +790,36 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
     return out
 
 
-def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, dgamma=None, dbeta=None, dx_dtype=torch.float32,
-           gmask=None) -> torch.Tensor:
-    """BatchNorm (train) backward with an optional ReLU mask (act > 0) on dout; dgamma/dbeta accumulate."""
+def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=None, dbeta=None,
+           dx_dtype=torch.float32, gmask=None) -> torch.Tensor:
+    """BatchNorm (train) backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
+    act > 0, or -- ``relu_beta`` = the BN's beta, for a BN followed by its own ReLU -- recomputed from y
+    like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again)."""
     rows, C = y2d.shape
     _check(_bn_c_ok(C) and dout2d.numel() == rows * C and dout2d.is_contiguous(), "bn_bwd: bad shapes")
+    _check(act is None or relu_beta is None, "bn_bwd: act and relu_beta are exclusive")
     if act is not None:
         _check(act.numel() == rows * C and act.is_contiguous(), "bn_bwd: act shape")
     if gmask is not None:
-        _check(gmask.dtype == torch.float32 and gmask.numel() == rows * C, "bn_bwd: gmask must be f32 [rows,C]")
+        _check(gmask.dtype == torch.float32 and gmask.numel() == rows * C and relu_beta is None,
+               "bn_bwd: gmask must be f32 [rows,C] (act-mask form only)")
     P = value("sv_bn_nparts", rows, C)
     part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
-         ptr(rstd), rows, C, ptr(part))
+    if relu_beta is not None:
+        call("sv_bn_relu_bwd_stats", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),
+             ptr(relu_beta), rows, C, ptr(part))
+    else:
+        call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), rows, C, ptr(part))
     sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
-    call("sv_bn_bwd_apply", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
-         ptr(rstd), ptr(gamma), ptr(sums), ptr(dx), dt(dx), ptr(gmask), rows, C)
+    if relu_beta is not None:
+        call("sv_bn_relu_bwd_apply", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),
+             ptr(relu_beta), ptr(sums), ptr(dx), dt(dx), rows, C)
+    else:
+        call("sv_bn_bwd_apply", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), ptr(gamma), ptr(sums), ptr(dx), dt(dx), ptr(gmask), rows, C)
     return dx
 
 

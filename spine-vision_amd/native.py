@@ -61,6 +61,8 @@ _SIGS = {
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
     "sv_gemm_set_workgroups_per_cu": [_i32],
     "sv_gemm_set_impl": [_i32],
+    "sv_gemm_set_priority": [_i32],
+    "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
     "sv_layernorm_bwd_nparts": [_i64, _i32],
     "sv_layernorm_bwd": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _i64, _i32, _p],
@@ -98,6 +100,8 @@ _SIGS = {
     "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _p],
     "sv_conv_fwd_stats": [_p, _p, _p, _i32, _i32, _CS, _p, _p],
     "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],
+    "sv_conv_fwd_split": [_p, _p, _p, _i32, _i32, _CS, _p, _p, _i32, _p],
+    "sv_conv_bwd_data_split": [_p, _p, _p, _i32, _i32, _i32, _CS, _p, _i32, _p],
     "sv_conv_bwd_weight_work_floats": [_CS],
     "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],
     "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],
@@ -109,6 +113,8 @@ _SIGS = {
     "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
+    "sv_bn_relu_bwd_stats": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p],
+    "sv_bn_relu_bwd_apply": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_apply": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _i64, _i32, _p],
     "sv_relu_mask": [_p, _i32, _p, _i32, _p, _i64, _p],
     "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
@@ -120,7 +126,8 @@ _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
 _VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
-                                                                     "sv_gemm_set_workgroups_per_cu", "sv_gemm_set_impl"}
+                                                                     "sv_gemm_set_workgroups_per_cu", "sv_gemm_set_impl",
+                                                                     "sv_gemm_set_priority"}
 
 _lib = None
 _lock = threading.Lock()

@@ -86,3 +86,24 @@ def test_gemm_family_bitwise_vs_dispatch(dev, impl, M, C):
     o = fc1_dgrad()
     r = dh.float() @ w1.float()
     assert float((o.float() - r).norm() / r.norm()) < 5e-3
+
+
+def test_gemm_priority_is_bitwise_neutral(dev):
+    """sv_gemm_set_priority only raises the waves' issue priority (the lean backward's side-stream
+    wgrads): the split-K weight gradient is bit-identical either way."""
+    g = torch.Generator().manual_seed(3)
+    bf = torch.bfloat16
+    dy = torch.randn(8192, 256, generator=g).to(bf).to(dev)
+    a = torch.randn(8192, 1024, generator=g).to(bf).to(dev)
+    prev_res = nv.value("sv_gemm_set_workgroups_per_cu", 1)  # the backward's residency policy
+    try:
+        ref = K.linear_wgrad(dy, a)
+        prev = nv.value("sv_gemm_set_priority", 1)
+        try:
+            got = K.linear_wgrad(dy, a)
+        finally:
+            nv.value("sv_gemm_set_priority", prev)
+        torch.cuda.synchronize()
+    finally:
+        nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
+    assert torch.equal(ref, got)

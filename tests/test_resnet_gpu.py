@@ -117,6 +117,54 @@ def test_conv_fwd_bn_stats_epilogue(dev, case):
     assert rel(rm2, rm1) < 1e-5 and rel(rv2, rv1) < 1e-4
 
 
+@pytest.mark.parametrize("case", [(4, 16, 16, 256, 256, 3, 1), (4, 8, 8, 512, 512, 3, 1), (4, 16, 16, 256, 512, 3, 2),
+                                  (4, 16, 16, 1024, 256, 1, 1), (4, 8, 8, 2048, 512, 1, 1), (3, 7, 5, 128, 64, 3, 1)])
+def test_conv_split_k_matches_unsplit(dev, case, monkeypatch):
+    """Split-K (f32 slabs + sv_gemm_slab_finish) for conv grids below one workgroup per CU -- the
+    ResNet layer3/4 shapes -- against the unsplit kernels on the same operands: forward (+ BN
+    statistics), backward-data (stride 1; plain and accumulate).  Only the f32 summation order
+    differs: f32 results within 1e-5, bf16 stores within a rare 1-ulp flip (1e-4 rel L2)."""
+    B, H, W, Cs, Cout, k, st = case
+    pad = k // 2
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, H, W, Cs, generator=g).to(torch.bfloat16).to(dev)
+    w = torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5
+    s = K.conv_shape(B, H, W, Cs, Cout, k, st, pad)
+    wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
+    OH, OW = K.conv_out_hw(H, W, k, st, pad)
+    M = B * OH * OW
+    assert K._conv_split(M, Cout, k * k * Cs) > 1, "case must exercise the split path"
+    y_s, part_s = K.conv_fwd_bn_stats(x, wp, s, torch.bfloat16)
+    y32_s = K.conv_fwd(x, wp, s, torch.float32)
+    dy = torch.randn(B, OH, OW, Cout, generator=g).to(torch.bfloat16).to(dev)
+    dx_s = dx_acc_s = None
+    if st == 1:
+        dx_s = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.float32)
+        dx_acc_s = torch.ones_like(dx_s)
+        K.conv_bwd_data(dy, wp, s, dx=dx_acc_s, accumulate=True)
+    with monkeypatch.context() as mp:
+        mp.setattr(K, "_conv_split", lambda *a: 1)
+        y_u, part_u = K.conv_fwd_bn_stats(x, wp, s, torch.bfloat16)
+        y32_u = K.conv_fwd(x, wp, s, torch.float32)
+        if st == 1:
+            dx_u = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert rel(y32_s, y32_u) < 1e-5
+    assert rel(y_s.float(), y_u.float()) < 1e-4
+    ref = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), w.to(torch.bfloat16).double(), stride=st, padding=pad)
+    assert rel(y32_s.permute(0, 3, 1, 2), ref) < 1e-5
+    rows = M
+    m_s, r_s = K.bn_stats_from_partials(part_s, rows)
+    m_u, r_u = K.bn_stats_from_partials(part_u, rows)
+    assert rel(m_s, m_u) < 1e-4 and rel(r_s, r_u) < 1e-4
+    yd = y_s.view(rows, Cout).double().cpu()
+    assert rel(m_s, yd.mean(0)) < 1e-5
+    assert rel(r_s, 1.0 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-4
+    if st == 1:
+        assert rel(dx_s, dx_u) < 1e-5
+        assert rel(dx_acc_s - 1.0, dx_s) < 1e-6
+
+
 @pytest.mark.parametrize("C", [64, 256, 2048])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_batchnorm_train_fwd_bwd(dev, C, precision):
@@ -156,6 +204,34 @@ def test_batchnorm_train_fwd_bwd(dev, C, precision):
     em, er = K.bn_eval_params(rm, rv)
     assert rel(em, rm) == 0.0
     assert rel(er, 1.0 / torch.sqrt(rv.cpu().double() + 1e-5)) < 1e-6
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048, 12])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_bn_relu_bwd_recomputed_mask_matches_act_mask(dev, C, precision):
+    """sv_bn_relu_bwd_*: the ReLU mask recomputed from y (as sv_bn_act_fwd computes the pre-activation)
+    gives bit for bit the backward of the act > 0 form, dgamma / dbeta included.  C = 12 takes the
+    4-channel kernels, the others the 8-channel (16-B) ones."""
+    dt_ = torch.bfloat16 if precision == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(C)
+    rows = 4099
+    y = torch.randn(rows, C, generator=g).to(dev, dt_)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.3).to(dev)
+    mean, rstd = K.bn_stats(y)
+    a = K.bn_act(y, mean, rstd, gam, bet, relu=True, out_dtype=dt_)
+    dout = torch.randn(rows, C, generator=g).to(dev, dt_)
+    dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dx1 = K.bn_bwd(dout, y, mean, rstd, gam, act=a, dgamma=dg1, dbeta=db1, dx_dtype=dt_)
+    dx2 = K.bn_bwd(dout, y, mean, rstd, gam, relu_beta=bet, dgamma=dg2, dbeta=db2, dx_dtype=dt_)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    # and both equal torch autograd of relu(batch_norm(y)) in f32
+    yr = y.double().cpu().requires_grad_(True)
+    o = torch.relu(F.batch_norm(yr, None, None, gam.double().cpu(), bet.double().cpu(), training=True, eps=1e-5))
+    o.backward(dout.double().cpu())
+    assert rel(dx2.float(), yr.grad) < (2e-2 if precision == "bf16" else 1e-3)  # + rare mask flips vs float64
 
 
 def test_bn_act_downsample_residual(dev):
