@@ -100,7 +100,7 @@ int sv_gemm_set_workgroups_per_cu(int32_t n);
  * issues first; 0 (default) = normal.  Returns the previous value.                                  */
 int sv_gemm_set_priority(int32_t p);
 /* Kernel family for the bf16 GEMMs launched after this call (host-side, process-wide, initially 0):
- * 0 = the measured per-shape dispatch, 2 / 3 / 8 = force that family where its contract holds
+ * 0 = the measured per-shape dispatch, 2 / 3 / 8 / 9 = force that family where its contract holds
  * (tests/test_gemm_family_gpu.py compares the families bit for bit; tools/gemm_bench.py times them).
  * Returns the previous value.                                                                      */
 int sv_gemm_set_impl(int32_t impl);

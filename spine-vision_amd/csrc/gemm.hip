@@ -372,8 +372,21 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     const long tiles8 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
     const bool v8_shape = tiles8 >= 256 && (d->epilogue == SV_EPI_BIAS_GELU_DUAL || d->epilogue == SV_EPI_BIAS_GELU ||
                                             ((d->epilogue == SV_EPI_BIAS_GAMMA_RES) && d->K >= 2048));
-    int rc;
-    if (impl == 0 && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);
+    // v9 (persistent 256x256, BK 64 phase-interleaved, register-direct epilogue) where the chip holds
+    // a full wave of its tiles and N fills the 256-wide tile
+    static int v9_mode = -1;
+    if (v9_mode < 0) {
+      const char* ev = getenv("SV_V9");
+      v9_mode = ev ? atoi(ev) : 2;
+    }
+    const int split9 = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
+    const bool v9_shape = d->N >= 256 && tiles8 * split9 >= 256 && d->epilogue != SV_EPI_BIAS_GELU2 &&
+                          (d->epilogue != SV_EPI_SLAB || d->M >= 256);
+    const bool v9_pick = impl == 0 && v9_shape && (v9_mode == 2 || (v9_mode == 1 && !g_gemm_wg_per_cu));
+    int rc = SV_ERR_UNSUPPORTED;
+    if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+    if ((impl == 0 || impl == 9) && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);
     else if (impl == 8) rc = launch_gemm8(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);
     else if (impl == 3) rc = launch_gemm3(d, s);

@@ -1,0 +1,612 @@
+// MFMA GEMM v9 (bf16 operands, f32 accumulate): persistent 256x256 tiles, BK 64, one 512-thread
+// workgroup per CU, 8 waves in 2(M) x 4(N) (128 x 64 per wave = 8 x 4 v_mfma_f32_16x16x32_bf16
+// fragments).  What is different from v3/v8:
+//
+//  * phase-interleaved K loop: a 64-deep K-tile is four phases, each {read a register subtile from
+//    LDS, issue part of the LDS-DMA of the K-tile TWO ahead, barrier, 16 MFMAs on one quadrant of the
+//    wave tile, barrier}; waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave reads
+//    while its partner multiplies;
+//  * two LDS buffers (2 x 64 KiB), each refilled region by region as soon as every wave has read it
+//    (A rows of quadrant 0 after phase 0, B after phase 1, A rows of quadrant 1 after phase 2): about
+//    1.5 K-tiles of DMA in flight, retired by counted `s_waitcnt vmcnt` (never 0 in the loop); an
+//    N/M-major A (weight gradients) cannot be refilled by quadrant, so it gets a third buffer;
+//  * persistent over the tiles with ONE K-tile stream: the DMA of the next tile's first K-tiles is
+//    issued during the current tile's last ones, and the epilogue's stores stay in flight while the
+//    next tile starts (the vmcnt counts include them);
+//  * register-direct epilogue: the MFMA runs with the operands swapped (D^T = B^T A^T), so a lane
+//    holds 4 consecutive OUTPUT COLUMNS of one row; for bf16 outputs the B rows are permuted inside
+//    each 32-column group (at DMA time for K-major B, in the fragment address for N-major B) so that
+//    a lane holds 8 consecutive columns -> one 16-B buffer store per 8 outputs, no LDS round trip,
+//    out-of-range rows/columns dropped by the buffer descriptor's range check (no branches, so every
+//    wave issues a fixed number of memory instructions per tile, which the vmcnt counts rely on).
+#include "common.h"
+#include "gemm_common.h"
+
+namespace sv {
+namespace g9 {
+
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512, NW = 8;
+constexpr int FM = 8, FN = 4;
+constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF_BYTES = A_BYTES + B_BYTES;
+// LDS: K-major A: two buffers of {A, B} (128 KiB); N/M-major A: A triple-buffered (it is refilled
+// only after the last phase that reads it), B double-buffered (160 KiB)
+template <bool AK>
+constexpr int lds_bytes() { return AK ? 2 * BUF_BYTES : 3 * A_BYTES + 2 * B_BYTES; }
+template <bool AK>
+__device__ __forceinline__ int a_off(int g) { return AK ? (g & 1) * BUF_BYTES : (g % 3) * A_BYTES; }
+template <bool AK>
+__device__ __forceinline__ int b_off(int g) { return AK ? (g & 1) * BUF_BYTES + A_BYTES : 3 * A_BYTES + (g & 1) * B_BYTES; }
+constexpr uint32_t OOB = 0x80000000u;     // buffer offset past every descriptor's range
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// K-major image [rows][64] bf16 (128-B rows): 16-B chunk c of row r stored at c ^ ((r >> 1) & 7), so
+// the 16 rows x one chunk of every ds_read_b128 lane group land on 16 distinct bank slots
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+// N/M-major image [64 k][256] bf16 (512-B rows), read with ds_read_b64_tr_b16
+__device__ __forceinline__ int mswz(int r) { return ((r & 3) << 1) ^ (((r >> 3) & 1) << 3); }
+// bf16-output column permutation inside a 32-row group of B: LDS row 16h + 4g + r holds column
+// 8g + 4h + r, so fragment pair (2q, 2q+1) gives lane group g the 8 consecutive columns 32q + 8g ..
+__device__ __forceinline__ int perm8(int rho) {
+  return (rho & ~31) | (((rho & 15) >> 2) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
+
+// LDS-DMA by buffer_load ... lds: the per-lane byte offset of each of a wave's pieces is computed
+// once per tile (voffset), the K position is the uniform soffset, rows / columns past the matrix get
+// an offset past the descriptor's range and land as zeros (their results are never stored)
+__device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
+}
+// A wave's DMA pieces of one operand differ only by whole rows (K-major: 64 rows; N/M-major: 16 k-rows)
+// and the source swizzle does not depend on the piece, so each operand needs ONE per-lane byte offset
+// (per tile) plus a uniform piece offset in soffset.  Rows / columns past the matrix read past the
+// descriptor's range (zeros) or garbage that only reaches outputs that are never stored.
+// K-major: piece wid + 8j covers rows 64j + 8wid + lane/8, 16-B chunk lane%8 (swizzled)
+template <bool PERM>
+__device__ __forceinline__ uint32_t vbase_k(int64_t ld, int row0, int wid) {
+  const int lane = threadIdx.x & 63;
+  const int row = 8 * wid + (lane >> 3), ch = lane & 7;
+  return (uint32_t)(((int64_t)(row0 + (PERM ? perm8(row) : row)) * ld + ((ch ^ kswz(row)) << 3)) * 2);
+}
+// N/M-major: piece wid + 8j covers k-rows 16j + 2wid + lane/32, 16-B chunk lane%32 (swizzled)
+__device__ __forceinline__ uint32_t vbase_m(int64_t ld, int col0, int wid) {
+  const int lane = threadIdx.x & 63;
+  const int krow = 2 * wid + (lane >> 5), ch = lane & 31;
+  return (uint32_t)(((int64_t)krow * ld + col0 + ((ch ^ mswz(krow)) << 3)) * 2);
+}
+
+// fragment: lane l holds X[row = base + (l & 15)][k = 32 kh + 8 (l >> 4) + 0..7]
+__device__ __forceinline__ bf16x8 frag_k(const char* __restrict__ region, int base, int kh) {
+  const int l = threadIdx.x & 63;
+  const int row = base + (l & 15), ch = kh * 4 + (l >> 4);
+  return *reinterpret_cast<const bf16x8*>(region + row * 128 + ((ch ^ kswz(row)) << 4));
+}
+// N/M-major fragment through the transposing read; lanes p = l & 3 fetch the 4-column run that
+// becomes fragment rows 4p .. 4p+3: run start chunk `ch(p)` and half `hf(p)`
+__device__ __forceinline__ bf16x8 frag_tr(const char* __restrict__ region, int ch, int hf, int kh) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, q = (l >> 2) & 3;
+  const int r0 = kh * 32 + 8 * g + q, r1 = r0 + 4;
+  const char* a0 = region + r0 * 512 + ((ch ^ mswz(r0)) << 4) + hf * 8;
+  const char* a1 = region + r1 * 512 + ((ch ^ mswz(r1)) << 4) + hf * 8;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// natural 16-row fragment at `base` (runs base + 4p)
+__device__ __forceinline__ bf16x8 frag_m(const char* __restrict__ region, int base, int kh) {
+  const int p = threadIdx.x & 3;
+  return frag_tr(region, (base >> 3) + (p >> 1), p & 1, kh);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct Geo {
+  int m0, n0, kbeg, split;
+};
+
+// descriptor extents (bytes) of the epilogue's buffers; a byte offset >= extent is dropped / reads 0
+struct Ext {
+  uint32_t c, c2, aux, a, b;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  // built from kernel arguments only: wave-uniform, so no waterfall loop around the buffer ops
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+  return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+}
+
+// vector-memory instructions one wave issues in an epilogue (all unconditional): the vmcnt counts of
+// the K loop's waits include them when an epilogue lies between a DMA and its wait
+template <int EPI, bool P8>
+struct EpiCount {
+  static constexpr int CH = P8 ? 2 : 4;  // column chunks per 16-row group
+  static constexpr int OUTS = (EPI == SV_EPI_BIAS_GELU_DUAL) ? 2 : 1;
+  static constexpr int AUX = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) ? CH
+                             : EPI == SV_EPI_BIAS_GAMMA_RES ? (P8 ? 2 * CH : CH)
+                                                            : 0;
+  static constexpr int E = FM * (CH * OUTS + AUX);
+};
+
+// Epilogue of one wave tile: rows m_w + 16 i + (l & 15), columns per chunk c:
+//   P8: n_w + 32c + 8(l >> 4) .. +7  (acc[i][2c][0..3], acc[i][2c+1][0..3]),
+//   P4: n_w + 16c + 4(l >> 4) .. +3  (acc[i][c][0..3]).
+// Arithmetic identical to wave_group_epilogue (gemm_common.h).
+template <int EPI, bool P8>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
+                                         int split) {
+  constexpr int CH = P8 ? 2 : 4, CW = P8 ? 8 : 4;
+  const int l = threadIdx.x & 63, ml = l & 15, gq = l >> 4;
+  int n[CH];
+  bool okn[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    n[c] = n_w + (P8 ? 32 * c + 8 * gq : 16 * c + 4 * gq);
+    okn[c] = n[c] < e.N;
+  }
+  const bool slab = EPI == SV_EPI_SLAB;
+  const bool has_bias = !slab && EPI != SV_EPI_GELU_GRAD && EPI != SV_EPI_MUL_AUX;
+  float bias[CH][CW], gam[CH][CW];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int w = 0; w < CW; ++w) bias[c][w] = 0.f, gam[c][w] = 1.f;
+  if (has_bias && e.bias) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (okn[c]) {
+#pragma unroll
+        for (int w = 0; w < CW; w += 4) {
+          const float4 b = *reinterpret_cast<const float4*>(e.bias + n[c] + w);
+          bias[c][w] = b.x, bias[c][w + 1] = b.y, bias[c][w + 2] = b.z, bias[c][w + 3] = b.w;
+        }
+      }
+  }
+  if (EPI == SV_EPI_BIAS_GAMMA_RES && e.gamma) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (okn[c]) {
+#pragma unroll
+        for (int w = 0; w < CW; w += 4) {
+          const float4 g = *reinterpret_cast<const float4*>(e.gamma + n[c] + w);
+          gam[c][w] = g.x, gam[c][w + 1] = g.y, gam[c][w + 2] = g.z, gam[c][w + 3] = g.w;
+        }
+      }
+  }
+  const int64_t ldc = slab ? e.N : e.ldc;
+  const char* cbase = reinterpret_cast<const char*>(e.C);
+  if (slab) cbase += (size_t)split * e.M * e.N * 4;
+  const auto rc = rsrc(cbase, x.c);
+  const auto rc2 = rsrc(e.C2 ? e.C2 : e.C, x.c2);
+  constexpr int CS = (EPI == SV_EPI_SLAB || !P8) ? 4 : 2;  // output element bytes: P8 <=> bf16 outputs
+  constexpr bool AUXBF = EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD;
+  constexpr bool AUXF = EPI == SV_EPI_BIAS_GAMMA_RES;
+  const auto ra = rsrc(e.aux ? e.aux : e.C, x.aux);
+  // epilogue operands of HALF row groups at a time (bf16: 32 VGPRs, f32 residual: 32 / 64 VGPRs)
+  constexpr int HALF = AUXF ? FM / 4 : FM / 2;
+#pragma unroll
+  for (int hb = 0; hb < FM / HALF; ++hb) {
+    u32x4 raw[HALF][CH][AUXF && P8 ? 2 : 1];
+    if constexpr (AUXBF || AUXF) {
+#pragma unroll
+      for (int ii = 0; ii < HALF; ++ii) {
+        const int m = m_w + 16 * (hb * HALF + ii) + ml;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const uint32_t base = okn[c] && m < e.M ? (uint32_t)((m * e.ld_aux + n[c]) * (AUXF ? 4 : 2)) : OOB;
+          if constexpr (AUXBF && P8) {
+            raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 0);
+          } else if constexpr (AUXBF) {
+            const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(ra, base, 0, 0);
+            raw[ii][c][0] = u32x4{t.x, t.y, 0u, 0u};
+          } else if constexpr (P8) {
+            raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 0);
+            raw[ii][c][AUXF && P8 ? 1 : 0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 16, 0, 0);
+          } else {
+            raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < HALF; ++ii) {
+      const int i = hb * HALF + ii;
+      const int m = m_w + 16 * i + ml;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        float v[CW];
+        if constexpr (P8) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][2 * c][r], v[4 + r] = acc[i][2 * c + 1][r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
+        }
+        const uint32_t off = okn[c] && m < e.M ? (uint32_t)((m * ldc + n[c]) * CS) : OOB;
+        float o[CW], o2[CW];
+        if (!slab) {
+#pragma unroll
+          for (int w = 0; w < CW; ++w) v[w] += bias[c][w];
+        }
+        float xa[CW];
+        if constexpr (AUXBF) {
+          const uint32_t wd[4] = {raw[ii][c][0].x, raw[ii][c][0].y, raw[ii][c][0].z, raw[ii][c][0].w};
+#pragma unroll
+          for (int w = 0; w < CW; w += 2) {
+            xa[w] = __uint_as_float(wd[w >> 1] << 16);
+            xa[w + 1] = __uint_as_float(wd[w >> 1] & 0xffff0000u);
+          }
+        } else if constexpr (AUXF) {
+#pragma unroll
+          for (int w = 0; w < CW; ++w) {
+            const u32x4 t = raw[ii][c][w >> 2];
+            const uint32_t wd = (w & 3) == 0 ? t.x : (w & 3) == 1 ? t.y : (w & 3) == 2 ? t.z : t.w;
+            xa[w] = __uint_as_float(wd);
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < CW; ++w) {
+          if constexpr (EPI == SV_EPI_SLAB || EPI == SV_EPI_STORE) {
+            o[w] = v[w];
+          } else if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) {
+            gelu_and_grad(v[w], o2[w], o[w]);  // C = GELU'(h), C2 = GELU(h)
+          } else if constexpr (EPI == SV_EPI_BIAS_GELU) {
+            o[w] = gelu_f(v[w]);
+          } else if constexpr (EPI == SV_EPI_MUL_AUX) {
+            o[w] = v[w] * xa[w];
+          } else if constexpr (EPI == SV_EPI_GELU_GRAD) {
+            o[w] = v[w] * gelu_grad_f(xa[w]);
+          } else {  // SV_EPI_BIAS_GAMMA_RES
+            o[w] = fmaf(gam[c][w], v[w], xa[w]);
+          }
+        }
+        if constexpr (P8) {
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, off, 0, 0);
+          if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) __builtin_amdgcn_raw_buffer_store_b128(pack8(o2), rc2, off, 0, 0);
+        } else {
+          const u32x4 d = {__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(d, rc, off, 0, 0);
+          if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) {
+            const u32x4 d2 = {__float_as_uint(o2[0]), __float_as_uint(o2[1]), __float_as_uint(o2[2]),
+                              __float_as_uint(o2[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(d2, rc2, off, 0, 0);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool P8>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int nk, int tilesM,
+             int tilesN, int nsplit, EpiArgs e, Ext x) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 2, wn = wid & 3;
+  const int nwg = tilesM * tilesN, total = nwg * nsplit;
+  const int my_tiles = (total - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= total)
+  const int kper = nk * BK;
+
+  auto geo = [&](int it) {
+    const int t = blockIdx.x + it * gridDim.x;
+    // XCD-aware order: tiles t = x (mod 8) run on XCD x, each XCD walks a contiguous range of tiles
+    const int xcd = t & 7, loc = t >> 3, q8 = total >> 3, r8 = total & 7;
+    const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const int split = wgi / nwg, wg = wgi - split * nwg;
+    Geo gg;
+    gg.m0 = (wg / tilesN) * BM;
+    gg.n0 = (wg % tilesN) * BN;
+    gg.split = split;
+    gg.kbeg = split * kper;
+    return gg;
+  };
+
+  // ---- DMA stream: K-tile l_g = (l_it, l_kt), two K-tiles ahead of the MFMAs.  Past the end of the
+  // stream it re-reads the last K-tile's data into the regions K-tile l_g would use (freed by the
+  // same schedule and never read again), so every phase issues the same number of DMAs.
+  const auto ra = rsrc(A, x.a), rb = rsrc(B, x.b);
+  int l_it = 0, l_kt = 0, l_g = 0;
+  Geo lg = geo(0);
+  uint32_t va = 0, vb = 0;  // this wave's per-lane DMA offsets for the load pointer's tile
+  auto set_voffs = [&]() {
+    va = AK ? vbase_k<false>(lda, lg.m0, wid) : vbase_m(lda, lg.m0, wid);
+    vb = BKM ? vbase_k<P8>(ldb, lg.n0, wid) : vbase_m(ldb, lg.n0, wid);
+  };
+  set_voffs();
+  // K-major A: part 1 = A rows of quadrant 0, part 2 = B, part 3 = A rows of quadrant 1.
+  // N/M-major A (a DMA piece spans both quadrants): part 1 = all of A (triple-buffered), part 2 = B.
+  auto issue_part = [&](int part) {
+    const int k0 = lg.kbeg + l_kt * BK;
+    if (part == 2) {
+      char* bb = smem + b_off<AK>(l_g);
+      const uint32_t so = BKM ? (uint32_t)k0 * 2 : (uint32_t)((int64_t)k0 * ldb * 2);
+      const uint32_t step = (uint32_t)((BKM ? 64 : 16) * ldb * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dma(rb, vb, so + j * step, bb + (wid + 8 * j) * 1024);
+    } else if constexpr (AK) {
+      char* ab = smem + a_off<AK>(l_g);
+      const int h = part == 1 ? 0 : 1;  // pieces h*8 + wid (rows 64h + ..) and h*8 + 16 + wid (+128 rows)
+      const uint32_t so = (uint32_t)k0 * 2 + (uint32_t)(64 * h * lda * 2);
+      dma(ra, va, so, ab + (h * 8 + wid) * 1024);
+      dma(ra, va, so + (uint32_t)(128 * lda * 2), ab + (h * 8 + 16 + wid) * 1024);
+    } else if (part == 1) {
+      char* ab = smem + a_off<AK>(l_g);
+      const uint32_t so = (uint32_t)((int64_t)k0 * lda * 2), step = (uint32_t)(16 * lda * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dma(ra, va, so + j * step, ab + (wid + 8 * j) * 1024);
+    }
+  };
+  auto advance = [&]() {
+    ++l_g;
+    if (++l_kt == nk) {
+      if (l_it + 1 < my_tiles) {
+        ++l_it;
+        l_kt = 0;
+        lg = geo(l_it);
+        set_voffs();
+      } else {
+        l_kt = nk - 1;  // past the end: repeat the last K-tile's data
+      }
+    }
+  };
+
+  constexpr int E = EpiCount<EPI, P8>::E;
+  // DMAs younger than the W1 / W2 targets in steady state (see the phase comments below)
+  constexpr int W1 = AK ? 10 : 8, W2 = 10;
+  constexpr int W1E = W1 + E > 63 ? 63 : W1 + E, W2E = W2 + E > 63 ? 63 : W2 + E;
+  // SV_EPI_SLAB with C2: the bias gradient sum_k A(m, k) of a weight-gradient GEMM (N/M-major A) from
+  // the A fragments this wave already holds: wave (wm, wn) sums fragment rows wn (quadrant 0) and
+  // 4 + wn (quadrant 1) of its 128 rows, so the 8 waves cover the tile's 256 rows once
+  const bool do_cs = EPI == SV_EPI_SLAB && !AK && e.C2 != nullptr;
+  float cs[2] = {0.f, 0.f};
+  auto colsum_frag = [&](const bf16x8 (&af)[4][2], float& acc_cs) {
+    // fragment wn of the quadrant, chosen by a wave-uniform branch (a dynamic index would spill af)
+    bf16x8 f0 = af[0][0], f1 = af[0][1];
+    if (wn == 1) f0 = af[1][0], f1 = af[1][1];
+    else if (wn == 2) f0 = af[2][0], f1 = af[2][1];
+    else if (wn == 3) f0 = af[3][0], f1 = af[3][1];
+    const bf16x8 f[2] = {f0, f1};
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+      const u32x4_t w = __builtin_bit_cast(u32x4_t, f[kh]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc_cs += __uint_as_float(w[q] << 16) + __uint_as_float(w[q] & 0xffff0000u);
+    }
+  };
+
+  // prologue: K-tiles 0 and 1, then K-tile 0 landed everywhere
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    issue_part(1);
+    issue_part(2);
+    if constexpr (AK) issue_part(3);
+    advance();
+  }
+  vm_wait<8>();
+  bar();
+  if (wm == 1) bar();  // waves 4-7 run one barrier behind
+
+  int g = 0;  // the MFMAs' K-tile in the stream
+  for (int it = 0; it < my_tiles; ++it) {
+    const Geo cg = geo(it);
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    cs[0] = cs[1] = 0.f;
+    for (int kt = 0; kt < nk; ++kt, ++g) {
+      const char* Ab = smem + a_off<AK>(g);
+      const char* Bb = smem + b_off<AK>(g);
+      bf16x8 af[4][2], bq[2][2][2];
+      auto read_a = [&](int qm) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+            af[i][kh] = AK ? frag_k(Ab, wm * 128 + 64 * qm + 16 * i, kh) : frag_m(Ab, wm * 128 + 64 * qm + 16 * i, kh);
+      };
+      auto read_b = [&](int qn) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) {
+            const int j = 2 * qn + jj;
+            if constexpr (BKM) {
+              bq[qn][jj][kh] = frag_k(Bb, wn * 64 + 16 * j, kh);
+            } else if constexpr (P8) {
+              const int p = threadIdx.x & 3;
+              bq[qn][jj][kh] = frag_tr(Bb, wn * 8 + 4 * qn + p, jj, kh);
+            } else {
+              bq[qn][jj][kh] = frag_m(Bb, wn * 64 + 16 * j, kh);
+            }
+          }
+      };
+      auto quad = [&](int qm, int qn) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[4 * qm + i][2 * qn + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  bq[qn][jj][kh], af[i][kh], acc[4 * qm + i][2 * qn + jj], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      };
+      // phase 0: A quadrant-0 rows and B columns 0-31 of the wave
+      read_a(0);
+      read_b(0);
+      lgkm0();
+      bar();
+      quad(0, 0);
+      bar();
+      // phase 1: B columns 32-63; the first DMA part of K-tile g+2 into its freed region.  K-major A:
+      // the A quadrant-1 rows of THIS K-tile (issued in phase 3 two K-tiles back) must have landed:
+      // younger DMAs = 2 + 4 + 2 (previous K-tile's phases 1-3) + 2 (this phase) [+ an epilogue]
+      read_b(1);
+      issue_part(1);
+      if (do_cs) colsum_frag(af, cs[0]);
+      if (AK) {
+        if (it > 0 && kt <= 1) vm_wait<W2E>();
+        else vm_wait<W2>();
+      }
+      lgkm0();
+      bar();
+      quad(0, 1);
+      bar();
+      // phase 2: A quadrant-1 rows; B of K-tile g+2
+      read_a(1);
+      issue_part(2);
+      lgkm0();
+      bar();
+      quad(1, 1);
+      bar();
+      // phase 3: (K-major A) the A quadrant-1 rows of K-tile g+2; then A quadrant-0 rows and B of
+      // K-tile g+1 must have landed: younger DMAs = 2 + (2 + 4 + 2) (K-major A) / 4 + 4 (N-major A:
+      // all of A in phase 1, B in phase 2) [+ an epilogue]
+      if constexpr (AK) issue_part(3);
+      advance();
+      if (do_cs) colsum_frag(af, cs[1]);
+      if (it > 0 && kt == 0) vm_wait<W1E>();
+      else vm_wait<W1>();
+      lgkm0();
+      bar();
+      quad(1, 0);
+      bar();
+    }
+    if (do_cs) {
+      // the 4 lane groups hold partial sums of the same row over different k: fold in a fixed order
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        cs[h] += __shfl_xor(cs[h], 16);
+        cs[h] += __shfl_xor(cs[h], 32);
+        const int m = cg.m0 + wm * 128 + 64 * h + 16 * wn + (threadIdx.x & 15);
+        if ((threadIdx.x & 63) < 16 && m < e.M) reinterpret_cast<float*>(e.C2)[(size_t)cg.split * e.M + m] = cs[h];
+      }
+    }
+    epilogue<EPI, P8>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split);
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
+  if (wm == 0) bar();
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <bool AK, bool BKM, int EPI, bool P8>
+static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
+  const int nk = d->K / split / BK;
+  const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
+  EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
+            d->aux, d->aux_dtype, d->ld_aux};
+  const int cs = d->c_dtype == SV_F32 ? 4 : 2;
+  Ext x;
+  if (EPI == SV_EPI_SLAB) {
+    x.c = (uint32_t)((size_t)d->M * d->N * 4);
+  } else {
+    x.c = (uint32_t)(((size_t)(d->M - 1) * d->ldc + d->N) * cs);
+  }
+  x.c2 = d->C2 ? (uint32_t)(((size_t)(d->M - 1) * d->ldc + d->N) * (d->c2_dtype == SV_F32 ? 4 : 2)) : 0u;
+  x.aux = d->aux ? (uint32_t)(((size_t)(d->M - 1) * d->ld_aux + d->N) * (d->aux_dtype == SV_F32 ? 4 : 2)) : 0u;
+  x.a = (uint32_t)((AK ? (size_t)(d->M - 1) * d->lda + d->K : (size_t)(d->K - 1) * d->lda + d->M) * 2);
+  x.b = (uint32_t)((BKM ? (size_t)(d->N - 1) * d->ldb + d->K : (size_t)(d->K - 1) * d->ldb + d->N) * 2);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<AK>());
+    attr_set = true;
+  }
+  const int total = tilesM * tilesN * split;
+  int grid = num_cus();
+  if (grid > total) grid = total;
+  gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_bytes<AK>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
+                                                                  reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
+                                                                  tilesM, tilesN, split, e, x);
+  return check_launch("sv_gemm(v9)");
+}
+
+template <bool AK, bool BKM>
+static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
+  const bool bf_out = d->c_dtype == SV_BF16;
+  switch (d->epilogue) {
+    case SV_EPI_STORE:
+      return bf_out ? launch<AK, BKM, SV_EPI_STORE, true>(d, split, s) : launch<AK, BKM, SV_EPI_STORE, false>(d, split, s);
+    case SV_EPI_BIAS_GELU_DUAL:
+      if (!bf_out || d->c2_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
+      return launch<AK, BKM, SV_EPI_BIAS_GELU_DUAL, true>(d, split, s);
+    case SV_EPI_BIAS_GELU:
+      if (!bf_out) return SV_ERR_UNSUPPORTED;
+      return launch<AK, BKM, SV_EPI_BIAS_GELU, true>(d, split, s);
+    case SV_EPI_BIAS_GAMMA_RES:
+      if (d->aux_dtype != SV_F32) return SV_ERR_UNSUPPORTED;
+      return bf_out ? launch<AK, BKM, SV_EPI_BIAS_GAMMA_RES, true>(d, split, s)
+                    : launch<AK, BKM, SV_EPI_BIAS_GAMMA_RES, false>(d, split, s);
+    case SV_EPI_MUL_AUX:
+      if (d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
+      return bf_out ? launch<AK, BKM, SV_EPI_MUL_AUX, true>(d, split, s)
+                    : launch<AK, BKM, SV_EPI_MUL_AUX, false>(d, split, s);
+    case SV_EPI_GELU_GRAD:
+      if (d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
+      return bf_out ? launch<AK, BKM, SV_EPI_GELU_GRAD, true>(d, split, s)
+                    : launch<AK, BKM, SV_EPI_GELU_GRAD, false>(d, split, s);
+    case SV_EPI_SLAB:
+      if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
+      return launch<AK, BKM, SV_EPI_SLAB, false>(d, split, s);
+    default:
+      return SV_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace g9
+
+int launch_gemm9(const sv_gemm_desc* d, hipStream_t s) {
+  using namespace g9;
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->a_scale_k)
+    return SV_ERR_UNSUPPORTED;
+  const int split = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
+  // uniform K-tiles per split, the epilogue's 8-column (bf16) / 4-column (f32) chunks whole, every
+  // buffer offset inside 31 bits
+  if (d->K % (split * BK) != 0 || d->N % 8 != 0) return SV_ERR_UNSUPPORTED;
+  if (d->epilogue != SV_EPI_SLAB && d->ldc % 8 != 0) return SV_ERR_UNSUPPORTED;
+  if (d->aux && d->ld_aux % 8 != 0) return SV_ERR_UNSUPPORTED;
+  const size_t lim = (size_t)1 << 31;
+  const size_t rows = (size_t)ceil_div(d->M, BM) * BM;
+  if (rows * (size_t)(d->epilogue == SV_EPI_SLAB ? d->N : d->ldc) * 4 * (size_t)split >= lim) return SV_ERR_UNSUPPORTED;
+  if (d->aux && rows * (size_t)d->ld_aux * 4 >= lim) return SV_ERR_UNSUPPORTED;
+  // operand extents: the DMA offsets (voffset + soffset) stay below the 0x7fffffff descriptor range
+  const size_t a_ext = d->a_kmajor ? (size_t)d->M * d->lda : (size_t)d->K * d->lda;
+  const size_t b_ext = d->b_kmajor ? (size_t)d->N * d->ldb : (size_t)d->K * d->ldb;
+  if ((a_ext + 4096) * 2 >= lim || (b_ext + 4096) * 2 >= lim) return SV_ERR_UNSUPPORTED;
+  if (d->a_kmajor && d->b_kmajor) return launch_epi<true, true>(d, split, s);
+  if (d->a_kmajor && !d->b_kmajor) return launch_epi<true, false>(d, split, s);
+  if (!d->a_kmajor && d->b_kmajor) return launch_epi<false, true>(d, split, s);
+  return launch_epi<false, false>(d, split, s);
+}
+
+}  // namespace sv

@@ -370,5 +370,7 @@ int launch_gemm2(const sv_gemm_desc* d, hipStream_t s);
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg = nullptr);
 // v8 entry (gemm8.hip, 256x256 tile, 8 waves, one workgroup per CU): same contract as v3
 int launch_gemm8(const sv_gemm_desc* d, hipStream_t s);
+// v9 entry (gemm9.hip, persistent 256x256 BK 64 phase-interleaved, register-direct epilogue)
+int launch_gemm9(const sv_gemm_desc* d, hipStream_t s);
 
 }  // namespace sv

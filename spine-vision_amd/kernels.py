@@ -165,6 +165,20 @@ def _wgrad_split(tiles: int, K: int) -> int:
     return max(1, min(split, K // 512 if K >= 512 else 1))
 
 
+def _wgrad_split_for(N: int, K: int, M: int) -> int:
+    """Split-K factor of a weight gradient G[N,K] = dY[M,N]^T X[M,K].  Outputs at least 256 x 256 run on
+    the persistent 256x256 kernel (gemm9.hip): one tile per CU (tiles * split ~ 256 CUs) with every K
+    slice a whole number of 64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
+    if N >= 256 and K >= 256:
+        tiles9 = -(-N // 256) * -(-K // 256)
+        split = max(1, 256 // tiles9)
+        while split > 1 and M % (split * 64):
+            split -= 1
+        if M % (split * 64) == 0:
+            return split
+    return _wgrad_split(-(-N // 128) * -(-K // 128), M)
+
+
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
                  compute_bf16=True, cols=None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
@@ -174,8 +188,7 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     M, N = dy2d.shape
     ldx = x2d.shape[1]
     K = ldx if cols is None else cols
-    tiles = -(-N // 128) * -(-K // 128)
-    split = _wgrad_split(tiles, M)
+    split = _wgrad_split_for(N, K, M)
     slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
     gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
@@ -205,8 +218,7 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     never materialised."""
     M, C = dsrc2d.shape
     K4 = a2d.shape[1]
-    tiles = -(-C // 128) * -(-K4 // 128)
-    split = _wgrad_split(tiles, M)
+    split = _wgrad_split_for(C, K4, M)
     slab = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.float32)
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
     gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,

@@ -1,0 +1,13 @@
+#!/bin/bash
+# v9 GEMM: family parity, standalone timings (impl 0 vs 9), then the step A/B of the dispatch modes
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${1:-g9b}
+mkdir -p "$OUT"
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gemm_family_gpu.py > "$OUT/tests.log" 2>&1
+rc=$?; echo "tests rc=$rc $(tail -1 $OUT/tests.log)"
+[ $rc -ne 0 ] && { grep -E "Error|assert|FAIL" "$OUT/tests.log" | head -20; exit $rc; }
+timeout -k 10 400 python -u tools/gemm_bench.py --stages S2,S3,S4 --iters 20 --impls 0,9 --cases fc2_wgrad,fc1_wgrad,fc1_fwd\(dual,fc2_dgrad\(mul > "$OUT/gemm.txt" 2> "$OUT/gemm.err"
+rc=$?; echo "gemm rc=$rc"; cat "$OUT/gemm.txt"
+[ $rc -ne 0 ] && exit $rc
+bash tools/gpu_v9ab.sh ${1:-g9b}/ab
