@@ -129,6 +129,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+// LDS read the compiler does not see: its alias analysis would otherwise drain every LDS-DMA in flight
+// (vmcnt(0)) before an LDS read it cannot prove disjoint from them; the data is ordered by the K
+// loop's own waits and barriers
+__device__ __forceinline__ float4 lds_f4(const float* p) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t v;
+  const uint32_t a = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
 }
@@ -151,7 +162,8 @@ struct EpiCount {
 // Arithmetic identical to wave_group_epilogue (gemm_common.h).
 template <int EPI, bool P8>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
-                                         int split) {
+                                         int split, const float* lbias) {
+  // lbias: the tile's bias[256] and gamma[256] staged in LDS (K loop, first K-tile), or nullptr
   constexpr int CH = P8 ? 2 : 4, CW = P8 ? 8 : 4;
   const int l = threadIdx.x & 63, ml = l & 15, gq = l >> 4;
   int n[CH];
@@ -168,27 +180,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int w = 0; w < CW; ++w) bias[c][w] = 0.f, gam[c][w] = 1.f;
+  const int wcol = n_w & 255;  // the wave's first column inside the tile
+  auto ld_vec = [&](const float* g, int lo, int c, float (&dst)[CH][CW]) {
+#pragma unroll
+    for (int w = 0; w < CW; w += 4) {
+      float4 b;
+      if (lbias) b = lds_f4(lbias + lo + wcol + (n[c] - n_w) + w);
+      else b = okn[c] ? *reinterpret_cast<const float4*>(g + n[c] + w) : make_float4(0.f, 0.f, 0.f, 0.f);
+      dst[c][w] = b.x, dst[c][w + 1] = b.y, dst[c][w + 2] = b.z, dst[c][w + 3] = b.w;
+    }
+  };
   if (has_bias && e.bias) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c)
-      if (okn[c]) {
-#pragma unroll
-        for (int w = 0; w < CW; w += 4) {
-          const float4 b = *reinterpret_cast<const float4*>(e.bias + n[c] + w);
-          bias[c][w] = b.x, bias[c][w + 1] = b.y, bias[c][w + 2] = b.z, bias[c][w + 3] = b.w;
-        }
-      }
+    for (int c = 0; c < CH; ++c) ld_vec(e.bias, 0, c, bias);
   }
   if (EPI == SV_EPI_BIAS_GAMMA_RES && e.gamma) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c)
-      if (okn[c]) {
-#pragma unroll
-        for (int w = 0; w < CW; w += 4) {
-          const float4 g = *reinterpret_cast<const float4*>(e.gamma + n[c] + w);
-          gam[c][w] = g.x, gam[c][w + 1] = g.y, gam[c][w + 2] = g.z, gam[c][w + 3] = g.w;
-        }
-      }
+    for (int c = 0; c < CH; ++c) ld_vec(e.gamma, 256, c, gam);
   }
   const int64_t ldc = slab ? e.N : e.ldc;
   const char* cbase = reinterpret_cast<const char*>(e.C);
@@ -368,6 +376,10 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   };
 
   constexpr int E = EpiCount<EPI, P8>::E;
+  // forward epilogues read the tile's bias (and gamma) from LDS, staged by DMA: a plain global load
+  // in the epilogue would make the compiler drain every DMA in flight (vmcnt(0)) at each tile's end
+  constexpr bool LBIAS = AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
+                                EPI == SV_EPI_BIAS_GAMMA_RES);
   // DMAs younger than the W1 / W2 targets in steady state (see the phase comments below)
   constexpr int W1 = AK ? 10 : 8, W2 = 10;
   constexpr int W1E = W1 + E > 63 ? 63 : W1 + E, W2E = W2 + E > 63 ? 63 : W2 + E;
@@ -455,6 +467,17 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       // phase 0: A quadrant-0 rows and B columns 0-31 of the wave
       read_a(0);
       read_b(0);
+      if constexpr (LBIAS) {
+        // the tile's bias / gamma columns into LDS (slot by tile parity: the other group may still be
+        // in the previous tile's epilogue); retired by the W1 wait of the next K-tile (nk >= 2) or
+        // by the wait before the epilogue
+        if (kt == 0 && wid < 2) {
+          const float* src = wid == 0 ? e.bias : e.gamma;
+          if (src && (wid == 0 || EPI == SV_EPI_BIAS_GAMMA_RES))
+            dma(rsrc(src, (uint32_t)e.N * 4), (uint32_t)(cg.n0 + (threadIdx.x & 63) * 4) * 4, 0,
+                smem + lds_bytes<AK>() + (it & 1) * 2048 + wid * 1024);
+        }
+      }
       lgkm0();
       bar();
       quad(0, 0);
@@ -503,10 +526,21 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
         if ((threadIdx.x & 63) < 16 && m < e.M) reinterpret_cast<float*>(e.C2)[(size_t)cg.split * e.M + m] = cs[h];
       }
     }
-    epilogue<EPI, P8>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split);
+    if (LBIAS && nk < 2) {  // the bias DMA was issued in this tile's only K-tile
+      vm_wait<0>();
+      bar();
+    }
+    epilogue<EPI, P8>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
+                      LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
   }
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
   if (wm == 0) bar();
+}
+
+template <bool AK, int EPI>
+constexpr int lds_total() {
+  return lds_bytes<AK>() + ((AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
+                                   EPI == SV_EPI_BIAS_GAMMA_RES)) ? 4096 : 0);
 }
 
 static int num_cus() {
@@ -539,13 +573,13 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<AK>());
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_total<AK, EPI>());
     attr_set = true;
   }
   const int total = tilesM * tilesN * split;
   int grid = num_cus();
   if (grid > total) grid = total;
-  gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_bytes<AK>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
+  gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_total<AK, EPI>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
                                                                   reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
                                                                   tilesM, tilesN, split, e, x);
   return check_launch("sv_gemm(v9)");

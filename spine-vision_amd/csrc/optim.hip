@@ -341,8 +341,20 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
   SV_REQUIRE(!n_b || (part_b && out_b), "sv_reduce_partials_pair: bad second segment");
   if (n_a % 4 == 0) SV_REQUIRE((((uintptr_t)part_a) & 15) == 0, "sv_reduce_partials_pair: part_a must be 16-B aligned");
   if (n_b % 4 == 0 && n_b) SV_REQUIRE((((uintptr_t)part_b) & 15) == 0, "sv_reduce_partials_pair: part_b must be 16-B aligned");
-  RedSeg a{part_a, n_a, out_a}, b{part_b, n_b, out_b};
   hipStream_t s = (hipStream_t)stream;
+  if (P <= 64 && n_a >= 65536 && n_a % 4 == 0 && (((uintptr_t)out_a) & 15) == 0) {
+    // a wide split-K slab (weight gradient): one thread per 4 columns summing the P slices in order
+    // with 8 loads in flight (the partial-row groups of the kernel below would each issue ONE load
+    // per thread before the LDS fold: latency-bound at ~1 TB/s); the narrow b segment follows
+    const int64_t t4 = n_a / 4;
+    reduce_partials_kernel<<<dim3((unsigned)((t4 + kThreads - 1) / kThreads), 1), kThreads, 0, s>>>(part_a, P, P, n_a,
+                                                                                                   out_a, alpha, accumulate);
+    const int rc = check_launch("sv_reduce_partials_pair");
+    if (rc != SV_OK || !n_b) return rc;
+    part_a = part_b, n_a = n_b, out_a = out_b;
+    part_b = nullptr, n_b = 0, out_b = nullptr;
+  }
+  RedSeg a{part_a, n_a, out_a}, b{part_b, n_b, out_b};
   // widest column block that still gives >= 512 workgroups (or 4 columns per workgroup); with few
   // partial rows (split-K slabs: P = 2..8) up to 256 columns, so that no partial-row group idles
   int cols = P <= 4 ? 256 : (P <= 8 ? 128 : 64);
