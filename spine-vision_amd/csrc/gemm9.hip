@@ -22,6 +22,8 @@
 #include "common.h"
 #include "gemm_common.h"
 
+#include <stdlib.h>
+
 namespace sv {
 namespace g9 {
 
@@ -395,13 +397,16 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     else if (wn == 2) f0 = af[2][0], f1 = af[2][1];
     else if (wn == 3) f0 = af[3][0], f1 = af[3][1];
     const bf16x8 f[2] = {f0, f1};
+    // one v_dot2_f32_bf16 against (1, 1) per bf16 pair (f32 accumulation, fixed order)
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    const bf16x2_t ones = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-      const u32x4_t w = __builtin_bit_cast(u32x4_t, f[kh]);
+    for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc_cs += __uint_as_float(w[q] << 16) + __uint_as_float(w[q] & 0xffff0000u);
-    }
+      for (int q = 0; q < 4; ++q) {
+        const bf16x2_t pr = {f[kh][2 * q], f[kh][2 * q + 1]};
+        acc_cs = __builtin_amdgcn_fdot2_f32_bf16(pr, ones, acc_cs, false);
+      }
   };
 
   // prologue: K-tiles 0 and 1, then K-tile 0 landed everywhere
