@@ -351,7 +351,12 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (!bf) return launch_layout<false, float, float>(d, s);
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
   const int impl = g_gemm_impl;
-  if (d->epilogue == SV_EPI_STORE_STATS) {  // only the v3 kernels carry the statistics epilogue
+  if (d->epilogue == SV_EPI_STORE_STATS) {  // the v3 and v9 kernels carry the statistics epilogue
+    const long t9 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
+    if ((impl == 0 || impl == 9) && d->N >= 256 && t9 >= 256 && d->a_kmajor) {
+      const int rc9 = launch_gemm9(d, s);
+      if (rc9 != SV_ERR_UNSUPPORTED) return rc9;
+    }
     const int rc = launch_gemm3(d, s);
     SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_STATS needs K %% 32 == 0 and bf16 operands");
     return rc;
@@ -380,8 +385,12 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
       v9_mode = ev ? atoi(ev) : 2;
     }
     const int split9 = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
-    const bool v9_shape = d->N >= 256 && tiles8 * split9 >= 256 && d->epilogue != SV_EPI_BIAS_GELU2 &&
-                          (d->epilogue != SV_EPI_SLAB || d->M >= 256);
+    // (weight gradients: outputs of at least 128 x 256 in either orientation, the split-K factor sized
+    // for one tile per CU by kernels._wgrad_split_for)
+    const bool v9_slab = d->epilogue == SV_EPI_SLAB && (d->M < d->N ? d->M : d->N) >= 128 &&
+                         (d->M > d->N ? d->M : d->N) >= 256 && tiles8 * split9 >= 128;
+    const bool v9_shape = v9_slab || (d->epilogue != SV_EPI_SLAB && d->epilogue != SV_EPI_BIAS_GELU2 && d->N >= 256 &&
+                                      tiles8 >= 256);
     const bool v9_pick = impl == 0 && v9_shape && (v9_mode == 2 || (v9_mode == 1 && !g_gemm_wg_per_cu));
     int rc = SV_ERR_UNSUPPORTED;
     if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below

@@ -211,8 +211,18 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
   const auto ra = rsrc(e.aux ? e.aux : e.C, x.aux);
   // epilogue operands of HALF row groups at a time (bf16: 32 VGPRs, f32 residual: 32 / 64 VGPRs)
   constexpr int HALF = AUXF ? FM / 4 : FM / 2;
+  // SV_EPI_STORE_STATS: per-lane column sums of one 64-row group (4 row groups = one HALF batch)
+  constexpr bool kStats = EPI == SV_EPI_STORE_STATS;
+  static_assert(!kStats || (P8 && HALF == 4), "statistics need bf16 output and 64-row batches");
+  float st1[kStats ? CH : 1][kStats ? 8 : 1], st2[kStats ? CH : 1][kStats ? 8 : 1];
 #pragma unroll
   for (int hb = 0; hb < FM / HALF; ++hb) {
+    if constexpr (kStats) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) st1[c][w] = st2[c][w] = 0.f;
+    }
     u32x4 raw[HALF][CH][AUXF && P8 ? 2 : 1];
     if constexpr (AUXBF || AUXF) {
 #pragma unroll
@@ -273,7 +283,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
         }
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
-          if constexpr (EPI == SV_EPI_SLAB || EPI == SV_EPI_STORE) {
+          if constexpr (EPI == SV_EPI_SLAB || EPI == SV_EPI_STORE || EPI == SV_EPI_STORE_STATS) {
             o[w] = v[w];
           } else if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) {
             gelu_and_grad(v[w], o2[w], o[w]);  // C = GELU'(h), C2 = GELU(h)
@@ -288,8 +298,21 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
           }
         }
         if constexpr (P8) {
-          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, off, 0, 0);
+          const u32x4 pk = pack8(o);
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
           if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) __builtin_amdgcn_raw_buffer_store_b128(pack8(o2), rc2, off, 0, 0);
+          if constexpr (EPI == SV_EPI_STORE_STATS) {
+            // statistics of the values AS STORED (bf16), rows past M excluded
+            if (m < e.M) {
+              const uint32_t wd[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+              for (int w = 0; w < 8; ++w) {
+                const float q = __uint_as_float((w & 1) ? (wd[w >> 1] & 0xffff0000u) : (wd[w >> 1] << 16));
+                st1[c][w] += q;
+                st2[c][w] = fmaf(q, q, st2[c][w]);
+              }
+            }
+          }
         } else {
           const u32x4 d = {__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
           __builtin_amdgcn_raw_buffer_store_b128(d, rc, off, 0, 0);
@@ -299,6 +322,31 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
             __builtin_amdgcn_raw_buffer_store_b128(d2, rc2, off, 0, 0);
           }
         }
+      }
+    }
+    if constexpr (kStats) {
+      // the 16 lanes l & 15 hold the group's 64 rows 4 at a time: fold them (fixed order), then lane
+      // group gq writes its 8 columns of the group's partial row [mb / 64][2][N] (one writer each)
+      const int mb = m_w + 64 * hb;
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) {
+            st1[c][w] += __shfl_xor(st1[c][w], off);
+            st2[c][w] += __shfl_xor(st2[c][w], off);
+          }
+      if (ml == 0 && mb < e.M) {
+        float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          if (okn[c]) {
+            *reinterpret_cast<float4*>(P + n[c]) = make_float4(st1[c][0], st1[c][1], st1[c][2], st1[c][3]);
+            *reinterpret_cast<float4*>(P + n[c] + 4) = make_float4(st1[c][4], st1[c][5], st1[c][6], st1[c][7]);
+            *reinterpret_cast<float4*>(P + e.N + n[c]) = make_float4(st2[c][0], st2[c][1], st2[c][2], st2[c][3]);
+            *reinterpret_cast<float4*>(P + e.N + n[c] + 4) = make_float4(st2[c][4], st2[c][5], st2[c][6], st2[c][7]);
+          }
       }
     }
   }
@@ -381,7 +429,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   // forward epilogues read the tile's bias (and gamma) from LDS, staged by DMA: a plain global load
   // in the epilogue would make the compiler drain every DMA in flight (vmcnt(0)) at each tile's end
   constexpr bool LBIAS = AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
-                                EPI == SV_EPI_BIAS_GAMMA_RES);
+                                EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS);
   // DMAs younger than the W1 / W2 targets in steady state (see the phase comments below)
   constexpr int W1 = AK ? 10 : 8, W2 = 10;
   constexpr int W1E = W1 + E > 63 ? 63 : W1 + E, W2E = W2 + E > 63 ? 63 : W2 + E;
@@ -545,7 +593,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 template <bool AK, int EPI>
 constexpr int lds_total() {
   return lds_bytes<AK>() + ((AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
-                                   EPI == SV_EPI_BIAS_GAMMA_RES)) ? 4096 : 0);
+                                   EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS)) ? 4096 : 0);
 }
 
 static int num_cus() {
@@ -614,6 +662,9 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
       if (d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
       return bf_out ? launch<AK, BKM, SV_EPI_GELU_GRAD, true>(d, split, s)
                     : launch<AK, BKM, SV_EPI_GELU_GRAD, false>(d, split, s);
+    case SV_EPI_STORE_STATS:
+      if (!bf_out || !AK || d->N % 8) return SV_ERR_UNSUPPORTED;
+      return launch<AK, BKM, SV_EPI_STORE_STATS, true>(d, split, s);
     case SV_EPI_SLAB:
       if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
       return launch<AK, BKM, SV_EPI_SLAB, false>(d, split, s);

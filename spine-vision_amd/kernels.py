@@ -166,10 +166,11 @@ def _wgrad_split(tiles: int, K: int) -> int:
 
 
 def _wgrad_split_for(N: int, K: int, M: int) -> int:
-    """Split-K factor of a weight gradient G[N,K] = dY[M,N]^T X[M,K].  Outputs at least 256 x 256 run on
-    the persistent 256x256 kernel (gemm9.hip): one tile per CU (tiles * split ~ 256 CUs) with every K
-    slice a whole number of 64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
-    if N >= 256 and K >= 256:
+    """Split-K factor of a weight gradient G[N,K] = dY[M,N]^T X[M,K].  Outputs of at least 128 x 256 run
+    on the persistent 256x256 kernel (gemm9.hip; a 128-row output half-fills its tiles and still beats
+    the 256x128 kernel): one tile per CU (tiles * split ~ 256 CUs) with every K slice a whole number of
+    64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
+    if min(N, K) >= 128 and max(N, K) >= 256:
         tiles9 = -(-N // 256) * -(-K // 256)
         split = max(1, 256 // tiles9)
         while split > 1 and M % (split * 64):
