@@ -75,45 +75,51 @@ __device__ __forceinline__ void wait_rows(int younger) {
 
 __device__ __forceinline__ int wave_id_uniform() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// Column offsets of a strip (uniform, computed once): colo[j] = (wstart + j) * C, or -1 when the
-// column lies outside the image.
-template <int NCOL>
-__device__ __forceinline__ void dw_cols(const DwGeo& g, int wstart, int (&colo)[NCOL]) {
-#pragma unroll
-  for (int j = 0; j < NCOL; ++j) {
-    const int w = wstart + j;
-    colo[j] = (w >= 0 && w < g.W) ? w * g.C : -1;
-  }
-}
+// LDS image of one input row: NCOL columns x the wave's 64 channels, packed ([column][channel], 64 *
+// sizeof(T) bytes per column).  DMA'd 16 B per lane (global_load_lds_dwordx4): one instruction moves
+// 1 KiB = CPD columns (4 f32 / 8 bf16), lane L fetching channels (L % LPC) * EPL .. of column L / LPC.
+// Round 1 moved one 4-B dword per lane per column (10 DMAs per f32 or bf16 row of a 4-wide strip,
+// 256 B each): the kernels took the same time for bf16 and f32 inputs, i.e. they were DMA-issue-bound.
+template <typename T>
+struct DwRow {
+  static constexpr int CB = 64 * (int)sizeof(T);  // bytes per column
+  static constexpr int CPD = 1024 / CB;           // columns per DMA instruction
+  static constexpr int LPC = 64 / CPD;            // lanes per column
+  static constexpr int EPL = 16 / (int)sizeof(T);  // elements per lane chunk
+  template <int NCOL>
+  static constexpr int nd() { return (NCOL + CPD - 1) / CPD; }  // DMA instructions per row
+  template <int NCOL>
+  static constexpr int bytes() { return nd<NCOL>() * 1024; }
+};
 
-// DMA NCOL columns of row h of the wave's 64-channel group into dst (one dword per lane per
-// column: LDS-DMA writes M0 + 4*lane whatever the load size, a bf16 lands zero-extended in the low
-// half).  xg = x + c0 (uniform); out-of-image columns/rows read the zero page.  Per column: one
-// scalar add + select for the address, one M0 write, one DMA.
+// DMA the NCOL columns wstart .. wstart+NCOL-1 of row h of the wave's channel group (xg = x + c0,
+// uniform) into dst.  Out-of-image rows / columns, and the columns past NCOL that fill the last
+// instruction, read the zero page, so every row costs the same fixed number of DMAs.
 template <int NCOL, typename T>
-__device__ __forceinline__ void dma_row(const T* __restrict__ xg, const DwGeo& g, int b, int h, const int (&colo)[NCOL],
-                                        int lane, char* dst) {
+__device__ __forceinline__ void dma_row(const T* __restrict__ xg, const DwGeo& g, int b, int h, int wstart, int lane,
+                                        char* dst) {
+  using R = DwRow<T>;
   const bool okh = h >= 0 && h < g.H;
   const T* rowp = xg + (size_t)((b * g.H + (okh ? h : 0)) * g.W) * g.C;
   const T* zero = reinterpret_cast<const T*>(dw_zero_page);
+  const int jl = lane / R::LPC, ch = (lane % R::LPC) * R::EPL;
 #pragma unroll
-  for (int j = 0; j < NCOL; ++j) {
-    const T* src = (okh && colo[j] >= 0) ? rowp + colo[j] : zero;
-    if constexpr (sizeof(T) == 4)
-      __builtin_amdgcn_global_load_lds((const void*)(src + lane), (dw_lds_void*)(dst + j * 256), 4, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)(src + lane), (dw_lds_void*)(dst + j * 256), 2, 0, 0);
+  for (int d = 0; d < R::template nd<NCOL>(); ++d) {
+    const int j = d * R::CPD + jl, w = wstart + j;
+    const bool ok = okh && j < NCOL && w >= 0 && w < g.W;
+    const T* src = ok ? rowp + (size_t)w * g.C + ch : zero + ch;
+    __builtin_amdgcn_global_load_lds((const void*)src, (dw_lds_void*)(dst + d * 1024), 16, 0, 0);
   }
 }
 template <typename T>
-__device__ __forceinline__ float lds_ld(const char* col, int lane) {
-  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const float*>(col + lane * 4);
-  else return bf2f(*reinterpret_cast<const uint16_t*>(col + lane * 4));
+__device__ __forceinline__ float lds_ld(const char* row, int j, int lane) {
+  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const float*>(row + j * DwRow<T>::CB + lane * 4);
+  else return bf2f(*reinterpret_cast<const uint16_t*>(row + j * DwRow<T>::CB + lane * 2));
 }
 
 template <int PF, int TW, typename TIN>
 constexpr size_t dw_ring_lds() {
-  return (size_t)(kDwThreads / 64) * PF * (TW + 6) * 256;
+  return (size_t)(kDwThreads / 64) * PF * DwRow<TIN>::template bytes<TW + 6>();
 }
 
 template <int PF, int TW, typename TIN, typename TOUT, bool FLIP, bool ACCUM>
@@ -124,7 +130,8 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_ring_kernel(const TIN* __r
                                                                   uint16_t* __restrict__ out_bf16, DwGeo g) {
   extern __shared__ __attribute__((aligned(16))) char dw_smem[];
   constexpr int TC = TW + 6;
-  constexpr int ROWB = TC * 256;
+  constexpr int ROWB = DwRow<TIN>::template bytes<TC>();
+  constexpr int NL = DwRow<TIN>::template nd<TC>();  // DMA instructions per row
   const int lane = threadIdx.x & 63, wv = wave_id_uniform();
   const int gw = blockIdx.x * (kDwThreads / 64) + wv;
   const int ncg = g.C / 64;
@@ -149,22 +156,20 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_ring_kernel(const TIN* __r
   float pcur[TW], pnew[TW];
 #pragma unroll
   for (int o = 0; o < TW; ++o) pcur[o] = pnew[o] = 0.f;
-  int colo[TC];
-  dw_cols(g, w0 - 3, colo);
 #pragma unroll
-  for (int p = 0; p < PF - 1; ++p) dma_row<TC>(xg, g, b, h0 - 3 + p, colo, lane, ring + p * ROWB);
+  for (int p = 0; p < PF - 1; ++p) dma_row<TC>(xg, g, b, h0 - 3 + p, w0 - 3, lane, ring + p * ROWB);
 #pragma nounroll
   for (int ib = 0; ib < TR; ib += 7) {
 #pragma unroll
     for (int u = 0; u < 7; ++u) {
       const int ir = ib + u;
       if (ir >= TR) break;
-      if (ir + PF - 1 < TR) dma_row<TC>(xg, g, b, h0 - 3 + ir + PF - 1, colo, lane, ring + ((ir + PF - 1) % PF) * ROWB);
+      if (ir + PF - 1 < TR) dma_row<TC>(xg, g, b, h0 - 3 + ir + PF - 1, w0 - 3, lane, ring + ((ir + PF - 1) % PF) * ROWB);
       const int rem = TR - 1 - ir;
-      wait_rows<PF, TC>(rem < PF - 1 ? rem : PF - 1);
+      wait_rows<PF, NL>(rem < PF - 1 ? rem : PF - 1);
       const char* row = ring + (ir % PF) * ROWB;
 #pragma unroll
-      for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row + j * 256, lane);
+      for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row, j, lane);
       if (ACCUM && ir >= 5 && ir - 5 < TH) {
         const int h = h0 + ir - 5;
         if (h < g.H) {
@@ -216,7 +221,7 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_ring_kernel(const TIN* __r
 // instruction count fixed and contributes nothing)
 template <int PF, int TW, typename TDZ, typename TIN>
 constexpr size_t dw_wgrad_ring_lds() {
-  return (size_t)(kDwThreads / 64) * PF * (2 * TW + 6) * 256;
+  return (size_t)(kDwThreads / 64) * PF * (DwRow<TIN>::template bytes<TW + 6>() + DwRow<TDZ>::template bytes<TW>());
 }
 
 template <int PF, int TW, typename TDZ, typename TIN>
@@ -226,9 +231,11 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
                                                                         float* __restrict__ db_part, DwGeo g) {
   extern __shared__ __attribute__((aligned(16))) char dw_smem[];
   constexpr int TC = TW + 6;
-  constexpr int ROWB = (TC + TW) * 256;
+  constexpr int XB = DwRow<TIN>::template bytes<TC>();  // x part of a ring slot; the dz row follows
+  constexpr int ROWB = XB + DwRow<TDZ>::template bytes<TW>();
+  constexpr int NL = DwRow<TIN>::template nd<TC>() + DwRow<TDZ>::template nd<TW>();
   const int lane = threadIdx.x & 63, wv = wave_id_uniform();
-  const int c0 = blockIdx.y * 64, c = c0 + lane;
+  const int c0 = blockIdx.y * 64;
   const TIN* xg = x + c0;
   const TDZ* dg = dz + c0;
   char* ring = dw_smem + wv * PF * ROWB;
@@ -239,13 +246,10 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
   for (int tile = blockIdx.x * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
     int b, h0, w0;
     dw_tile(g, tile, b, h0, w0);
-    int colx[TC], cold[TW];
-    dw_cols(g, w0 - 3, colx);
-    dw_cols(g, w0, cold);
     auto issue = [&](int ir) {
       char* slot = ring + (ir % PF) * ROWB;
-      dma_row<TC>(xg, g, b, h0 - 3 + ir, colx, lane, slot);
-      dma_row<TW>(dg, g, b, ir < TH ? h0 + ir : -1, cold, lane, slot + TC * 256);
+      dma_row<TC>(xg, g, b, h0 - 3 + ir, w0 - 3, lane, slot);
+      dma_row<TW>(dg, g, b, ir < TH ? h0 + ir : -1, w0, lane, slot + XB);
     };
     float dzb[7][TW];
     float in[TC];
@@ -259,14 +263,14 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
         if (ir >= TR) break;
         if (ir + PF - 1 < TR) issue(ir + PF - 1);
         const int rem = TR - 1 - ir;
-        wait_rows<PF, TC + TW>(rem < PF - 1 ? rem : PF - 1);
+        wait_rows<PF, NL>(rem < PF - 1 ? rem : PF - 1);
         const char* row = ring + (ir % PF) * ROWB;
 #pragma unroll
-        for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row + j * 256, lane);
+        for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row, j, lane);
         if (ir < TH) {
 #pragma unroll
           for (int o = 0; o < TW; ++o) {
-            const float v = lds_ld<TDZ>(row + (TC + o) * 256, lane);
+            const float v = lds_ld<TDZ>(row + XB, o, lane);
             dzb[u][o] = v;
             dbacc += v;
           }
