@@ -379,11 +379,6 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
                                             ((d->epilogue == SV_EPI_BIAS_GAMMA_RES) && d->K >= 2048));
     // v9 (persistent 256x256, BK 64 phase-interleaved, register-direct epilogue) where the chip holds
     // a full wave of its tiles and N fills the 256-wide tile
-    static int v9_mode = -1;
-    if (v9_mode < 0) {
-      const char* ev = getenv("SV_V9");
-      v9_mode = ev ? atoi(ev) : 2;
-    }
     const int split9 = d->epilogue == SV_EPI_SLAB ? (d->split_k < 1 ? 1 : d->split_k) : 1;
     // (weight gradients: outputs of at least 128 x 256 in either orientation, the split-K factor sized
     // for one tile per CU by kernels._wgrad_split_for)
@@ -391,7 +386,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
                          (d->M > d->N ? d->M : d->N) >= 256 && tiles8 * split9 >= 128;
     const bool v9_shape = v9_slab || (d->epilogue != SV_EPI_SLAB && d->epilogue != SV_EPI_BIAS_GELU2 && d->N >= 256 &&
                                       tiles8 >= 256);
-    const bool v9_pick = impl == 0 && v9_shape && (v9_mode == 2 || (v9_mode == 1 && !g_gemm_wg_per_cu));
+    const bool v9_pick = impl == 0 && v9_shape;
     int rc = SV_ERR_UNSUPPORTED;
     if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below
     if (rc != SV_ERR_UNSUPPORTED) return rc;
