@@ -433,7 +433,24 @@ def test_layernorm_bwd_bf16_io(dev, C, dy_f32):
     assert rel(db, dy.double().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64)])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64), (1, 37, 45, 256), (2, 9, 7, 192)])
+def test_dwconv7_fwd_bf16_io(dev, shape):
+    """bf16 input / bf16 output forward (the bf16 step's x is f32, the lean paths feed bf16); C % 128 == 0
+    runs the two-channels-per-lane kernel, 64 / 192 the one-channel kernel."""
+    B, H, W, C = shape
+    g = torch.Generator().manual_seed(B * H * W + C + 11)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    w = torch.randn(C, 1, 7, 7, generator=g) * 0.1
+    bias = torch.randn(C, generator=g) * 0.1
+    ones, zeros = torch.ones(C), torch.zeros(C)
+    z, _, _, _ = K.dwconv7_ln_fwd(x.to(dev), w.to(dev), bias.to(dev), ones.to(dev), zeros.to(dev),
+                                  act_dtype=torch.bfloat16)
+    zr = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), bias.double(), padding=3, groups=C)
+    assert z.dtype == torch.bfloat16
+    assert rel(z.view(B, H, W, C), zr.permute(0, 2, 3, 1)) < 8e-3  # output rounded to bf16
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 16, 128), (1, 13, 11, 64), (1, 37, 45, 256)])
 def test_dwconv7_bwd_bf16_dz(dev, shape):
     B, H, W, C = shape
     g = torch.Generator().manual_seed(B * H * W + C + 7)
