@@ -312,10 +312,14 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
   if (threadIdx.x < 64) db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = redb[threadIdx.x];
 }
 
-// ring depths: PF 4 rows for fwd / bwd-data; the wgrad ring holds x AND dz rows (14 columns), so depth 2
-// keeps 4 workgroups per CU (measured: 2 >= 3, 4 on the S1/S3 shapes).  Strip width 4 keeps a lane
+// ring depths: f32 input rows (3 KiB for a 4-wide strip) 3 deep, so four workgroups fit a CU as with bf16
+// rows (2 KiB) 4 deep (measured, f32 4 -> 3: S3 bwd-data over an f32 gradient 57-64 -> 46-51 us, the step
+// unchanged within noise; bf16 4 -> 5 or 6 slower); the wgrad ring holds x AND dz rows (14 columns), so
+// depth 2 keeps 4 workgroups per CU (measured: 2 >= 3, 4 on the S1/S3 shapes).  Strip width 4 keeps a lane
 // within 3 waves/SIMD; the register-prefetch (no ring) kernels and 8-wide strips measured slower (round 1).
-constexpr int DW_PF = 4, DW_WGRAD_PF = 2, DW_TW = 4;
+constexpr int DW_PF_F32 = 3, DW_PF_BF16 = 4, DW_WGRAD_PF = 2, DW_TW = 4;
+template <typename T>
+constexpr int dw_pf() { return sizeof(T) == 4 ? DW_PF_F32 : DW_PF_BF16; }
 
 static DwGeo dw_geo(int B, int H, int W, int C) {
   DwGeo g{B, H, W, C, DW_TW, (W + DW_TW - 1) / DW_TW, (H + TH - 1) / TH, 0};
@@ -342,7 +346,7 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
 #define RLAUNCH(TI, TO)                                                                                         \
-  dwconv7_ring_kernel<DW_PF, DW_TW, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<DW_PF, DW_TW, TI>(), s>>>( \
+  dwconv7_ring_kernel<dw_pf<TI>(), DW_TW, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<dw_pf<TI>(), DW_TW, TI>(), s>>>( \
       (const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
   if (x_dtype == SV_F32 && z_dtype == SV_F32) RLAUNCH(float, float);
   else if (x_dtype == SV_F32 && z_dtype == SV_BF16) RLAUNCH(float, uint16_t);
@@ -366,7 +370,7 @@ int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, floa
   const DwGeo g = dw_geo(B, H, W, C);
   const int grid = dw_blocks(g);
 #define RBWD(TD, ACC)                                                                                             \
-  dwconv7_ring_kernel<DW_PF, DW_TW, TD, float, true, ACC><<<grid, kDwThreads, dw_ring_lds<DW_PF, DW_TW, TD>(), s>>>( \
+  dwconv7_ring_kernel<dw_pf<TD>(), DW_TW, TD, float, true, ACC><<<grid, kDwThreads, dw_ring_lds<dw_pf<TD>(), DW_TW, TD>(), s>>>( \
       (const TD*)dz, wdw, nullptr, dx, dx_bf16, g)
   if (dz_dtype == SV_F32) {
     if (accumulate) RBWD(float, true); else RBWD(float, false);
