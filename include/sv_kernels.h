@@ -316,7 +316,10 @@ int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, i
  * long K = taps x channels): the gathered GEMM writes `split` f32 slabs [split][M][N] into `work`
  * (split * M * N floats), then sv_gemm_slab_finish sums them into y (+ the STORE_STATS partials when
  * stats != NULL) / into dx (+= when accumulate, f32 dx).  bf16 gathered-operand shapes only (as
- * sv_conv_fwd_stats; dgrad: stride 1, Cout >= 32); others are an error.                             */
+ * sv_conv_fwd_stats; dgrad: stride 1, Cout >= 32); others are an error.
+ * Stride-2 dgrad (bf16, Cout >= 32, Cs % 8 == 0): one gathered GEMM per output parity class writes
+ * compact slabs into `work` (split * B*H*W*Cs floats in all), one pass scatters them into dx (+= when
+ * accumulate; dx f32 or bf16).                                                                       */
 int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
                       float* stats, float* work, int32_t split, sv_stream_t stream);
 int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,

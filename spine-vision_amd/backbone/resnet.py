@@ -20,6 +20,7 @@ spine_vision/training/models/backbone.py:166-170 (names at backbone.py:27,29; ti
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -115,6 +116,11 @@ class ResNetHip(nn.Module):
         self.num_features = inplanes
         self.grad_ready_hook: Callable[[list], None] | None = None
         self._shadow: dict[int, torch.Tensor] | None = None
+        # bf16 backward: the weight gradients (split-K gather GEMMs + slab finishes) of each block run on a
+        # side stream beside the data-gradient / BatchNorm chain of the next one, one main->side hand-off
+        # per block (SV_SIDE_STREAM=0: off, every kernel on the current stream, bitwise the same result)
+        self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
+        self._side: dict = {}
         self._init_weights()
 
     def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
@@ -261,12 +267,35 @@ class ResNetHip(nn.Module):
         if self.grad_ready_hook is not None:
             self.grad_ready_hook(params)
 
+    def _side_stream(self, device) -> torch.cuda.Stream:
+        if device not in self._side:
+            self._side[device] = torch.cuda.Stream(device=device)
+        return self._side[device]
+
+    def _flush_wgrads(self, jobs: list, params: list, side, keep: list) -> None:
+        """Run the block's weight gradients (conv_bwd_weight jobs) and report its parameters ready.  With a
+        side stream: one hand-off (the side stream waits for everything the main stream has issued, so the
+        grad-ready event it records also covers the BatchNorm gradients), and the operands stay referenced
+        in ``keep`` until the streams join (the main stream's allocator may not reuse them earlier)."""
+        if side is None:
+            for dy4, x, s, dw in jobs:
+                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
+            self._ready(params)
+            return
+        side.wait_event(torch.cuda.current_stream().record_event())
+        with torch.cuda.stream(side):
+            for dy4, x, s, dw in jobs:
+                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
+            self._ready(params)
+        keep.append(jobs)
+
     @torch.no_grad()
-    def _block_backward(self, blk, saved_block, d: torch.Tensor) -> torch.Tensor:
+    def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None) -> torch.Tensor:
         """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
         block's parameter gradients and returns dL/d(block input) (f32)."""
         act = self.act_dtype
         g = self._grad
+        jobs = []
         x_in, saved, ds_saved, out = saved_block
         convs = blk.convs()
         Bq, Hq, Wq, Cq = out.shape
@@ -282,7 +311,7 @@ class ResNetHip(nn.Module):
             conv, bn, _, _, _, _ = convs[ci]
             cur_in, y, mean, rstd, a, wp, s = saved[ci]
             dy4 = dy.view(y.shape)
-            K.conv_bwd_weight(dy4, cur_in, s, dw=g(conv.weight), accumulate=True)
+            jobs.append((dy4, cur_in, s, g(conv.weight)))
             params.append(conv.weight)
             if ci == 0:
                 break
@@ -302,30 +331,36 @@ class ResNetHip(nn.Module):
             dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
                            dx_dtype=act)
             dyd4 = dyd.view(yd.shape)
-            K.conv_bwd_weight(dyd4, x_in, sd, dw=g(dconv.weight), accumulate=True)
+            jobs.append((dyd4, x_in, sd, g(dconv.weight)))
             dx = K.conv_bwd_data(dyd4, wpd, sd, dx_dtype=torch.float32)
             params += [dconv.weight, dbn.weight, dbn.bias]
         else:
             dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
         K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
-        self._ready(params)
+        self._flush_wgrads(jobs, params, side, keep)
         return dx
 
     @torch.no_grad()
     def _backward_impl(self, tape: _Tape, dfeat: torch.Tensor) -> None:
         act = self.act_dtype
         g = self._grad
+        main = torch.cuda.current_stream()
+        side = self._side_stream(main.device) if (self.overlap_wgrad and self.compute_bf16) else None
+        keep: list = []
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
         for blk, saved_block in zip(reversed(list(self.blocks())), reversed(tape.blocks)):
-            d = self._block_backward(blk, saved_block, d)
+            d = self._block_backward(blk, saved_block, d, side, keep)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
         da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
         dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
                        dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act)
-        K.conv_bwd_weight(dy0.view(y0.shape), x0, s0, dw=g(self.conv1.weight), accumulate=True)
-        self._ready([self.conv1.weight, self.bn1.weight, self.bn1.bias])
+        self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
+                           [self.conv1.weight, self.bn1.weight, self.bn1.bias], side, keep)
+        if side is not None:
+            main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
+        keep.clear()
 
 
 def create_resnet(name: str, precision: str = "bf16") -> ResNetHip:

@@ -475,6 +475,75 @@ __global__ void wgrad_finish_kernel(const float* __restrict__ slab, int split, i
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
+// transposed-slab form (CONV 4): dw[co][c][t] (+)= sum_s slab[s][t*Cs + c][co].  A workgroup owns 64
+// consecutive slab elements (lane = element: 256-B coalesced loads) and its 4 waves take every 4th split
+// (4 loads in flight each), folded through LDS in a fixed order; the split sums were a serial chain per
+// thread over up to ~170 slabs on 100-150 workgroups (42-61 us for 25 MB).
+__global__ void __launch_bounds__(256) wgrad_finish_t_kernel(const float* __restrict__ slab, int split, int Cout,
+                                                             int Cin, int T_, int Cs, float* __restrict__ dw,
+                                                             int accumulate) {
+  __shared__ float red[4][64];
+  const int64_t n = (int64_t)Cout * T_ * Cs;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    int q = w;
+    for (; q + 12 < split; q += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += slab[(size_t)(q + 4 * u) * n + i];
+    }
+    for (; q < split; q += 4) a[0] += slab[(size_t)q * n + i];
+  }
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (w != 0 || i >= n) return;
+  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  const int co = (int)(i % Cout);
+  const int m = (int)(i / Cout);
+  const int c = m % Cs, t = m / Cs;
+  if (c >= Cin) return;
+  float* o = dw + ((size_t)co * Cin + c) * T_ + t;
+  *o = accumulate ? *o + s : s;
+}
+
+// stride-2 dgrad on the gathered GEMM: each output parity class (py, px) was computed into its own
+// compact f32 slab region [split][B*GHc*GWc][Cs]; this pass sums the splits and scatters the rows back
+// into dx [B][H][W][Cs] (+= when accumulating).  One thread per 4 channels, dx in natural order.
+struct ClassSlabs {
+  const float* base[4];  // nullptr: the class receives no gradient (1x1 stride 2: three of the four)
+  int GH[4], GW[4];
+};
+template <typename T>
+__global__ void __launch_bounds__(256) dgrad_s2_scatter_kernel(ClassSlabs cs, int split, int B, int H, int W, int Cs,
+                                                               T* __restrict__ dx, int accumulate) {
+  const int64_t n4 = (int64_t)B * H * W * Cs / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int c = (int)((i * 4) % Cs);
+  const int64_t pix = i * 4 / Cs;
+  const int x = (int)(pix % W);
+  const int64_t by = pix / W;
+  const int y = (int)(by % H), b = (int)(by / H);
+  const int cls = ((y & 1) << 1) | (x & 1);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* sb = cs.base[cls];
+  if (sb) {
+    const int64_t rows = (int64_t)B * cs.GH[cls] * cs.GW[cls];
+    const int64_t r = ((int64_t)b * cs.GH[cls] + (y >> 1)) * cs.GW[cls] + (x >> 1);
+    for (int q = 0; q < split; ++q) {
+      const float4 u = *reinterpret_cast<const float4*>(sb + ((size_t)q * rows + r) * Cs + c);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+  }
+  const size_t o = (size_t)pix * Cs + c;
+  if (accumulate) {
+    const float4 d = ld4(dx, o);
+    v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+  }
+  st4(dx, o, v);
+}
+
 // ---- host helpers -----------------------------------------------------------------------------
 static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 static int ilog2(int v) {
@@ -736,7 +805,55 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
     const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
-  SV_REQUIRE(!slab, "sv_conv_bwd_data_split: shape not on the gathered bf16 GEMM path (stride 1, Cout >= 32)");
+  if (dtype == SV_BF16 && st == 2 && slab && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
+    // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass
+    ClassSlabs cs{};
+    float* next = slab;
+    for (int py = 0; py < 2; ++py)
+      for (int px = 0; px < 2; ++px) {
+        const int cls = py * 2 + px;
+        const int GH = (s->H - py + 1) / 2, GW = (s->W - px + 1) / 2;
+        cs.GH[cls] = GH;
+        cs.GW[cls] = GW;
+        cs.base[cls] = nullptr;
+        if (GH <= 0 || GW <= 0) continue;
+        ConvG g = make_convg(OH, OW, s->Cout, GH, GW, 1);
+        g.lcout = ilog2(s->Cout);
+        g.Tw = T_;
+        g.Cs = s->Cs;
+        int nt = 0;
+        for (int kh = 0; kh < s->KH; ++kh) {
+          const int ry = py + s->pad - kh;
+          if (ry & 1) continue;
+          for (int kw = 0; kw < s->KW; ++kw) {
+            const int rx = px + s->pad - kw;
+            if (rx & 1) continue;
+            g.tdy[nt] = (int8_t)(ry >> 1);  // arithmetic shift: floor division of an even value
+            g.tdx[nt] = (int8_t)(rx >> 1);
+            g.twt[nt] = (uint8_t)(kh * s->KW + kw);
+            ++nt;
+          }
+        }
+        if (nt == 0) continue;
+        const int M = s->B * GH * GW;
+        sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, nt * s->Cout, 0, (int64_t)T_ * s->Cs, next, SV_F32);
+        d.epilogue = SV_EPI_SLAB;
+        d.split_k = split;
+        if (int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream)) return rc;
+        cs.base[cls] = next;
+        next += (size_t)split * M * s->Cs;
+      }
+    const int64_t n4 = (int64_t)s->B * s->H * s->W * s->Cs / 4;
+    const int blocks = (int)((n4 + 255) / 256);
+    if (dx_dtype == SV_BF16)
+      dgrad_s2_scatter_kernel<uint16_t><<<blocks, 256, 0, (hipStream_t)stream>>>(cs, split, s->B, s->H, s->W, s->Cs,
+                                                                                 (uint16_t*)dx, accumulate);
+    else
+      dgrad_s2_scatter_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>(cs, split, s->B, s->H, s->W, s->Cs,
+                                                                              (float*)dx, accumulate);
+    return check_launch("sv_conv_bwd_data(stride-2 scatter)");
+  }
+  SV_REQUIRE(!slab, "sv_conv_bwd_data_split: shape not on the gathered bf16 GEMM path (Cout >= 32)");
   for (int py = 0; py < st; ++py)
     for (int px = 0; px < st; ++px) {
       Args a{};
@@ -795,14 +912,38 @@ extern "C" int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, 
   return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, work, split);
 }
 
-// split-K depth of the v3 gather wgrad: ~512 workgroups over its 256x128 tiles, >= 512 pixels per slice
+// the transposed wgrad (mode 4: taps*channels on the 256-row side, Cout on the 128-column side) when
+// it wastes fewer MFMA rows than mode 3 (Cout on the 256-row side): ResNet layer1/2 3x3 convs and the
+// stem (Cout 64 / 128) -- 0.225 -> 0.375 / 0.5 -> 0.9 / 0.19 -> 0.38 of the tile's MFMA work is useful
+static bool wgrad_transposed(const sv_conv_shape* s) {
+  const int64_t tc = (int64_t)s->KH * s->KW * s->Cs;
+  const double e3 = (double)s->Cout / (256.0 * ceil_div(s->Cout, 256)) * (double)tc / (128.0 * ceil_div(tc, 128));
+  const double e4 = (double)tc / (256.0 * ceil_div(tc, 256)) * (double)s->Cout / (128.0 * ceil_div(s->Cout, 128));
+  return e4 > 1.1 * e3;
+}
+
+// split-K depth of the v3 gather wgrad.  Mode 3: ~512 workgroups over its 256x128 tiles, >= 512 pixels
+// per slice.  Mode 4 (few output tiles, Cout < 256): 192-256 workgroups with >= 2048 pixels per slice
+// where the pixel count allows -- fewer, longer slices halve the slab round trip of the layer1 3x3
+// (76 -> 60 us) and the stem (131 -> 119 us) against the 512-workgroup split (tools/conv_bench.py)
 static int wgrad_split3(const sv_conv_shape* s) {
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
   const int64_t K = (int64_t)s->B * OH * OW;
-  const int tiles = ceil_div(s->Cout, 256) * ceil_div((int64_t)s->KH * s->KW * s->Cs, 128);
-  int64_t split = ceil_div(512, tiles);
-  const int64_t maxs = K / 512 > 0 ? K / 512 : 1;
-  if (split > maxs) split = maxs;
+  const int64_t tc = (int64_t)s->KH * s->KW * s->Cs;
+  int64_t split;
+  if (wgrad_transposed(s)) {
+    const int64_t tiles = ceil_div(tc, 256) * ceil_div(s->Cout, 128);
+    const int64_t lo = ceil_div(192, tiles), hi = ceil_div(256, tiles);
+    split = K / 2048 > lo ? K / 2048 : lo;
+    if (split > hi) split = hi;
+    const int64_t maxs = K / 512 > 0 ? K / 512 : 1;
+    if (split > maxs) split = maxs;
+  } else {
+    const int64_t tiles = ceil_div(s->Cout, 256) * ceil_div(tc, 128);
+    split = ceil_div(512, tiles);
+    const int64_t maxs = K / 512 > 0 ? K / 512 : 1;
+    if (split > maxs) split = maxs;
+  }
   if (split > 256) split = 256;
   return split < 1 ? 1 : (int)split;
 }
@@ -830,16 +971,22 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
         g.tdy[kh * s->KW + kw] = (int8_t)(kh - s->pad);
         g.tdx[kh * s->KW + kw] = (int8_t)(kw - s->pad);
       }
-    sv_gemm_desc d = conv_desc(dy, x, s->Cout, T_ * s->Cs, (int)npix, 0, T_ * s->Cs, work, SV_F32);
+    const bool tr = wgrad_transposed(s);
+    sv_gemm_desc d = tr ? conv_desc(x, dy, T_ * s->Cs, s->Cout, (int)npix, 0, s->Cout, work, SV_F32)
+                        : conv_desc(dy, x, s->Cout, T_ * s->Cs, (int)npix, 0, T_ * s->Cs, work, SV_F32);
     d.a_kmajor = 0;
-    d.lda = s->Cout;
+    d.lda = tr ? T_ * s->Cs : s->Cout;
     d.epilogue = SV_EPI_SLAB;
     d.split_k = sp;
-    const int rc = launch_gemm3_conv(&d, g, 3, st);
+    const int rc = launch_gemm3_conv(&d, g, tr ? 4 : 3, st);
     if (rc == SV_OK) {
       const int64_t n = (int64_t)s->Cout * T_ * s->Cs;
-      wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, sp, s->Cout, s->Cin, T_, s->Cs, dw,
-                                                                    accumulate);
+      if (tr)
+        wgrad_finish_t_kernel<<<(int)((n + 63) / 64), 256, 0, st>>>(work, sp, s->Cout, s->Cin, T_, s->Cs, dw,
+                                                                      accumulate);
+      else
+        wgrad_finish_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(work, sp, s->Cout, s->Cin, T_, s->Cs, dw,
+                                                                      accumulate);
       return check_launch("sv_conv_bwd_weight(finish)");
     }
     if (rc != SV_ERR_UNSUPPORTED) return rc;

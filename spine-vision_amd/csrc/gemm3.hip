@@ -274,10 +274,30 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
         bx[j] = n < e.N ? cg.tdx[t] : 0;
       }
     }
+    // transposed weight-gradient gather (CONV 4, small Cout): A(m = t*SC + c, k = pixel) gathered
+    // M-major, this lane's k-row and (tap, channel) per DMA piece; B = dy [pixel][Cout] N-contiguous
+    int ak[C::A_PER_WAVE], ac[C::A_PER_WAVE], ay[C::A_PER_WAVE], ax[C::A_PER_WAVE];
+    if constexpr (CONV == 4) {
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < C::A_PER_WAVE; ++j) {
+        const int byte = (wid + NW * j) * 1024 + lane * 16;
+        const int krow = byte / (BM * 2), ch = (byte % (BM * 2)) >> 4;
+        const int m = m0 + (ch ^ mswz(krow)) * 8;
+        const int t = m >> cg.lsc;
+        ak[j] = krow;
+        ac[j] = m < e.M ? m & ((1 << cg.lsc) - 1) : -1;
+        ay[j] = m < e.M ? cg.tdy[t] : 0;
+        ax[j] = m < e.M ? cg.tdx[t] : 0;
+      }
+    }
     auto issue = [&](int kt) {
       char* st = smem + (kt % S) * C::STAGE_BYTES;
       const int k0 = kbeg + kt * BKT;
-      if constexpr (CONV == 3) {
+      if constexpr (CONV == 4) {
+        issue_gather_n<BKT, C::A_PER_WAVE>(A, cg, K, k0, ak, ac, ay, ax, st, wid);
+        issue_tile<false, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
+      } else if constexpr (CONV == 3) {
         issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
         issue_gather_n<BKT, C::B_PER_WAVE>(B, cg, K, k0, bk, bc, by, bx, st + C::A_BYTES, wid);
       } else if constexpr (CONV == 0) {
@@ -418,7 +438,7 @@ static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
 
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
-  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && g.lsc < 5))
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode < 3 && g.lsc < 5))
     return SV_ERR_UNSUPPORTED;
   if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
   if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
@@ -433,6 +453,8 @@ int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream
     return launch<true, false, SV_EPI_SLAB, 32, 3, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
     return launch<false, false, SV_EPI_SLAB, 32, 4, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 4 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
+    return launch<false, false, SV_EPI_SLAB, 32, 4, 4>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   return SV_ERR_UNSUPPORTED;
 }
 

@@ -361,7 +361,9 @@ inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
   mul = (uint32_t)((((1ull << l) - D) << 32) / D + 1);
 }
 // fprop (mode 1) / stride-1 dgrad (mode 2) through the v3 kernel; d describes the GEMM view
-// (M = pixels, N = Cout or Cs, K = taps * channels), epilogue STORE or BIAS_GAMMA_RES (accumulate)
+// (M = pixels, N = Cout or Cs, K = taps * channels), epilogue STORE or BIAS_GAMMA_RES (accumulate).
+// Weight gradients, split-K slabs: mode 3 dW = dy^T gather(x) (M = Cout, N = taps * channels), mode 4
+// the transposed product dW^T = gather(x)^T dy (M = taps * channels, N = Cout) for Cout < 256
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s);
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract

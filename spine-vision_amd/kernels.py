@@ -716,6 +716,15 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
             call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
                  ctypes.byref(s), ptr(work), split)
             return dx
+    if wp.dtype == torch.bfloat16 and s.stride == 2 and s.Cout >= 32 and s.Cs % 8 == 0:
+        # stride 2: one gathered GEMM per output parity class into compact f32 slabs + one scatter pass
+        # (csrc/conv.hip dgrad_s2_scatter_kernel); the workspace holds every class's slabs
+        M = s.B * s.H * s.W
+        split = _conv_split(M // 4, s.Cs, max(32, (T * s.Cout) // 4))
+        work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
+        call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
+             ctypes.byref(s), ptr(work), split)
+        return dx
     call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s))
     return dx
 

@@ -153,3 +153,27 @@ def test_convnext_bf16_schedule_knobs_match_default(dev, knob):
         grads.append([p.grad.detach().cpu().clone() for p in hip.parameters()])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+def test_resnet_bf16_side_stream_matches_single_stream(dev):
+    """ResNet bf16 backward: the per-block weight gradients on the side stream (default) against every
+    kernel on the current stream (SV_SIDE_STREAM=0): same kernels, so every gradient and the BatchNorm
+    running statistics must be equal bit for bit."""
+    from spine_vision_amd.backbone import create_resnet
+
+    ref = ow.fill_module(orn.create("resnet50"))
+    img, _ = ow.classification_batch(2, 128, 128)
+    out = []
+    for overlap in (True, False):
+        hip = create_resnet("resnet50", precision="bf16")
+        hip.load_state_dict(ref.state_dict(), strict=True)
+        hip = hip.to(dev).train()
+        hip.overlap_wgrad = overlap
+        f = hip(img.to(dev))
+        dfeat = torch.from_numpy(ow.uniform("dfeat", f.numel(), -1, 1).reshape(f.shape)).to(dev)
+        f.backward(dfeat)
+        torch.cuda.synchronize()
+        out.append([p.grad.detach().cpu().clone() for p in hip.parameters()] +
+                   [b.detach().cpu().clone() for b in hip.buffers()])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

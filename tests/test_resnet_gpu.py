@@ -44,6 +44,9 @@ CONV_CASES = [
     (2, 16, 16, 256, 512, 1, 2, 0),
     (2, 7, 7, 256, 128, 1, 2, 0),
     (3, 32, 32, 3, 64, 7, 2, 3),  # stem (Cin 3, zero-padded channels)
+    # ResNet-50 @256 geometry at B=2: layer2's strided 3x3 (transposed wgrad, Cout 128) and the stem
+    (2, 64, 64, 128, 128, 3, 2, 1),
+    (2, 128, 128, 3, 64, 7, 2, 3),
 ]
 
 
