@@ -70,6 +70,11 @@ def parse():
     ap.add_argument("--inference", action="store_true",
                     help="secondary line (row f2): the validation / predict forward (eval mode, no tape) instead "
                          "of the training step")
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="replay the training step as a captured HIP graph (StepEngine(cuda_graph=True), "
+                         "classification only: ConvNeXt's lean side-stream release queries events).  Measured "
+                         "(profiles/r3/graph_ab.txt): ResNet-50 3197-3228 img/s replayed vs 3395-3443 eager with "
+                         "the side-stream weight gradients, 3300 single-stream replayed -- off by default")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU sample budget")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -346,7 +351,9 @@ def main():
     else:
         model = CoordinateRegressor(args.backbone, pretrained=False, precision=args.precision)
     model = model.to(device).train()
-    engine = StepEngine(model, device, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+    graphed = args.graph == "on" and cls and world == 1
+    engine = StepEngine(model, device, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
+                        cuda_graph=graphed and not args.inference)
     if cls:
         img, targets = synthetic_cls_batch(args.batch, args.image_size, args.image_size, device, 1234 + rank)
 
@@ -468,6 +475,7 @@ def main():
             "batch_per_gpu": args.batch,
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
+            "hip_graph": bool(engine.cuda_graph),
         },
         "roofline": roof,
         "loss": round(final_loss, 6),

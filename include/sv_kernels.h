@@ -258,6 +258,13 @@ int sv_clip_coef(const float* part, int32_t nparts, float max_norm, float* out, 
 int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n,
                   float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                   const float* grad_scale, sv_stream_t stream);
+/* sv_adamw_flat with the per-step scalars read from DEVICE memory: hyper = f32 [lr, 1 - b1^step,
+ * sqrt(1 - b2^step)] (the host values sv_adamw_flat derives from `step`, rounded to f32 the same way).
+ * A captured HIP graph replays the update with the scalars the host writes into `hyper` before each
+ * launch (StepEngine(cuda_graph=True)).                                                             */
+int sv_adamw_flat_dev(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float beta1,
+                      float beta2, float eps, float weight_decay, const float* hyper, const float* grad_scale,
+                      sv_stream_t stream);
 /* out[r][k] = bf16(W[r][k] * scale[r]): fc2 weight with the layer-scale gamma folded in, so the fc2
  * dgrad GEMM reads bf16 operands only.                                                              */
 int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,

@@ -272,8 +272,14 @@ __global__ void __launch_bounds__(kThreads) adamw_kernel(float* __restrict__ p, 
                                                          uint16_t* __restrict__ pb, int64_t n, float lr,
                                                          float b1, float b2, float eps, float wd,
                                                          float bc1, float bc2_sqrt,
-                                                         const float* __restrict__ gscale) {
+                                                         const float* __restrict__ gscale,
+                                                         const float* __restrict__ hyper) {
   const float sc = gscale ? *gscale : 1.0f;
+  if (hyper) {  // graph replay: [lr, bc1, sqrt(bc2)] of this step from device memory
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2_sqrt = hyper[2];
+  }
   const float step_size = lr / bc1;
   const float decay = 1.0f - lr * wd;
   const int64_t n4 = n / 4;
@@ -471,8 +477,21 @@ int sv_adamw_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16
   const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
   const float bc2 = (float)(1.0 - pow((double)beta2, (double)step));
   adamw_kernel<<<stream_grid(n, 4), kThreads, 0, (hipStream_t)stream>>>(
-      p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale);
+      p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2), grad_scale, nullptr);
   return check_launch("sv_adamw_flat");
+}
+
+int sv_adamw_flat_dev(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float beta1,
+                      float beta2, float eps, float weight_decay, const float* hyper, const float* grad_scale,
+                      sv_stream_t stream) {
+  SV_REQUIRE(p && g && m && v && hyper, "sv_adamw_flat_dev: bad args");
+  SV_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                 (((uintptr_t)p_bf16) & 7) == 0,
+             "sv_adamw_flat_dev: buffers must be 16-byte aligned");
+  if (n <= 0) return SV_OK;
+  adamw_kernel<<<stream_grid(n, 4), kThreads, 0, (hipStream_t)stream>>>(
+      p, g, m, v, p_bf16, n, 0.f, beta1, beta2, eps, weight_decay, 1.f, 1.f, grad_scale, hyper);
+  return check_launch("sv_adamw_flat_dev");
 }
 
 int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,

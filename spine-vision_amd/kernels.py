@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import native as nv
@@ -513,9 +514,24 @@ def grad_clip_coef(g_flat: torch.Tensor, max_norm: float) -> torch.Tensor:
     return out
 
 
-def adamw_flat(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=None):
+def adamw_hyper(lr: float, beta1: float, beta2: float, step: int) -> list[float]:
+    """[lr, 1 - b1^step, sqrt(1 - b2^step)] as f32 values, rounded exactly as sv_adamw_flat derives
+    them on the host (double power, f32 rounding, f32 sqrt) -- the device operand of adamw_flat(hyper=)."""
+    b1, b2 = float(np.float32(beta1)), float(np.float32(beta2))  # the C ABI takes the betas as f32
+    bc1 = np.float32(1.0 - b1 ** step)
+    bc2 = np.float32(1.0 - b2 ** step)
+    return [float(np.float32(lr)), float(bc1), float(np.sqrt(bc2, dtype=np.float32))]
+
+
+def adamw_flat(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=None, hyper=None):
+    """``hyper``: optional f32 device tensor [3] (adamw_hyper) replacing lr/step -- graph replay."""
     n = p.numel()
     _check(g.numel() == n and m.numel() == n and v.numel() == n, "adamw_flat: size mismatch")
+    if hyper is not None:
+        _check(hyper.dtype == torch.float32 and hyper.is_cuda and hyper.numel() >= 3, "adamw_flat: hyper")
+        call("sv_adamw_flat_dev", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(beta1), float(beta2),
+             float(eps), float(weight_decay), ptr(hyper), ptr(grad_scale))
+        return
     call("sv_adamw_flat", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(lr), float(beta1), float(beta2),
          float(eps), float(weight_decay), int(step), ptr(grad_scale))
 

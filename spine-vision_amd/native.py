@@ -93,6 +93,7 @@ _SIGS = {
     "sv_sqnorm_partial": [_p, _i64, _p, _p],
     "sv_clip_coef": [_p, _i32, _f32, _p, _p],
     "sv_adamw_flat": [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _p, _p],
+    "sv_adamw_flat_dev": [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _p, _p, _p],
     "sv_scale_rows_bf16": [_p, _p, _p, _i32, _i32, _p],
     "sv_cast_f32_bf16": [_p, _p, _i64, _p],
     # ResNet

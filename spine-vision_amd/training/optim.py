@@ -67,6 +67,29 @@ class FlatAdamW(torch.optim.Optimizer):
                 runs.append([o, e, self._steps[i]])
         return [tuple(r) for r in runs]
 
+    # -- graph replay (StepEngine(cuda_graph=True)) ----------------------------------------------
+    def begin_graph_step(self) -> tuple[tuple, list[list[float]]]:
+        """Advance the step counts as step() would and return (the runs' [start, end) ranges, per run the
+        f32 [lr, 1 - b1^step, sqrt(1 - b2^step)] the captured update reads from device memory)."""
+        group = self.param_groups[0]
+        b1, b2 = group["betas"]
+        runs = self._runs()
+        return (tuple((s, e) for s, e, _ in runs),
+                [K.adamw_hyper(group["lr"], b1, b2, st) + [0.0] for _, _, st in runs])
+
+    @torch.no_grad()
+    def step_graph(self, ranges: tuple, hyper: torch.Tensor, grad_scale: torch.Tensor | None = None) -> None:
+        """The update of step() for the given runs with lr / bias corrections from ``hyper`` [runs][4]
+        (device): what a captured graph replays; the host counts advance in begin_graph_step."""
+        group = self.param_groups[0]
+        a = self.arena
+        shadow = a.shadow_flat
+        for i, (s, e) in enumerate(ranges):
+            K.adamw_flat(a.param_flat[s:e], a.grad_flat[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e],
+                         shadow[s:e] if shadow is not None else None, lr=0.0, beta1=group["betas"][0],
+                         beta2=group["betas"][1], eps=group["eps"], weight_decay=group["weight_decay"], step=1,
+                         grad_scale=grad_scale, hyper=hyper[i])
+
     @property
     def _step(self) -> int:
         """Largest per-parameter step count (the count of an optimizer that never froze anything)."""

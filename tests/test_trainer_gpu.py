@@ -171,3 +171,82 @@ def test_classification_step_matches_oracle(dev):
         # fp32 noise of zero can move one element by at most 2 lr, never more
         # (Adam's first step is sign-like, so the update itself is not compared in relative L2)
         assert float((du - dr).abs().max()) <= 2.0 * lr * 1.001 + 1e-7, k
+
+
+@pytest.mark.parametrize("backbone", ["resnet18", "resnet50"])
+def test_graphed_step_matches_eager(dev, backbone):
+    """StepEngine(cuda_graph=True): the captured step (zero grads, HIP forward/backward incl. the side-stream
+    weight gradients, clip, AdamW with device-side lr / bias corrections) against the eager step over 7 steps
+    (eager warm-up, capture + replay, replays, then a second input signature with its own warm-up and
+    capture): losses, every gradient and every parameter equal bit for bit.  (A bias correction derived
+    from the f64 beta instead of the f32 one the C ABI receives differed by a few ulp: with bf16
+    activations, that flipped roundings and moved layer3/4 gradients by 1e-3 two steps later.)"""
+    from spine_vision_amd.training import StepEngine
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(7)
+        model = Classifier(backbone, tasks=tasks, pretrained=False, dropout=0.0, precision="bf16").to(dev).train()
+        eng = StepEngine(model, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, cuda_graph=graphed)
+        g = torch.Generator().manual_seed(3)
+        losses = []
+        grads2 = None
+        for step in range(7):
+            B = 4 if step < 5 else 2  # a second signature: eager warm-up, then its own capture
+            img = torch.rand(B, 3, 64, 64, generator=g).to(dev)
+            tg = {"pfirrmann": torch.randint(0, 5, (B,), generator=g).to(dev),
+                  "modic": torch.randint(0, 4, (B,), generator=g).to(dev),
+                  "herniation": torch.randint(0, 2, (B,), generator=g).float().to(dev)}
+            losses.append(eng.step_classification(img, tg))
+            if step in (1, 2):  # capture + first replay, second replay: gradients against the eager step's
+                torch.cuda.synchronize()
+                grads2 = (grads2 or []) + [{n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()}]
+        torch.cuda.synchronize()
+        assert len(eng._graphs) == (2 if graphed else 0)
+        runs.append(([float(x) for x in losses], [p.detach().cpu().clone() for p in model.parameters()], grads2))
+    (la, pa, ga), (lb, pb, gb) = runs
+    assert la == lb
+    for k in range(2):
+        assert all(torch.equal(ga[k][n], gb[k][n]) for n in ga[k])
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+
+
+def test_adamw_graph_replay_bitwise(dev):
+    """FlatAdamW.step_graph with device [lr, 1-b1^t, sqrt(1-b2^t)] (sv_adamw_flat_dev), captured once and
+    replayed with the scalars of each step, equals the eager step() bit for bit (same f32 rounding of the
+    bias corrections as sv_adamw_flat derives on the host), including an lr change between steps."""
+    from spine_vision_amd.training.flat import FlatArena
+    from spine_vision_amd.training.optim import FlatAdamW
+
+    def make():
+        torch.manual_seed(5)
+        m = torch.nn.Sequential(torch.nn.Linear(64, 96), torch.nn.Linear(96, 10)).to(dev)
+        arena = FlatArena(m, dev, with_shadow=True)
+        return m, arena, FlatAdamW(arena, lr=1e-3, weight_decay=1e-2)
+
+    grads = [torch.randn(4096, generator=torch.Generator().manual_seed(i)) for i in range(4)]
+    (m1, a1, o1), (m2, a2, o2) = make(), make()
+    scale = torch.tensor([0.7], device=dev)
+    graph = hyper = None
+    for i, gr in enumerate(grads):
+        lr = 1e-3 if i < 2 else 5e-4
+        for o, a in ((o1, a1), (o2, a2)):
+            o.param_groups[0]["lr"] = lr
+            a.grad_flat.zero_()
+            a.grad_flat[: gr.numel()].copy_(gr.to(dev)[: a.grad_flat.numel()])
+        o1.step(grad_scale=scale)
+        ranges, vals = o2.begin_graph_step()
+        if graph is None:
+            hyper = torch.zeros(len(ranges), 4, device=dev)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                o2.step_graph(ranges, hyper, grad_scale=scale)
+        hyper.copy_(torch.tensor(vals))
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a1.param_flat, a2.param_flat)
+    assert torch.equal(o1.exp_avg, o2.exp_avg) and torch.equal(o1.exp_avg_sq, o2.exp_avg_sq)
+    assert torch.equal(a1.shadow_flat, a2.shadow_flat)
