@@ -3,7 +3,7 @@
 # stats, PMC FETCH_SIZE / WRITE_SIZE passes (separate runs) over a short bench, classification line
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${1:-r2m}
+OUT=gpurun_out/${1:-r3m}
 mkdir -p "$OUT"
 ROOTDIR=$(pwd)
 if [ "${TESTS:-1}" = "1" ]; then
