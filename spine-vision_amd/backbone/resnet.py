@@ -72,7 +72,7 @@ class Bottleneck(nn.Module):
 class _ResNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, model):  # noqa: D401 - autograd signature
-        feat, tape = model._forward_impl(x, save=True)
+        feat, tape = model._forward_train(x)
         ctx.model = model
         ctx.tape = tape
         return feat
@@ -121,6 +121,12 @@ class ResNetHip(nn.Module):
         # per block (SV_SIDE_STREAM=0: off, every kernel on the current stream, bitwise the same result)
         self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
         self._side: dict = {}
+        # training forward replayed from a captured HIP graph (per input signature; the first call runs
+        # eagerly): ~250 launches of host enqueue become one, so the host stays ahead of the GPU while
+        # it issues the eager backward (SV_GRAPH_FORWARD=0: eager forward, bitwise the same result)
+        self.graph_forward = os.environ.get("SV_GRAPH_FORWARD", "1") != "0"
+        self._fgraphs: dict = {}
+        self._fwarm: set = set()
         self._init_weights()
 
     def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
@@ -198,6 +204,32 @@ class ResNetHip(nn.Module):
             y, part = K.conv_fwd_bn_stats(x4d, wp, s, self.act_dtype)
             return y, wp, s, part
         return K.conv_fwd(x4d, wp, s, self.act_dtype), wp, s, None
+
+    @torch.no_grad()
+    def _forward_train(self, img: torch.Tensor):
+        """_forward_impl(img, save=True), from a captured graph when graph_forward is on: the graph owns the
+        static input, the activations saved for the backward (the tape, reused by every replay) and the
+        features; the caller gets a copy of the features.  BatchNorm running statistics, weight packing and
+        the bf16 shadow reads all run inside the graph, so a replay is the eager forward kernel for kernel."""
+        if not (self.graph_forward and img.is_cuda) or torch.cuda.is_current_stream_capturing():
+            return self._forward_impl(img, save=True)  # (inside a whole-step capture: no nested graph)
+        key = (tuple(img.shape), img.dtype, img.device)
+        ent = self._fgraphs.get(key)
+        if ent is None:
+            if key not in self._fwarm:  # first call: eager (lazy kernel attributes, caches)
+                self._fwarm.add(key)
+                return self._forward_impl(img, save=True)
+            static = img.clone()
+            torch.cuda.synchronize(img.device)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                feat, tape = self._forward_impl(static, save=True)
+            ent = self._fgraphs[key] = (static, graph, feat, tape)
+        static, graph, feat, tape = ent
+        if static.data_ptr() != img.data_ptr():
+            static.copy_(img)
+        graph.replay()
+        return feat.clone(), tape
 
     @torch.no_grad()
     def _forward_impl(self, img: torch.Tensor, save: bool):

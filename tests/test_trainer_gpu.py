@@ -250,3 +250,40 @@ def test_adamw_graph_replay_bitwise(dev):
     assert torch.equal(a1.param_flat, a2.param_flat)
     assert torch.equal(o1.exp_avg, o2.exp_avg) and torch.equal(o1.exp_avg_sq, o2.exp_avg_sq)
     assert torch.equal(a1.shadow_flat, a2.shadow_flat)
+
+
+@pytest.mark.parametrize("backbone", ["resnet18", "resnet50"])
+def test_resnet_graph_forward_matches_eager(dev, backbone):
+    """ResNetHip.graph_forward (default): the training forward replayed from a captured graph, the backward
+    eager from its static tape.  Same kernels as the eager forward: losses, gradients, parameters and BN
+    running statistics equal bit for bit over 7 steps (warm-up, capture + replay, replays, a second input
+    signature with its own capture), side stream on."""
+    from spine_vision_amd.training import StepEngine
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
+    runs = []
+    for gf in (False, True):
+        torch.manual_seed(7)
+        model = Classifier(backbone, tasks=tasks, pretrained=False, dropout=0.0, precision="bf16").to(dev).train()
+        model.backbone.graph_forward = gf
+        eng = StepEngine(model, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+        g = torch.Generator().manual_seed(3)
+        losses, grads = [], []
+        for step in range(7):
+            B = 4 if step < 5 else 2
+            img = torch.rand(B, 3, 64, 64, generator=g).to(dev)
+            tg = {"pfirrmann": torch.randint(0, 5, (B,), generator=g).to(dev),
+                  "modic": torch.randint(0, 4, (B,), generator=g).to(dev),
+                  "herniation": torch.randint(0, 2, (B,), generator=g).float().to(dev)}
+            losses.append(float(eng.step_classification(img, tg)))
+            torch.cuda.synchronize()
+            grads.append([p.grad.detach().cpu().clone() for p in model.parameters()])
+        assert len(model.backbone._fgraphs) == (2 if gf else 0)
+        runs.append((losses, grads, [p.detach().cpu().clone() for p in model.parameters()],
+                     [b.detach().cpu().clone() for b in model.buffers()]))
+    (la, ga, pa, ba), (lb, gb, pb, bb) = runs
+    assert la == lb
+    assert all(torch.equal(x, y) for sa, sb in zip(ga, gb) for x, y in zip(sa, sb))
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert all(torch.equal(x, y) for x, y in zip(ba, bb))
