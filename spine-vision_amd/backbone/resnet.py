@@ -364,11 +364,14 @@ class ResNetHip(nn.Module):
                            dx_dtype=act)
             dyd4 = dyd.view(yd.shape)
             jobs.append((dyd4, x_in, sd, g(dconv.weight)))
-            dx = K.conv_bwd_data(dyd4, wpd, sd, dx_dtype=torch.float32)
+            # conv1's data gradient first (a plain store), then the strided shortcut's added onto the
+            # one output parity class its 1x1 taps reach (the other three are skipped, not rewritten)
+            dx = K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx_dtype=torch.float32)
+            K.conv_bwd_data(dyd4, wpd, sd, dx=dx, accumulate=True)
             params += [dconv.weight, dbn.weight, dbn.bias]
         else:
             dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
-        K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
+            K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
         self._flush_wgrads(jobs, params, side, keep)
         return dx
 

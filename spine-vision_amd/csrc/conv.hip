@@ -528,6 +528,7 @@ __global__ void __launch_bounds__(256) dgrad_s2_scatter_kernel(ClassSlabs cs, in
   const int cls = ((y & 1) << 1) | (x & 1);
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* sb = cs.base[cls];
+  if (!sb && accumulate) return;  // a class without taps adds nothing (1x1 stride 2: three of four)
   if (sb) {
     const int64_t rows = (int64_t)B * cs.GH[cls] * cs.GW[cls];
     const int64_t r = ((int64_t)b * cs.GH[cls] + (y >> 1)) * cs.GW[cls] + (x >> 1);
@@ -806,43 +807,78 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   if (dtype == SV_BF16 && st == 2 && slab && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
-    // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass
+    // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass.  Even H, W
+    // and no split: all four classes share one GH x GW grid and run as ONE launch (mode 5) -- the
+    // per-class launches are each below one wave of workgroups (64-128 tiles for the ResNet-50 3x3s)
     ClassSlabs cs{};
-    float* next = slab;
-    for (int py = 0; py < 2; ++py)
-      for (int px = 0; px < 2; ++px) {
-        const int cls = py * 2 + px;
-        const int GH = (s->H - py + 1) / 2, GW = (s->W - px + 1) / 2;
-        cs.GH[cls] = GH;
-        cs.GW[cls] = GW;
-        cs.base[cls] = nullptr;
-        if (GH <= 0 || GW <= 0) continue;
-        ConvG g = make_convg(OH, OW, s->Cout, GH, GW, 1);
-        g.lcout = ilog2(s->Cout);
-        g.Tw = T_;
-        g.Cs = s->Cs;
-        int nt = 0;
+    if (split == 1 && s->H % 2 == 0 && s->W % 2 == 0 && s->KH * s->KW > 1) {
+      const int GH = s->H / 2, GW = s->W / 2, M = s->B * GH * GW;
+      ConvG g = make_convg(OH, OW, s->Cout, GH, GW, 1);
+      g.lcout = ilog2(s->Cout);
+      g.Tw = T_;
+      g.Cs = s->Cs;
+      int nt = 0, maxt = 0;
+      for (int cls = 0; cls < 4; ++cls) {
+        const int py = cls >> 1, px = cls & 1;
+        g.ctap0[cls] = (uint8_t)nt;
         for (int kh = 0; kh < s->KH; ++kh) {
           const int ry = py + s->pad - kh;
           if (ry & 1) continue;
           for (int kw = 0; kw < s->KW; ++kw) {
             const int rx = px + s->pad - kw;
             if (rx & 1) continue;
-            g.tdy[nt] = (int8_t)(ry >> 1);  // arithmetic shift: floor division of an even value
+            g.tdy[nt] = (int8_t)(ry >> 1);
             g.tdx[nt] = (int8_t)(rx >> 1);
             g.twt[nt] = (uint8_t)(kh * s->KW + kw);
             ++nt;
           }
         }
-        if (nt == 0) continue;
-        const int M = s->B * GH * GW;
-        sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, nt * s->Cout, 0, (int64_t)T_ * s->Cs, next, SV_F32);
-        d.epilogue = SV_EPI_SLAB;
-        d.split_k = split;
-        if (int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream)) return rc;
-        cs.base[cls] = next;
-        next += (size_t)split * M * s->Cs;
+        g.ctaps[cls] = (uint8_t)(nt - g.ctap0[cls]);
+        if (g.ctaps[cls] > maxt) maxt = g.ctaps[cls];
+        cs.GH[cls] = GH;
+        cs.GW[cls] = GW;
+        cs.base[cls] = g.ctaps[cls] ? slab + (size_t)cls * M * s->Cs : nullptr;
       }
+      sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, slab, SV_F32);
+      d.epilogue = SV_EPI_SLAB;
+      if (int rc = launch_gemm3_conv(&d, g, 5, (hipStream_t)stream)) return rc;
+    } else {
+      float* next = slab;
+      for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+          const int cls = py * 2 + px;
+          const int GH = (s->H - py + 1) / 2, GW = (s->W - px + 1) / 2;
+          cs.GH[cls] = GH;
+          cs.GW[cls] = GW;
+          cs.base[cls] = nullptr;
+          if (GH <= 0 || GW <= 0) continue;
+          ConvG g = make_convg(OH, OW, s->Cout, GH, GW, 1);
+          g.lcout = ilog2(s->Cout);
+          g.Tw = T_;
+          g.Cs = s->Cs;
+          int nt = 0;
+          for (int kh = 0; kh < s->KH; ++kh) {
+            const int ry = py + s->pad - kh;
+            if (ry & 1) continue;
+            for (int kw = 0; kw < s->KW; ++kw) {
+              const int rx = px + s->pad - kw;
+              if (rx & 1) continue;
+              g.tdy[nt] = (int8_t)(ry >> 1);  // arithmetic shift: floor division of an even value
+              g.tdx[nt] = (int8_t)(rx >> 1);
+              g.twt[nt] = (uint8_t)(kh * s->KW + kw);
+              ++nt;
+            }
+          }
+          if (nt == 0) continue;
+          const int M = s->B * GH * GW;
+          sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, nt * s->Cout, 0, (int64_t)T_ * s->Cs, next, SV_F32);
+          d.epilogue = SV_EPI_SLAB;
+          d.split_k = split;
+          if (int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream)) return rc;
+          cs.base[cls] = next;
+          next += (size_t)split * M * s->Cs;
+        }
+    }
     const int64_t n4 = (int64_t)s->B * s->H * s->W * s->Cs / 4;
     const int blocks = (int)((n4 + 255) / 256);
     if (dx_dtype == SV_BF16)

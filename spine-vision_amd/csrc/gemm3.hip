@@ -223,9 +223,13 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     const int split = wgi / nwg, wg = wgi - split * nwg;
     const int tm = wg / tilesN, tn = wg % tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = split * kper;
+    int kbeg = split * kper;
     int kend = kbeg + kper;
     if (kend > K) kend = K;
+    if constexpr (CONV == 5) {  // "split" = the parity class: its own tap run, its own slab
+      kbeg = 0;
+      kend = (int)cg.ctaps[split] << cg.lsc;
+    }
     const int nk = kend > kbeg ? (kend - kbeg) / BKT : 0;
 
     const bool do_cs = EPI == SV_EPI_SLAB && colsum != nullptr && tn == 0;  // compile-time off otherwise
@@ -304,7 +308,8 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
         issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
         issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
       } else {
-        const int jt = k0 >> cg.lsc, cb = k0 & ((1 << cg.lsc) - 1);  // wave-uniform tap / channel base
+        const int jt = (CONV == 5 ? (int)cg.ctap0[split] : 0) + (k0 >> cg.lsc);  // wave-uniform tap
+        const int cb = k0 & ((1 << cg.lsc) - 1);                                  // and channel base
         issue_gather<BKT, C::A_PER_WAVE>(A, cg, gb, gy, gx, cg.tdy[jt], cg.tdx[jt], cb, st, wid);
         if constexpr (CONV == 1) {
           issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
@@ -438,7 +443,7 @@ static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
 
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
-  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode < 3 && g.lsc < 5))
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && mode != 4 && g.lsc < 5))
     return SV_ERR_UNSUPPORTED;
   if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
   if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
@@ -453,6 +458,7 @@ int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream
     return launch<true, false, SV_EPI_SLAB, 32, 3, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
     return launch<false, false, SV_EPI_SLAB, 32, 4, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, 3, 5>(d, 4, s, &g);
   if (mode == 4 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
     return launch<false, false, SV_EPI_SLAB, 32, 4, 4>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   return SV_ERR_UNSUPPORTED;

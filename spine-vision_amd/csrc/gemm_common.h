@@ -352,6 +352,7 @@ struct ConvG {
   int lcout, Tw, Cs;    // dgrad: B rows
   int8_t tdy[CONV_MAX_TAPS], tdx[CONV_MAX_TAPS];
   uint8_t twt[CONV_MAX_TAPS];
+  uint8_t ctap0[4], ctaps[4];  // mode 5: each output parity class's run of taps in tdy/tdx/twt
 };
 // d = n / D for n < 2^31: (umulhi(n, mul) + n) >> shift
 inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
@@ -363,7 +364,9 @@ inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
 // fprop (mode 1) / stride-1 dgrad (mode 2) through the v3 kernel; d describes the GEMM view
 // (M = pixels, N = Cout or Cs, K = taps * channels), epilogue STORE or BIAS_GAMMA_RES (accumulate).
 // Weight gradients, split-K slabs: mode 3 dW = dy^T gather(x) (M = Cout, N = taps * channels), mode 4
-// the transposed product dW^T = gather(x)^T dy (M = taps * channels, N = Cout) for Cout < 256
+// the transposed product dW^T = gather(x)^T dy (M = taps * channels, N = Cout) for Cout < 256.
+// Mode 5: the stride-2 dgrad of all four output parity classes in one launch (even H, W: every class
+// has the same GH x GW grid; class c takes taps ctap0[c] .. + ctaps[c] and writes slab c, epilogue SLAB)
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s);
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract
