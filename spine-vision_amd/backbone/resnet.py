@@ -170,7 +170,7 @@ class ResNetHip(nn.Module):
         if need_grad:
             anchor = torch.zeros((), device=x.device, requires_grad=True)
             return _ResNetFn.apply(x, anchor, self)
-        feat, _ = self._forward_impl(x, save=False)
+        feat, _ = self._forward_graphed(x, save=False)
         return feat
 
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
@@ -207,23 +207,28 @@ class ResNetHip(nn.Module):
 
     @torch.no_grad()
     def _forward_train(self, img: torch.Tensor):
-        """_forward_impl(img, save=True), from a captured graph when graph_forward is on: the graph owns the
+        return self._forward_graphed(img, save=True)
+
+    @torch.no_grad()
+    def _forward_graphed(self, img: torch.Tensor, save: bool):
+        """_forward_impl(img, save), from a captured graph when graph_forward is on: the graph owns the
         static input, the activations saved for the backward (the tape, reused by every replay) and the
-        features; the caller gets a copy of the features.  BatchNorm running statistics, weight packing and
-        the bf16 shadow reads all run inside the graph, so a replay is the eager forward kernel for kernel."""
+        features; the caller gets a copy of the features.  BatchNorm statistics (batch or running), weight
+        packing and the bf16 shadow reads all run inside the graph, so a replay is the eager forward kernel
+        for kernel.  Used for the training forward and the tape-free eval / predict forward."""
         if not (self.graph_forward and img.is_cuda) or torch.cuda.is_current_stream_capturing():
-            return self._forward_impl(img, save=True)  # (inside a whole-step capture: no nested graph)
-        key = (tuple(img.shape), img.dtype, img.device)
+            return self._forward_impl(img, save=save)  # (inside a whole-step capture: no nested graph)
+        key = (tuple(img.shape), img.dtype, img.device, save, self.training)
         ent = self._fgraphs.get(key)
         if ent is None:
             if key not in self._fwarm:  # first call: eager (lazy kernel attributes, caches)
                 self._fwarm.add(key)
-                return self._forward_impl(img, save=True)
+                return self._forward_impl(img, save=save)
             static = img.clone()
             torch.cuda.synchronize(img.device)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                feat, tape = self._forward_impl(static, save=True)
+                feat, tape = self._forward_impl(static, save=save)
             ent = self._fgraphs[key] = (static, graph, feat, tape)
         static, graph, feat, tape = ent
         if static.data_ptr() != img.data_ptr():

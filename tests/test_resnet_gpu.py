@@ -454,3 +454,27 @@ def test_classifier_logits_match_reference(dev, backbone):
         r = float((out[k].cpu() - ref).abs().max() / ref.abs().max())
         assert r < 1e-3, (k, r)
     assert abs(float(loss) - float(g["loss"])) / float(g["loss"]) < 1e-3
+
+
+@pytest.mark.parametrize("train_mode", [False, True])
+def test_graph_forward_no_grad_matches_eager(dev, train_mode):
+    """The tape-free forward (validation / predict) replayed from a captured graph (graph_forward, the
+    default) equals the eager forward bit for bit over several inputs: eval mode (running statistics) and
+    train mode under no_grad (batch statistics, running statistics updated like the eager path)."""
+    torch.manual_seed(0)
+    a = create_resnet("resnet50", precision="bf16").to(dev)
+    b = create_resnet("resnet50", precision="bf16").to(dev)
+    b.load_state_dict(a.state_dict())
+    a.graph_forward, b.graph_forward = True, False
+    a.train(train_mode)
+    b.train(train_mode)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(4):
+        x = torch.rand(4, 3, 96, 96, generator=g).to(dev)
+        with torch.no_grad():
+            fa, fb = a(x), b(x)
+        torch.cuda.synchronize()
+        assert torch.equal(fa, fb)
+    assert len(a._fgraphs) == 1
+    for ba, bb in zip(a.buffers(), b.buffers()):
+        assert torch.equal(ba, bb)
