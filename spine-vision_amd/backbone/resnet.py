@@ -227,7 +227,9 @@ class ResNetHip(nn.Module):
             static = img.clone()
             torch.cuda.synchronize(img.device)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            # thread_local: another thread's HIP calls (RCCL's proxy, a data-loader pin thread) during
+            # the capture do not invalidate it
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 feat, tape = self._forward_impl(static, save=save)
             ent = self._fgraphs[key] = (static, graph, feat, tape)
         static, graph, feat, tape = ent

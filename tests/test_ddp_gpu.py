@@ -156,3 +156,68 @@ def test_rccl_bucketer_world1_matches_single_process(dev):
     assert torch.equal(g, eng.arena.grad_flat.cpu())
     assert torch.equal(prm, eng.arena.param_flat.cpu())
     assert stats["buckets"] == nb and stats["allreduce_ms_per_step"] > 0
+
+
+def _resnet_rank(rank, world, port, backend, out):
+    """3 classification steps per rank (eager warm-up, forward capture + replay, replay) with the DDP
+    bucketer, the BN-buffer broadcast and the side-stream weight gradients; graph_forward on, then off."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    import torch.distributed as dist
+
+    from spine_vision_amd.training import Classifier, StepEngine
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
+    res = []
+    for gf in (True, False):
+        torch.manual_seed(11)
+        m = Classifier("resnet50", tasks=tasks, pretrained=False, dropout=0.0, precision="bf16").to(dev).train()
+        m.backbone.graph_forward = gf
+        eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=16.0)
+        g = torch.Generator().manual_seed(100 + rank)
+        losses = []
+        for _ in range(3):
+            img = torch.rand(2, 3, 64, 64, generator=g).to(dev)
+            tg = {"pfirrmann": torch.randint(0, 5, (2,), generator=g).to(dev),
+                  "modic": torch.randint(0, 4, (2,), generator=g).to(dev),
+                  "herniation": torch.randint(0, 2, (2,), generator=g).float().to(dev)}
+            losses.append(float(eng.step_classification(img, tg)))
+        torch.cuda.synchronize()
+        res.append((losses, eng.arena.param_flat.cpu().clone(), len(m.backbone._fgraphs)))
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_resnet_graph_forward(dev):
+    """Data-parallel ResNet-50 steps with the graph-replayed forward (two ranks on the box's GPU, gloo):
+    the replicas stay identical (bucketed all-reduce from the side-stream grad-ready events, rank-0 BN
+    buffer broadcast before each forward replay), and the trajectory equals the eager forward's bit for bit."""
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_resnet_rank, args=(r, 2, port, "gloo", out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    (g0, e0), (g1, e1) = out[0], out[1]
+    assert g0[2] == 1 and e0[2] == 0  # the graphed run captured its forward
+    assert torch.equal(g0[1], g1[1]) and torch.equal(e0[1], e1[1])  # replicas in sync
+    assert g0[0] == e0[0] and g1[0] == e1[0]  # per-rank losses: graph == eager
+    assert torch.equal(g0[1], e0[1])
