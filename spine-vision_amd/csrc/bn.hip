@@ -328,7 +328,25 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
   const int64_t r0 = (int64_t)blockIdx.y * rpp;
   int64_t r1 = r0 + rpp;
   if (r1 > rows) r1 = rows;
-  for (int64_t r = r0 + rsub; r < r1; r += rp) {
+  int64_t r = r0 + rsub;
+  // two rows per iteration: both rows' loads are issued before either is accumulated (the thread's
+  // rows are still summed in ascending order, so the partials are bit-identical to the one-row loop)
+  for (; r + rp < r1; r += 2 * rp) {
+    const size_t e0 = (size_t)r * C + c, e1 = e0 + (size_t)rp * C;
+    float v0[V], g0[V], v1[V], g1[V];
+    ldv<V>(y, ydt, e0, v0);
+    ldv<V>(y, ydt, e1, v1);
+    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0);
+    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s1[q] += g0[q];
+      s2[q] = fmaf(g0[q], (v0[q] - mu[q]) * rs[q], s2[q]);
+      s1[q] += g1[q];
+      s2[q] = fmaf(g1[q], (v1[q] - mu[q]) * rs[q], s2[q]);
+    }
+  }
+  for (; r < r1; r += rp) {
     const size_t e = (size_t)r * C + c;
     float v[V], g[V];
     ldv<V>(y, ydt, e, v);
@@ -369,7 +387,8 @@ template <int V, bool RELU_Y>
 __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
   const int64_t nv = a.rows * a.C / V;
   const float inv_n = 1.0f / (float)a.rows;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     const size_t e = (size_t)i * V;
     const int c = (int)(e % a.C);
     float v[V], mu[V], rs[V], ga[V], sg[V], sgx[V], g[V], o[V];
