@@ -311,7 +311,7 @@ class ResNetHip(nn.Module):
             self._side[device] = torch.cuda.Stream(device=device)
         return self._side[device]
 
-    def _flush_wgrads(self, jobs: list, params: list, side, keep: list) -> None:
+    def _flush_wgrads(self, jobs: list, params: list, side, keep: list, deferred: list | None = None) -> None:
         """Run the block's weight gradients (conv_bwd_weight jobs) and report its parameters ready.  With a
         side stream: one hand-off (the side stream waits for everything the main stream has issued, so the
         grad-ready event it records also covers the BatchNorm gradients), and the operands stay referenced
@@ -319,7 +319,10 @@ class ResNetHip(nn.Module):
         if side is None:
             for dy4, x, s, dw in jobs:
                 K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
-            self._ready(params)
+            if deferred is not None:  # reported after the streams join (a bucket may hold side-stream grads)
+                deferred.extend(params)
+            else:
+                self._ready(params)
             return
         side.wait_event(torch.cuda.current_stream().record_event())
         with torch.cuda.stream(side):
@@ -329,7 +332,7 @@ class ResNetHip(nn.Module):
         keep.append(jobs)
 
     @torch.no_grad()
-    def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None) -> torch.Tensor:
+    def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None) -> torch.Tensor:
         """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
         block's parameter gradients and returns dL/d(block input) (f32)."""
         act = self.act_dtype
@@ -379,7 +382,7 @@ class ResNetHip(nn.Module):
         else:
             dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
             K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
-        self._flush_wgrads(jobs, params, side, keep)
+        self._flush_wgrads(jobs, params, side, keep, deferred)
         return dx
 
     @torch.no_grad()
@@ -389,9 +392,13 @@ class ResNetHip(nn.Module):
         main = torch.cuda.current_stream()
         side = self._side_stream(main.device) if (self.overlap_wgrad and self.compute_bf16) else None
         keep: list = []
+        deferred: list | None = [] if side is not None else None
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
-        for blk, saved_block in zip(reversed(list(self.blocks())), reversed(tape.blocks)):
-            d = self._block_backward(blk, saved_block, d, side, keep)
+        blocks = list(self.blocks())
+        for i, (blk, saved_block) in zip(range(len(blocks) - 1, -1, -1), zip(reversed(blocks), reversed(tape.blocks))):
+            # the first block's (and below, the stem's) weight gradients stay on the main stream: nothing
+            # is left for the main stream to overlap them with, while the side stream drains its queue
+            d = self._block_backward(blk, saved_block, d, side if i > 0 else None, keep, deferred)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
@@ -399,9 +406,10 @@ class ResNetHip(nn.Module):
         dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
                        dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act)
         self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
-                           [self.conv1.weight, self.bn1.weight, self.bn1.bias], side, keep)
+                           [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
+            self._ready(deferred)
         keep.clear()
 
 
