@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-2 measurement set: full GPU suite, the default bench line (with cpu_baseline), rocprof kernel
+# round measurement set: full GPU suite, the default bench line (with cpu_baseline), rocprof kernel
 # stats, PMC FETCH_SIZE / WRITE_SIZE passes (separate runs) over a short bench, classification line
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
