@@ -30,6 +30,7 @@ import torch.nn as nn
 from .. import kernels as K
 
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
+_MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
 BN_EPS = 1e-5
 
 
@@ -221,6 +222,8 @@ class ResNetHip(nn.Module):
         key = (tuple(img.shape), img.dtype, img.device, save, self.training)
         ent = self._fgraphs.get(key)
         if ent is None:
+            if len(self._fgraphs) >= _MAX_FORWARD_GRAPHS:  # each graph keeps its activations' memory pool
+                return self._forward_impl(img, save=save)
             if key not in self._fwarm:  # first call: eager (lazy kernel attributes, caches)
                 self._fwarm.add(key)
                 return self._forward_impl(img, save=save)
