@@ -18,5 +18,6 @@ run large --backbone convnext_large --batch 64 --steps 5 --warmup 2
 run cls --workload classification --steps 10 --warmup 3
 run cls_r18 --workload classification --backbone resnet18 --steps 10 --warmup 3
 run inf --inference --steps 10 --warmup 3
+run inf_cls --workload classification --inference --steps 20 --warmup 5
 run base2 --steps 10 --warmup 3
 exit 0
