@@ -90,6 +90,10 @@ typedef struct {
 } sv_gemm_desc;
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
+/* Process-wide cap on the workgroup count of subsequent v3 / v9 GEMM launches (persistent over their
+ * tiles; 0 = off); returns the previous value.  The ResNet backward issues its side-stream weight
+ * gradients under a cap so part of the chip stays free for the data-gradient / BatchNorm chain.       */
+int sv_gemm_set_grid_cap(int32_t n);
 /* Residency policy for the bf16 GEMMs launched after this call (host-side, process-wide):
  * 0 (default) = one workgroup per output tile; n > 0 = persistent grids of n workgroups per CU, so
  * that GEMMs issued concurrently on two streams (data gradients + weight gradients) are co-resident

@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from .. import kernels as K
+from .. import native as nv
 
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
 _MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
@@ -121,6 +122,10 @@ class ResNetHip(nn.Module):
         # side stream beside the data-gradient / BatchNorm chain of the next one, one main->side hand-off
         # per block (SV_SIDE_STREAM=0: off, every kernel on the current stream, bitwise the same result)
         self.overlap_wgrad = os.environ.get("SV_SIDE_STREAM", "1") != "0"
+        # the side stream's GEMMs run on at most 3/4 of the CUs (persistent over their tiles): a v3 wgrad
+        # workgroup fills its CU's register file, so an uncapped side grid kept the dgrad / BN chain's small
+        # kernels waiting for CUs (192 of 256: 3427-3438 -> 3489-3503 img/s; 128 / 160 / 224 in between)
+        self.side_grid_cap: int | None = None  # None: 3/4 of the device's CUs
         self._side: dict = {}
         # training forward replayed from a captured HIP graph (per input signature; the first call runs
         # eagerly): ~250 launches of host enqueue become one, so the host stays ahead of the GPU while
@@ -328,10 +333,14 @@ class ResNetHip(nn.Module):
                 self._ready(params)
             return
         side.wait_event(torch.cuda.current_stream().record_event())
+        if self.side_grid_cap is None:
+            self.side_grid_cap = torch.cuda.get_device_properties(side.device).multi_processor_count * 3 // 4
+        prev = nv.value("sv_gemm_set_grid_cap", self.side_grid_cap)
         with torch.cuda.stream(side):
             for dy4, x, s, dw in jobs:
                 K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
             self._ready(params)
+        nv.value("sv_gemm_set_grid_cap", prev)
         keep.append(jobs)
 
     @torch.no_grad()

@@ -295,6 +295,7 @@ using namespace sv;
 namespace sv {
 int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
 int g_gemm_prio = 0;       // sv_gemm_set_priority
+int g_gemm_grid_cap = 0;   // sv_gemm_set_grid_cap
 }
 
 static int g_gemm_impl = 0;  // sv_gemm_set_impl: 0 = measured per-shape dispatch, 2/3/8 = force a family
@@ -308,6 +309,12 @@ extern "C" int sv_gemm_set_impl(int32_t impl) {
 extern "C" int sv_gemm_set_priority(int32_t p) {
   const int prev = g_gemm_prio;
   g_gemm_prio = p ? 1 : 0;
+  return prev;
+}
+
+extern "C" int sv_gemm_set_grid_cap(int32_t n) {
+  const int prev = g_gemm_grid_cap;
+  g_gemm_grid_cap = n < 0 ? 0 : n;
   return prev;
 }
 

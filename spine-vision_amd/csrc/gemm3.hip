@@ -23,6 +23,7 @@
 
 namespace sv {
 extern int g_gemm_wg_per_cu;
+extern int g_gemm_grid_cap;
 extern int g_gemm_prio;
 namespace g3 {
 
@@ -406,6 +407,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
     const int slots = g_gemm_wg_per_cu * num_cus();
     grid = total > slots ? slots : total;
   }
+  if (g_gemm_grid_cap > 0 && grid > g_gemm_grid_cap) grid = g_gemm_grid_cap;  // persistent over the rest
   gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
       tilesM, tilesN, split, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,

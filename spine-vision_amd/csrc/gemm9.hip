@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 namespace sv {
+extern int g_gemm_grid_cap;
 namespace g9 {
 
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512, NW = 8;
@@ -631,6 +632,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   }
   const int total = tilesM * tilesN * split;
   int grid = num_cus();
+  if (g_gemm_grid_cap > 0 && grid > g_gemm_grid_cap) grid = g_gemm_grid_cap;
   if (grid > total) grid = total;
   gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_total<AK, EPI>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
                                                                   reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,

@@ -60,6 +60,7 @@ _SIGS = {
     "sv_build_target": [],
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
     "sv_gemm_set_workgroups_per_cu": [_i32],
+    "sv_gemm_set_grid_cap": [_i32],
     "sv_gemm_set_impl": [_i32],
     "sv_gemm_set_priority": [_i32],
     "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
@@ -128,7 +129,7 @@ _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.
 # entry points that return a value (size / count) rather than an sv_status
 _VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
                                                                      "sv_gemm_set_workgroups_per_cu", "sv_gemm_set_impl",
-                                                                     "sv_gemm_set_priority"}
+                                                                     "sv_gemm_set_priority", "sv_gemm_set_grid_cap"}
 
 _lib = None
 _lock = threading.Lock()

@@ -110,3 +110,39 @@ def test_gemm_priority_is_bitwise_neutral(dev):
     finally:
         nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
     assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("impl", [0, 3, 9])
+def test_gemm_grid_cap_bitwise(dev, impl):
+    """sv_gemm_set_grid_cap (the ResNet side stream's weight gradients run under a cap): the kernels are
+    persistent over their tiles, so a capped grid computes every tile exactly as the full grid does --
+    forward, data-gradient and split-K weight-gradient GEMMs equal bit for bit at caps of 37 and 96."""
+    g = torch.Generator().manual_seed(5)
+    bf = torch.bfloat16
+    M, C = 8192, 256
+    y = torch.randn(M, C, generator=g).to(bf).to(dev)
+    w1 = (torch.randn(4 * C, C, generator=g) * 0.05).to(bf).to(dev)
+    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+
+    def run():
+        o = torch.empty(M, 4 * C, device=dev, dtype=bf)
+        K.linear_fwd(y, w1, out=o)
+        d = torch.empty(M, C, device=dev, dtype=bf)
+        K.linear_dgrad(dh, w1, out=d, compute_bf16=True)
+        wg = K.linear_wgrad(dh, y, compute_bf16=True)
+        torch.cuda.synchronize()
+        return o.float(), d.float(), wg
+
+    prev_impl = _impl(impl)
+    try:
+        ref = run()
+        for cap in (37, 96):
+            prev = nv.value("sv_gemm_set_grid_cap", cap)
+            try:
+                out = run()
+            finally:
+                nv.value("sv_gemm_set_grid_cap", prev)
+            for a, b in zip(ref, out):
+                assert torch.equal(a, b)
+    finally:
+        _impl(prev_impl)
