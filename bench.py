@@ -48,7 +48,14 @@ PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, S
               "fwd": (True, True)}
 PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsample, stem; side stream)",
                "fc2_dgrad": "fc2 data gradient dh = (dY (W2 gamma)) * GELU'(h) (critical path)",
-               "fwd": "forward GEMMs: fc1 (+GELU), fc2 (+gamma, residual), stem, downsample"}
+               "fwd": "forward GEMMs: fc1 (+GELU), fc2 (+gamma, residual), stem, downsample",
+               "dw_fwd": "depthwise 7x7 + LayerNorm forward (sv_dwconv7_ln_fwd)",
+               "dw_bwd_data": "depthwise 7x7 backward-data (sv_dwconv7_bwd_data, gradient stream += and bf16 copy)",
+               "dw_wgrad": "depthwise 7x7 weight gradient (sv_dwconv7_bwd_weight, partials only)",
+               "ln_bwd": "block LayerNorm backward (sv_layernorm_bwd)",
+               "adamw": "fused AdamW over the flat buffers (+ bf16 shadow refresh)"}
+# HBM-bound kernel classes timed by kernels.OpProbe (reported separately against 8 TB/s)
+OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw")
 
 
 def parse():
@@ -295,7 +302,7 @@ def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: d
     tflops = flops / (avg_ms * 1e-3) / 1e12 if probe.launches else 0.0
     gbs = nbytes / (avg_ms * 1e-3) / 1e9 if probe.launches else 0.0
     hbm_bound = nbytes / (PEAK_HBM_GBS * 1e9) > flops / (peak * 1e12)
-    tr = traffic.get(f"{name}_bytes_per_launch")
+    tr = traffic.get(f"{name}_bytes_per_launch")  # None unless a PMC pass of THIS configuration exists
     return {
         "kernel": PROBE_NAMES[name],
         "bound": "hbm" if hbm_bound else "mfma",
@@ -384,6 +391,7 @@ def main():
 
     bf = args.precision == "bf16"
     probes = {k: K.GemmProbe(v[:2] + (bf,) + v[2:], k) for k, v in PROBE_KEYS.items()}
+    op_probes = {k: K.OpProbe(k) for k in OP_PROBE_KEYS}
     # The probes' HIP events bracket every launch of their classes in the LAST timed step: each timing
     # event is a release packet that writes back L2, and probing all K steps cost 2.3% of the step
     # (tools/gpu_probe_ab.sh).  The classification line reports the whole-step rate and takes no probe;
@@ -391,19 +399,46 @@ def main():
     probe_mode = os.environ.get("SV_BENCH_PROBE", "1")
     use_probe = not cls and not args.inference and probe_mode != "0"
     bucketer = engine.bucketer
+    # world 1: rehearse the data-parallel exchange -- when each 64 MB bucket's gradients become final in
+    # the last timed step, and a prediction of the exposed all-reduce at N ranks (comm.BucketTimeline)
+    timeline = None
+    tl_ev: dict = {}
+    if world == 1 and not args.inference and os.environ.get("SV_BENCH_TIMELINE", "1") != "0":
+        from spine_vision_amd.training.comm import BucketTimeline
+
+        timeline = BucketTimeline(engine.arena, model, bucket_mb=64.0)
+
+        def _bwd_end():
+            if timeline.active:
+                tl_ev["bwd_end"] = torch.cuda.Event(enable_timing=True)
+                tl_ev["bwd_end"].record()
+
+        engine.after_backward = _bwd_end
     t0 = time.perf_counter()
     for i in range(args.steps):
         last = i == args.steps - 1
-        K.PROBES = list(probes.values()) if use_probe and (probe_mode == "all" or last) else []
+        if timeline is not None:
+            timeline.reset()
+            timeline.active = last
+            if last:
+                tl_ev["start"] = torch.cuda.Event(enable_timing=True)
+                tl_ev["start"].record()
+        probing = use_probe and (probe_mode == "all" or last)
+        K.PROBES = list(probes.values()) if probing else []
+        K.OP_PROBES = dict(op_probes) if probing else {}
         if bucketer is not None:
             bucketer.timing = last
         loss = run_step()
+        if timeline is not None and last:
+            tl_ev["end"] = torch.cuda.Event(enable_timing=True)
+            tl_ev["end"].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     K.PROBES = []
+    K.OP_PROBES = {}
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -413,10 +448,13 @@ def main():
     mstats = torch.cuda.memory_stats(device)
 
     peak = PEAK_BF16_TFLOPS if bf else PEAK_F32_MFMA_TFLOPS
+    # PMC traffic per launch, keyed by the exact configuration it was measured on (profiles/traffic.json
+    # "configs"): a line without a matching pass reports traffic null, never another configuration's bytes
+    traffic_key = f"{args.backbone}/{args.image_size}/bs{args.batch}/{args.precision}"
     traffic = {}
     if os.path.exists(args.traffic_file):
         try:
-            traffic = json.load(open(args.traffic_file))
+            traffic = json.load(open(args.traffic_file)).get("configs", {}).get(traffic_key, {})
         except Exception:
             traffic = {}
 
@@ -445,10 +483,12 @@ def main():
         nprobed = args.steps if probe_mode == "all" else 1
         kern = {k: kernel_roofline(k, p_, nprobed, peak, traffic) for k, p_ in probes.items() if p_.launches}
         dominant = max(kern, key=lambda k: kern[k]["ms_per_step"])
+        kern.update({k: kernel_roofline(k, p_, nprobed, peak, traffic) for k, p_ in op_probes.items() if p_.launches})
         roof = dict(kern[dominant])
         roof["kernel"] = f"{dominant}: {roof['kernel']} (dominant GEMM class by device time)"
         roof["step_tflops_per_gpu"] = round(step_tflops, 1) if step_tflops else None
         roof["step_mfma_frac"] = step_frac
+        roof["traffic_config"] = traffic_key if traffic else None
         roof["kernels"] = kern
     else:
         # no per-kernel probe: report the whole-step model FLOP rate against the peak
@@ -498,6 +538,20 @@ def main():
         comm["allreduce_full_mb"] = round(g.numel() * 4 / 2**20, 1)
         comm["allreduce_full_busbw_gbs"] = round(2.0 * (world - 1) / world * g.numel() * 4 / t_ar / 1e9, 1)
         result["comm"] = comm
+    if timeline is not None and "bwd_end" in tl_ev:
+        timeline.active = False
+        ready = timeline.ready_ms(tl_ev["start"])
+        bwd_end = tl_ev["start"].elapsed_time(tl_ev["bwd_end"])
+        step_last = tl_ev["start"].elapsed_time(tl_ev["end"])
+        # xGMI bus bandwidth of RCCL's ring all-reduce on 8 MI355X: not measurable on a 1-GPU box; the
+        # prediction is given at 200 / 300 / 400 GB/s (DESIGN.md "Multi-GPU": 7 links x ~153 GB/s per GPU)
+        result["dp_rehearsal"] = {
+            "buckets_mb_ready_ms": ready,
+            "backward_end_ms": round(bwd_end, 3), "step_ms_last": round(step_last, 3),
+            "predictions": [timeline.predict(ready, bwd_end, ms, 8, bw) for bw in (200.0, 300.0, 400.0)],
+        }
+    if world > 1:
+        result["config"]["comm_reserve_cus"] = int(os.environ.get("SV_COMM_RESERVE_CUS", "32"))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
         if not cls and not args.inference:

@@ -38,6 +38,13 @@ CONVNEXT_CFGS = {
 }
 
 
+def _comm_cap(device, reserve: int) -> int:
+    """GEMM grid cap that leaves ``reserve`` CUs to the comm stream (0: no cap)."""
+    if reserve <= 0:
+        return 0
+    return max(1, torch.cuda.get_device_properties(device).multi_processor_count - reserve)
+
+
 class _Mlp(nn.Module):
     def __init__(self, dim: int, hidden: int) -> None:
         super().__init__()
@@ -129,6 +136,13 @@ class ConvNeXtHip(nn.Module):
         # record_stream -- every cross-stream event / allocator event is a release packet (L2 write-back)
         self.lean_sync = os.environ.get("SV_LEAN_SYNC", "1") != "0"
         self._side: dict = {}
+        # the lean backward polls side-stream events (_release_side), which a stream capture forbids:
+        # StepEngine(cuda_graph=True) refuses this backbone
+        self.graph_safe = False
+        # data-parallel runs (StepEngine, world > 1): the backward's persistent GEMM grids leave this many
+        # CUs free so RCCL's all-reduce kernels on the comm stream find a CU (a v9 workgroup holds its CU's
+        # LDS for the whole launch); 0 = every CU
+        self.comm_reserve_cus = 0
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -308,6 +322,7 @@ class ConvNeXtHip(nn.Module):
         side = self._side_stream(main.device) if self.overlap_wgrad else None
         # block GEMMs of the two streams: one persistent workgroup per CU each, so they share every CU
         prev_res = nv.value("sv_gemm_set_workgroups_per_cu", self.side_wg_per_cu if side is not None else 0)
+        prev_cap = nv.value("sv_gemm_set_grid_cap", _comm_cap(main.device, self.comm_reserve_cus))
         lean = side is not None and bf and self.lean_sync
         # lean mode: the side stream's weight-gradient GEMMs run at raised wave priority where they share a
         # CU with the main stream's data-gradient GEMMs (+1.0% step, interleaved A/B gpurun_out prio2;
@@ -431,6 +446,7 @@ class ConvNeXtHip(nn.Module):
                        db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
         nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
         nv.value("sv_gemm_set_priority", prev_prio)
+        nv.value("sv_gemm_set_grid_cap", prev_cap)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
             pending.clear()  # safe: later main-stream allocations are ordered after the join

@@ -21,6 +21,7 @@ spine_vision/training/models/backbone.py:166-170 (names at backbone.py:27,29; ti
 from __future__ import annotations
 
 import os
+import weakref
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -74,16 +75,25 @@ class Bottleneck(nn.Module):
 class _ResNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, model):  # noqa: D401 - autograd signature
-        feat, tape = model._forward_train(x)
+        feat, tape, lease = model._forward_train(x)
         ctx.model = model
         ctx.tape = tape
+        ctx.lease = lease  # keeps a graph-owned tape marked live until backward (or until ctx is freed)
         return feat
 
     @staticmethod
     def backward(ctx, dfeat):
         ctx.model._backward_impl(ctx.tape, dfeat)
         ctx.tape = None
+        ctx.lease = None
         return None, None, None
+
+
+class _TapeLease:
+    """Marks a captured graph's static tape as holding activations a pending backward still needs.  The
+    graph entry keeps only a weak reference: the lease dies when backward has consumed the tape or when the
+    autograd graph that holds it is freed, and only while it is alive does a replay of the same graph fall
+    back to the eager forward (which allocates a fresh tape) instead of overwriting it."""
 
 
 @dataclass
@@ -91,6 +101,7 @@ class _Tape:
     stem: tuple = ()
     blocks: list = field(default_factory=list)
     out_shape: tuple = ()
+    batch_stats: bool = True  # train-mode BN (batch statistics) in the forward that made the tape
 
 
 class ResNetHip(nn.Module):
@@ -133,6 +144,11 @@ class ResNetHip(nn.Module):
         self.graph_forward = os.environ.get("SV_GRAPH_FORWARD", "1") != "0"
         self._fgraphs: dict = {}
         self._fwarm: set = set()
+        self._fgraph_storage = None  # device storage the captured graphs read (see _storage_sig)
+        self.graph_safe = True  # the whole step may be captured (StepEngine(cuda_graph=True))
+        # data-parallel runs: the backward's GEMM grids (both streams) leave this many CUs to RCCL (see
+        # ConvNeXtHip.comm_reserve_cus); 0 = every CU
+        self.comm_reserve_cus = 0
         self._init_weights()
 
     def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
@@ -140,6 +156,20 @@ class ResNetHip(nn.Module):
         whose channels need no padding (Cs == Cin) reads its shadow directly: [Cout][Cin][1][1] is
         already the packed [Cout][1][Cs] layout, so no per-step pack launch."""
         self._shadow = shadow
+        self._drop_forward_graphs()
+
+    def _drop_forward_graphs(self) -> None:
+        self._fgraphs.clear()
+        self._fwarm.clear()
+        self._fgraph_storage = None
+
+    def _storage_sig(self) -> tuple:
+        """Addresses a captured forward graph has baked in: every parameter's and buffer's storage and the
+        bf16 shadow views.  FlatArena (p.data rebinding), BufferSync (buffer rebinding), model.to() and a
+        new shadow all change it; the graphs are then dropped and re-captured."""
+        sh = self._shadow
+        return (tuple(p.data_ptr() for p in self.parameters()), tuple(b.data_ptr() for b in self.buffers()),
+                id(sh), tuple(t.data_ptr() for t in sh.values()) if sh else ())
 
     # timm ResNet.init_weights: kaiming_normal_(fan_out, relu) for convs, BN weight 1 / bias 0, and
     # zero_init_last=True: the last BN of every block starts at weight 0
@@ -213,25 +243,37 @@ class ResNetHip(nn.Module):
 
     @torch.no_grad()
     def _forward_train(self, img: torch.Tensor):
-        return self._forward_graphed(img, save=True)
+        """(features, tape, lease): the lease is None for an eager tape (a fresh allocation)."""
+        return self._forward_graphed(img, save=True, leased=True)
 
     @torch.no_grad()
-    def _forward_graphed(self, img: torch.Tensor, save: bool):
+    def _forward_graphed(self, img: torch.Tensor, save: bool, leased: bool = False):
         """_forward_impl(img, save), from a captured graph when graph_forward is on: the graph owns the
         static input, the activations saved for the backward (the tape, reused by every replay) and the
         features; the caller gets a copy of the features.  BatchNorm statistics (batch or running), weight
         packing and the bf16 shadow reads all run inside the graph, so a replay is the eager forward kernel
-        for kernel.  Used for the training forward and the tape-free eval / predict forward."""
+        for kernel.  Used for the training forward and the tape-free eval / predict forward.
+
+        A training replay whose tape a pending backward still holds (two forwards before one backward:
+        a two-view loss, say) runs eagerly instead of overwriting it (``_TapeLease``)."""
+        def eager():
+            feat, tape = self._forward_impl(img, save=save)
+            return (feat, tape, None) if leased else (feat, tape)
+
         if not (self.graph_forward and img.is_cuda) or torch.cuda.is_current_stream_capturing():
-            return self._forward_impl(img, save=save)  # (inside a whole-step capture: no nested graph)
+            return eager()  # (inside a whole-step capture: no nested graph)
+        sig = self._storage_sig()
+        if sig != self._fgraph_storage:  # weights / buffers / shadow rebound since the capture
+            self._drop_forward_graphs()
+            self._fgraph_storage = sig
         key = (tuple(img.shape), img.dtype, img.device, save, self.training)
         ent = self._fgraphs.get(key)
         if ent is None:
             if len(self._fgraphs) >= _MAX_FORWARD_GRAPHS:  # each graph keeps its activations' memory pool
-                return self._forward_impl(img, save=save)
+                return eager()
             if key not in self._fwarm:  # first call: eager (lazy kernel attributes, caches)
                 self._fwarm.add(key)
-                return self._forward_impl(img, save=save)
+                return eager()
             static = img.clone()
             torch.cuda.synchronize(img.device)
             graph = torch.cuda.CUDAGraph()
@@ -239,12 +281,18 @@ class ResNetHip(nn.Module):
             # the capture do not invalidate it
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 feat, tape = self._forward_impl(static, save=save)
-            ent = self._fgraphs[key] = (static, graph, feat, tape)
-        static, graph, feat, tape = ent
+            ent = self._fgraphs[key] = [static, graph, feat, tape, None]
+        static, graph, feat, tape, lease_ref = ent
+        if leased and lease_ref is not None and lease_ref() is not None:
+            return eager()  # the static tape still belongs to a pending backward
         if static.data_ptr() != img.data_ptr():
             static.copy_(img)
         graph.replay()
-        return feat.clone(), tape
+        if not leased:
+            return feat.clone(), tape
+        lease = _TapeLease()
+        ent[4] = weakref.ref(lease)
+        return feat.clone(), tape, lease
 
     @torch.no_grad()
     def _forward_impl(self, img: torch.Tensor, save: bool):
@@ -259,7 +307,7 @@ class ResNetHip(nn.Module):
         m0, r0 = self._bn(self.bn1, y0.view(-1, C), p0)
         a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act).view(B, H, W, C)
         x, idx = K.maxpool_fwd(a0)
-        tape = _Tape() if save else None
+        tape = _Tape(batch_stats=self.training) if save else None
         if save:
             tape.stem = (x0, y0, m0, r0, a0, idx, wp0, s0)
         for blk in self.blocks():
@@ -333,9 +381,13 @@ class ResNetHip(nn.Module):
                 self._ready(params)
             return
         side.wait_event(torch.cuda.current_stream().record_event())
+        ncu = torch.cuda.get_device_properties(side.device).multi_processor_count
         if self.side_grid_cap is None:
-            self.side_grid_cap = torch.cuda.get_device_properties(side.device).multi_processor_count * 3 // 4
-        prev = nv.value("sv_gemm_set_grid_cap", self.side_grid_cap)
+            self.side_grid_cap = ncu * 3 // 4
+        cap = self.side_grid_cap
+        if self.comm_reserve_cus > 0:
+            cap = min(cap, max(1, ncu - self.comm_reserve_cus))
+        prev = nv.value("sv_gemm_set_grid_cap", cap)
         with torch.cuda.stream(side):
             for dy4, x, s, dw in jobs:
                 K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
@@ -344,7 +396,8 @@ class ResNetHip(nn.Module):
         keep.append(jobs)
 
     @torch.no_grad()
-    def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None) -> torch.Tensor:
+    def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None,
+                        batch_stats: bool = True) -> torch.Tensor:
         """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
         block's parameter gradients and returns dL/d(block input) (f32)."""
         act = self.act_dtype
@@ -359,7 +412,8 @@ class ResNetHip(nn.Module):
         conv, bn, _, _, _, _ = convs[-1]
         cur_in, y, mean, rstd, _, wp, s = saved[-1]
         dy = K.bn_bwd(d.reshape(rows, Cq), y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
-                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm)
+                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm,
+                      batch_stats=batch_stats)
         params = [bn.weight, bn.bias]
         for ci in range(len(convs) - 1, -1, -1):
             conv, bn, _, _, _, _ = convs[ci]
@@ -375,7 +429,8 @@ class ResNetHip(nn.Module):
             Cp = py.shape[-1]
             # the inner BN's own ReLU: mask recomputed from y (the activation pa is not read again)
             dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, relu_beta=pbn.bias.detach(),
-                          dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act)
+                          dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act,
+                          batch_stats=batch_stats)
             params += [pbn.weight, pbn.bias]
         # dy is now the gradient at conv1's output; conv1's input is x_in
         s1, wp1 = saved[0][6], saved[0][5]
@@ -383,7 +438,7 @@ class ResNetHip(nn.Module):
             yd, md, rd, wpd, sd = ds_saved
             dconv, dbn = blk.downsample[0], blk.downsample[1]
             dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
-                           dx_dtype=act)
+                           dx_dtype=act, batch_stats=batch_stats)
             dyd4 = dyd.view(yd.shape)
             jobs.append((dyd4, x_in, sd, g(dconv.weight)))
             # conv1's data gradient first (a plain store), then the strided shortcut's added onto the
@@ -403,6 +458,10 @@ class ResNetHip(nn.Module):
         g = self._grad
         main = torch.cuda.current_stream()
         side = self._side_stream(main.device) if (self.overlap_wgrad and self.compute_bf16) else None
+        main_cap = 0
+        if self.comm_reserve_cus > 0:
+            main_cap = max(1, torch.cuda.get_device_properties(main.device).multi_processor_count - self.comm_reserve_cus)
+        prev_cap = nv.value("sv_gemm_set_grid_cap", main_cap)
         keep: list = []
         deferred: list | None = [] if side is not None else None
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
@@ -410,18 +469,21 @@ class ResNetHip(nn.Module):
         for i, (blk, saved_block) in zip(range(len(blocks) - 1, -1, -1), zip(reversed(blocks), reversed(tape.blocks))):
             # the first block's (and below, the stem's) weight gradients stay on the main stream: nothing
             # is left for the main stream to overlap them with, while the side stream drains its queue
-            d = self._block_backward(blk, saved_block, d, side if i > 0 else None, keep, deferred)
+            d = self._block_backward(blk, saved_block, d, side if i > 0 else None, keep, deferred,
+                                     batch_stats=tape.batch_stats)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
         da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
         dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
-                       dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act)
+                       dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
+                       batch_stats=tape.batch_stats)
         self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
                            [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
             self._ready(deferred)
+        nv.value("sv_gemm_set_grid_cap", prev_cap)
         keep.clear()
 
 

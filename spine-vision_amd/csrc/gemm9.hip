@@ -28,6 +28,23 @@ namespace sv {
 extern int g_gemm_grid_cap;
 namespace g9 {
 
+#ifdef SV_CLOCK_STAMPS
+// diagnostic build only (tools/build_stamp.sh, MI355X_MICROARCH.md "DVFS give-back" item 6): per workgroup
+// s_memtime / s_memrealtime at the start and the end of the launch, in a buffer of their own that no other
+// code reads; the in-kernel clock is d(memtime) / d(memrealtime) x 100 MHz.  Not part of libsv_kernels.so.
+__device__ unsigned long long g_stamps[1024][4];
+__device__ __forceinline__ void stamp(int slot) {
+  const unsigned long long t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {
+    volatile unsigned long long* p = g_stamps[blockIdx.x];
+    p[2 * slot] = t;
+    p[2 * slot + 1] = r;
+  }
+}
+#else
+__device__ __forceinline__ void stamp(int) {}
+#endif
+
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512, NW = 8;
 constexpr int FM = 8, FN = 4;
 constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF_BYTES = A_BYTES + B_BYTES;
@@ -458,6 +475,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       }
   };
 
+  stamp(0);
   // prologue: K-tiles 0 and 1, then K-tile 0 landed everywhere
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -589,6 +607,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
   if (wm == 0) bar();
+  stamp(1);
 }
 
 template <bool AK, int EPI>
@@ -676,6 +695,14 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
 }
 
 }  // namespace g9
+
+#ifdef SV_CLOCK_STAMPS
+extern "C" int sv_diag_clock_stamps(unsigned long long* host, int n) {
+  if (n > 1024) n = 1024;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g9::g_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int launch_gemm9(const sv_gemm_desc* d, hipStream_t s) {
   using namespace g9;

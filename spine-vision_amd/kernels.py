@@ -48,6 +48,42 @@ PROBES: list[GemmProbe] = []
 PROBE: GemmProbe | None = None
 
 
+class OpProbe:
+    """Times every launch of one HBM-bound kernel (depthwise conv fwd / bwd-data / wgrad, LayerNorm
+    backward, AdamW) with HIP events on the launching stream; ``bytes`` are the kernel's ALGORITHMIC HBM
+    bytes (every operand read once, every required output written once; partial sums it chooses to
+    write for a later fold are not counted)."""
+
+    def __init__(self, name: str) -> None:
+        self.name = name
+        self.events: list = []
+        self.flops = 0.0
+        self.bytes = 0.0
+        self.launches = 0
+
+    def elapsed_ms(self) -> float:
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+OP_PROBES: dict[str, OpProbe] = {}  # name -> probe; bench.py fills it for the timed step it probes
+
+
+def _timed_call(op: str, nbytes: float, *args) -> None:
+    """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed."""
+    pr = OP_PROBES.get(op)
+    if pr is None:
+        call(*args)
+        return
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    call(*args)
+    ev1.record()
+    pr.events.append((ev0, ev1))
+    pr.bytes += nbytes
+    pr.launches += 1
+
+
 def _check(cond: bool, msg: str) -> None:
     if not cond:
         raise ValueError(msg)
@@ -288,8 +324,10 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
         dx = torch.empty(rows, C, device=x2d.device, dtype=out_dtype)
     P = value("sv_layernorm_bwd_nparts", rows, C)
     pw = torch.empty(2, P * C, device=x2d.device, dtype=torch.float32)
-    call("sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(dx), dt(dx),
-         int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
+    # algorithmic: dy, x read; dx written (read too when accumulating); mean / rstd read
+    nb = rows * C * (dy2d.element_size() + x2d.element_size() + dx.element_size() * (2 if accumulate_dx else 1)) + rows * 8
+    _timed_call("ln_bwd", nb, "sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w),
+                ptr(dx), dt(dx), int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
     if defer_reduce:
         def finish(record: bool = True):
             if record:  # the caller may instead keep pw alive until the streams have joined
@@ -314,8 +352,11 @@ def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN):
     y = torch.empty(B * H * W, C, device=x4d.device, dtype=act_dtype)
     mean = torch.empty(B * H * W, device=x4d.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
-    call("sv_dwconv7_ln_fwd", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw), ptr(lnw), ptr(lnb), eps, ptr(z), dt(z),
-         ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C)
+    n = B * H * W * C
+    # algorithmic: x read once; z (saved for the LN backward) and y (the fc1 operand) written; mean / rstd
+    nb = n * (x4d.element_size() + z.element_size() + y.element_size()) + B * H * W * 8
+    _timed_call("dw_fwd", nb, "sv_dwconv7_ln_fwd", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw), ptr(lnw), ptr(lnb), eps, ptr(z),
+                dt(z), ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C)
     return z, y, mean, rstd
 
 
@@ -324,7 +365,11 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
     _check(dx4d.shape == dz4d.shape and dx4d.dtype == torch.float32, "dwconv7_bwd_data: shape")
     if dx_bf16 is not None:
         _check(dx_bf16.numel() == dx4d.numel() and dx_bf16.dtype == torch.bfloat16, "dwconv7_bwd_data: bf16 copy")
-    call("sv_dwconv7_bwd_data", ptr(dz4d), dt(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16), int(accumulate), B, H, W, C)
+    n = B * H * W * C
+    # algorithmic: dz read; the f32 gradient stream dx written (and read when accumulating); its bf16 copy
+    nb = n * (dz4d.element_size() + 4 * (2 if accumulate else 1) + (2 if dx_bf16 is not None else 0))
+    _timed_call("dw_bwd_data", nb, "sv_dwconv7_bwd_data", ptr(dz4d), dt(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16),
+                int(accumulate), B, H, W, C)
 
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
@@ -332,7 +377,10 @@ def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
     P = value("sv_dwconv7_bwd_weight_nparts", B, H, W, C)
     pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
     pb = torch.empty(P * C, device=dz4d.device, dtype=torch.float32)
-    call("sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb), B, H, W, C)
+    # algorithmic: dz and x read once, the [C,49] + [C] gradient written (the partials are a design choice)
+    nb = B * H * W * C * (dz4d.element_size() + x4d.element_size()) + C * 50 * 4
+    _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
+                B, H, W, C)
     reduce_pair(pw, dw, pb, db, P)
 
 
@@ -532,8 +580,10 @@ def adamw_flat(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, weight_decay, step,
         call("sv_adamw_flat_dev", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(beta1), float(beta2),
              float(eps), float(weight_decay), ptr(hyper), ptr(grad_scale))
         return
-    call("sv_adamw_flat", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(lr), float(beta1), float(beta2),
-         float(eps), float(weight_decay), int(step), ptr(grad_scale))
+    # algorithmic: p, g, m, v read; p, m, v written; the bf16 shadow written (30 B / parameter)
+    nb = n * (28 + (2 if p_bf16 is not None else 0))
+    _timed_call("adamw", nb, "sv_adamw_flat", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), n, float(lr), float(beta1),
+                float(beta2), float(eps), float(weight_decay), int(step), ptr(grad_scale))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -829,10 +879,13 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
 
 
 def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=None, dbeta=None,
-           dx_dtype=torch.float32, gmask=None) -> torch.Tensor:
-    """BatchNorm (train) backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
+           dx_dtype=torch.float32, gmask=None, batch_stats: bool = True) -> torch.Tensor:
+    """BatchNorm backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
     act > 0, or -- ``relu_beta`` = the BN's beta, for a BN followed by its own ReLU -- recomputed from y
-    like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again)."""
+    like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again).
+    ``batch_stats``: train mode (mean / rstd are the batch's own, so dx carries the two mean corrections);
+    False: eval mode (running statistics, an affine map: dx = gamma * rstd * dout, the apply kernel reading
+    zero correction sums)."""
     rows, C = y2d.shape
     _check(_bn_c_ok(C) and dout2d.numel() == rows * C and dout2d.is_contiguous(), "bn_bwd: bad shapes")
     _check(act is None or relu_beta is None, "bn_bwd: act and relu_beta are exclusive")
@@ -851,6 +904,8 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
              ptr(rstd), rows, C, ptr(part))
     sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
+    if not batch_stats:
+        sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
     if relu_beta is not None:
         call("sv_bn_relu_bwd_apply", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),

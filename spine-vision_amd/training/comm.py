@@ -20,10 +20,49 @@ logic is backend-agnostic (gloo on CPU tensors in the unit tests).
 
 from __future__ import annotations
 
+from collections import deque
+
 import torch
 import torch.distributed as dist
 
 from .flat import FlatArena
+
+
+def plan_buckets(arena: FlatArena, bucket_mb: float) -> list[tuple[int, int, list[int]]]:
+    """Contiguous buckets (start, end, param indices) of the flat gradient buffer, built from its END
+    (backward produces gradients in reverse parameter order), each at least ``bucket_mb``."""
+    cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
+    buckets: list[tuple[int, int, list[int]]] = []
+    cur: list[int] = []
+    cur_end = None
+    n = len(arena.params)
+    for i in reversed(range(n)):
+        s = arena.offsets[i]
+        e = arena.offsets[i + 1] if i + 1 < n else arena.numel
+        if cur_end is None:
+            cur_end = e
+        cur.append(i)
+        if cur_end - s >= cap:
+            buckets.append((s, cur_end, cur))
+            cur, cur_end = [], None
+    if cur:
+        buckets.append((arena.offsets[cur[-1]], cur_end, cur))
+    return buckets
+
+
+def _attach_ready(model: torch.nn.Module, arena: FlatArena, mark_ready) -> list:
+    """Route gradient readiness to ``mark_ready``: backbones report per block (grad_ready_hook), the
+    autograd-managed parameters (the torch head) through post-accumulate hooks.  Returns the hook handles."""
+    backbone_params = set()
+    for m in model.modules():
+        if hasattr(m, "grad_ready_hook"):
+            m.grad_ready_hook = mark_ready
+            backbone_params |= {id(p) for p in m.parameters()}
+    hooks = []
+    for p in arena.params:
+        if id(p) not in backbone_params and p.requires_grad:
+            hooks.append(p.register_post_accumulate_grad_hook(lambda t: mark_ready([t])))
+    return hooks
 
 
 class GradBucketer:
@@ -31,23 +70,8 @@ class GradBucketer:
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group)
-        cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
         # buckets over parameter indices, built from the end of the buffer
-        self.buckets: list[tuple[int, int, list[int]]] = []  # (start, end, param indices)
-        cur: list[int] = []
-        cur_end = None
-        n = len(arena.params)
-        for i in reversed(range(n)):
-            s = arena.offsets[i]
-            e = arena.offsets[i + 1] if i + 1 < n else arena.numel
-            if cur_end is None:
-                cur_end = e
-            cur.append(i)
-            if cur_end - s >= cap:
-                self.buckets.append((s, cur_end, cur))
-                cur, cur_end = [], None
-        if cur:
-            self.buckets.append((arena.offsets[cur[-1]], cur_end, cur))
+        self.buckets: list[tuple[int, int, list[int]]] = plan_buckets(arena, bucket_mb)  # (start, end, params)
         self.param_bucket = {}
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
@@ -58,7 +82,7 @@ class GradBucketer:
         # timing (bench.py): HIP events around every bucket's all-reduce on the comm stream, and around
         # the compute stream's join (the exposed, un-overlapped part of the exchange)
         self.timing = False
-        self._bucket_ev: list = []
+        self._bucket_ev = deque(maxlen=64 * len(self.buckets))  # the last 64 steps' bucket events
         self._join_ev = None
         self.reset()
 
@@ -70,14 +94,7 @@ class GradBucketer:
 
     def attach(self, model: torch.nn.Module) -> None:
         """Route readiness from backbones (grad_ready_hook) and autograd-managed params."""
-        backbone_params = set()
-        for m in model.modules():
-            if hasattr(m, "grad_ready_hook"):
-                m.grad_ready_hook = self.mark_ready
-                backbone_params |= {id(p) for p in m.parameters()}
-        for p in self.arena.params:
-            if id(p) not in backbone_params and p.requires_grad:
-                self._hooks.append(p.register_post_accumulate_grad_hook(lambda t: self.mark_ready([t])))
+        self._hooks += _attach_ready(model, self.arena, self.mark_ready)
 
     def mark_ready(self, params) -> None:
         for p in params:
@@ -103,16 +120,18 @@ class GradBucketer:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e0.record()
                 w = dist.all_reduce(view, op=op, group=self.group, async_op=True)
-                # the comm stream waits on RCCL's internal stream (no host block), so later buckets,
-                # the timing event and the compute stream's join are all ordered after this reduce
-                w.wait()
-                if op == dist.ReduceOp.SUM and self.world > 1:
-                    view.div_(self.world)
+                if op == dist.ReduceOp.AVG:
+                    # RCCL: the comm stream waits on RCCL's internal stream (no host block), so later
+                    # buckets, the timing event and the compute stream's join are ordered after it
+                    w.wait()
+                    w = None
                 if e0 is not None:
                     e1 = torch.cuda.Event(enable_timing=True)
                     e1.record()
                     self._bucket_ev.append((e0, e1, view.numel() * view.element_size()))
-            self.works.append((None, view, op))
+            # gloo on device tensors: wait() blocks the host until the reduce is done, so it is deferred
+            # to finish() (the backward keeps being enqueued meanwhile)
+            self.works.append((w, view, op))
         else:
             w = dist.all_reduce(view, op=op, group=self.group, async_op=True)
             self.works.append((w, view, op))
@@ -125,6 +144,12 @@ class GradBucketer:
                 self._launch(b)
         for w, view, op in self.works:
             if w is None:
+                continue
+            if self.use_streams:
+                with torch.cuda.stream(self.comm_stream):
+                    w.wait()
+                    if op == dist.ReduceOp.SUM and self.world > 1:
+                        view.div_(self.world)
                 continue
             w.wait()
             if op == dist.ReduceOp.SUM and self.world > 1:
@@ -171,6 +196,63 @@ class GradBucketer:
     def clear_timing(self) -> None:
         self._bucket_ev.clear()
         self._join_ev = None
+
+
+class BucketTimeline:
+    """Single-GPU rehearsal of the data-parallel exchange (bench.py, world 1): the bucket plan GradBucketer
+    would use, an event recorded on the stream where each bucket's last gradient becomes final (the moment
+    its all-reduce would launch), and the backward's start / end events.  ``predict`` replays those ready
+    times through a model of the comm stream (buckets in ready order, each taking its ring all-reduce time at
+    a given bus bandwidth) to estimate the exposed exchange and the N-GPU scaling."""
+
+    def __init__(self, arena: FlatArena, model: torch.nn.Module, bucket_mb: float = 64.0) -> None:
+        self.arena = arena
+        self.buckets = plan_buckets(arena, bucket_mb)
+        self.param_bucket = {id(arena.params[i]): b for b, (_, _, idx) in enumerate(self.buckets) for i in idx}
+        self.active = False
+        self._hooks = _attach_ready(model, arena, self.mark_ready)
+        self.reset()
+
+    def reset(self) -> None:
+        self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.seen: set[int] = set()
+        self.ready_ev: list = [None] * len(self.buckets)
+
+    def mark_ready(self, params) -> None:
+        if not self.active:
+            return
+        for p in params:
+            if id(p) in self.seen or id(p) not in self.param_bucket:
+                continue
+            self.seen.add(id(p))
+            b = self.param_bucket[id(p)]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()  # on the stream that made the gradient final (the side stream for most blocks)
+                self.ready_ev[b] = ev
+
+    def ready_ms(self, start_ev) -> list:
+        """Per bucket: (MB, ms after ``start_ev`` at which it became ready, or None)."""
+        torch.cuda.synchronize()
+        out = []
+        for (s, e, _), ev in zip(self.buckets, self.ready_ev):
+            out.append((round((e - s) * 4 / 2**20, 2), round(start_ev.elapsed_time(ev), 3) if ev is not None else None))
+        return out
+
+    @staticmethod
+    def predict(ready: list, bwd_end_ms: float, step_ms: float, world: int, busbw_gbs: float) -> dict:
+        """Exposed exchange and scaling at ``world`` ranks if every bucket's ring all-reduce takes
+        2 (n-1)/n x bytes / busbw on one comm stream, launched at its ready time (a bucket never ready in the
+        backward launches at its end); the step grows by what finishes after the backward's end."""
+        t = 0.0
+        for mb, r in sorted(ready, key=lambda x: (x[1] is None, x[1] if x[1] is not None else 0.0)):
+            start = max(t, r if r is not None else bwd_end_ms)
+            t = start + 2.0 * (world - 1) / world * mb * 2**20 / (busbw_gbs * 1e9) * 1e3
+        exposed = max(0.0, t - bwd_end_ms)
+        return {"world": world, "busbw_gbs": busbw_gbs, "comm_end_ms": round(t, 3), "exposed_ms": round(exposed, 3),
+                "predicted_step_ms": round(step_ms + exposed, 3),
+                "predicted_scaling": round(world * step_ms / (step_ms + exposed), 3)}
 
 
 class BufferSync:

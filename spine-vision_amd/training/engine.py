@@ -100,6 +100,12 @@ class StepEngine:
                  weight_decay: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  grad_clip: float | None = 1.0, distributed: bool | None = None, bucket_mb: float = 64.0,
                  cuda_graph: bool = False) -> None:
+        # a backbone whose backward queries events (ConvNeXt's lean side-stream release) declares
+        # graph_safe = False and cannot be captured: asking for it is an error, not a silent fallback.
+        if cuda_graph:
+            unsafe = [type(m).__name__ for m in model.modules() if getattr(m, "graph_safe", True) is False]
+            if unsafe:
+                raise ValueError(f"cuda_graph=True: {unsafe[0]} is not capture-safe (graph_safe = False)")
         self.model = model
         self.device = torch.device(device)
         self.grad_clip = grad_clip
@@ -111,16 +117,22 @@ class StepEngine:
         self.bucketer = None
         self.buffer_sync = None
         if distributed:
+            if self.device.type == "cuda":
+                # RCCL's kernels need free CUs during the backward (SV_COMM_RESERVE_CUS, default 32 of 256)
+                reserve = int(os.environ.get("SV_COMM_RESERVE_CUS", "32"))
+                for m in model.modules():
+                    if hasattr(m, "comm_reserve_cus"):
+                        m.comm_reserve_cus = reserve
             broadcast_parameters(self.arena, model)
             self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb)
             self.bucketer.attach(model)
             self.buffer_sync = BufferSync(model)
         self.last_grad_norm: torch.Tensor | None = None
+        self.after_backward: Callable[[], None] | None = None  # called once the backward is enqueued (bench)
         self.limiter = InflightLimiter() if self.device.type == "cuda" else None
         # cuda_graph: the whole step (zero grads, forward, backward, clip, AdamW) captured once per input
         # signature as a HIP graph and replayed -- for the launch-bound ResNet step the host enqueue of
-        # ~700 kernels (9.6 ms) exceeded the GPU time.  Single-process only (no RCCL inside the graph);
-        # backbones whose backward queries events (ConvNeXt's lean side-stream release) stay eager.
+        # ~700 kernels (9.6 ms) exceeded the GPU time.  Single-process only (no RCCL inside the graph).
         self.cuda_graph = bool(cuda_graph) and not distributed and self.device.type == "cuda"
         self._graphs: dict = {}
         self._warm: set = set()
@@ -134,6 +146,8 @@ class StepEngine:
         loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
+        if self.after_backward is not None:
+            self.after_backward()
         scale = None
         if self.grad_clip:
             nc = K.grad_clip_coef(self.arena.grad_flat, self.grad_clip)

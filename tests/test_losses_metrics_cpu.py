@@ -61,3 +61,39 @@ def test_localization_metrics_match_reference():
     assert set(got) == set(g["metrics"]), (sorted(got), sorted(g["metrics"]))
     for k, v in g["metrics"].items():
         assert got[k] == pytest.approx(v, rel=1e-6, abs=1e-7), k
+
+
+@pytest.mark.parametrize("loss_type", ["mse", "smooth_l1", "huber"])
+def test_regressor_loss_variants_match_reference(loss_type):
+    """CoordinateRegressor.get_loss for every loss_type against the reference module's own outputs
+    (tests/golden/loss_variants.json, make_golden_r3.py; reference generic.py:354-361, 393-417): loss and
+    dL/dpred with mask=None, a partial mask and a single valid level.
+
+    All-invalid mask (documented divergence, DESIGN.md "Losses"): the reference returns a constant
+    torch.tensor(0.0) without a graph, so its accelerator.backward() raises; the build returns a
+    differentiable 0 (no host sync to detect the case), whose gradient is exactly zero -- the step then
+    runs AdamW on zero gradients (weight decay and moment decay only)."""
+    from spine_vision_amd.training import CoordinateRegressor
+
+    g = _load("loss_variants.json")
+    shape = g["shape"]
+    pred0 = torch.tensor(g["pred"]).reshape(shape)
+    tgt = torch.tensor(g["target"]).reshape(shape)
+    model = CoordinateRegressor("resnet18", pretrained=False, dropout=0.0, loss_type=loss_type)
+    cases = [c for c in g["cases"] if c["loss_type"] == loss_type]
+    assert len(cases) == 4
+    for c in cases:
+        m = g["masks"][c["mask"]]
+        mask = None if m is None else torch.tensor(m).reshape(shape[:2])
+        p = pred0.clone().requires_grad_(True)
+        loss = model.get_loss(p, tgt, mask=mask)
+        if c["requires_grad"]:
+            loss.backward()
+            np.testing.assert_allclose(float(loss), c["loss"], rtol=1e-6, atol=0)
+            np.testing.assert_allclose(p.grad.reshape(-1).numpy(), np.array(c["grad"], np.float32), rtol=1e-5,
+                                       atol=1e-9)
+        else:
+            assert c["mask"] == "all_invalid" and c["loss"] == 0.0
+            assert float(loss) == 0.0
+            loss.backward()
+            assert float(p.grad.abs().max()) == 0.0

@@ -89,47 +89,6 @@ def test_convnext_bf16_geometry(dev, name, res, B):
     assert pred < bp and worst < bw and med < bm, (pred, worst, med)
 
 
-def test_resnet50_bf16_256(dev):
-    """ResNet-50 @256, B=2, bf16, whole model (3-head Classifier): logits and every gradient.
-
-    With these synthetic weights the train-mode-BN network is chaotic under ANY bf16 arithmetic: torch's
-    own CPU bf16 autocast of the same model is 7-21% off the fp32 logits and ~1.3 (median) off the fp32
-    gradients (measured in the build container).  A fixed bound against fp32 would therefore test the
-    weights, not the kernels.  The bar is relative to that intrinsic error instead: the HIP bf16 error
-    must stay within 2x of torch-bf16-autocast's error on the same inputs.  The per-block bf16 kernel
-    error at this geometry is pinned separately by test_resnet_block_backward_teacher_forced."""
-    import copy
-
-    from spine_vision_amd.training import Classifier
-    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
-
-    tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
-    ref = oh.Classifier(orn.create("resnet50"), 2048, dropout=0.0)
-    ow.fill_module(ref)
-    auto = copy.deepcopy(ref).train()
-    hip = Classifier(backbone="resnet50", tasks=tasks, pretrained=False, dropout=0.0, precision="bf16")
-    hip.load_state_dict(ref.state_dict(), strict=True)
-    ref.train()
-    hip = hip.to(dev).train()
-    img, targets = ow.classification_batch(2, 256, 256)
-    o_ref = ref(img)
-    ref.get_loss(o_ref, targets).backward()
-    with torch.autocast("cpu", dtype=torch.bfloat16):
-        o_auto = auto(img)
-        l_auto = auto.get_loss(o_auto, targets)
-    l_auto.backward()
-    o_hip = hip(img.to(dev))
-    hip.get_loss(o_hip, {k: v.to(dev) for k, v in targets.items()}).backward()
-    torch.cuda.synchronize()
-    pred = max(rel(o_hip[k], o_ref[k]) for k in o_ref)
-    pred_auto = max(rel(o_auto[k].float(), o_ref[k]) for k in o_ref)
-    errs = {n: rel(b.grad, a.grad) for (n, a), b in zip(ref.named_parameters(), hip.parameters())}
-    errs_auto = {n: rel(b.grad.float(), a.grad) for (n, a), b in zip(ref.named_parameters(), auto.parameters())}
-    worst, med = _report("resnet50@256 B2 bf16 (HIP)", pred, errs)
-    worst_a, med_a = _report("resnet50@256 B2 bf16 (torch CPU autocast)", pred_auto, errs_auto)
-    assert pred < 2 * pred_auto and med < 2 * med_a and worst < 2 * worst_a, (pred, pred_auto, med, med_a)
-
-
 @pytest.mark.parametrize("knob", ["lean_sync", "overlap_wgrad"])
 def test_convnext_bf16_schedule_knobs_match_default(dev, knob):
     """SV_LEAN_SYNC=0 / SV_SIDE_STREAM=0 change only WHERE the same kernels run (one main->side hand-off

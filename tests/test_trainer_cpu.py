@@ -227,3 +227,14 @@ def test_classification_config_device_transform_reaches_datasets(tmp_path):
     CpuCls(cfg, model=TinyCls(_create_tasks_for_training(labels)), train_dataset=tr_ds, val_dataset=va_ds)
     assert tr_ds.device_transform and va_ds.device_transform
     assert tr_ds[0]["image"].dtype == torch.uint8 and tr_ds[0]["image"].shape == (16, 16, 3)
+
+
+def test_step_engine_refuses_graph_for_unsafe_backbone():
+    """ConvNeXt's lean backward polls side-stream events, which a stream capture forbids, so
+    StepEngine(cuda_graph=True) must refuse it up front instead of failing at the second step."""
+    from spine_vision_amd.backbone import create_convnext, create_resnet
+    from spine_vision_amd.training import StepEngine
+
+    assert create_resnet("resnet18").graph_safe is True
+    with pytest.raises(ValueError, match="capture-safe"):
+        StepEngine(create_convnext("convnext_tiny"), "cpu", cuda_graph=True)

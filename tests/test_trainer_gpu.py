@@ -4,6 +4,7 @@ flat fused AdamW, device-side clip; two epochs on synthetic 64x64 data, checkpoi
 import pytest
 import torch
 
+from spine_vision_amd.backbone import create_resnet
 from spine_vision_amd.training import Classifier, CoordinateRegressor, LocalizationConfig, LocalizationTrainer
 from spine_vision_amd.training.datasets import SyntheticLocalizationDataset
 
@@ -287,3 +288,72 @@ def test_resnet_graph_forward_matches_eager(dev, backbone):
     assert all(torch.equal(x, y) for sa, sb in zip(ga, gb) for x, y in zip(sa, sb))
     assert all(torch.equal(x, y) for x, y in zip(pa, pb))
     assert all(torch.equal(x, y) for x, y in zip(ba, bb))
+
+
+def test_resnet_graph_forward_follows_rebound_storage(dev):
+    """a captured forward graph bakes in the weights', buffers' and bf16 shadows' addresses.  After
+    the graph is captured, (1) a FlatArena rebinds every parameter and installs a bf16 shadow, (2) a BufferSync
+    rebinds the BatchNorm buffers, (3) the new storage is updated in place.  Each time the next forward must
+    read the new storage (graphs dropped and re-captured): it equals a graph-less twin's bit for bit."""
+    from spine_vision_amd.training.comm import BufferSync
+    from spine_vision_amd.training.flat import FlatArena
+
+    torch.manual_seed(0)
+    a = create_resnet("resnet18", precision="bf16").to(dev).eval()
+    b = create_resnet("resnet18", precision="bf16").to(dev).eval()
+    b.load_state_dict(a.state_dict())
+    b.graph_forward = False
+    x = torch.rand(4, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
+
+    def check(n=3):
+        with torch.no_grad():
+            fa = [a(x) for _ in range(n)]
+            fb = b(x)
+        torch.cuda.synchronize()
+        assert all(torch.equal(f, fb) for f in fa)
+
+    check()
+    assert len(a._fgraphs) == 1
+    arenas = [FlatArena(net, dev, with_shadow=True) for net in (a, b)]  # (1)
+    check()
+    for net in (a, b):  # (2)
+        BufferSync(net)
+    with torch.no_grad():
+        for net in (a, b):
+            for name, buf in net.named_buffers():
+                if name.endswith("running_mean"):
+                    buf.add_(0.25)
+    check()
+    with torch.no_grad():  # (3) in place: the addresses stay, the graphs read the new values
+        for ar in arenas:
+            ar.param_flat.mul_(0.5)
+            ar.refresh_shadow()
+    check()
+    assert len(a._fgraphs) == 1
+
+
+def test_resnet_graph_forward_two_forwards_one_backward(dev):
+    """two training forwards before one backward (a two-view loss).  The second forward must not
+    overwrite the first one's graph-owned tape: every gradient equals the eager model's bit for bit."""
+    torch.manual_seed(0)
+    a = create_resnet("resnet18", precision="bf16").to(dev).train()
+    b = create_resnet("resnet18", precision="bf16").to(dev).train()
+    b.load_state_dict(a.state_dict())
+    b.graph_forward = False
+    g = torch.Generator().manual_seed(2)
+    xs = [torch.rand(4, 3, 64, 64, generator=g).to(dev) for _ in range(4)]
+    for net in (a, b):  # warm-up + capture for the graph model (single-forward steps)
+        for x in xs[:2]:
+            net(x).sum().backward()
+    grads = []
+    for net in (a, b):
+        for p in net.parameters():
+            p.grad = None
+        f1 = net(xs[2])
+        f2 = net(xs[3])
+        (f1.square().sum() + 0.5 * f2.sum()).backward()
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().cpu().clone() for p in net.parameters()])
+    assert len(a._fgraphs) == 1
+    for ga, gb in zip(*grads):
+        assert torch.equal(ga, gb)
