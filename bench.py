@@ -82,6 +82,15 @@ def parse():
                          "classification only: ConvNeXt's lean side-stream release queries events).  Measured "
                          "(profiles/r3/graph_ab.txt): ResNet-50 3197-3228 img/s replayed vs 3395-3443 eager with "
                          "the side-stream weight gradients, 3300 single-stream replayed -- off by default")
+    ap.add_argument("--trainer", action="store_true",
+                    help="secondary line (row f1): LocalizationTrainer._train_epoch fed by its DataLoader from "
+                         "synthetic grayscale PNGs on disk (decode in the workers, resize / augment / normalise on "
+                         "the GPU with --transform device) instead of HBM-resident batches")
+    ap.add_argument("--transform", default="device", choices=["device", "host"],
+                    help="--trainer: device = device_transform (GPU resize + augment + normalise), host = the "
+                         "reference's PIL / torchvision chain in the workers")
+    ap.add_argument("--workers", type=int, default=4, help="--trainer: DataLoader workers per rank (reference: 4)")
+    ap.add_argument("--native", type=int, default=640, help="--trainer: side of the PNGs on disk (resized to 512)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU sample budget")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -293,6 +302,92 @@ def selftest(args, world: int, rank: int) -> None:
         dist.destroy_process_group()
 
 
+def _write_pngs(root: str, n: int, side: int) -> None:
+    """n synthetic grayscale MRI-like PNGs (smooth anatomy-scale structure + noise, side x side) and the
+    reference's annotations.csv layout (image_path, level, relative_x, relative_y, series_type, source)."""
+    import csv
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    from PIL import Image
+
+    os.makedirs(os.path.join(root, "img"), exist_ok=True)
+    yy, xx = np.meshgrid(np.linspace(0, 1, side), np.linspace(0, 1, side), indexing="ij")
+
+    def one(i):
+        rng = np.random.default_rng(i)
+        base = 110 + 70 * np.sin(9 * xx + 4 * yy + i) * np.cos(5 * yy - 3 * xx)
+        img = np.clip(base + rng.normal(0, 12, (side, side)), 0, 255).astype(np.uint8)
+        Image.fromarray(img, "L").save(os.path.join(root, "img", f"s{i}.png"))
+
+    with ThreadPoolExecutor(16) as ex:
+        list(ex.map(one, range(n)))
+    levels = ("L1/L2", "L2/L3", "L3/L4", "L4/L5", "L5/S1")
+    with open(os.path.join(root, "annotations.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["image_path", "level", "relative_x", "relative_y", "series_type", "source"])
+        w.writeheader()
+        for i in range(n):
+            for k, lv in enumerate(levels):
+                w.writerow({"image_path": f"img/s{i}.png", "level": lv, "relative_x": 0.45 + 0.01 * k,
+                            "relative_y": 0.2 + 0.15 * k, "series_type": "sag_t2", "source": "synthetic"})
+
+
+def trainer_line(args) -> dict:
+    """--trainer: images/sec of LocalizationTrainer._train_epoch (the reference's epoch loop, base.py:547-569)
+    fed by its own DataLoader over PNGs on disk: decode (+ host transform) in ``--workers`` worker processes,
+    then the MI355X step.  The second epoch is timed (the first starts the workers and warms the kernels).
+    Also times the per-image host work of one worker alone, which bounds the loader at workers / that."""
+    import shutil
+    import tempfile
+
+    pkg = __graft_entry__.load_package()  # noqa: F841
+    from spine_vision_amd.training import LocalizationConfig, LocalizationTrainer
+    from spine_vision_amd.training.datasets import LocalizationCollator, LocalizationDataset
+
+    steps = max(args.steps, 10)
+    root = tempfile.mkdtemp(prefix="sv_trainer_")
+    try:
+        n = int(args.batch * steps / 0.95) + args.batch  # the dataset's test split keeps 5% aside
+        _write_pngs(root, n, args.native)
+        dev_t = args.transform == "device"
+        cfg = LocalizationConfig(data_path=root, output_path=os.path.join(root, "out"), batch_size=args.batch,
+                                 num_epochs=1, num_workers=args.workers, pin_memory=True, device_transform=dev_t,
+                                 augment=True, image_size=(512, 512), pretrained=False, val_split=0.0,
+                                 log_frequency=10**9, save_frequency=10**9, early_stopping=False,
+                                 visualize_predictions=False, use_trackio=False, precision=args.precision)
+        tr = LocalizationTrainer(cfg)
+        nb = len(tr.train_loader)
+        tr._train_epoch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr._train_epoch()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        # one worker's host cost per image (decode + the dataset's host work + collation), single process
+        ds = LocalizationDataset(root, split="train", image_size=(512, 512), augment=True, device_transform=dev_t,
+                                 val_ratio=0.0)
+        col = LocalizationCollator()
+        k = min(len(ds), 4 * args.batch)
+        h0 = time.perf_counter()
+        for j in range(0, k, args.batch):
+            col([ds[i] for i in range(j, min(k, j + args.batch))])
+        per_img = (time.perf_counter() - h0) / k
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    imgs = nb * args.batch
+    return {"metric": "images/sec training, LocalizationTrainer epoch over PNGs on disk (DataLoader-fed), "
+                      f"{args.backbone} 512x512, bs{args.batch}",
+            "value": round(imgs / el, 3), "unit": "images/sec", "n_gpus": 1, "steps": nb, "warmup": nb,
+            "ms_per_step": round(el / nb * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.precision,
+            "data": f"synthetic {args.native}x{args.native} grayscale PNGs on local disk, decoded by the loader",
+            "config": {"workload": "LocalizationTrainer._train_epoch (+ its DataLoader)", "transform": args.transform,
+                       "workers": args.workers, "native_side": args.native, "image_size": 512,
+                       "batch_per_gpu": args.batch, "augment": True},
+            "host_ms_per_image_one_worker": round(per_img * 1e3, 3),
+            "host_bound_img_s": round(args.workers / per_img, 1)}
+
+
 def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: dict) -> dict:
     """Roofline of one probed GEMM class: algorithmic FLOPs / bytes per launch against the mean launch
     duration from HIP events; the binding roof is the larger of FLOPs/peak and bytes/HBM peak."""
@@ -336,6 +431,11 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.selftest:
         return selftest(args, world, rank)
+    if args.trainer:
+        if world != 1:
+            raise SystemExit("bench.py --trainer runs on one GPU")
+        print(json.dumps(trainer_line(args)), flush=True)
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -358,6 +458,10 @@ def main():
     else:
         model = CoordinateRegressor(args.backbone, pretrained=False, precision=args.precision)
     model = model.to(device).train()
+    if os.environ.get("SV_BENCH_RESERVE"):  # A/B at world 1: the CU reservation a multi-GPU run applies
+        for m in model.modules():
+            if hasattr(m, "comm_reserve_cus"):
+                m.comm_reserve_cus = int(os.environ["SV_BENCH_RESERVE"])
     graphed = args.graph == "on" and cls and world == 1
     engine = StepEngine(model, device, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
                         cuda_graph=graphed and not args.inference)

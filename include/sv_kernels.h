@@ -193,6 +193,18 @@ int sv_normalize_u8_gray(const uint8_t* img, const float* norm_mean, const float
 int sv_augment_u8(const uint8_t* in, uint8_t* out, int32_t B, int32_t H, int32_t W, int32_t C, const double* params,
                   int32_t* row_sums, sv_stream_t stream);
 
+/* ---- resize of decoded uint8 images (row f1) ---------------------------------------------------
+ * Replaces the reference's first transform, torchvision Resize(size) on a PIL image
+ * (training/datasets/localization.py:199, classification.py:250) = PIL Image.resize((W, H),
+ * BILINEAR): Pillow's two-pass fixed-point resample (libImaging/Resample.c, PRECISION_BITS 22, the
+ * horizontal pass rounded to uint8), bit for bit.  Ragged batch of B source images [h][w][C] at byte
+ * offsets in src; desc int64 [B][8] = {src offset, h, w, x-table offset, x taps, y-table offset, y
+ * taps, 0}; coef int32 tables (per axis: bounds[out][2] = {first tap, count}, then coef[out][taps]),
+ * built on the host exactly as Pillow's precompute_coeffs / normalize_coeffs_8bpc
+ * (spine_vision_amd.training.datasets.resize).  dst uint8 [B][H][W][C], C = 1 or 3.              */
+int sv_resize_u8(const uint8_t* src, const int64_t* desc, const int32_t* coef, int32_t B, int32_t H, int32_t W,
+                 int32_t C, uint8_t* dst, sv_stream_t stream);
+
 /* ---- ConvNeXt stage downsample: LayerNorm2d + 2x2/s2 patch gather (GEMM A operand) ------------
  * x [B,H,W,C] f32 -> patches [B*(H/2)*(W/2)][C*4] with k = c*4 + kh*2 + kw (= timm conv weight
  * [2C,C,2,2] flattened), so the Conv2d(k2,s2) is one sv_gemm with b_kmajor=1 on the weight.        */

@@ -143,6 +143,9 @@ class ConvNeXtHip(nn.Module):
         # CUs free so RCCL's all-reduce kernels on the comm stream find a CU (a v9 workgroup holds its CU's
         # LDS for the whole launch); 0 = every CU
         self.comm_reserve_cus = 0
+        # the lean side stream's GEMMs on at most this many workgroups (None: every CU; SV_SIDE_GRID_CAP)
+        cap = os.environ.get("SV_SIDE_GRID_CAP")
+        self.side_grid_cap: int | None = int(cap) if cap else None
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -490,6 +493,10 @@ class ConvNeXtHip(nn.Module):
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
         nv.value("sv_gemm_set_priority", 1)
+        side_cap = self.side_grid_cap
+        if side_cap is not None and self.comm_reserve_cus > 0:
+            side_cap = min(side_cap, _comm_cap(main.device, self.comm_reserve_cus))
+        prev_cap = nv.value("sv_gemm_set_grid_cap", side_cap) if side_cap is not None else None
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
@@ -502,6 +509,8 @@ class ConvNeXtHip(nn.Module):
                          blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
             pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a)))
         nv.value("sv_gemm_set_priority", 0)
+        if prev_cap is not None:
+            nv.value("sv_gemm_set_grid_cap", prev_cap)
         # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
         db = torch.empty_like(db)
         K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)

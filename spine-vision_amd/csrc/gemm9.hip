@@ -173,7 +173,11 @@ struct EpiCount {
   static constexpr int AUX = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) ? CH
                              : EPI == SV_EPI_BIAS_GAMMA_RES ? (P8 ? 2 * CH : CH)
                                                             : 0;
+#ifdef SV_DIAG_NOSTORE
+  static constexpr int E = 0;  // diagnostic build: the epilogue issues no memory instruction
+#else
   static constexpr int E = FM * (CH * OUTS + AUX);
+#endif
 };
 
 // Epilogue of one wave tile: rows m_w + 16 i + (l & 15), columns per chunk c:
@@ -183,6 +187,16 @@ struct EpiCount {
 template <int EPI, bool P8>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
                                          int split, const float* lbias) {
+#ifdef SV_DIAG_NOSTORE
+  // diagnostic build (tools/build_diag.sh): the K loop alone -- keep the accumulators live, store nothing
+  float sink = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  asm volatile("" ::"v"(sink));
+  return;
+#endif
   // lbias: the tile's bias[256] and gamma[256] staged in LDS (K loop, first K-tile), or nullptr
   constexpr int CH = P8 ? 2 : 4, CW = P8 ? 8 : 4;
   const int l = threadIdx.x & 63, ml = l & 15, gq = l >> 4;

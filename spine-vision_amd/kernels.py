@@ -483,6 +483,39 @@ def augment_u8(img_u8: torch.Tensor, params: torch.Tensor, out: torch.Tensor | N
     return out
 
 
+def resize_u8(src: torch.Tensor, desc: torch.Tensor, coef: torch.Tensor, B: int, H: int, W: int, C: int,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """PIL Image.resize((W, H), BILINEAR) of a ragged uint8 batch on the device (row f1, sv_resize_u8):
+    ``src`` flat uint8, ``desc`` int64 [B,8] and ``coef`` int32 tables from
+    ``training.datasets.resize.ragged_batch``.  Returns uint8 [B,H,W] (C = 1) or [B,H,W,3]."""
+    _check(src.dtype == torch.uint8 and src.is_contiguous(), "resize_u8: src must be contiguous uint8")
+    _check(desc.dtype == torch.int64 and tuple(desc.shape) == (B, 8) and desc.is_contiguous(), "resize_u8: desc [B,8]")
+    _check(coef.dtype == torch.int32 and coef.is_contiguous(), "resize_u8: coef must be int32")
+    _check(C in (1, 3), "resize_u8: C must be 1 or 3")
+    shape = (B, H, W) if C == 1 else (B, H, W, 3)
+    if out is None:
+        out = torch.empty(shape, device=src.device, dtype=torch.uint8)
+    _check(tuple(out.shape) == shape and out.dtype == torch.uint8 and out.is_contiguous(), "resize_u8: bad out")
+    call("sv_resize_u8", ptr(src), ptr(desc), ptr(coef), B, H, W, C, ptr(out))
+    return out
+
+
+def device_images(batch: dict, device) -> torch.Tensor:
+    """The decoded uint8 image batch of a device_transform loader on ``device``, resized (ragged batch:
+    "resize" = ragged_batch(...)) and augmented ("augment") there -- the reference's Resize -> [flip /
+    affine / jitter] on the GPU; ToTensor -> Normalize then run inside the backbone's stem gather."""
+    rz = batch.get("resize")
+    if rz is not None:
+        H, W, C = (int(v) for v in rz["out_hw"])
+        img = resize_u8(rz["src"].to(device, non_blocking=True), rz["desc"].to(device, non_blocking=True),
+                        rz["coef"].to(device, non_blocking=True), rz["desc"].shape[0], H, W, C)
+    else:
+        img = batch["image"].to(device, non_blocking=True)
+    if "augment" in batch:
+        img = augment_u8(img, batch["augment"].to(device, non_blocking=True))
+    return img
+
+
 def downsample_fwd(x4d, lnw, lnb, *, act_dtype, eps=EPS_LN):
     B, H, W, C = x4d.shape
     _check(H % 2 == 0 and W % 2 == 0, "downsample: H, W must be even")

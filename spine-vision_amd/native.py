@@ -78,6 +78,7 @@ _SIGS = {
     "sv_stem_weight_pack": [_p, _p, _i32, _p],
     "sv_normalize_u8_gray": [_p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_augment_u8": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p],
+    "sv_resize_u8": [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p],
     "sv_downsample_ln_patch2_fwd": [_p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_downsample_ln_patch2_bwd_nparts": [_i32, _i32, _i32, _i32],
     "sv_downsample_ln_patch2_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p],

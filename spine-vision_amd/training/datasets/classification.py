@@ -15,6 +15,7 @@ from torch.utils.data import Dataset, WeightedRandomSampler
 
 from ...core.tasks import AVAILABLE_TASK_NAMES, get_task
 from .localization import IDX_TO_LEVEL, normalize_u8
+from .resize import collate_images
 from .stratification import split_patients
 
 
@@ -64,7 +65,7 @@ class ClassificationCollator:
         for lab in labels:
             dtype = torch.long if get_task(lab).is_multiclass else torch.float32
             tg[lab] = torch.tensor([s["targets"][lab] for s in samples], dtype=dtype)
-        out = {"image": torch.stack([s["image"] for s in samples]), "targets": DynamicTargets(tg),
+        out = {**collate_images(samples), "targets": DynamicTargets(tg),
                "level_idx": torch.tensor([s.get("level_idx", 0) for s in samples], dtype=torch.long),
                "metadata": [s.get("metadata", {}) for s in samples]}
         if "augment" in samples[0]:  # device_transform: per-sample augmentation parameters [B,10]
@@ -167,14 +168,15 @@ class ClassificationDataset(Dataset):
         t2 = np.array(Image.open(r["t2_path"]).convert("L")) if r["t2_path"] is not None else None
         rgb = construct_3channel(None if t2 is None else torch.from_numpy(t2),
                                  None if t1 is None else torch.from_numpy(t1)).numpy()
-        im = Image.fromarray(rgb).resize((self.output_size[1], self.output_size[0]), Image.BILINEAR)
         params = sample_params(self.output_size[0], self.output_size[1], flip=False) if self.augment else None
         out: dict[str, Any] = {}
-        if self.device_transform:
-            image = torch.from_numpy(np.asarray(im, dtype=np.uint8).copy())  # [H,W,3]
+        if self.device_transform:  # [h,w,3] at native size: Resize on the GPU (kernels.resize_u8)
+            image = torch.from_numpy(np.ascontiguousarray(rgb))
+            out["resize_to"] = tuple(self.output_size)
             if params is not None:
                 out["augment"] = params
         else:
+            im = Image.fromarray(rgb).resize((self.output_size[1], self.output_size[0]), Image.BILINEAR)
             if params is not None:
                 im = apply_pil(im, params)
             x = torch.from_numpy(np.asarray(im, dtype=np.uint8).copy()).permute(2, 0, 1)

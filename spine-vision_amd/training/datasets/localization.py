@@ -11,6 +11,8 @@ import numpy as np
 import torch
 from torch.utils.data import Dataset
 
+from .resize import collate_images
+
 LEVELS = ("L1/L2", "L2/L3", "L3/L4", "L4/L5", "L5/S1")
 NUM_LEVELS = len(LEVELS)
 IDX_TO_LEVEL = dict(enumerate(LEVELS))
@@ -34,9 +36,10 @@ class LocalizationDataset(Dataset):
     augmenting] -> ToTensor -> Normalize), coords [5,2], mask [5], series_type_idx, metadata -- the
     reference's record layout, transform chain (localization.py:196-233, 254) and image split.
 
-    ``device_transform``: yield the resized uint8 plane [H,W] (and, when augmenting, the sample's
-    augmentation parameters under "augment", drawn like torchvision); the trainer runs the flip /
-    affine / jitter (``kernels.augment_u8``) and ToTensor -> Normalize on the GPU.  MRI PNGs are
+    ``device_transform``: yield the decoded uint8 plane [h,w] at its native size (and, when augmenting, the
+    sample's augmentation parameters under "augment", drawn like torchvision); the trainer runs the Resize
+    (``kernels.resize_u8``), the flip / affine / jitter (``kernels.augment_u8``) and ToTensor -> Normalize
+    on the GPU.  MRI PNGs are
     grayscale; an image whose RGB channels differ raises in this mode (use the host transform).
     ``augment_coords``: move the keypoints with the flip / affine (the reference does not)."""
 
@@ -78,26 +81,30 @@ class LocalizationDataset(Dataset):
     def __len__(self) -> int:
         return len(self.image_list)
 
-    def _load(self, rel: str):
-        """convert("RGB") -> Resize (torchvision Resize on PIL = Image.resize((w, h), BILINEAR))."""
+    def _load(self, rel: str, resize: bool = True):
+        """convert("RGB") -> Resize (torchvision Resize on PIL = Image.resize((w, h), BILINEAR)); the
+        device_transform path leaves the resize to the GPU (kernels.resize_u8, bit-identical)."""
         from PIL import Image
 
-        return Image.open(self.data_path / rel).convert("RGB").resize((self.image_size[1], self.image_size[0]),
-                                                                      Image.BILINEAR)
+        im = Image.open(self.data_path / rel).convert("RGB")
+        if not resize:
+            return im
+        return im.resize((self.image_size[1], self.image_size[0]), Image.BILINEAR)
 
     def __getitem__(self, i: int) -> dict[str, Any]:
         from .augment import apply_pil, sample_params, transform_coords
 
         rel = self.image_list[i]
         rec = self.image_records[rel]
-        im = self._load(rel)
+        im = self._load(rel, resize=not self.device_transform)
         params = sample_params(self.image_size[0], self.image_size[1], flip=True) if self.augment else None
         out: dict[str, Any] = {}
-        if self.device_transform:  # uint8 [H,W]; augmented + normalised on the GPU
+        if self.device_transform:  # decoded uint8 [h,w] at native size; resized, augmented, normalised on the GPU
             rgb = np.asarray(im, dtype=np.uint8)
             if not (np.array_equal(rgb[..., 0], rgb[..., 1]) and np.array_equal(rgb[..., 0], rgb[..., 2])):
                 raise ValueError(f"{rel}: device_transform expects grayscale images (RGB channels differ)")
             image = torch.from_numpy(rgb[..., 0].copy())
+            out["resize_to"] = self.image_size
             if params is not None:
                 out["augment"] = params
         else:
@@ -173,7 +180,7 @@ class LocalizationCollator:
 
     def __call__(self, samples: list[dict[str, Any]]) -> dict[str, Any]:
         out = {
-            "image": torch.stack([s["image"] for s in samples]),
+            **collate_images(samples),  # stacked, or a ragged batch for the device resize
             "coords": torch.stack([s["coords"] for s in samples]),
             "mask": torch.stack([s["mask"] for s in samples]),
             "series_type_idx": torch.tensor([s["series_type_idx"] for s in samples], dtype=torch.long),

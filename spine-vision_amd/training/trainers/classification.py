@@ -111,21 +111,22 @@ class ClassificationTrainer(BaseTrainer):
         return batch["image"], batch["targets"]
 
     def _train_step(self, batch: dict[str, Any]) -> torch.Tensor:
-        image = batch["image"].to(self.device, non_blocking=True)
-        if "augment" in batch:  # device_transform: affine / jitter of the uint8 crops on the GPU
-            from ... import kernels as K
+        from ... import kernels as K
 
-            image = K.augment_u8(image, batch["augment"].to(self.device, non_blocking=True))
+        # device_transform: Resize (ragged batch) and affine / jitter of the uint8 crops on the GPU
+        image = K.device_images(batch, self.device)
         targets = batch["targets"].to(self.device).to_dict()
         return self._optimize(lambda: self.model.get_loss(self.model(image), targets))
 
     def _validate_epoch(self) -> tuple[float, dict[str, float]]:
+        from ... import kernels as K
+
         self.model.eval()
         self.metrics.reset()
         total, n = 0.0, 0
         with torch.no_grad():
             for batch in self.val_loader:
-                image = batch["image"].to(self.device)
+                image = K.device_images(batch, self.device) if "resize" in batch else batch["image"].to(self.device)
                 targets = batch["targets"].to(self.device)
                 pred = self.model(image)
                 total += float(self.model.get_loss(pred, targets.to_dict()))

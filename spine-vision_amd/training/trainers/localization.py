@@ -76,24 +76,26 @@ class LocalizationTrainer(BaseTrainer):
         return batch["image"], batch["coords"]
 
     def _train_step(self, batch: dict[str, Any]) -> torch.Tensor:
-        dev = self.device
-        image = batch["image"].to(dev, non_blocking=True)
-        if "augment" in batch:  # device_transform: flip / affine / jitter of the uint8 batch on the GPU
-            from ... import kernels as K
+        from ... import kernels as K
 
-            image = K.augment_u8(image, batch["augment"].to(dev, non_blocking=True))
+        dev = self.device
+        # device_transform: Resize (ragged batch) and flip / affine / jitter of the uint8 batch on the GPU
+        image = K.device_images(batch, dev)
         coords = batch["coords"].to(dev, non_blocking=True)
         mask = batch["mask"].to(dev, non_blocking=True)
         return self._optimize(lambda: self.model.get_loss(self.model(image), coords, mask=mask))
 
     def _validate_epoch(self) -> tuple[float, dict[str, float]]:
+        from ... import kernels as K
+
         self.model.eval()
         total, n = 0.0, 0
         P, T, Mk = [], [], []
         dev = self.device
         with torch.no_grad():
             for batch in self.val_loader:
-                image, coords, mask = (batch[k].to(dev) for k in ("image", "coords", "mask"))
+                coords, mask = (batch[k].to(dev) for k in ("coords", "mask"))
+                image = K.device_images(batch, dev) if "resize" in batch else batch["image"].to(dev)
                 pred = self.model(image)
                 total += float(self.model.get_loss(pred, coords, mask=mask))
                 n += 1

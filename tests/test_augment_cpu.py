@@ -154,7 +154,12 @@ def test_classification_dataset_from_disk(tmp_path):
     assert b["targets"].herniation.shape == (3, 1) and b["targets"].pfirrmann.dtype == torch.int64
     dev = ClassificationDataset(tmp_path, split="train", device_transform=True, **kw)
     sd = dev[0]
-    assert sd["image"].shape == (32, 32, 3) and sd["image"].dtype == torch.uint8 and sd["augment"].shape == (10,)
+    # device_transform: the crop at its native size (40 x 36 on disk), resized on the GPU (row f1)
+    assert sd["image"].shape == (40, 36, 3) and sd["image"].dtype == torch.uint8 and sd["augment"].shape == (10,)
+    assert tuple(sd["resize_to"]) == (32, 32)
+    bd = ClassificationCollator()([dev[i] for i in range(3)])
+    assert bd["image"] is None and tuple(bd["resize"]["desc"].shape) == (3, 8)
+    assert bd["resize"]["out_hw"].tolist() == [32, 32, 3] and bd["augment"].shape == (3, 10)
     only_t2 = ClassificationDataset(tmp_path, split="all", series_types=["sag_t2"], **kw)
     assert len(only_t2) == 24  # (like the reference, the filter only requires T2; a present T1 is still paired)
     assert tr.get_stats()["num_samples"] == len(tr)
@@ -205,14 +210,17 @@ def test_localization_dataset_augment_paths(tmp_path):
     torch.manual_seed(5)
     dev = LocalizationDataset(tmp_path, split="train", device_transform=True, **kw)
     d = dev[0]
-    assert a["image"].shape == (3, 32, 32) and d["image"].shape == (32, 32) and d["image"].dtype == torch.uint8
-    # same RNG draws -> the host image is exactly the PIL augmentation of the device path's input
+    # device_transform: the decoded plane at its native size (50 x 40), resized on the GPU (row f1)
+    assert a["image"].shape == (3, 32, 32) and d["image"].shape == (50, 40) and d["image"].dtype == torch.uint8
+    assert tuple(d["resize_to"]) == (32, 32)
+    # same RNG draws -> the host image is exactly the PIL resize + augmentation of the device path's input
     from spine_vision_amd.training.datasets.localization import normalize_u8
 
-    ref = apply_pil(Image.fromarray(d["image"].numpy(), "L").convert("RGB"), d["augment"])
+    resized = Image.fromarray(d["image"].numpy(), "L").convert("RGB").resize((32, 32), Image.BILINEAR)
+    ref = apply_pil(resized, d["augment"])
     assert torch.equal(normalize_u8(torch.from_numpy(np.asarray(ref).copy()).permute(2, 0, 1)), a["image"])
     assert torch.equal(a["coords"], d["coords"])  # the reference moves no keypoint
     moved = LocalizationDataset(tmp_path, split="train", augment_coords=True, **kw)[0]
     assert moved["coords"].shape == (5, 2)
     b = LocalizationCollator()([dev[i] for i in range(2)])
-    assert b["augment"].shape == (2, 10) and b["image"].shape == (2, 32, 32)
+    assert b["augment"].shape == (2, 10) and b["image"] is None and b["resize"]["out_hw"].tolist() == [32, 32, 1]

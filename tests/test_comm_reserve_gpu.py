@@ -27,15 +27,15 @@ def _latencies(dev, reserve):
     eng = StepEngine(model, dev)
     model.backbone.comm_reserve_cus = reserve
     comm = torch.cuda.Stream(device=dev, priority=-1)
-    buf = torch.randn(1 << 20, device=dev)
-    out = torch.empty((), device=dev)
+    buf = torch.randn(1024, 1024, device=dev)
+    out = torch.empty(1024, device=dev)
     with torch.cuda.stream(comm):  # standalone duration of the proxy
         for _ in range(3):
-            torch.sum(buf, out=out)
+            torch.sum(buf, dim=0, out=out)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(20):
-            torch.sum(buf, out=out)
+            torch.sum(buf, dim=0, out=out)
         e1.record()
     torch.cuda.synchronize()
     alone_us = e0.elapsed_time(e1) * 1e3 / 20
@@ -48,7 +48,7 @@ def _latencies(dev, reserve):
         with torch.cuda.stream(comm):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            torch.sum(buf, out=out)
+            torch.sum(buf, dim=0, out=out)
             b.record()
         marks.append((ev, b))
 

@@ -17,7 +17,8 @@ __graft_entry__.load_package()
 from spine_vision_amd import kernels as K  # noqa: E402
 from spine_vision_amd import native as nv  # noqa: E402
 
-STAGES = {"S1": (524288, 128), "S2": (131072, 256), "S3": (32768, 512), "S4": (8192, 1024)}
+STAGES = {"S1": (524288, 128), "S2": (131072, 256), "S3": (32768, 512), "S4": (8192, 1024),
+          "BIG": (16384, 2048)}  # BIG: a long-K calibration shape (fc1 dgrad K 8192), not in the model
 
 
 def cases(M, C, dev):
