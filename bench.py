@@ -357,12 +357,27 @@ def trainer_line(args) -> dict:
                                  visualize_predictions=False, use_trackio=False, precision=args.precision)
         tr = LocalizationTrainer(cfg)
         nb = len(tr.train_loader)
+        stamps: list = []
+        step0 = tr._train_step
+
+        def stamped(batch):  # host time after each step is enqueued (InflightLimiter: <= 2 steps ahead)
+            out = step0(batch)
+            stamps.append(time.perf_counter())
+            return out
+
+        tr._train_step = stamped
         tr._train_epoch()
         torch.cuda.synchronize()
+        stamps.clear()
         t0 = time.perf_counter()
         tr._train_epoch()
         torch.cuda.synchronize()
-        el = time.perf_counter() - t0
+        t_end = time.perf_counter()
+        el = t_end - t0
+        # steady state: from the 5th step of the timed epoch to its end (worker start-up and the first
+        # batches' decode excluded -- the reference's DataLoader restarts its workers every epoch)
+        skip = min(5, nb - 2)
+        steady = (nb - skip) * args.batch / (t_end - stamps[skip - 1]) if nb > skip + 1 else None
         # one worker's host cost per image (decode + the dataset's host work + collation), single process
         ds = LocalizationDataset(root, split="train", image_size=(512, 512), augment=True, device_transform=dev_t,
                                  val_ratio=0.0)
@@ -384,6 +399,8 @@ def trainer_line(args) -> dict:
             "config": {"workload": "LocalizationTrainer._train_epoch (+ its DataLoader)", "transform": args.transform,
                        "workers": args.workers, "native_side": args.native, "image_size": 512,
                        "batch_per_gpu": args.batch, "augment": True},
+            "steady_state_img_s": round(steady, 1) if steady else None,
+            "first_batch_s": round(stamps[0] - t0, 3) if stamps else None,
             "host_ms_per_image_one_worker": round(per_img * 1e3, 3),
             "host_bound_img_s": round(args.workers / per_img, 1)}
 
