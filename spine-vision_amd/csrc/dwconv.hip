@@ -384,7 +384,17 @@ int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, floa
 int sv_dwconv7_bwd_weight_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
   const DwGeo g = dw_geo(B, H, W, C);
   const int ncg = C / 64 > 0 ? C / 64 : 1;
-  int np = 512 / ncg;  // ~2048 waves over all channel groups
+  // ~1024 workgroups (4096 waves, about 4 workgroups per CU) over all channel groups: with the 2-row ring a
+  // wave has only ~6 KiB in flight, so the HBM latency is hidden by waves per CU (round 3, tools/dw_bench.py:
+  // 512 -> 1024 workgroups S1 143 -> 129 us, S2 72 -> 62, S3 37.7 -> 33.2 (bf16 dz), S4 equal; 2048 no
+  // better; step 1052-1054 -> 1059-1060 img/s, profiles/round3/r4i_*).  SV_DW_WGRAD_WGS overrides.
+  static int wgs = -1;
+  if (wgs < 0) {
+    const char* v = getenv("SV_DW_WGRAD_WGS");
+    wgs = v ? atoi(v) : 1024;
+    if (wgs < 64) wgs = 64;
+  }
+  int np = wgs / ncg;
   if (np < 1) np = 1;
   const int need = ceil_div(g.ntiles, 4);
   return need < np ? need : np;
