@@ -234,6 +234,20 @@ int sv_pool_ln_bwd(const float* dfeat, const float* pooled, const float* mean, c
  * The host reduces deep split-K slabs in two passes (groups, then the group sums).                 */
 /* one-launch variant for two independent segments sharing the partial count P (a weight gradient and
  * its bias gradient): out_s[i] (+)= alpha * sum_p part_s[p*n_s + i]; n_b = 0 for a single segment.   */
+/* Up to SV_MAX_RED_SEGS independent partial reductions (out_s (+)= alpha * sum_p part_s[p][:]) in ONE launch
+ * -- the per-block weight-gradient folds the reference gets from autograd's accumulation (fc1 wgrad slab +
+ * bias, LayerNorm and depthwise weight / bias partials), each in a fixed order (deterministic).  segs is a
+ * HOST array.                                                                                         */
+#define SV_MAX_RED_SEGS 8
+typedef struct {
+  const float* part; /* [P][n] f32 partial rows (16-B aligned when n % 4 == 0) */
+  float* out;        /* [n] f32 */
+  int64_t n;
+  int32_t P;
+  int32_t accumulate;
+} sv_red_seg;
+int sv_reduce_partials_multi(const sv_red_seg* segs, int32_t nseg, float alpha, sv_stream_t stream);
+
 int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, const float* part_b, int64_t n_b,
                             float* out_b, int32_t P, float alpha, int32_t accumulate, sv_stream_t stream);
 int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,

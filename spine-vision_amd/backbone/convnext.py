@@ -143,6 +143,9 @@ class ConvNeXtHip(nn.Module):
         # CUs free so RCCL's all-reduce kernels on the comm stream find a CU (a v9 workgroup holds its CU's
         # LDS for the whole launch); 0 = every CU
         self.comm_reserve_cus = 0
+        # a block's fc1 wgrad slab / bias, LayerNorm and depthwise partials folded by ONE launch
+        # (sv_reduce_partials_multi) instead of four (SV_MERGED_FOLDS=0: one launch per fold, A/B only)
+        self.merge_folds = os.environ.get("SV_MERGED_FOLDS", "1") != "0"
         # the lean side stream's GEMMs on at most this many workgroups (None: every CU; SV_SIDE_GRID_CAP)
         cap = os.environ.get("SV_SIDE_GRID_CAP")
         self.side_grid_cap: int | None = int(cap) if cap else None
@@ -387,9 +390,10 @@ class ConvNeXtHip(nn.Module):
                     side.wait_event(main.record_event())
                     for t_ in (dh, y):
                         t_.record_stream(side)
+                folds: list | None = [] if self.merge_folds else None  # one fold launch for the block
                 with torch.cuda.stream(side) if side is not None else _nullctx():
                     K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True,
-                                   bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf)
+                                   bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf, defer=folds)
                 dy = torch.empty(M, C, device=d.device, dtype=act)
                 K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
                 # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
@@ -405,8 +409,10 @@ class ConvNeXtHip(nn.Module):
                     for t_ in (dz, x):
                         t_.record_stream(side)
                 with torch.cuda.stream(side) if side is not None else _nullctx():
-                    ln_finish()
-                    K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+                    ln_finish(defer=folds)
+                    K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias), defer=folds)
+                    if folds is not None:
+                        K.reduce_multi(folds)
                     # every gradient of the block is final on this stream now: the bucketer's event
                     # covers them all
                     self._ready(blk_params)
@@ -501,13 +507,18 @@ class ConvNeXtHip(nn.Module):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
                                compute_bf16=True)
+            # the block's remaining folds (fc1 wgrad slab + bias, LayerNorm and depthwise weight / bias
+            # partials) in ONE launch instead of four
+            folds: list | None = [] if self.merge_folds else None
             K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
-                           compute_bf16=True)
-            ln_finish(record=False)
-            K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias))
+                           compute_bf16=True, defer=folds)
+            ln_finish(record=False, defer=folds)
+            K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias), defer=folds)
+            if folds is not None:
+                K.reduce_multi(folds)
             self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias, blk.mlp.fc1.weight,
                          blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
-            pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a)))
+            pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a, folds)))
         nv.value("sv_gemm_set_priority", 0)
         if prev_cap is not None:
             nv.value("sv_gemm_set_grid_cap", prev_cap)

@@ -146,6 +146,123 @@ __global__ void __launch_bounds__(kThreads) reduce_pair_kernel(RedSeg a, RedSeg 
   }
 }
 
+// Up to SV_MAX_RED_SEGS independent partial reductions in ONE launch (a block's weight-gradient folds on the
+// side stream: the fc1 wgrad slab and its bias column sums, the LayerNorm and depthwise weight / bias
+// partials): segment s owns workgroups [blk0, blk0 + nblk).  A "wide" segment (a split-K slab: few partial
+// rows, many columns) runs reduce_partials_kernel's body (one thread per 4 columns, the P rows in order, 8
+// loads in flight); a "deep" one (many partial rows, few columns) the partial-group body of
+// reduce_pair_kernel<16> (64 columns per workgroup, 16 partial-row groups folded through LDS in a fixed
+// order).  Deterministic; the wide body is bitwise reduce_partials_kernel's.
+struct MultiSeg {
+  const float* part;
+  float* out;
+  int64_t n;
+  int64_t blk0;
+  int32_t P;
+  int32_t wide;
+  int32_t accumulate;
+};
+struct MultiSegs {
+  MultiSeg s[SV_MAX_RED_SEGS];
+  int32_t nseg;
+};
+
+__global__ void __launch_bounds__(kThreads) reduce_multi_kernel(MultiSegs segs, float alpha) {
+  int si = 0;
+  for (int k = 1; k < segs.nseg; ++k)
+    if ((int64_t)blockIdx.x >= segs.s[k].blk0) si = k;
+  const MultiSeg sg = segs.s[si];
+  const int64_t blk = blockIdx.x - sg.blk0;
+  if (sg.wide) {
+    const int64_t i4 = (blk * kThreads + threadIdx.x) * 4;
+    if (i4 >= sg.n) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int p = 0;
+    for (; p + 8 <= sg.P; p += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sg.part + (size_t)(p + u) * sg.n + i4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; p < sg.P; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(sg.part + (size_t)p * sg.n + i4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    acc.x *= alpha; acc.y *= alpha; acc.z *= alpha; acc.w *= alpha;
+    float4* op = reinterpret_cast<float4*>(sg.out + i4);
+    if (sg.accumulate) {
+      const float4 q = *op;
+      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+    }
+    *op = acc;
+    return;
+  }
+  // deep segment: the body of reduce_pair_kernel<16>
+  constexpr int C4 = 16, PG = kThreads / C4;
+  __shared__ float4 red[PG][C4];
+  const int c4 = threadIdx.x % C4, pg = threadIdx.x / C4;
+  const int64_t col = blk * (4 * C4) + c4 * 4;
+  const int P = sg.P;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col + 4 <= sg.n) {
+    int p = pg;
+    for (; p + 3 * PG < P; p += 4 * PG) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sg.part + (size_t)(p + PG * u) * sg.n + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; p < P; p += PG) {
+      const float4 v = *reinterpret_cast<const float4*>(sg.part + (size_t)p * sg.n + col);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  } else if (col < sg.n) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = pg; p < P; p += PG)
+      for (int j = 0; j < 4 && col + j < sg.n; ++j) t[j] += sg.part[(size_t)p * sg.n + col + j];
+    acc = make_float4(t[0], t[1], t[2], t[3]);
+  }
+  red[pg][c4] = acc;
+  __syncthreads();
+  float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int F = PG >= 16 ? 16 : PG;
+  if (threadIdx.x < C4 * F) {
+    const int cc = threadIdx.x % C4, f = threadIdx.x / C4;
+    for (int g = f; g < PG; g += F) {
+      const float4 v = red[g][cc];
+      sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C4 * F) red[threadIdx.x / C4][threadIdx.x % C4] = sm;
+  __syncthreads();
+  if (threadIdx.x < C4) {
+    float4 t = red[0][threadIdx.x];
+    for (int g = 1; g < F; ++g) {
+      const float4 v = red[g][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const int64_t cl = blk * (4 * C4) + threadIdx.x * 4;
+    const float r[4] = {t.x * alpha, t.y * alpha, t.z * alpha, t.w * alpha};
+    if (cl + 4 <= sg.n && ((reinterpret_cast<uintptr_t>(sg.out + cl) & 15) == 0)) {
+      float4 o = make_float4(r[0], r[1], r[2], r[3]);
+      if (sg.accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(sg.out + cl);
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *reinterpret_cast<float4*>(sg.out + cl) = o;
+    } else {
+      for (int j = 0; j < 4 && cl + j < sg.n; ++j) sg.out[cl + j] = sg.accumulate ? sg.out[cl + j] + r[j] : r[j];
+    }
+  }
+}
+
 // column sums: workgroup b sums rows [b*rpb, (b+1)*rpb) of all C columns -> part[b][C]
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, int64_t rows, int C,
@@ -377,6 +494,30 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
     default: reduce_pair_kernel<1><<<(unsigned)(ba + bb), kThreads, 0, s>>>(a, b, ba, P, alpha, accumulate); break;
   }
   return check_launch("sv_reduce_partials_pair");
+}
+
+int sv_reduce_partials_multi(const sv_red_seg* segs, int32_t nseg, float alpha, sv_stream_t stream) {
+  SV_REQUIRE(segs && nseg >= 1 && nseg <= SV_MAX_RED_SEGS, "sv_reduce_partials_multi: 1..%d segments", SV_MAX_RED_SEGS);
+  MultiSegs m{};
+  int64_t blocks = 0;
+  int k = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const sv_red_seg& g = segs[i];
+    SV_REQUIRE(g.part && g.out && g.P >= 1 && g.n >= 0, "sv_reduce_partials_multi: bad segment %d", i);
+    if (g.n == 0) continue;
+    // the wide body needs whole 16-B column groups; sv_reduce_partials_pair's choice of body
+    const bool wide = g.P <= 64 && g.n >= 65536 && g.n % 4 == 0 && (((uintptr_t)g.out) & 15) == 0;
+    if (g.n % 4 == 0) SV_REQUIRE((((uintptr_t)g.part) & 15) == 0, "sv_reduce_partials_multi: partials must be 16-B aligned");
+    const int64_t nb = wide ? (g.n / 4 + kThreads - 1) / kThreads : (g.n + 63) / 64;
+    m.s[k] = MultiSeg{g.part, g.out, g.n, blocks, g.P, wide ? 1 : 0, g.accumulate ? 1 : 0};
+    blocks += nb;
+    ++k;
+  }
+  m.nseg = k;
+  if (k == 0) return SV_OK;
+  SV_REQUIRE(blocks < (1ll << 31), "sv_reduce_partials_multi: too many workgroups");
+  reduce_multi_kernel<<<(unsigned)blocks, kThreads, 0, (hipStream_t)stream>>>(m, alpha);
+  return check_launch("sv_reduce_partials_multi");
 }
 
 int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,

@@ -218,11 +218,12 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
 
 
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
-                 compute_bf16=True, cols=None) -> torch.Tensor:
+                 compute_bf16=True, cols=None, defer: list | None = None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
     writes -- or, with ``accumulate``, adds -- into ``out``).  With ``bias_out`` the column sums of
     dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum).  ``cols``: use only the
-    first ``cols`` columns of x2d (the stem's 48 of its 64-wide padded patch rows)."""
+    first ``cols`` columns of x2d (the stem's 48 of its 64-wide padded patch rows).  ``defer`` (a list, with
+    ``out`` given): append the slab folds to it for one ``reduce_multi`` launch instead of reducing here."""
     M, N = dy2d.shape
     ldx = x2d.shape[1]
     K = ldx if cols is None else cols
@@ -239,6 +240,11 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
         out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
         accumulate = False
     _check(out.numel() == N * K and out.is_contiguous(), "linear_wgrad: bad out")
+    if defer is not None:
+        defer.append((slab, out, split, accumulate))
+        if cs is not None:
+            defer.append((cs, bias_out, split, bias_accumulate))
+        return out
     if cs is not None and bias_accumulate == accumulate:
         reduce_pair(slab, out, cs, bias_out, split, accumulate=accumulate)
     else:
@@ -287,6 +293,20 @@ def reduce_pair(part_a: torch.Tensor, out_a: torch.Tensor, part_b: torch.Tensor 
          int(accumulate))
 
 
+def reduce_multi(segs: list, alpha: float = 1.0) -> None:
+    """Independent partial reductions out (+)= alpha * sum_p part[p] in one launch per SV_MAX_RED_SEGS
+    segments (sv_reduce_partials_multi).  segs: (part, out, P, accumulate) tuples, f32 contiguous."""
+    for i in range(0, len(segs), nv.SV_MAX_RED_SEGS):
+        chunk = segs[i:i + nv.SV_MAX_RED_SEGS]
+        arr = (nv.RedSeg * len(chunk))()
+        for j, (part, out, P, acc) in enumerate(chunk):
+            n = out.numel()
+            _check(out.dtype == torch.float32 and out.is_contiguous() and part.numel() >= P * n,
+                   "reduce_multi: bad segment")
+            arr[j] = nv.RedSeg(ptr(part), ptr(out), n, int(P), int(bool(acc)))
+        call("sv_reduce_partials_multi", arr, len(chunk), float(alpha))
+
+
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = True):
     rows, C = x2d.shape
     P = value("sv_colsum_nparts", rows, C)
@@ -329,9 +349,12 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
     _timed_call("ln_bwd", nb, "sv_layernorm_bwd", ptr(dy2d), dt(dy2d), ptr(x2d), dt(x2d), ptr(mean), ptr(rstd), ptr(w),
                 ptr(dx), dt(dx), int(accumulate_dx), ptr(pw[0]), ptr(pw[1]), rows, C)
     if defer_reduce:
-        def finish(record: bool = True):
+        def finish(record: bool = True, defer: list | None = None):
             if record:  # the caller may instead keep pw alive until the streams have joined
                 pw.record_stream(torch.cuda.current_stream())
+            if defer is not None:  # folded by the caller's reduce_multi launch
+                defer += [(pw[0], dw, P, True), (pw[1], db, P, True)]
+                return
             reduce_pair(pw[0], dw, pw[1], db, P)
         return dx, finish
     if dw is not None and db is not None:
@@ -372,7 +395,7 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
                 int(accumulate), B, H, W, C)
 
 
-def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
+def dwconv7_bwd_weight(dz4d, x4d, *, dw, db, defer: list | None = None):
     B, H, W, C = dz4d.shape
     P = value("sv_dwconv7_bwd_weight_nparts", B, H, W, C)
     pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
@@ -381,6 +404,9 @@ def dwconv7_bwd_weight(dz4d, x4d, *, dw, db):
     nb = B * H * W * C * (dz4d.element_size() + x4d.element_size()) + C * 50 * 4
     _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
                 B, H, W, C)
+    if defer is not None:
+        defer += [(pw, dw, P, True), (pb, db, P, True)]
+        return
     reduce_pair(pw, dw, pb, db, P)
 
 

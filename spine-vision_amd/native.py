@@ -46,6 +46,14 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class RedSeg(ctypes.Structure):
+    """sv_red_seg (include/sv_kernels.h): one partial reduction of sv_reduce_partials_multi."""
+    _fields_ = [("part", _p), ("out", _p), ("n", _i64), ("P", _i32), ("accumulate", _i32)]
+
+
+SV_MAX_RED_SEGS = 8
+
+
 class ConvShape(ctypes.Structure):
     _fields_ = [("B", _i32), ("H", _i32), ("W", _i32), ("Cs", _i32), ("Cout", _i32), ("KH", _i32), ("KW", _i32),
                 ("stride", _i32), ("pad", _i32), ("Cin", _i32)]
@@ -86,6 +94,7 @@ _SIGS = {
     "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_reduce_partials": [_p, _i32, _i32, _i64, _p, _f32, _i32, _p],
     "sv_reduce_partials_pair": [_p, _i64, _p, _p, _i64, _p, _i32, _f32, _i32, _p],
+    "sv_reduce_partials_multi": [ctypes.POINTER(RedSeg), _i32, _f32, _p],
     "sv_colsum_nparts": [_i64, _i32],
     "sv_colsum": [_p, _i32, _i64, _i32, _p, _p],
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],

@@ -533,3 +533,26 @@ def test_gemm_v8_dispatch_shapes(dev, case):
         K.linear_fwd(Ad, Wd, out=out, bias=b.to(dev), gamma=gam.to(dev), residual=x.to(dev),
                      epilogue=nv.SV_EPI_BIAS_GAMMA_RES)
         assert rel(out[rows.to(dev)], x[rows] + gam * ref) < 1e-5 + 2e-3
+
+
+def test_reduce_multi_matches_pair_and_torch(dev):
+    """sv_reduce_partials_multi (one launch for a block's weight-gradient folds): a wide split-K slab is
+    summed in reduce_partials' order (bitwise equal to reduce_into), deep narrow partials (LayerNorm /
+    depthwise shapes, ragged n) within f32 rounding of a float64 sum; accumulate honoured per segment."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [(16, 2048 * 512, True), (16, 512, True), (300, 1024, True), (64, 512 * 49, True), (64, 510, False),
+              (7, 70000, False)]
+    parts = [torch.randn(P, n, generator=g).to(dev) for P, n, _ in shapes]
+    outs = [torch.randn(n, generator=g).to(dev) for _, n, _ in shapes]
+    ref_outs = [o.clone() for o in outs]
+    K.reduce_multi([(p, o, P, acc) for p, o, (P, _, acc) in zip(parts, outs, shapes)])
+    torch.cuda.synchronize()
+    # the wide slab: bitwise what the pair path computes
+    pair = ref_outs[0].clone()
+    K.reduce_into(parts[0], 16, pair, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], pair)
+    for p, o, r, (P, n, acc) in zip(parts, outs, ref_outs, shapes):
+        ref = p.double().sum(0) + (r.double() if acc else 0)
+        err = float((o.double() - ref).abs().max() / (ref.abs().max() + 1e-30))
+        assert err < 1e-5, (P, n, acc, err)
