@@ -392,6 +392,12 @@ int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, const float
 int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                     int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
                     sv_stream_t stream);
+/* sv_bn_bwd_stats for an f32 dout with the act mask, also overwriting dout with g = dout * (act > 0)
+ * in place (the residual block's output gradient: the apply pass then runs with act == NULL and the
+ * shortcut reads dout itself — no separate masked copy).                                            */
+int sv_bn_bwd_stats_mask(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
+                         const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
+                         sv_stream_t stream);
 int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
                      sv_stream_t stream);
 int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,

@@ -407,12 +407,13 @@ class ResNetHip(nn.Module):
         convs = blk.convs()
         Bq, Hq, Wq, Cq = out.shape
         rows = Bq * Hq * Wq
-        # last BN of the main path, with the block-output ReLU mask; gm = the masked gradient
-        gm = torch.empty(rows, Cq, device=d.device, dtype=torch.float32)
+        # last BN of the main path, with the block-output ReLU mask; gm = the masked gradient, written over
+        # d by the statistics pass (d is this block's own: the next block's dx or the pooling gradient)
+        gm = d.reshape(rows, Cq)
         conv, bn, _, _, _, _ = convs[-1]
         cur_in, y, mean, rstd, _, wp, s = saved[-1]
-        dy = K.bn_bwd(d.reshape(rows, Cq), y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
-                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, gmask=gm,
+        dy = K.bn_bwd(gm, y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
+                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, mask_inplace=True,
                       batch_stats=batch_stats)
         params = [bn.weight, bn.bias]
         for ci in range(len(convs) - 1, -1, -1):

@@ -5,7 +5,7 @@
 // (timm/models/resnet.py, built at spine_vision/training/models/backbone.py:166) and their autograd
 // backward.  All kernels are HBM-bound streaming passes: one thread owns 4 consecutive channels
 // (16-B f32 / 8-B bf16 accesses), channel statistics are reduced per block into deterministic
-// partials [nparts][2][C] and finished by a 16-wave fold per 64 channels (no atomics, bit-stable).
+// partials [nparts][2][C] and finished by a 16-wave fold per 32 channels (no atomics, bit-stable).
 // Batch statistics use shifted sums (shift = the channel's value in row 0) so mean^2 >> var does
 // not cancel catastrophically in f32.
 #include <math.h>
@@ -158,42 +158,63 @@ __global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict_
   reduce_write<V>(s1, s2, tpr, rp, c, C, part);
 }
 
-// Sum of the per-block partials [P][2][C] for 64 channels per workgroup: the 16 waves of the
-// workgroup take every 16th partial (lane = channel, 256-B coalesced loads, 4 independent accumulator
-// pairs in flight), then the wave sums are folded through LDS in a fixed order (bit-stable).  The old
-// one-thread-per-channel loop walked all P partials serially (156 us per BatchNorm at P = 1024).
-constexpr int kFinWaves = 16;
-__device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int P, int C, float& s1, float& s2) {
-  __shared__ float red[2][kFinWaves][64];
+// Sum of the per-block partials [P][2][C] for kFinCh = 32 channels per workgroup.  Lane l of wave w
+// reads channels 4 (l & 7) .. +3 of its slice (one 16-B load per sum; 8 lanes cover a 128-B row
+// segment) from partials j, j + 128, j + 256, .. with j = 8 w + (l >> 3): 128 partial streams per
+// workgroup, each lane with 4 partials (8 loads) in flight.  Wave 0 then folds the 128 stream sums in a
+// fixed order through LDS (lanes 0-31: S1, lanes 32-63: S2), so the result is bit-stable.  Round 2's
+// version (64 channels per workgroup, lane = channel, one 4-B load per lane and sum) kept a quarter of
+// the bytes in flight on half the workgroups: 7-8 us per finish at P = 512-2048.
+constexpr int kFinWaves = 16, kFinCh = 32, kFinStreams = kFinWaves * 64 / (kFinCh / 4);
+__device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int P, int C, float& s1, float& s2,
+                                              int& c_out) {
+  __shared__ float red[2][kFinStreams][kFinCh];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < C) {
-    int p = w;
-    for (; p + 3 * kFinWaves < P; p += 4 * kFinWaves) {
+  const int q = lane & 7, j = w * 8 + (lane >> 3);
+  const int c = blockIdx.x * kFinCh + 4 * q;
+  float4 a1[4], a2[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a1[u] = a2[u] = f4(0.f);
+  if (c < C) {  // C % 4 == 0: a 4-channel group is wholly in or out
+    int p = j;
+    for (; p + 3 * kFinStreams < P; p += 4 * kFinStreams) {
+      float4 x1[4], x2[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float* q = part + (size_t)(p + u * kFinWaves) * 2 * C + c;
-        a1[u] += q[0];
-        a2[u] += q[C];
+        const float* r = part + (size_t)(p + u * kFinStreams) * 2 * C + c;
+        x1[u] = ld4f(r, 0);
+        x2[u] = ld4f(r + C, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1[u].x += x1[u].x; a1[u].y += x1[u].y; a1[u].z += x1[u].z; a1[u].w += x1[u].w;
+        a2[u].x += x2[u].x; a2[u].y += x2[u].y; a2[u].z += x2[u].z; a2[u].w += x2[u].w;
       }
     }
-    for (; p < P; p += kFinWaves) {
-      a1[0] += part[(size_t)p * 2 * C + c];
-      a2[0] += part[(size_t)p * 2 * C + C + c];
+    for (; p < P; p += kFinStreams) {
+      const float* r = part + (size_t)p * 2 * C + c;
+      const float4 x1 = ld4f(r, 0), x2 = ld4f(r + C, 0);
+      a1[0].x += x1.x; a1[0].y += x1.y; a1[0].z += x1.z; a1[0].w += x1.w;
+      a2[0].x += x2.x; a2[0].y += x2.y; a2[0].z += x2.z; a2[0].w += x2.w;
     }
   }
-  red[0][w][lane] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-  red[1][w][lane] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  const float4 t1 = make_float4((a1[0].x + a1[1].x) + (a1[2].x + a1[3].x), (a1[0].y + a1[1].y) + (a1[2].y + a1[3].y),
+                                (a1[0].z + a1[1].z) + (a1[2].z + a1[3].z), (a1[0].w + a1[1].w) + (a1[2].w + a1[3].w));
+  const float4 t2 = make_float4((a2[0].x + a2[1].x) + (a2[2].x + a2[3].x), (a2[0].y + a2[1].y) + (a2[2].y + a2[3].y),
+                                (a2[0].z + a2[1].z) + (a2[2].z + a2[3].z), (a2[0].w + a2[1].w) + (a2[2].w + a2[3].w));
+  *reinterpret_cast<float4*>(&red[0][j][4 * q]) = t1;
+  *reinterpret_cast<float4*>(&red[1][j][4 * q]) = t2;
   __syncthreads();
-  if (w != 0 || c >= C) return false;
-  s1 = 0.f;
-  s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < kFinWaves; ++i) {
-    s1 += red[0][i][lane];
-    s2 += red[1][i][lane];
-  }
+  if (w != 0) return false;
+  const int which = lane >> 5, ch = lane & 31;
+  float s = 0.f;
+#pragma unroll 16
+  for (int i = 0; i < kFinStreams; ++i) s += red[which][i][ch];
+  const float other = __shfl_xor(s, 32);
+  c_out = blockIdx.x * kFinCh + ch;
+  if (which != 0 || c_out >= C) return false;
+  s1 = s;
+  s2 = other;
   return true;
 }
 
@@ -203,8 +224,8 @@ __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
     float* __restrict__ rvar, int64_t* __restrict__ nbt) {
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   float s1, s2;
-  if (!fold_partials(part, P, C, s1, s2)) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  int c;
+  if (!fold_partials(part, P, C, s1, s2, c)) return;
   // shift k: row 0 of y (sv_bn_stats partials); y == NULL: unshifted partials (SV_EPI_STORE_STATS)
   const float k = y == nullptr ? 0.f
                   : ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
@@ -316,7 +337,10 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int64_t rows, int C,
-                                                             int tpr, int rp, int64_t rpp, float* __restrict__ part) {
+                                                             int tpr, int rp, int64_t rpp, float* __restrict__ part,
+                                                             float* gout) {
+  // gout (act-mask form, f32 dout): g = dout * (act > 0) written back over dout by the thread that read
+  // it, so the apply pass and the block's shortcut read the masked gradient without a separate copy
   const int t = threadIdx.x;
   const int c = (blockIdx.x * tpr + t % tpr) * V;
   const int rsub = t / tpr;
@@ -338,6 +362,10 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
     ldv<V>(y, ydt, e1, v1);
     grad_masked<V, RELU_Y>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0);
     grad_masked<V, RELU_Y>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1);
+    if (gout) {
+      stv<V>(gout, SV_F32, e0, g0);
+      stv<V>(gout, SV_F32, e1, g1);
+    }
 #pragma unroll
     for (int q = 0; q < V; ++q) {
       s1[q] += g0[q];
@@ -351,6 +379,7 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
     float v[V], g[V];
     ldv<V>(y, ydt, e, v);
     grad_masked<V, RELU_Y>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g);
+    if (gout) stv<V>(gout, SV_F32, e, g);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
       s1[q] += g[q];
@@ -365,8 +394,8 @@ __global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float*
                                                                      float* __restrict__ dgamma,
                                                                      float* __restrict__ dbeta) {
   float s1, s2;
-  if (!fold_partials(part, P, C, s1, s2)) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  int c;
+  if (!fold_partials(part, P, C, s1, s2, c)) return;
   sums[c] = s1;
   sums[C + c] = s2;
   if (dgamma) dgamma[c] += s2;
@@ -552,9 +581,9 @@ extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t
 extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows,
                                   int32_t C, float eps, float momentum, float* mean, float* rstd, float* running_mean,
                                   float* running_var, int64_t* num_batches_tracked, sv_stream_t stream) {
-  SV_REQUIRE(part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && dt_ok(y_dtype),
+  SV_REQUIRE(part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && C % 4 == 0 && dt_ok(y_dtype),
              "sv_bn_stats_finish: bad arguments");
-  stats_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
+  stats_finish_kernel<<<(C + kFinCh - 1) / kFinCh, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
                                                                         momentum, mean, rstd, running_mean, running_var,
                                                                         num_batches_tracked);
   return check_launch("sv_bn_stats_finish");
@@ -587,7 +616,8 @@ extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, 
 
 static int bwd_stats_launch(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                             int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
-                            const float* beta, int64_t rows, int32_t C, float* part, sv_stream_t stream) {
+                            const float* beta, int64_t rows, int32_t C, float* part, sv_stream_t stream,
+                            float* gout = nullptr) {
   const RedGeo g = red_geo(C);
   const int P = nparts_for(rows, C);
   const int64_t rpp = (rows + P - 1) / P;
@@ -595,7 +625,7 @@ static int bwd_stats_launch(const void* dout, int32_t dout_dtype, const void* ac
   hipStream_t st = (hipStream_t)stream;
 #define BWDS(VV, RY)                                                                                              \
   bwd_stats_kernel<VV, RY><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, \
-                                                      beta, rows, C, g.tpr, g.rp, rpp, part)
+                                                      beta, rows, C, g.tpr, g.rp, rpp, part, gout)
   if (beta) {
     if (g.vec == 8) BWDS(8, true); else BWDS(4, true);
   } else {
@@ -616,6 +646,16 @@ extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void*
                           stream);
 }
 
+extern "C" int sv_bn_bwd_stats_mask(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
+                                    const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
+                                    sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_bwd_stats_mask");
+  SV_REQUIRE(dout && act && y && mean && rstd && part && rows > 0 && dt_ok(act_dtype) && dt_ok(y_dtype),
+             "sv_bn_bwd_stats_mask: bad arguments");
+  return bwd_stats_launch(dout, SV_F32, act, act_dtype, y, y_dtype, mean, rstd, nullptr, nullptr, rows, C, part,
+                          stream, dout);
+}
+
 extern "C" int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype,
                                     const float* mean, const float* rstd, const float* gamma, const float* beta,
                                     int64_t rows, int32_t C, float* part, sv_stream_t stream) {
@@ -628,8 +668,8 @@ extern "C" int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const 
 
 extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
                                 sv_stream_t stream) {
-  SV_REQUIRE(part && sums && nparts > 0 && C > 0, "sv_bn_bwd_finish: bad arguments");
-  bwd_finish_kernel<<<(C + 63) / 64, 64 * kFinWaves, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
+  SV_REQUIRE(part && sums && nparts > 0 && C > 0 && C % 4 == 0, "sv_bn_bwd_finish: bad arguments");
+  bwd_finish_kernel<<<(C + kFinCh - 1) / kFinCh, 64 * kFinWaves, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
   return check_launch("sv_bn_bwd_finish");
 }
 

@@ -45,6 +45,12 @@ __device__ __forceinline__ void stamp(int slot) {
 __device__ __forceinline__ void stamp(int) {}
 #endif
 
+// wave priority in the K loop: 0 = s_setprio 1 around each MFMA quadrant; 1 = static priority 1 for
+// waves 4-7 (the second-dispatched half), no per-segment flips; 2 = none (A/B builds only)
+#ifndef SV_G9_PRIO
+#define SV_G9_PRIO 0
+#endif
+
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512, NW = 8;
 constexpr int FM = 8, FN = 4;
 constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF_BYTES = A_BYTES + B_BYTES;
@@ -501,6 +507,9 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   vm_wait<8>();
   bar();
   if (wm == 1) bar();  // waves 4-7 run one barrier behind
+  if constexpr (SV_G9_PRIO == 1) {
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+  }
 
   int g = 0;  // the MFMAs' K-tile in the stream
   for (int it = 0; it < my_tiles; ++it) {
@@ -539,7 +548,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
           }
       };
       auto quad = [&](int qm, int qn) {
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (SV_G9_PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -548,7 +557,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
             for (int jj = 0; jj < 2; ++jj)
               acc[4 * qm + i][2 * qn + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   bq[qn][jj][kh], af[i][kh], acc[4 * qm + i][2 * qn + jj], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (SV_G9_PRIO == 0) __builtin_amdgcn_s_setprio(0);
       };
       // phase 0: A quadrant-0 rows and B columns 0-31 of the wave
       read_a(0);

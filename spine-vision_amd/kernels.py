@@ -938,10 +938,13 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
 
 
 def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=None, dbeta=None,
-           dx_dtype=torch.float32, gmask=None, batch_stats: bool = True) -> torch.Tensor:
+           dx_dtype=torch.float32, gmask=None, mask_inplace: bool = False, batch_stats: bool = True) -> torch.Tensor:
     """BatchNorm backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
     act > 0, or -- ``relu_beta`` = the BN's beta, for a BN followed by its own ReLU -- recomputed from y
     like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again).
+    ``mask_inplace`` (act form, f32 dout): the statistics pass overwrites dout with the masked gradient
+    (sv_bn_bwd_stats_mask), which the apply pass then reads without the mask and the caller keeps as the
+    shortcut's gradient; ``gmask`` instead writes it to a separate f32 buffer from the apply pass.
     ``batch_stats``: train mode (mean / rstd are the batch's own, so dx carries the two mean corrections);
     False: eval mode (running statistics, an affine map: dx = gamma * rstd * dout, the apply kernel reading
     zero correction sums)."""
@@ -953,11 +956,18 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     if gmask is not None:
         _check(gmask.dtype == torch.float32 and gmask.numel() == rows * C and relu_beta is None,
                "bn_bwd: gmask must be f32 [rows,C] (act-mask form only)")
+    if mask_inplace:
+        _check(act is not None and gmask is None and dout2d.dtype == torch.float32,
+               "bn_bwd: mask_inplace needs act, an f32 dout and no gmask")
     P = value("sv_bn_nparts", rows, C)
     part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
     if relu_beta is not None:
         call("sv_bn_relu_bwd_stats", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),
              ptr(relu_beta), rows, C, ptr(part))
+    elif mask_inplace:
+        call("sv_bn_bwd_stats_mask", ptr(dout2d), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
+             rows, C, ptr(part))
+        act = None  # dout now holds the masked gradient
     else:
         call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
              ptr(rstd), rows, C, ptr(part))

@@ -124,6 +124,7 @@ _SIGS = {
     "sv_bn_eval_params": [_p, _p, _f32, _p, _p, _i32, _p],
     "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
+    "sv_bn_bwd_stats_mask": [_p, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
     "sv_bn_relu_bwd_stats": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_relu_bwd_apply": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],

@@ -239,6 +239,33 @@ def test_bn_relu_bwd_recomputed_mask_matches_act_mask(dev, C, precision):
     assert rel(dx2.float(), yr.grad) < (2e-2 if precision == "bf16" else 1e-3)  # + rare mask flips vs float64
 
 
+@pytest.mark.parametrize("rows,C", [(131072, 256), (4099, 12), (2048, 2048), (3000, 64)])
+def test_bn_bwd_mask_inplace_matches_gmask(dev, rows, C):
+    """sv_bn_bwd_stats_mask (the block output's masked gradient written over dout by the statistics
+    pass, the apply pass then reading it unmasked) is bit for bit the gmask form: dx, dgamma, dbeta and
+    the masked gradient.  rows = 131072 x C = 256 is ResNet-50 layer1 at 256^2, bs32 (1024 partials)."""
+    g = torch.Generator().manual_seed(rows + C)
+    y = torch.randn(rows, C, generator=g).to(dev, torch.bfloat16)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.3).to(dev)
+    mean, rstd = K.bn_stats(y)
+    a = K.bn_act(y, mean, rstd, gam, bet, relu=True, out_dtype=torch.bfloat16)
+    dout = torch.randn(rows, C, generator=g).to(dev)
+    dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    gm = torch.empty(rows, C, device=dev)
+    dx1 = K.bn_bwd(dout, y, mean, rstd, gam, act=a, dgamma=dg1, dbeta=db1, dx_dtype=torch.bfloat16, gmask=gm)
+    d2 = dout.clone()
+    dx2 = K.bn_bwd(d2, y, mean, rstd, gam, act=a, dgamma=dg2, dbeta=db2, dx_dtype=torch.bfloat16,
+                   mask_inplace=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    assert torch.equal(d2, gm) and torch.equal(gm, dout * (a > 0).float())
+    # the finish over many partials against a float64 sum of the masked gradient
+    g64 = (dout * (a > 0).float()).double()
+    assert rel(db1, g64.sum(0)) < 1e-5
+
+
 def test_bn_act_downsample_residual(dev):
     rows, C = 64, 256
     y, r = _rand((rows, C), 11), _rand((rows, C), 12)
