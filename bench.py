@@ -42,20 +42,23 @@ METRIC = "images/sec training, ConvNeXt-base 512x512 loc, bs32, at 1/2/4/8 MI355
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_F32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (guide: ~8 TB/s)
-SV_EPI_SLAB, SV_EPI_MUL_AUX = 4, 6  # include/sv_kernels.h (checked against native at run time)
+SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX = 0, 4, 6  # include/sv_kernels.h (checked against native at run time)
 # probed GEMM classes: (a_kmajor, b_kmajor[, epilogue])
 PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, SV_EPI_MUL_AUX),
-              "fwd": (True, True)}
+              "dgrad": (True, False, SV_EPI_STORE), "fwd": (True, True)}
 PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsample, stem; side stream)",
                "fc2_dgrad": "fc2 data gradient dh = (dY (W2 gamma)) * GELU'(h) (critical path)",
+               "dgrad": "fc1 / downsample data gradients dX = dY W (plain store)",
                "fwd": "forward GEMMs: fc1 (+GELU), fc2 (+gamma, residual), stem, downsample",
                "dw_fwd": "depthwise 7x7 + LayerNorm forward (sv_dwconv7_ln_fwd)",
                "dw_bwd_data": "depthwise 7x7 backward-data (sv_dwconv7_bwd_data, gradient stream += and bf16 copy)",
                "dw_wgrad": "depthwise 7x7 weight gradient (sv_dwconv7_bwd_weight, partials only)",
                "ln_bwd": "block LayerNorm backward (sv_layernorm_bwd)",
-               "adamw": "fused AdamW over the flat buffers (+ bf16 shadow refresh)"}
+               "adamw": "fused AdamW over the flat buffers (+ bf16 shadow refresh)",
+               "fold": "split-K / partial-sum folds (reduce_multi, reduce_pair, layer-scale fold): bytes = the slab "
+                       "bytes they move, overhead of split-K rather than algorithmic work"}
 # HBM-bound kernel classes timed by kernels.OpProbe (reported separately against 8 TB/s)
-OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw")
+OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "fold")
 
 
 def parse():
@@ -436,6 +439,27 @@ def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: d
     }
 
 
+def step_floor(kern: dict, ms: float, peak: float) -> dict:
+    """The step against its own floor: for every probed class of algorithmic work, launches x max(algorithmic
+    bytes / 8 TB/s, FLOPs / bf16 peak) per launch, summed (the split-K folds are overhead, not algorithmic,
+    and count zero).  Kernels outside the probed classes (stem / downsample LayerNorms, pooling, head, loss,
+    clip) add to the step but not to this floor, so ``frac`` is a lower bound of the step's distance from it."""
+    floor_ms, work_ms = 0.0, 0.0
+    for k, v in kern.items():
+        if k == "fold":
+            continue
+        n = v["launches_per_step"]
+        floor_ms += n * max(v["algorithmic_bytes_per_launch"] / (PEAK_HBM_GBS * 1e9),
+                            v["algorithmic_gflop_per_launch"] * 1e9 / (peak * 1e12)) * 1e3
+        work_ms += v["ms_per_step"]
+    return {"ms": round(floor_ms, 3), "frac": round(floor_ms / ms, 4) if ms else None,
+            "classes": sorted(k for k in kern if k != "fold"),
+            "classes_ms_per_step": round(work_ms, 3),
+            "fold_ms_per_step": kern["fold"]["ms_per_step"] if "fold" in kern else None,
+            "note": "sum over the probed classes of max(algorithmic bytes / 8 TB/s, FLOPs / bf16 peak) per launch; "
+                    "classes_ms_per_step adds their in-step durations, which overlap across the two streams"}
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -464,7 +488,7 @@ def main():
     from spine_vision_amd import native as nv
     from spine_vision_amd.training import Classifier, CoordinateRegressor, StepEngine
 
-    assert (nv.SV_EPI_SLAB, nv.SV_EPI_MUL_AUX) == (SV_EPI_SLAB, SV_EPI_MUL_AUX)
+    assert (nv.SV_EPI_STORE, nv.SV_EPI_SLAB, nv.SV_EPI_MUL_AUX) == (SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX)
     torch.manual_seed(42)
     cls = args.workload == "classification"
     if cls:
@@ -610,6 +634,7 @@ def main():
         roof["step_tflops_per_gpu"] = round(step_tflops, 1) if step_tflops else None
         roof["step_mfma_frac"] = step_frac
         roof["traffic_config"] = traffic_key if traffic else None
+        roof["step_floor"] = step_floor(kern, ms, peak)
         roof["kernels"] = kern
     else:
         # no per-kernel probe: report the whole-step model FLOP rate against the peak

@@ -267,8 +267,9 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
     gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
-    call("sv_layerscale_wgrad_reduce", ptr(slab), ptr(cs), split, ptr(w2), ptr(gamma), ptr(b2), ptr(dw2),
-         ptr(dgamma), ptr(db2), None, C, K4)
+    _timed_call("fold", 4.0 * ((split + 2) * C * K4 + (split + 4) * C),
+                "sv_layerscale_wgrad_reduce", ptr(slab), ptr(cs), split, ptr(w2), ptr(gamma), ptr(b2), ptr(dw2),
+                ptr(dgamma), ptr(db2), None, C, K4)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -289,8 +290,9 @@ def reduce_pair(part_a: torch.Tensor, out_a: torch.Tensor, part_b: torch.Tensor 
         nb = out_b.numel()
         _check(part_b is not None and part_b.numel() >= nparts * nb, "reduce_pair: partial buffer b too small")
         _check(out_b.dtype == torch.float32 and out_b.is_contiguous(), "reduce_pair: out must be contiguous f32")
-    call("sv_reduce_partials_pair", ptr(part_a), na, ptr(out_a), ptr(part_b), nb, ptr(out_b), nparts, float(alpha),
-         int(accumulate))
+    moved = 4.0 * (na + nb) * (nparts + 1 + int(bool(accumulate)))  # slabs read, out written (+ read)
+    _timed_call("fold", moved, "sv_reduce_partials_pair", ptr(part_a), na, ptr(out_a), ptr(part_b), nb, ptr(out_b),
+                nparts, float(alpha), int(accumulate))
 
 
 def reduce_multi(segs: list, alpha: float = 1.0) -> None:
@@ -299,12 +301,14 @@ def reduce_multi(segs: list, alpha: float = 1.0) -> None:
     for i in range(0, len(segs), nv.SV_MAX_RED_SEGS):
         chunk = segs[i:i + nv.SV_MAX_RED_SEGS]
         arr = (nv.RedSeg * len(chunk))()
+        moved = 0.0
         for j, (part, out, P, acc) in enumerate(chunk):
             n = out.numel()
             _check(out.dtype == torch.float32 and out.is_contiguous() and part.numel() >= P * n,
                    "reduce_multi: bad segment")
             arr[j] = nv.RedSeg(ptr(part), ptr(out), n, int(P), int(bool(acc)))
-        call("sv_reduce_partials_multi", arr, len(chunk), float(alpha))
+            moved += 4.0 * n * (P + 1 + int(bool(acc)))
+        _timed_call("fold", moved, "sv_reduce_partials_multi", arr, len(chunk), float(alpha))
 
 
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = True):
@@ -712,7 +716,8 @@ def _gathered(s: nv.ConvShape, dtype: torch.dtype) -> bool:
 
 def _slab_finish(work: torch.Tensor, split: int, M: int, N: int, C: torch.Tensor, *, accumulate: bool = False,
                  stats: torch.Tensor | None = None) -> None:
-    call("sv_gemm_slab_finish", ptr(work), split, M, N, ptr(C), dt(C), N, int(accumulate), ptr(stats))
+    _timed_call("fold", 4.0 * M * N * (split + 1 + int(bool(accumulate))), "sv_gemm_slab_finish", ptr(work), split, M,
+                N, ptr(C), dt(C), N, int(accumulate), ptr(stats))
 
 
 def _pointwise_fwd(x, wp, s, y, M, stats=None):
