@@ -9,6 +9,7 @@ missing library or a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -194,6 +195,8 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
 
 
 _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
+# persistent 256x256 wgrads: tiles x split ~ this many workgroups (one per CU; SV_WGRAD9_WGS for A/B runs)
+_WGRAD9_TARGET = int(os.environ.get("SV_WGRAD9_WGS", "256"))
 
 
 def _wgrad_split(tiles: int, K: int) -> int:
@@ -209,7 +212,7 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
     64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
     if min(N, K) >= 128 and max(N, K) >= 256:
         tiles9 = -(-N // 256) * -(-K // 256)
-        split = max(1, 256 // tiles9)
+        split = max(1, _WGRAD9_TARGET // tiles9)
         while split > 1 and M % (split * 64):
             split -= 1
         if M % (split * 64) == 0:

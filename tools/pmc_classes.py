@@ -31,7 +31,8 @@ CLASSES = {
     "dw_wgrad": [("dwconv7_wgrad_ring_kernel<",)],
     "ln_bwd": [("ln_bwd_vec_kernel<",), ("ln_bwd_kernel<",)],
     "adamw": [("adamw_kernel",)],
-    "reductions": [("reduce_pair_kernel",), ("reduce_partials_kernel",), ("layerscale_reduce_kernel",)],
+    "fold": [("reduce_pair_kernel",), ("reduce_partials_kernel",), ("reduce_multi_kernel",),
+             ("layerscale_reduce_kernel",)],
 }
 
 
