@@ -323,6 +323,15 @@ typedef struct sv_conv_shape {
 } sv_conv_shape;
 /* wp[co][t][c] = w[co][c][t] (c < Cin) else 0, cast to `dtype`; w = torch [Cout][Cin][KH][KW] f32. */
 int sv_conv_weight_pack(const float* w, void* wp, int32_t dtype, const sv_conv_shape* s, sv_stream_t stream);
+/* Up to SV_MAX_PACK_SEGS sv_conv_weight_pack calls in one launch: segment k packs w [Cout][Cin][T] f32 into
+ * wp [Cout][T][Cs] (dtype; channels >= Cin zero), T = KH*KW.                                        */
+#define SV_MAX_PACK_SEGS 32
+typedef struct {
+  const float* w;
+  void* wp;
+  int32_t Cout, Cin, T, Cs;
+} sv_pack_seg;
+int sv_conv_weight_pack_multi(const sv_pack_seg* segs, int32_t nseg, int32_t dtype, sv_stream_t stream);
 /* y = conv(x, w).  y_dtype may differ from dtype (f32 or bf16 store).                             */
 int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
                 sv_stream_t stream);

@@ -31,6 +31,9 @@ import torch.nn as nn
 from .. import kernels as K
 from .. import native as nv
 
+# SV_MULTI_PACK=0: one weight-pack launch per conv in the forward (A/B runs)
+_MULTI_PACK = os.environ.get("SV_MULTI_PACK", "1") != "0"
+
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
 _MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
 BN_EPS = 1e-5
@@ -226,14 +229,17 @@ class ResNetHip(nn.Module):
             return mean, rstd
         return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
 
-    def _conv(self, x4d, conv, k, stride, pad, Cin=None):
+    def _conv(self, x4d, conv, k, stride, pad, Cin=None, packed=None):
         """conv(x) -> (y, packed weight, shape, BN-statistics partials or None); y in the activation dtype.
-        In train mode (bf16) the conv GEMM's epilogue also emits the following BatchNorm's statistics."""
+        In train mode (bf16) the conv GEMM's epilogue also emits the following BatchNorm's statistics.
+        ``packed``: id(weight) -> its packed form from the forward's one multi-segment pack launch."""
         B, H, W, Cs = x4d.shape
         s = K.conv_shape(B, H, W, Cs, conv.weight.shape[0], k, stride, pad, Cin)
         sh = self._shadow
         if k == 1 and self.compute_bf16 and sh is not None and id(conv.weight) in sh and Cs == conv.weight.shape[1]:
             wp = sh[id(conv.weight)].view(conv.weight.shape[0], 1, Cs)
+        elif packed is not None and id(conv.weight) in packed and packed[id(conv.weight)].shape[-1] == Cs:
+            wp = packed[id(conv.weight)]
         else:
             wp = K.conv_weight_pack(conv.weight.detach(), Cs, self.act_dtype)
         if self.training and self.compute_bf16:
@@ -302,7 +308,14 @@ class ResNetHip(nn.Module):
             x0 = K.image_u8_hwc_to_nhwc(img, cs0, act)
         else:
             x0 = K.image_to_nhwc(img, cs0, act)
-        y0, wp0, s0, p0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3)
+        packed = None
+        if self.compute_bf16 and _MULTI_PACK:
+            # every weight the convs below pack (the stem's, the 3x3s') in ONE launch instead of one each
+            ws = [(self.conv1.weight, cs0)] + [(conv.weight, conv.weight.shape[1]) for blk in self.blocks()
+                                               for conv, _, k, _, _, _ in blk.convs() if k > 1]
+            packed = {id(w): wp for (w, _), wp in zip(ws, K.conv_weight_pack_multi(
+                [(w.detach(), c) for w, c in ws], act))}
+        y0, wp0, s0, p0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3, packed=packed)
         B, H, W, C = y0.shape
         m0, r0 = self._bn(self.bn1, y0.view(-1, C), p0)
         a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act).view(B, H, W, C)
@@ -316,7 +329,7 @@ class ResNetHip(nn.Module):
             saved = []
             convs = blk.convs()
             for ci, (conv, bn, k, st, pad, relu) in enumerate(convs):
-                y, wp, s, part = self._conv(cur, conv, k, st, pad)
+                y, wp, s, part = self._conv(cur, conv, k, st, pad, packed=packed)
                 Bq, Hq, Wq, Cq = y.shape
                 mean, rstd = self._bn(bn, y.view(-1, Cq), part)
                 last = ci == len(convs) - 1

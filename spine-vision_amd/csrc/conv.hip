@@ -648,6 +648,52 @@ extern "C" int sv_conv_weight_pack(const float* w, void* wp, int32_t dtype, cons
   return check_launch("sv_conv_weight_pack");
 }
 
+// Several packs in one launch: block ranges per segment (the ResNet forward packs its 7x7 / 3x3 weights,
+// 17 launches of 3-6 us each, as one)
+struct PackSegs {
+  sv_pack_seg s[SV_MAX_PACK_SEGS];
+  int64_t first_block[SV_MAX_PACK_SEGS + 1];
+  int n;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) weight_pack_multi_kernel(const PackSegs segs) {
+  int k = 0;
+  while (k + 1 < segs.n && (int64_t)blockIdx.x >= segs.first_block[k + 1]) ++k;  // block-uniform
+  const sv_pack_seg& g = segs.s[k];
+  const int64_t i = ((int64_t)blockIdx.x - segs.first_block[k]) * 256 + threadIdx.x;
+  const int64_t n = (int64_t)g.Cout * g.T * g.Cs;
+  if (i >= n) return;
+  const int c = (int)(i % g.Cs);
+  const int t = (int)((i / g.Cs) % g.T);
+  const int co = (int)(i / ((int64_t)g.Cs * g.T));
+  const float v = c < g.Cin ? g.w[((int64_t)co * g.Cin + c) * g.T + t] : 0.f;
+  st(reinterpret_cast<T*>(g.wp), (size_t)i, v);
+}
+
+extern "C" int sv_conv_weight_pack_multi(const sv_pack_seg* segs, int32_t nseg, int32_t dtype, sv_stream_t stream) {
+  SV_REQUIRE(segs && nseg >= 1 && nseg <= SV_MAX_PACK_SEGS, "sv_conv_weight_pack_multi: 1..%d segments",
+             SV_MAX_PACK_SEGS);
+  SV_REQUIRE(dtype == SV_BF16 || dtype == SV_F32, "sv_conv_weight_pack_multi: bad dtype");
+  PackSegs a{};
+  a.n = nseg;
+  int64_t blocks = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const sv_pack_seg& g = segs[k];
+    SV_REQUIRE(g.w && g.wp && g.Cout > 0 && g.Cin > 0 && g.T > 0 && g.Cs >= g.Cin,
+               "sv_conv_weight_pack_multi: bad segment %d", k);
+    a.s[k] = g;
+    a.first_block[k] = blocks;
+    blocks += ((int64_t)g.Cout * g.T * g.Cs + 255) / 256;
+  }
+  a.first_block[nseg] = blocks;
+  if (dtype == SV_BF16)
+    weight_pack_multi_kernel<uint16_t><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
+  else
+    weight_pack_multi_kernel<float><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
+  return check_launch("sv_conv_weight_pack_multi");
+}
+
 extern "C" int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                                 int32_t Cs, sv_stream_t stream) {
   SV_REQUIRE(img && out, "sv_image_to_nhwc: null pointer");

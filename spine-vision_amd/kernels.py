@@ -686,6 +686,24 @@ def conv_weight_pack(w: torch.Tensor, Cs: int, dtype: torch.dtype) -> torch.Tens
     return wp
 
 
+def conv_weight_pack_multi(items: list, dtype: torch.dtype) -> list:
+    """conv_weight_pack for several weights in one launch per SV_MAX_PACK_SEGS (sv_conv_weight_pack_multi).
+    items: (w f32 [Cout][Cin][k][k], Cs) pairs -> the packed [Cout][k*k][Cs] tensors, in order."""
+    out = []
+    for i in range(0, len(items), nv.SV_MAX_PACK_SEGS):
+        chunk = items[i:i + nv.SV_MAX_PACK_SEGS]
+        segs = (nv.PackSeg * len(chunk))()
+        for j, (w, Cs) in enumerate(chunk):
+            Cout, Cin, KH, KW = w.shape
+            _check(w.dtype == torch.float32 and w.is_contiguous() and KH == KW and Cs >= Cin,
+                   "conv_weight_pack_multi: need contiguous f32 [Co,Ci,k,k] and Cs >= Ci")
+            wp = torch.empty(Cout, KH * KW, Cs, device=w.device, dtype=dtype)
+            segs[j] = nv.PackSeg(ptr(w), ptr(wp), Cout, Cin, KH * KW, Cs)
+            out.append(wp)
+        call("sv_conv_weight_pack_multi", segs, len(chunk), SV_BF16 if dtype == torch.bfloat16 else SV_F32)
+    return out
+
+
 def _conv_check_x(x: torch.Tensor, s: nv.ConvShape, dtype: torch.dtype, who: str) -> None:
     _check(x.is_contiguous() and tuple(x.shape) == (s.B, s.H, s.W, s.Cs) and x.dtype == dtype,
            f"{who}: x must be contiguous {dtype} [B,H,W,Cs]={(s.B, s.H, s.W, s.Cs)}, got {tuple(x.shape)} {x.dtype}")

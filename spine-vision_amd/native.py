@@ -54,6 +54,14 @@ class RedSeg(ctypes.Structure):
 SV_MAX_RED_SEGS = 8
 
 
+class PackSeg(ctypes.Structure):
+    """sv_pack_seg (include/sv_kernels.h): one weight pack of sv_conv_weight_pack_multi."""
+    _fields_ = [("w", _p), ("wp", _p), ("Cout", _i32), ("Cin", _i32), ("T", _i32), ("Cs", _i32)]
+
+
+SV_MAX_PACK_SEGS = 32
+
+
 class ConvShape(ctypes.Structure):
     _fields_ = [("B", _i32), ("H", _i32), ("W", _i32), ("Cs", _i32), ("Cout", _i32), ("KH", _i32), ("KW", _i32),
                 ("stride", _i32), ("pad", _i32), ("Cin", _i32)]
@@ -109,6 +117,7 @@ _SIGS = {
     "sv_cast_f32_bf16": [_p, _p, _i64, _p],
     # ResNet
     "sv_conv_weight_pack": [_p, _p, _i32, _CS, _p],
+    "sv_conv_weight_pack_multi": [ctypes.POINTER(PackSeg), _i32, _i32, _p],
     "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _p],
     "sv_conv_fwd_stats": [_p, _p, _p, _i32, _i32, _CS, _p, _p],
     "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],

@@ -239,6 +239,21 @@ def test_bn_relu_bwd_recomputed_mask_matches_act_mask(dev, C, precision):
     assert rel(dx2.float(), yr.grad) < (2e-2 if precision == "bf16" else 1e-3)  # + rare mask flips vs float64
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_conv_weight_pack_multi_matches_single(dev, dtype):
+    """sv_conv_weight_pack_multi (the forward's one launch for the stem and every 3x3 weight) is bit for
+    bit the per-weight sv_conv_weight_pack, over more segments than one launch takes (35 > 32)."""
+    g = torch.Generator().manual_seed(7)
+    shapes = [(64, 3, 7, 7, 8)] + [(c, c, 3, 3, c) for c in (64, 128, 256, 512)] * 8 + [(16, 5, 3, 3, 8),
+                                                                                       (8, 8, 1, 1, 8)]
+    items = [(torch.randn(co, ci, kh, kw, generator=g).to(dev), cs) for co, ci, kh, kw, cs in shapes]
+    multi = K.conv_weight_pack_multi(items, dtype)
+    torch.cuda.synchronize()
+    assert len(multi) == len(items)
+    for (w, cs), wp in zip(items, multi):
+        assert torch.equal(wp, K.conv_weight_pack(w, cs, dtype))
+
+
 @pytest.mark.parametrize("rows,C", [(131072, 256), (4099, 12), (2048, 2048), (3000, 64)])
 def test_bn_bwd_mask_inplace_matches_gmask(dev, rows, C):
     """sv_bn_bwd_stats_mask (the block output's masked gradient written over dout by the statistics
