@@ -33,6 +33,8 @@ from .. import native as nv
 
 # SV_MULTI_PACK=0: one weight-pack launch per conv in the forward (A/B runs)
 _MULTI_PACK = os.environ.get("SV_MULTI_PACK", "1") != "0"
+# SV_FIRST_BLOCK_SIDE=0: the first block's weight gradients on the main stream (A/B runs)
+_FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
 
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
 _MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
@@ -481,9 +483,12 @@ class ResNetHip(nn.Module):
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
         blocks = list(self.blocks())
         for i, (blk, saved_block) in zip(range(len(blocks) - 1, -1, -1), zip(reversed(blocks), reversed(tape.blocks))):
-            # the first block's (and below, the stem's) weight gradients stay on the main stream: nothing
-            # is left for the main stream to overlap them with, while the side stream drains its queue
-            d = self._block_backward(blk, saved_block, d, side if i > 0 else None, keep, deferred,
+            # every block's weight gradients on the side stream: the first block's run beside the main
+            # stream's tail (its data gradients, the max-pool / stem BatchNorm backward and the stem's
+            # weight gradient, which stays on the main stream as the last producer); the side queue is
+            # empty by then (r4k trace), so they no longer wait behind a backlog: +0.5 % (r4s A/B)
+            d = self._block_backward(blk, saved_block, d, side if (i > 0 or _FIRST_BLOCK_SIDE) else None, keep,
+                                     deferred,
                                      batch_stats=tape.batch_stats)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
