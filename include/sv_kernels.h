@@ -421,6 +421,18 @@ int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const void* y, in
 int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const void* y, int32_t y_dtype, const float* mean,
                          const float* rstd, const float* gamma, const float* beta, const float* sums, void* dx,
                          int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
+/* The stem's BN + ReLU backward fed by the max-pool 3x3/2 (pad 1) backward: the incoming gradient of
+ * input pixel p is the sum of dpool [B][OH][OW][C] (f32) over the windows whose argmax tap (idx, as
+ * sv_maxpool3s2_fwd writes it) is p, gathered inside both passes in sv_maxpool3s2_bwd's order (bit for
+ * bit sv_maxpool3s2_bwd then sv_bn_relu_bwd_*, without writing the [B][H][W][C] f32 gradient).
+ * y [B*H*W][C]; dpool 16-B and idx 4-B aligned.                                                     */
+int sv_bn_relu_bwd_stats_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W, const void* y,
+                              int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                              const float* beta, int32_t C, float* part, sv_stream_t stream);
+int sv_bn_relu_bwd_apply_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W, const void* y,
+                              int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                              const float* beta, const float* sums, void* dx, int32_t dx_dtype, int32_t C,
+                              sv_stream_t stream);
 /* g = dout * (act > 0), f32 out (block-output ReLU of the residual join).                         */
 int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g, int64_t n,
                  sv_stream_t stream);

@@ -33,6 +33,8 @@ from .. import native as nv
 
 # SV_MULTI_PACK=0: one weight-pack launch per conv in the forward (A/B runs)
 _MULTI_PACK = os.environ.get("SV_MULTI_PACK", "1") != "0"
+# SV_POOLED_STEM_BWD=0: the max-pool backward as its own pass before the stem BatchNorm's (A/B runs)
+_POOLED_STEM_BWD = os.environ.get("SV_POOLED_STEM_BWD", "1") != "0"
 # SV_FIRST_BLOCK_SIDE=0: the first block's weight gradients on the main stream (A/B runs)
 _FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
 
@@ -493,10 +495,15 @@ class ResNetHip(nn.Module):
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
-        da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
-        dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
-                       dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
-                       batch_stats=tape.batch_stats)
+        if _POOLED_STEM_BWD:  # the max-pool backward gathered inside the stem BN's two passes
+            dy0 = K.bn_relu_bwd_pooled(d, idx, H, W, y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias.detach(),
+                                       dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
+                                       batch_stats=tape.batch_stats)
+        else:
+            da0 = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
+            dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
+                           dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
+                           batch_stats=tape.batch_stats)
         self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
                            [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred)
         if side is not None:

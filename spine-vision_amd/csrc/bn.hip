@@ -305,13 +305,63 @@ __device__ __forceinline__ float4 masked(float4 g, const void* act, int adt, siz
   return g;
 }
 
+__host__ __device__ __forceinline__ int pool_out(int n) { return (n + 2 - 3) / 2 + 1; }
+
+// The max-pool 3x3/2 (pad 1) backward as a gather, for BatchNorm passes that read the pooled layer's
+// input gradient without materialising it: channels c .. c+V-1 of input pixel e / C, the sum of the
+// output gradients d [B][OH][OW][C] (f32) whose argmax tap (idx) is this pixel, windows taken in the
+// order of maxpool_bwd_kernel (oy, then ox, ascending) so the values are bit for bit its output.
+struct PoolSrc {
+  const float* d;
+  const uint8_t* idx;
+  int H, W;
+};
+
+template <int V>
+__device__ __forceinline__ void pool_grad(const PoolSrc& p, int C, size_t e, float (&g)[V]) {
+  const int OH = pool_out(p.H), OW = pool_out(p.W);
+  const int c = (int)(e % C);
+  const int64_t pix = (int64_t)(e / C);
+  const int ix = (int)(pix % p.W), iy = (int)((pix / p.W) % p.H);
+  const int64_t b = pix / ((int64_t)p.W * p.H);
+#pragma unroll
+  for (int q = 0; q < V; ++q) g[q] = 0.f;
+  const int oy0 = iy / 2, oy1 = (iy + 1) / 2;
+  const int ox0 = ix / 2, ox1 = (ix + 1) / 2;
+  for (int oy = oy0; oy <= oy1 && oy < OH; ++oy) {
+    const int kh = iy - (2 * oy - 1);
+    if (kh < 0 || kh > 2) continue;
+    for (int ox = ox0; ox <= ox1 && ox < OW; ++ox) {
+      const int kw = ix - (2 * ox - 1);
+      if (kw < 0 || kw > 2) continue;
+      const size_t o = (size_t)((b * OH + oy) * OW + ox) * C + c;
+      const int tap = kh * 3 + kw;
+      uint32_t ib[V / 4];
+#pragma unroll
+      for (int k = 0; k < V / 4; ++k) ib[k] = *reinterpret_cast<const uint32_t*>(p.idx + o + 4 * k);
+      float dv[V];
+#pragma unroll
+      for (int k = 0; k < V; k += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(p.d + o + k);
+        dv[k] = x.x; dv[k + 1] = x.y; dv[k + 2] = x.z; dv[k + 3] = x.w;
+      }
+#pragma unroll
+      for (int q = 0; q < V; ++q)
+        if ((int)((ib[q >> 2] >> (8 * (q & 3))) & 0xffu) == tap) g[q] += dv[q];
+    }
+  }
+}
+
 // g = dout * mask: mask = (act > 0), or (RELU_Y) recomputed from y as act_kernel computes the
-// pre-activation -- fmaf(gamma rstd, y - mean, beta) > 0 -- so the activation is not read again
-template <int V, bool RELU_Y>
+// pre-activation -- fmaf(gamma rstd, y - mean, beta) > 0 -- so the activation is not read again.
+// POOL: dout is the max-pool backward of `pool` (pool_grad), gathered in place of a load.
+template <int V, bool RELU_Y, bool POOL = false>
 __device__ __forceinline__ void grad_masked(const void* dout, int ddt, const void* act, int adt, size_t e,
                                             const float (&v)[V], const float (&mu)[V], const float (&rs)[V],
-                                            const float* gamma, const float* beta, int c, float (&g)[V]) {
-  ldv<V>(dout, ddt, e, g);
+                                            const float* gamma, const float* beta, int c, float (&g)[V],
+                                            const PoolSrc* pool = nullptr, int C = 0) {
+  if constexpr (POOL) pool_grad<V>(*pool, C, e, g);
+  else ldv<V>(dout, ddt, e, g);
   if constexpr (RELU_Y) {
     float ga[V], be[V];
     ldp<V>(gamma, c, ga);
@@ -329,7 +379,7 @@ __device__ __forceinline__ void grad_masked(const void* dout, int ddt, const voi
 }
 
 // backward statistics: sum g and sum g * xhat
-template <int V, bool RELU_Y>
+template <int V, bool RELU_Y, bool POOL = false>
 __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restrict__ dout, int ddt,
                                                              const void* __restrict__ act, int adt,
                                                              const void* __restrict__ y, int ydt,
@@ -338,7 +388,7 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int64_t rows, int C,
                                                              int tpr, int rp, int64_t rpp, float* __restrict__ part,
-                                                             float* gout) {
+                                                             float* gout, const PoolSrc pool) {
   // gout (act-mask form, f32 dout): g = dout * (act > 0) written back over dout by the thread that read
   // it, so the apply pass and the block's shortcut read the masked gradient without a separate copy
   const int t = threadIdx.x;
@@ -360,8 +410,8 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
     float v0[V], g0[V], v1[V], g1[V];
     ldv<V>(y, ydt, e0, v0);
     ldv<V>(y, ydt, e1, v1);
-    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0);
-    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0, &pool, C);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1, &pool, C);
     if (gout) {
       stv<V>(gout, SV_F32, e0, g0);
       stv<V>(gout, SV_F32, e1, g1);
@@ -378,7 +428,7 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restr
     const size_t e = (size_t)r * C + c;
     float v[V], g[V];
     ldv<V>(y, ydt, e, v);
-    grad_masked<V, RELU_Y>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g, &pool, C);
     if (gout) stv<V>(gout, SV_F32, e, g);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
@@ -410,9 +460,10 @@ struct BwdArgs {
   void* dx; int xdt;
   float* gmask;
   int64_t rows; int C;
+  PoolSrc pool;  // POOL instantiations: dout is the max-pool backward of pool.d (gathered)
 };
 
-template <int V, bool RELU_Y>
+template <int V, bool RELU_Y, bool POOL = false>
 __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
   const int64_t nv = a.rows * a.C / V;
   const float inv_n = 1.0f / (float)a.rows;
@@ -424,7 +475,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
     ldv<V>(a.y, a.ydt, e, v);
     ldp<V>(a.mean, c, mu);
     ldp<V>(a.rstd, c, rs);
-    grad_masked<V, RELU_Y>(a.dout, a.ddt, a.act, a.adt, e, v, mu, rs, a.gamma, a.beta, c, g);
+    grad_masked<V, RELU_Y, POOL>(a.dout, a.ddt, a.act, a.adt, e, v, mu, rs, a.gamma, a.beta, c, g, &a.pool, a.C);
     ldp<V>(a.gamma, c, ga);
     ldp<V>(a.sums, c, sg);
     ldp<V>(a.sums + a.C, c, sgx);
@@ -446,7 +497,6 @@ __global__ void __launch_bounds__(kThreads) relu_mask_kernel(const void* __restr
 }
 
 // ---- pooling -------------------------------------------------------------------------------------
-__host__ __device__ __forceinline__ int pool_out(int n) { return (n + 2 - 3) / 2 + 1; }
 
 __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y,
                                                                uint8_t* __restrict__ idx, int B, int H, int W, int C) {
@@ -617,16 +667,24 @@ extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, 
 static int bwd_stats_launch(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                             int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
                             const float* beta, int64_t rows, int32_t C, float* part, sv_stream_t stream,
-                            float* gout = nullptr) {
+                            float* gout = nullptr, const PoolSrc* pool = nullptr) {
   const RedGeo g = red_geo(C);
   const int P = nparts_for(rows, C);
   const int64_t rpp = (rows + P - 1) / P;
   const dim3 grid(g.cslices, P);
   hipStream_t st = (hipStream_t)stream;
+  const PoolSrc ps = pool ? *pool : PoolSrc{nullptr, nullptr, 0, 0};
 #define BWDS(VV, RY)                                                                                              \
   bwd_stats_kernel<VV, RY><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, \
-                                                      beta, rows, C, g.tpr, g.rp, rpp, part, gout)
-  if (beta) {
+                                                      beta, rows, C, g.tpr, g.rp, rpp, part, gout, ps)
+  if (pool) {  // the stem's BatchNorm (its own ReLU) reading the max-pool backward
+    if (g.vec == 8)
+      bwd_stats_kernel<8, true, true><<<grid, kThreads, 0, st>>>(nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd,
+                                                                 gamma, beta, rows, C, g.tpr, g.rp, rpp, part, nullptr, ps);
+    else
+      bwd_stats_kernel<4, true, true><<<grid, kThreads, 0, st>>>(nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd,
+                                                                 gamma, beta, rows, C, g.tpr, g.rp, rpp, part, nullptr, ps);
+  } else if (beta) {
     if (g.vec == 8) BWDS(8, true); else BWDS(4, true);
   } else {
     if (g.vec == 8) BWDS(8, false); else BWDS(4, false);
@@ -677,7 +735,10 @@ static int bwd_apply_launch(const BwdArgs& a, sv_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v8 = vec_for(a.C) == 8;
   const int grid = grid_for(a.rows * a.C / (v8 ? 8 : 4));
-  if (a.beta) {
+  if (a.pool.d) {
+    if (v8) bwd_apply_kernel<8, true, true><<<grid, kThreads, 0, st>>>(a);
+    else bwd_apply_kernel<4, true, true><<<grid, kThreads, 0, st>>>(a);
+  } else if (a.beta) {
     if (v8) bwd_apply_kernel<8, true><<<grid, kThreads, 0, st>>>(a);
     else bwd_apply_kernel<4, true><<<grid, kThreads, 0, st>>>(a);
   } else {
@@ -710,6 +771,37 @@ extern "C" int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const 
              "sv_bn_relu_bwd_apply: bad arguments");
   BwdArgs a{dout, dout_dtype, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, sums, dx, dx_dtype, nullptr,
             rows, C};
+  return bwd_apply_launch(a, stream);
+}
+
+// The stem: BatchNorm (+ its own ReLU) backward whose incoming gradient is the max-pool 3x3/2 backward of
+// dpool [B][OH][OW][C] (f32) through idx, gathered inside both passes instead of materialised
+static bool pool_args_ok(const float* dpool, const uint8_t* idx, int B, int H, int W, int C) {
+  return dpool && idx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && ((uintptr_t)dpool & 15) == 0 &&
+         ((uintptr_t)idx & 3) == 0;
+}
+
+extern "C" int sv_bn_relu_bwd_stats_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W,
+                                         const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                                         const float* gamma, const float* beta, int32_t C, float* part,
+                                         sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_relu_bwd_stats_pool");
+  SV_REQUIRE(pool_args_ok(dpool, idx, B, H, W, C) && y && mean && rstd && gamma && beta && part && dt_ok(y_dtype),
+             "sv_bn_relu_bwd_stats_pool: bad arguments");
+  const PoolSrc ps{dpool, idx, H, W};
+  return bwd_stats_launch(nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, (int64_t)B * H * W, C,
+                          part, stream, nullptr, &ps);
+}
+
+extern "C" int sv_bn_relu_bwd_apply_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W,
+                                         const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                                         const float* gamma, const float* beta, const float* sums, void* dx,
+                                         int32_t dx_dtype, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(pool_args_ok(dpool, idx, B, H, W, C) && y && mean && rstd && gamma && beta && sums && dx &&
+                 dt_ok(y_dtype) && dt_ok(dx_dtype),
+             "sv_bn_relu_bwd_apply_pool: bad arguments");
+  BwdArgs a{nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, sums, dx, dx_dtype, nullptr,
+            (int64_t)B * H * W, C, PoolSrc{dpool, idx, H, W}};
   return bwd_apply_launch(a, stream);
 }
 

@@ -1011,6 +1011,29 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     return dx
 
 
+def bn_relu_bwd_pooled(dpool4d: torch.Tensor, idx: torch.Tensor, H: int, W: int, y2d, mean, rstd, gamma, beta, *,
+                       dgamma=None, dbeta=None, dx_dtype=torch.float32, batch_stats: bool = True) -> torch.Tensor:
+    """bn_bwd(maxpool_bwd(dpool, idx, H, W), y, ..., relu_beta=beta) without materialising the max-pool
+    backward: both BatchNorm passes gather it from dpool / idx (sv_bn_relu_bwd_*_pool), bit for bit."""
+    B, OH, OW, C = dpool4d.shape
+    rows = y2d.shape[0]
+    _check(dpool4d.dtype == torch.float32 and dpool4d.is_contiguous() and idx.shape == dpool4d.shape
+           and idx.is_contiguous() and (OH, OW) == conv_out_hw(H, W, 3, 2, 1) and rows == B * H * W
+           and y2d.shape[1] == C and _bn_c_ok(C), "bn_relu_bwd_pooled: shape mismatch")
+    P = value("sv_bn_nparts", rows, C)
+    part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_relu_bwd_stats_pool", ptr(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
+         ptr(gamma), ptr(beta), C, ptr(part))
+    sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
+    if not batch_stats:
+        sums.zero_()
+    dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+    call("sv_bn_relu_bwd_apply_pool", ptr(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
+         ptr(gamma), ptr(beta), ptr(sums), ptr(dx), dt(dx), C)
+    return dx
+
+
 def maxpool_fwd(x4d: torch.Tensor):
     B, H, W, C = x4d.shape
     _check(x4d.is_contiguous() and C % 4 == 0, "maxpool_fwd: need contiguous NHWC, C % 4 == 0")

@@ -137,6 +137,8 @@ _SIGS = {
     "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
     "sv_bn_relu_bwd_stats": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_relu_bwd_apply": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
+    "sv_bn_relu_bwd_stats_pool": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _i32, _p, _p],
+    "sv_bn_relu_bwd_apply_pool": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_bn_bwd_apply": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _i64, _i32, _p],
     "sv_relu_mask": [_p, _i32, _p, _i32, _p, _i64, _p],
     "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],

@@ -239,6 +239,31 @@ def test_bn_relu_bwd_recomputed_mask_matches_act_mask(dev, C, precision):
     assert rel(dx2.float(), yr.grad) < (2e-2 if precision == "bf16" else 1e-3)  # + rare mask flips vs float64
 
 
+@pytest.mark.parametrize("B,H,W,C,dt_", [(32, 128, 128, 64, torch.bfloat16), (2, 33, 30, 64, torch.bfloat16),
+                                          (3, 17, 21, 12, torch.float32), (2, 64, 64, 64, torch.float32)])
+def test_bn_relu_bwd_pooled_matches_maxpool_then_bn(dev, B, H, W, C, dt_):
+    """The stem's BatchNorm backward with the max-pool backward gathered inside its two passes
+    (sv_bn_relu_bwd_*_pool) is bit for bit sv_maxpool3s2_bwd followed by the relu_beta BatchNorm
+    backward: dx, dgamma, dbeta.  32 x 128^2 x 64 is ResNet-50's stem at 256^2, bs32; the odd sizes take
+    the edge windows; C = 12 the 4-channel kernels."""
+    g = torch.Generator().manual_seed(B * H + W + C)
+    y = torch.randn(B * H * W, C, generator=g).to(dev, dt_)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.3).to(dev)
+    mean, rstd = K.bn_stats(y)
+    a = K.bn_act(y, mean, rstd, gam, bet, relu=True, out_dtype=dt_).view(B, H, W, C)
+    _, idx = K.maxpool_fwd(a)
+    OH, OW = idx.shape[1], idx.shape[2]
+    d = torch.randn(B, OH, OW, C, generator=g).to(dev)
+    dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    da = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
+    dx1 = K.bn_bwd(da.view(-1, C), y, mean, rstd, gam, relu_beta=bet, dgamma=dg1, dbeta=db1, dx_dtype=dt_)
+    dx2 = K.bn_relu_bwd_pooled(d, idx, H, W, y, mean, rstd, gam, bet, dgamma=dg2, dbeta=db2, dx_dtype=dt_)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_conv_weight_pack_multi_matches_single(dev, dtype):
     """sv_conv_weight_pack_multi (the forward's one launch for the stem and every 3x3 weight) is bit for
