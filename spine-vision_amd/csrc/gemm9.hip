@@ -190,7 +190,7 @@ struct EpiCount {
 //   P8: n_w + 32c + 8(l >> 4) .. +7  (acc[i][2c][0..3], acc[i][2c+1][0..3]),
 //   P4: n_w + 16c + 4(l >> 4) .. +3  (acc[i][c][0..3]).
 // Arithmetic identical to wave_group_epilogue (gemm_common.h).
-template <int EPI, bool P8>
+template <int EPI, bool P8, bool AK>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
                                          int split, const float* lbias) {
 #ifdef SV_DIAG_NOSTORE
@@ -247,8 +247,14 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
   constexpr bool AUXBF = EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD;
   constexpr bool AUXF = EPI == SV_EPI_BIAS_GAMMA_RES;
   const auto ra = rsrc(e.aux ? e.aux : e.C, x.aux);
-  // epilogue operands of HALF row groups at a time (bf16: 32 VGPRs, f32 residual: 32 / 64 VGPRs)
-  constexpr int HALF = AUXF ? FM / 4 : FM / 2;
+  // epilogue operands of HALF row groups at a time: the bf16 operand in ONE batch per tile (64 VGPRs), the f32
+  // residual in two (64); the K loop's fragment registers are dead by then (212-251 VGPRs, no scratch).  Round 3:
+  // step 1048 -> 1055-1056 img/s interleaved against two / four batches (-DSV_G9_AUXB=0, 32 VGPRs per batch;
+  // standalone shapes within noise, profiles/round3/r5e_g9_aux_batch.txt)
+#ifndef SV_G9_AUXB
+#define SV_G9_AUXB 1
+#endif
+  constexpr int HALF = AUXF ? (SV_G9_AUXB && AK ? FM / 2 : FM / 4) : (AUXBF && SV_G9_AUXB ? FM : FM / 2);
   // SV_EPI_STORE_STATS: per-lane column sums of one 64-row group (4 row groups = one HALF batch)
   constexpr bool kStats = EPI == SV_EPI_STORE_STATS;
   static_assert(!kStats || (P8 && HALF == 4), "statistics need bf16 output and 64-row batches");
@@ -625,7 +631,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       vm_wait<0>();
       bar();
     }
-    epilogue<EPI, P8>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
+    epilogue<EPI, P8, AK>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
                       LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
   }
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
