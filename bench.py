@@ -42,6 +42,9 @@ METRIC = "images/sec training, ConvNeXt-base 512x512 loc, bs32, at 1/2/4/8 MI355
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_F32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (guide: ~8 TB/s)
+# f32 VALU FMA issue: 256 CUs x 4 SIMDs x 16 lanes per cycle x 2.4 GHz (a wave64 v_fma_f32 every 4 cycles; the
+# packed v_pk_fma_f32 measured no faster, profiles/round3/r5b_dw_packed_rejected.txt)
+PEAK_VALU_TFMA = 1024 * 16 * 2.4e9 / 1e12
 SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX = 0, 4, 6  # include/sv_kernels.h (checked against native at run time)
 # probed GEMM classes: (a_kmajor, b_kmajor[, epilogue])
 PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, SV_EPI_MUL_AUX),
@@ -409,22 +412,27 @@ def trainer_line(args) -> dict:
 
 
 def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: dict) -> dict:
-    """Roofline of one probed GEMM class: algorithmic FLOPs / bytes per launch against the mean launch
-    duration from HIP events; the binding roof is the larger of FLOPs/peak and bytes/HBM peak."""
+    """Roofline of one probed kernel class: algorithmic FLOPs / bytes (/ f32 VALU FMAs) per launch against the
+    mean launch duration from HIP events; the binding roof is the largest of FLOPs / MFMA peak, bytes / HBM
+    peak and, for the depthwise convolutions, FMAs / VALU peak (1024 SIMDs x 16 FMA/clk x 2.4 GHz)."""
     n = max(probe.launches, 1)
     avg_ms = probe.elapsed_ms() / n
-    flops, nbytes = probe.flops / n, probe.bytes / n
+    flops, nbytes, fma = probe.flops / n, probe.bytes / n, getattr(probe, "fma", 0.0) / n
     tflops = flops / (avg_ms * 1e-3) / 1e12 if probe.launches else 0.0
     gbs = nbytes / (avg_ms * 1e-3) / 1e9 if probe.launches else 0.0
-    hbm_bound = nbytes / (PEAK_HBM_GBS * 1e9) > flops / (peak * 1e12)
+    tfma = fma / (avg_ms * 1e-3) / 1e12 if probe.launches else 0.0
+    t_roof = {"hbm": nbytes / (PEAK_HBM_GBS * 1e9), "mfma": flops / (peak * 1e12), "valu": fma / (PEAK_VALU_TFMA * 1e12)}
+    bound = max(t_roof, key=t_roof.get)
+    ach, pk, unit = {"hbm": (gbs, PEAK_HBM_GBS, "GB/s"), "mfma": (tflops, peak, "TFLOP/s"),
+                     "valu": (tfma, PEAK_VALU_TFMA, "T FMA/s")}[bound]
     tr = traffic.get(f"{name}_bytes_per_launch")  # None unless a PMC pass of THIS configuration exists
-    return {
+    out = {
         "kernel": PROBE_NAMES[name],
-        "bound": "hbm" if hbm_bound else "mfma",
-        "achieved": round(gbs, 1) if hbm_bound else round(tflops, 2),
-        "peak": PEAK_HBM_GBS if hbm_bound else peak,
-        "unit": "GB/s" if hbm_bound else "TFLOP/s",
-        "frac": round(gbs / PEAK_HBM_GBS if hbm_bound else tflops / peak, 4),
+        "bound": bound,
+        "achieved": round(ach, 2 if bound != "hbm" else 1),
+        "peak": pk,
+        "unit": unit,
+        "frac": round(ach / pk, 4),
         "traffic": tr,
         "traffic_ratio": round(tr / nbytes, 3) if tr and nbytes else None,
         "launches_per_step": round(probe.launches / max(steps_probed, 1), 1),
@@ -437,6 +445,10 @@ def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: d
         "hbm_gbs": round(gbs, 1),
         "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
     }
+    if fma:
+        out.update({"valu_gfma_per_launch": round(fma / 1e9, 3), "valu_tfma": round(tfma, 2),
+                    "valu_frac": round(tfma / PEAK_VALU_TFMA, 4)})
+    return out
 
 
 def step_floor(kern: dict, ms: float, peak: float) -> dict:
@@ -450,13 +462,15 @@ def step_floor(kern: dict, ms: float, peak: float) -> dict:
             continue
         n = v["launches_per_step"]
         floor_ms += n * max(v["algorithmic_bytes_per_launch"] / (PEAK_HBM_GBS * 1e9),
-                            v["algorithmic_gflop_per_launch"] * 1e9 / (peak * 1e12)) * 1e3
+                            v["algorithmic_gflop_per_launch"] * 1e9 / (peak * 1e12),
+                            v.get("valu_gfma_per_launch", 0.0) * 1e9 / (PEAK_VALU_TFMA * 1e12)) * 1e3
         work_ms += v["ms_per_step"]
     return {"ms": round(floor_ms, 3), "frac": round(floor_ms / ms, 4) if ms else None,
             "classes": sorted(k for k in kern if k != "fold"),
             "classes_ms_per_step": round(work_ms, 3),
             "fold_ms_per_step": kern["fold"]["ms_per_step"] if "fold" in kern else None,
-            "note": "sum over the probed classes of max(algorithmic bytes / 8 TB/s, FLOPs / bf16 peak) per launch; "
+            "note": "sum over the probed classes of max(algorithmic bytes / 8 TB/s, FLOPs / bf16 peak, depthwise f32 "
+                    "FMAs / VALU peak) per launch; "
                     "classes_ms_per_step adds their in-step durations, which overlap across the two streams"}
 
 

@@ -564,19 +564,39 @@ __global__ void __launch_bounds__(kLnThreads) ds_fwd_kernel(const float* __restr
   const int Ho = H / 2, Wo = W / 2;
   const int64_t np = (int64_t)B * Ho * Wo;
   const float invC = 1.0f / (float)C;
-  for (int64_t p = wave; p < np; p += nwaves) {
-    const int j = (int)(p % Wo), i = (int)((p / Wo) % Ho), b = (int)(p / ((int64_t)Wo * Ho));
-    float v[4][CPL];
+  // C = 128 (the S1 downsample, 32 patches per wave): the next patch's 4 pixels are loaded while this one is
+  // normalised (same arithmetic, bit for bit): 157-158 -> 122 us at bs32; for C = 256 it measured 12 % slower
+  // (tools/ds_bench.py, profiles/round3/r5g_ds_prefetch.txt), so wider rows keep one patch in flight
+  constexpr bool PF = CPL <= 2;
+  auto pixel = [&](int64_t pp, int q) {
+    const int j = (int)(pp % Wo), i = (int)((pp / Wo) % Ho), b = (int)(pp / ((int64_t)Wo * Ho));
+    return ((int64_t)b * H + 2 * i + (q >> 1)) * W + 2 * j + (q & 1);
+  };
+  float nv[4][CPL];
+  auto load = [&](int64_t pp) {
+    if (pp >= np) return;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int64_t pix = ((int64_t)b * H + 2 * i + (q >> 1)) * W + 2 * j + (q & 1);
-      const float* xr = x + (size_t)pix * C;
+      const float* xr = x + (size_t)pixel(pp, q) * C;
+#pragma unroll
+      for (int t = 0; t < CPL; ++t) nv[q][t] = xr[lane + 64 * t];
+    }
+  };
+  if (PF) load(wave);
+  for (int64_t p = wave; p < np; p += nwaves) {
+    float v[4][CPL];
+    if (!PF) load(p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int t = 0; t < CPL; ++t) v[q][t] = nv[q][t];
+    if (PF) load(p + nwaves);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t pix = pixel(p, q);
       float s = 0.f;
 #pragma unroll
-      for (int t = 0; t < CPL; ++t) {
-        v[q][t] = xr[lane + 64 * t];
-        s += v[q][t];
-      }
+      for (int t = 0; t < CPL; ++t) s += v[q][t];
       const float mu = wave_sum(s) * invC;
       float qq = 0.f;
 #pragma unroll

@@ -60,6 +60,7 @@ class OpProbe:
         self.events: list = []
         self.flops = 0.0
         self.bytes = 0.0
+        self.fma = 0.0  # f32 VALU FMAs (the depthwise convolutions: 49 per output element)
         self.launches = 0
 
     def elapsed_ms(self) -> float:
@@ -70,8 +71,9 @@ class OpProbe:
 OP_PROBES: dict[str, OpProbe] = {}  # name -> probe; bench.py fills it for the timed step it probes
 
 
-def _timed_call(op: str, nbytes: float, *args) -> None:
-    """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed."""
+def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0) -> None:
+    """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed; ``fma``: the
+    launch's algorithmic f32 VALU FMAs (its roof when they outlast its bytes)."""
     pr = OP_PROBES.get(op)
     if pr is None:
         call(*args)
@@ -82,6 +84,7 @@ def _timed_call(op: str, nbytes: float, *args) -> None:
     ev1.record()
     pr.events.append((ev0, ev1))
     pr.bytes += nbytes
+    pr.fma += fma
     pr.launches += 1
 
 
@@ -386,7 +389,7 @@ def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN):
     # algorithmic: x read once; z (saved for the LN backward) and y (the fc1 operand) written; mean / rstd
     nb = n * (x4d.element_size() + z.element_size() + y.element_size()) + B * H * W * 8
     _timed_call("dw_fwd", nb, "sv_dwconv7_ln_fwd", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw), ptr(lnw), ptr(lnb), eps, ptr(z),
-                dt(z), ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C)
+                dt(z), ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C, fma=49.0 * n)
     return z, y, mean, rstd
 
 
@@ -399,7 +402,7 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
     # algorithmic: dz read; the f32 gradient stream dx written (and read when accumulating); its bf16 copy
     nb = n * (dz4d.element_size() + 4 * (2 if accumulate else 1) + (2 if dx_bf16 is not None else 0))
     _timed_call("dw_bwd_data", nb, "sv_dwconv7_bwd_data", ptr(dz4d), dt(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16),
-                int(accumulate), B, H, W, C)
+                int(accumulate), B, H, W, C, fma=49.0 * n)
 
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db, defer: list | None = None):
@@ -410,7 +413,7 @@ def dwconv7_bwd_weight(dz4d, x4d, *, dw, db, defer: list | None = None):
     # algorithmic: dz and x read once, the [C,49] + [C] gradient written (the partials are a design choice)
     nb = B * H * W * C * (dz4d.element_size() + x4d.element_size()) + C * 50 * 4
     _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
-                B, H, W, C)
+                B, H, W, C, fma=49.0 * B * H * W * C)
     if defer is not None:
         defer += [(pw, dw, P, True), (pb, db, P, True)]
         return

@@ -316,10 +316,11 @@ def test_stem_mfma_path(dev):
     assert rel(db, dz.float().sum(0)) < 1e-4
 
 
-@pytest.mark.parametrize("C", [128, 256])
-def test_downsample(dev, C):
+@pytest.mark.parametrize("C,B,H,W", [(128, 2, 8, 6), (256, 2, 8, 6), (128, 2, 128, 128), (256, 6, 64, 64)])
+def test_downsample(dev, C, B, H, W):
+    """Small shapes, and shapes with more patches than the launch has waves (B*H*W/4 > 4096), where each wave
+    walks several patches with the next one's loads in flight (C <= 256)."""
     g = torch.Generator().manual_seed(C + 1)
-    B, H, W = 2, 8, 6
     x = torch.randn(B, H, W, C, generator=g)
     lnw = torch.rand(C, generator=g) + 0.5
     lnb = torch.randn(C, generator=g) * 0.1
