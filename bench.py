@@ -42,9 +42,10 @@ METRIC = "images/sec training, ConvNeXt-base 512x512 loc, bs32, at 1/2/4/8 MI355
 PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_F32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (guide: ~8 TB/s)
-# f32 VALU FMA issue: 256 CUs x 4 SIMDs x 16 lanes per cycle x 2.4 GHz (a wave64 v_fma_f32 every 4 cycles; the
-# packed v_pk_fma_f32 measured no faster, profiles/round3/r5b_dw_packed_rejected.txt)
-PEAK_VALU_TFMA = 1024 * 16 * 2.4e9 / 1e12
+# f32 VALU FMA peak: 256 CUs x 4 SIMDs x 32 FMA per cycle x 2.4 GHz = 78.6 T FMA/s (the guide's 157 TFLOP/s f32
+# vector peak); tools/valu_rate.hip: v_fma_f32 reaches 27.7 and v_pk_fma_f32 29.7 FMA/cycle/SIMD at 8 waves per SIMD
+# (profiles/round3/r5i_valu_rate.txt), so packing does not raise it
+PEAK_VALU_TFMA = 1024 * 32 * 2.4e9 / 1e12
 SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX = 0, 4, 6  # include/sv_kernels.h (checked against native at run time)
 # probed GEMM classes: (a_kmajor, b_kmajor[, epilogue])
 PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, SV_EPI_MUL_AUX),

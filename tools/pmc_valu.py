@@ -1,5 +1,6 @@
-"""Per-kernel issue-bound summary from the pmc_run.sh passes: VALU pipe busy (SQ_INSTS_VALU x 4 cycles per
-wave64 instruction over 1024 SIMDs, against GRBM_GUI_ACTIVE / 8 XCDs), the wave-cycle split (active /
+"""Per-kernel issue-bound summary from the pmc_run.sh passes: VALU pipe busy (SQ_INSTS_VALU x 2 cycles per
+wave64 instruction -- a SIMD retires 32 f32 FMA lanes per cycle, tools/valu_rate.hip -- over 1024 SIMDs, against
+GRBM_GUI_ACTIVE / 8 XCDs), the wave-cycle split (active /
 issue-stalled / parked on s_waitcnt or a barrier; SQ_* quad-cycle units cancel), and FETCH / WRITE bytes.
 
     python tools/pmc_valu.py gpurun_out/r5a/pmc [name-substring]
@@ -25,7 +26,7 @@ for (nm, grid), cs in sorted(vals.items()):
     if "GRBM_GUI_ACTIVE" not in a or "SQ_INSTS_VALU" not in a:
         continue
     cyc = a["GRBM_GUI_ACTIVE"] / 8
-    valu = a["SQ_INSTS_VALU"] * 4 / 1024 / cyc
+    valu = a["SQ_INSTS_VALU"] * 2 / 1024 / cyc
     wc = a.get("SQ_WAVE_CYCLES", 0) or 1
     print(f"{nm[:60]:60s} {grid:>8s} {valu:9.2f} {a.get('SQ_ACTIVE_INST_ANY', 0) / wc:7.2f} "
           f"{a.get('SQ_WAIT_INST_ANY', 0) / wc:7.2f} {a.get('SQ_WAIT_ANY', 0) / wc:7.2f} "
