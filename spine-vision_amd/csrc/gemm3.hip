@@ -205,6 +205,17 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most min(younger, S-2) younger tiles' LOADS-per-tile DMAs are outstanding
+template <int LOADS, int S>
+__device__ __forceinline__ void ring_wait(int younger) {
+  if constexpr (S > 2) {
+    if (younger >= S - 2) vm_wait<(S - 2) * LOADS>();
+    else ring_wait<LOADS, S - 1>(younger);
+  } else {
+    vm_wait<0>();
+  }
+}
+
 template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC, int CONV = 0>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
@@ -327,10 +338,7 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       if (p < nk) issue(p);
     for (int kt = 0; kt < nk; ++kt) {
       // tile kt must have landed; the min(S-2, nk-1-kt) younger tiles may stay in flight
-      const int younger = nk - 1 - kt < S - 2 ? nk - 1 - kt : S - 2;
-      if (S > 3 && younger >= 2) vm_wait<(S > 3 ? 2 * C::LOADS : 0)>();
-      else if (S > 2 && younger >= 1) vm_wait<(S > 2 ? C::LOADS : 0)>();
-      else vm_wait<0>();
+      ring_wait<C::LOADS, S>(nk - 1 - kt);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -443,27 +451,43 @@ static int launch_cfg(const sv_gemm_desc* d, int split, hipStream_t s) {
 
 }  // namespace g3
 
+namespace g3 {
+// gathered fprop / dgrad (modes 1, 2, 5) at S ring stages
+template <int S>
+static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
+  if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, S, 1>(d, 1, s, &g);
+  if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
+    return launch<true, true, SV_EPI_STORE_STATS, 32, S, 1>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 2>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
+    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 2>(d, 1, s, &g);
+  // split-K fprop / dgrad for grids below one workgroup per CU: f32 slabs, summed by sv_gemm_slab_finish
+  if (mode == 1 && d->epilogue == SV_EPI_SLAB)
+    return launch<true, true, SV_EPI_SLAB, 32, S, 1>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_SLAB)
+    return launch<true, false, SV_EPI_SLAB, 32, S, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, S, 5>(d, 4, s, &g);
+  return SV_ERR_UNSUPPORTED;
+}
+// gathered weight gradients (modes 3, 4) at S ring stages
+template <int S>
+static int conv_w(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
+  if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
+    return launch<false, false, SV_EPI_SLAB, 32, S, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  if (mode == 4 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
+    return launch<false, false, SV_EPI_SLAB, 32, S, 4>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
+  return SV_ERR_UNSUPPORTED;
+}
+}  // namespace g3
+
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
   if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && mode != 4 && g.lsc < 5))
     return SV_ERR_UNSUPPORTED;
-  if (mode == 1 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, 3, 1>(d, 1, s, &g);
-  if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
-    return launch<true, true, SV_EPI_STORE_STATS, 32, 3, 1>(d, 1, s, &g);
-  if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, 3, 2>(d, 1, s, &g);
-  if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
-    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, 3, 2>(d, 1, s, &g);
-  // split-K fprop / dgrad for grids below one workgroup per CU: f32 slabs, summed by sv_gemm_slab_finish
-  if (mode == 1 && d->epilogue == SV_EPI_SLAB)
-    return launch<true, true, SV_EPI_SLAB, 32, 3, 1>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
-  if (mode == 2 && d->epilogue == SV_EPI_SLAB)
-    return launch<true, false, SV_EPI_SLAB, 32, 3, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
-  if (mode == 3 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
-    return launch<false, false, SV_EPI_SLAB, 32, 4, 3>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
-  if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, 3, 5>(d, 4, s, &g);
-  if (mode == 4 && d->epilogue == SV_EPI_SLAB && !d->a_kmajor && !d->b_kmajor)
-    return launch<false, false, SV_EPI_SLAB, 32, 4, 4>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
-  return SV_ERR_UNSUPPORTED;
+  // ring depth: 3 stages (fprop / dgrad, two workgroups per CU) and 4 (wgrads); 6 stages (144 KiB, five
+  // tiles in flight) measured no faster for any ResNet-50 conv pass (profiles/round3/r6b_conv_ring_depth.txt)
+  if (mode == 3 || mode == 4) return conv_w<4>(d, g, mode, s);
+  return conv_fd<3>(d, g, mode, s);
 }
 
 int launch_gemm3(const sv_gemm_desc* d, hipStream_t s, const char* cfg) {
