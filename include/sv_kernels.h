@@ -68,11 +68,26 @@ typedef enum {
   SV_EPI_MUL_AUX = 6,        /* C = acc * aux[m,n]                       (fc2 dgrad through GELU)    */
   SV_EPI_BIAS_GELU = 7,      /* C = GELU_erf(acc + bias[n])   (fc1 of the tape-free eval forward:   */
                              /* one output, no GELU' for a backward that will not run)             */
-  SV_EPI_STORE_STATS = 8     /* C = acc (+ bias[n]) and the train-mode BatchNorm statistics of C:  */
+  SV_EPI_STORE_STATS = 8,    /* C = acc (+ bias[n]) and the train-mode BatchNorm statistics of C:  */
                              /* C2 (f32) [ceil(M/64)][2][N] = per 64-row group, column sum and sum */
                              /* of squares of the values as stored (rounded to c_dtype); bf16 only, */
                              /* N % 8 == 0, v3 kernels (a shape they cannot take is an error)      */
+  SV_EPI_STORE_BN_BWD = 9    /* C = acc (bf16: the gradient g0 at a BatchNorm + ReLU output, e.g. a */
+                             /* data gradient) and that BatchNorm's backward statistics: C2 (f32)   */
+                             /* [ceil(M/64)][2][N] = per 64-row group, sum g and sum g*xhat, g = C  */
+                             /* as stored * (fmaf(gamma*rstd, y-mean, beta) > 0), xhat =            */
+                             /* (y-mean)*rstd, y = aux (bf16, the BatchNorm input), the parameters */
+                             /* in `bn`; bias NULL, N % 8 == 0, k-major A, m-major B, v3 kernels    */
 } sv_epilogue;
+
+/* The BatchNorm whose backward statistics SV_EPI_STORE_BN_BWD / sv_gemm_slab_finish_bn_bwd compute
+ * (device pointers, f32 [N]; the forward's batch mean / rstd and the affine parameters).             */
+typedef struct {
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+} sv_bn_ref;
 
 typedef struct {
   int32_t M, N, K;
@@ -87,6 +102,7 @@ typedef struct {
   const void* aux; int32_t aux_dtype; int64_t ld_aux; /* residual / pre-activation input          */
   int32_t split_k;           /* SV_EPI_SLAB: number of K slices (>= 1); slab stride = M*N floats  */
   int32_t compute;           /* SV_BF16: bf16 MFMA (operands rounded to bf16); SV_F32: f32 MFMA    */
+  const sv_bn_ref* bn;       /* SV_EPI_STORE_BN_BWD: the BatchNorm (NULL otherwise)                */
 } sv_gemm_desc;
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
@@ -114,6 +130,13 @@ int sv_gemm_set_impl(int32_t impl);
  * N, ldc multiples of 4; slab, C, stats 16-byte aligned.                                          */
 int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, void* C, int32_t c_dtype, int64_t ldc,
                         int32_t accumulate, float* stats, sv_stream_t stream);
+/* The same finish into a bf16 C (the split-K data gradient g0 at the output of a BatchNorm + ReLU) plus
+ * that BatchNorm's backward statistics: part (f32) [ceil(M/64)][2][N] = per 64-row group, sum g and
+ * sum g*xhat, g = g0 as stored * (fmaf(gamma*rstd, y-mean, beta) > 0), xhat = (y-mean)*rstd, y (bf16,
+ * row stride N) the BatchNorm input -- the products of sv_bn_relu_bwd_stats, so bn_bwd needs no
+ * statistics pass.  N % 4 == 0; slab, C, y, part and the bn vectors 16-byte aligned.                */
+int sv_gemm_slab_finish_bn_bwd(const float* slab, int32_t split, int32_t M, int32_t N, void* C, const void* y,
+                               const sv_bn_ref* bn, float* part, sv_stream_t stream);
 
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.
@@ -370,6 +393,14 @@ int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, i
                       float* stats, float* work, int32_t split, sv_stream_t stream);
 int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
                            int32_t dtype, const sv_conv_shape* s, float* work, int32_t split, sv_stream_t stream);
+/* Stride-1 data gradient dx (bf16) of the gathered bf16 path (as sv_conv_bwd_data, no accumulate) plus
+ * the backward statistics partials [ceil(B*H*W/64)][2][Cs] of the BatchNorm + ReLU that produced the
+ * conv's input (y = that BatchNorm's input [B][H][W][Cs] bf16): split == 1 from the GEMM epilogue
+ * (SV_EPI_STORE_BN_BWD), split >= 2 through f32 slabs in `work` (split * B*H*W*Cs floats) and
+ * sv_gemm_slab_finish_bn_bwd.  Other shapes are an error.                                            */
+int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int32_t dtype, const sv_conv_shape* s,
+                        const void* y, const sv_bn_ref* bn, float* part, float* work, int32_t split,
+                        sv_stream_t stream);
 /* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
 int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                      int32_t Cs, sv_stream_t stream);

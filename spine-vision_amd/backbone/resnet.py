@@ -37,6 +37,10 @@ _MULTI_PACK = os.environ.get("SV_MULTI_PACK", "1") != "0"
 _POOLED_STEM_BWD = os.environ.get("SV_POOLED_STEM_BWD", "1") != "0"
 # SV_FIRST_BLOCK_SIDE=0: the first block's weight gradients on the main stream (A/B runs)
 _FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
+# SV_BN_BWD_EPI: the inner BatchNorms' backward statistics from the split-K finish of their data gradient
+# (split, default: +2.2 %), also from the unsplit GEMMs' epilogue (1: no faster than a separate pass, the
+# layer1/2 epilogues absorb what the pass saved), or from their own pass everywhere (0) -- r6e A/B
+_BN_BWD_EPI = os.environ.get("SV_BN_BWD_EPI", "split")
 
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
 _MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
@@ -441,14 +445,19 @@ class ResNetHip(nn.Module):
             params.append(conv.weight)
             if ci == 0:
                 break
-            da = K.conv_bwd_data(dy4, wp, s, dx_dtype=act)
             pconv, pbn, _, _, _, _ = convs[ci - 1]
             _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
             Cp = py.shape[-1]
+            # the inner BN's backward statistics from the data gradient's GEMM epilogue / split-K finish where
+            # that path carries them (stride 1, bf16), else from bn_bwd's own statistics pass
+            fused = (K.conv_bwd_data_bn(dy4, wp, s, py, pmean, prstd, pbn.weight, pbn.bias,
+                                        unsplit=_BN_BWD_EPI != "split")
+                     if _BN_BWD_EPI != "0" and act == torch.bfloat16 else None)
+            da, bpart = fused if fused is not None else (K.conv_bwd_data(dy4, wp, s, dx_dtype=act), None)
             # the inner BN's own ReLU: mask recomputed from y (the activation pa is not read again)
             dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, relu_beta=pbn.bias.detach(),
                           dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act,
-                          batch_stats=batch_stats)
+                          batch_stats=batch_stats, part=bpart)
             params += [pbn.weight, pbn.bias]
         # dy is now the gradient at conv1's output; conv1's input is x_in
         s1, wp1 = saved[0][6], saved[0][5]

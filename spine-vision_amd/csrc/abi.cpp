@@ -27,7 +27,7 @@ int check_launch(const char* what) {
 
 extern "C" {
 
-int sv_version(void) { return 1; }
+int sv_version(void) { return 2; }
 
 const char* sv_last_error_string(void) { return sv::g_err; }
 

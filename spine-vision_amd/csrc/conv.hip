@@ -811,8 +811,11 @@ extern "C" int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t
   return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream, work, split);
 }
 
+// bn != NULL (sv_conv_bwd_data_bn): bf16 dx of the stride-1 gathered path plus the backward statistics of the
+// BatchNorm + ReLU whose output the conv read (y = that BatchNorm's input), from the epilogue or the finish
 static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                              int32_t dtype, const sv_conv_shape* s, sv_stream_t stream, float* slab, int split) {
+                              int32_t dtype, const sv_conv_shape* s, sv_stream_t stream, float* slab, int split,
+                              const void* bny = nullptr, const sv_bn_ref* bn = nullptr, float* bnpart = nullptr) {
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_data")) return rc;
   SV_REQUIRE(dy && wp && dx, "sv_conv_bwd_data: null pointer");
   SV_REQUIRE(dx_dtype == SV_BF16 || dx_dtype == SV_F32, "sv_conv_bwd_data: bad dx dtype");
@@ -841,7 +844,18 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
       d.split_k = split;
       const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
       if (rc) return rc;
+      if (bn) return sv_gemm_slab_finish_bn_bwd(slab, split, d.M, d.N, dx, bny, bn, bnpart, stream);
       return sv_gemm_slab_finish(slab, split, d.M, d.N, dx, dx_dtype, s->Cs, accumulate, nullptr, stream);
+    }
+    if (bn) {
+      d.epilogue = SV_EPI_STORE_BN_BWD;
+      d.aux = bny;
+      d.aux_dtype = SV_BF16;
+      d.ld_aux = s->Cs;
+      d.bn = bn;
+      d.C2 = bnpart;
+      d.c2_dtype = SV_F32;
+      return launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
     }
     if (accumulate) {  // dx += conv^T(dy): residual epilogue with gamma = 1 reading dx in place
       d.epilogue = SV_EPI_BIAS_GAMMA_RES;
@@ -992,6 +1006,18 @@ extern "C" int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, 
                                       sv_stream_t stream) {
   SV_REQUIRE(work && split >= 1, "sv_conv_bwd_data_split: need a workspace and split >= 1");
   return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, work, split);
+}
+
+extern "C" int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int32_t dtype, const sv_conv_shape* s,
+                                   const void* y, const sv_bn_ref* bn, float* part, float* work, int32_t split,
+                                   sv_stream_t stream) {
+  if (int rc = check_shape(s, dtype, "sv_conv_bwd_data_bn")) return rc;
+  SV_REQUIRE(y && bn && part && bn->mean && bn->rstd && bn->gamma && bn->beta && split >= 1 && (split == 1 || work),
+             "sv_conv_bwd_data_bn: null pointer / split > 1 without a workspace");
+  SV_REQUIRE(dtype == SV_BF16 && s->stride == 1 && s->Cout >= 32 && pow2(s->Cout) && s->Cs % 8 == 0 &&
+                 ((int64_t)s->KH * s->KW * s->Cout) % 32 == 0,
+             "sv_conv_bwd_data_bn: only the bf16 stride-1 gathered path (Cout >= 32, power of two; Cs %% 8 == 0)");
+  return conv_bwd_data_impl(dy, wp, dx, SV_BF16, 0, dtype, s, stream, split > 1 ? work : nullptr, split, y, bn, part);
 }
 
 // the transposed wgrad (mode 4: taps*channels on the 256-row side, Cout on the 128-column side) when

@@ -328,7 +328,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
-  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_STORE_STATS, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_STORE_BN_BWD, "sv_gemm: bad epilogue %d", d->epilogue);
   if (d->M == 0 || d->N == 0) return SV_OK;
   const bool bf = d->compute == SV_BF16;
   SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
@@ -352,12 +352,21 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   if (d->epilogue == SV_EPI_STORE_STATS)
     SV_REQUIRE(bf && d->C2 && al16(d->C2) && d->N % 8 == 0, "sv_gemm: STORE_STATS needs bf16, an aligned C2, N %% 8 == 0");
   if (d->epilogue == SV_EPI_GELU_GRAD || d->epilogue == SV_EPI_MUL_AUX) SV_REQUIRE(d->aux, "sv_gemm: aux missing");
+  if (d->epilogue == SV_EPI_STORE_BN_BWD)
+    SV_REQUIRE(bf && d->c_dtype == SV_BF16 && d->C2 && d->N % 8 == 0 && d->aux && d->aux_dtype == SV_BF16 && !d->bias &&
+                   d->bn && d->bn->mean && d->bn->rstd && d->bn->gamma && d->bn->beta,
+               "sv_gemm: STORE_BN_BWD needs bf16 C and aux, C2, N %% 8 == 0, no bias and the bn parameters");
   if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
   hipStream_t s = (hipStream_t)stream;
   if (!bf) return launch_layout<false, float, float>(d, s);
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
   const int impl = g_gemm_impl;
+  if (d->epilogue == SV_EPI_STORE_BN_BWD) {  // the v3 kernels carry the BatchNorm-backward epilogue
+    const int rc = launch_gemm3(d, s);
+    SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_BN_BWD needs K %% 32 == 0, bf16 operands, k-major A, m-major B");
+    return rc;
+  }
   if (d->epilogue == SV_EPI_STORE_STATS) {  // the v3 and v9 kernels carry the statistics epilogue
     const long t9 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
     if ((impl == 0 || impl == 9) && d->N >= 256 && t9 >= 256 && d->a_kmajor) {
@@ -480,8 +489,82 @@ __global__ void __launch_bounds__(SF_THREADS) slab_finish_kernel(const float* __
     *reinterpret_cast<float4*>(o + N + n) = s2;
   }
 }
+
+// the same finish into bf16 C plus the BatchNorm + ReLU backward statistics of the values as stored (the
+// split-K data gradient at a BatchNorm + ReLU output): g = C * (fmaf(gamma rstd, y - mean, beta) > 0), the
+// mask and products of sv_bn_relu_bwd_stats; sums of g and g * xhat per 64-row group
+__global__ void __launch_bounds__(SF_THREADS) slab_finish_bnb_kernel(const float* __restrict__ slab, int split, int M,
+                                                                     int N, uint16_t* __restrict__ C,
+                                                                     const uint16_t* __restrict__ y, sv_bn_ref bn,
+                                                                     float* __restrict__ part) {
+  const int q = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + q * 4, m0 = blockIdx.y * 64;
+  const size_t sstride = (size_t)M * N;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    const float4 mu4 = *reinterpret_cast<const float4*>(bn.mean + n), rs4 = *reinterpret_cast<const float4*>(bn.rstd + n);
+    const float4 ga4 = *reinterpret_cast<const float4*>(bn.gamma + n), be4 = *reinterpret_cast<const float4*>(bn.beta + n);
+    const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
+    const float ga[4] = {ga4.x, ga4.y, ga4.z, ga4.w}, be[4] = {be4.x, be4.y, be4.z, be4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + ph + 16 * i;
+      if (m >= M) break;
+      const float* p = slab + (size_t)m * N + n;
+      float4 v = *reinterpret_cast<const float4*>(p);
+      for (int sl = 1; sl < split; ++sl) {
+        const float4 w = *reinterpret_cast<const float4*>(p + sl * sstride);
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+      const size_t ci = (size_t)m * N + n;
+      const uint2 u = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+      *reinterpret_cast<uint2*>(C + ci) = u;
+      const uint2 yu = *reinterpret_cast<const uint2*>(y + ci);
+      const float o[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                          __uint_as_float(u.y & 0xffff0000u)};
+      const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
+                           __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = fmaf(ga[j] * rs[j], yv[j] - mu[j], be[j]) > 0.f ? o[j] : 0.f;
+        s1[j] += g;
+        s2[j] = fmaf(g, (yv[j] - mu[j]) * rs[j], s2[j]);
+      }
+    }
+  }
+  __shared__ float4 red[2][SF_THREADS];
+  red[0][threadIdx.x] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  red[1][threadIdx.x] = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    float4 a1 = red[0][q], a2 = red[1][q];
+    for (int k = 1; k < 16; ++k) {
+      const float4 a = red[0][k * 16 + q], b = red[1][k * 16 + q];
+      a1.x += a.x; a1.y += a.y; a1.z += a.z; a1.w += a.w;
+      a2.x += b.x; a2.y += b.y; a2.z += b.z; a2.w += b.w;
+    }
+    float* o = part + (size_t)blockIdx.y * 2 * N;
+    *reinterpret_cast<float4*>(o + n) = a1;
+    *reinterpret_cast<float4*>(o + N + n) = a2;
+  }
+}
 }  // namespace
 }  // namespace sv
+
+extern "C" int sv_gemm_slab_finish_bn_bwd(const float* slab, int32_t split, int32_t M, int32_t N, void* C, const void* y,
+                                          const sv_bn_ref* bn, float* part, sv_stream_t stream) {
+  SV_REQUIRE(slab && C && y && bn && part && bn->mean && bn->rstd && bn->gamma && bn->beta,
+             "sv_gemm_slab_finish_bn_bwd: null pointer");
+  SV_REQUIRE(split >= 1 && M >= 0 && N >= 0 && N % 4 == 0, "sv_gemm_slab_finish_bn_bwd: bad sizes (N multiple of 4)");
+  SV_REQUIRE(al16(slab) && al16(C) && al16(y) && al16(part) && al16(bn->mean) && al16(bn->rstd) && al16(bn->gamma) &&
+                 al16(bn->beta),
+             "sv_gemm_slab_finish_bn_bwd: operands must be 16-byte aligned");
+  if (M == 0 || N == 0) return SV_OK;
+  const dim3 grid((unsigned)ceil_div(N, 64), (unsigned)ceil_div(M, 64));
+  sv::slab_finish_bnb_kernel<<<grid, sv::SF_THREADS, 0, (hipStream_t)stream>>>(
+      slab, split, M, N, reinterpret_cast<uint16_t*>(C), reinterpret_cast<const uint16_t*>(y), *bn, part);
+  return check_launch("sv_gemm_slab_finish_bn_bwd");
+}
 
 extern "C" int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, void* C, int32_t c_dtype,
                                    int64_t ldc, int32_t accumulate, float* stats, sv_stream_t stream) {

@@ -373,7 +373,7 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     }
     if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
     // the epilogue operand is bf16 (GELU'(h), pre-activation) or the f32 residual stream
-    constexpr int AUXT = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) ? SV_BF16
+    constexpr int AUXT = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD || EPI == SV_EPI_STORE_BN_BWD) ? SV_BF16
                          : EPI == SV_EPI_BIAS_GAMMA_RES ? SV_F32 : -1;
     wave_tile_epilogue<4, 2, EPI, AUXT>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64,
                                   n0 + wn * 64, e, split);
@@ -396,12 +396,19 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
   // the kernels are specialised for the operand dtype each epilogue carries in the bf16 model
   if ((EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) && d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
   if (EPI == SV_EPI_BIAS_GAMMA_RES && d->aux_dtype != SV_F32) return SV_ERR_UNSUPPORTED;
+  if (EPI == SV_EPI_STORE_BN_BWD && (d->aux_dtype != SV_BF16 || !d->bn || d->c_dtype != SV_BF16)) return SV_ERR_UNSUPPORTED;
   constexpr int OCC = C::TWO_PER_CU ? 4 : 2;
   const int kper = ceil_div(ceil_div(d->K, split), BKT) * BKT;
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
   e.prio = g_gemm_prio;
+  if (EPI == SV_EPI_STORE_BN_BWD) {
+    e.bn_mu = d->bn->mean;
+    e.bn_rs = d->bn->rstd;
+    e.bn_be = d->bn->beta;
+    e.gamma = d->bn->gamma;
+  }
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>),
@@ -436,6 +443,9 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
     case SV_EPI_MUL_AUX: return launch<AK, BKM, SV_EPI_MUL_AUX, BKT, S>(d, split, s);
     case SV_EPI_BIAS_GELU: return launch<AK, BKM, SV_EPI_BIAS_GELU, BKT, S>(d, split, s);
     case SV_EPI_STORE_STATS: return launch<AK, BKM, SV_EPI_STORE_STATS, BKT, S>(d, split, s);
+    case SV_EPI_STORE_BN_BWD:  // data gradients into a BatchNorm + ReLU (A k-major = dy rows)
+      if constexpr (AK && !BKM) return launch<AK, BKM, SV_EPI_STORE_BN_BWD, BKT, S>(d, split, s);
+      return SV_ERR_UNSUPPORTED;
     default: return SV_ERR_UNSUPPORTED;
   }
 }
@@ -461,6 +471,8 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 2>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
     return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 2>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_STORE_BN_BWD)
+    return launch<true, false, SV_EPI_STORE_BN_BWD, 32, S, 2>(d, 1, s, &g);
   // split-K fprop / dgrad for grids below one workgroup per CU: f32 slabs, summed by sv_gemm_slab_finish
   if (mode == 1 && d->epilogue == SV_EPI_SLAB)
     return launch<true, true, SV_EPI_SLAB, 32, S, 1>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);

@@ -22,6 +22,10 @@ struct EpiArgs {
   const float* gamma;
   const void* aux; int aux_dtype; int64_t ld_aux;
   int prio = 0;  // 1: the kernel's waves issue at raised priority (sv_gemm_set_priority)
+  // SV_EPI_STORE_BN_BWD: the BatchNorm's batch mean / rstd and beta (gamma in `gamma`, its input in aux)
+  const float* bn_mu = nullptr;
+  const float* bn_rs = nullptr;
+  const float* bn_be = nullptr;
 };
 
 __device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
@@ -127,6 +131,20 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
   const bool need_aux = e.epi == SV_EPI_BIAS_GAMMA_RES || e.epi == SV_EPI_GELU_GRAD || e.epi == SV_EPI_MUL_AUX;
   // SV_EPI_STORE_STATS (compile-time kernels only): per-lane column sums of the stored values
   constexpr bool kStats = EPI == SV_EPI_STORE_STATS;
+  // SV_EPI_STORE_BN_BWD: a plain store, plus the backward statistics of the BatchNorm + ReLU whose output
+  // gradient this is, summed column-per-lane from the staged slab (lane l owns column nb + l: one
+  // parameter set and two sums per lane, so the epilogue stays within the kernel's register budget;
+  // the mask and products are sv_bn_relu_bwd_stats', bit for bit, summed in another order)
+  constexpr bool kBnb = EPI == SV_EPI_STORE_BN_BWD;
+  const int bn_n = nb + l;
+  const bool bn_ok = kBnb && bn_n < e.N;
+  float bn_a = 0.f, bn_mu = 0.f, bn_rs = 0.f, bn_be = 0.f, bn_s1 = 0.f, bn_s2 = 0.f;
+  if (bn_ok) {
+    bn_mu = e.bn_mu[bn_n];
+    bn_rs = e.bn_rs[bn_n];
+    bn_a = e.gamma[bn_n] * bn_rs;
+    bn_be = e.bn_be[bn_n];
+  }
   float cs1[8], cs2[8];
   if constexpr (kStats) {
 #pragma unroll
@@ -204,6 +222,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
   for (int i = 0; i < 4; ++i) {
     const int si = PRE == 1 ? i : 0;
     if constexpr (PRE == 0) load_aux(i, 0);
+
     if constexpr (PRE == 2) {
       if (i + 1 < 4) fetch_raw(i + 1, rnxt);
 #pragma unroll
@@ -217,6 +236,17 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) slab[(4 * (l >> 4) + r) * EPI_LD + j * 16 + (l & 15)] = acc[i0 + i][J0 + j][r];
+    // kBnb: the BatchNorm input of this lane's column over the slab's 16 rows (loaded once the slab's
+    // accumulators are in LDS, so their registers are free; waited on after the slab's stores are issued)
+    float bn_y[16];
+    if constexpr (kBnb) {
+      const uint16_t* yp = reinterpret_cast<const uint16_t*>(e.aux);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + i * 16 + r;
+        bn_y[r] = bn_ok && m < e.M ? __uint_as_float((uint32_t)yp[(size_t)m * e.ld_aux + bn_n] << 16) : 0.f;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -240,7 +270,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       va = add4(va, b0);
       vb = add4(vb, b1);
       float4 oa, ob;
-      if (e.epi == SV_EPI_STORE || e.epi == SV_EPI_BIAS_GELU2 || e.epi == SV_EPI_STORE_STATS) {
+      if (e.epi == SV_EPI_STORE || e.epi == SV_EPI_BIAS_GELU2 || e.epi == SV_EPI_STORE_STATS || kBnb) {
         oa = va;
         ob = vb;
       } else if (e.epi == SV_EPI_BIAS_GELU_DUAL) {
@@ -282,9 +312,27 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         else st4_any(e.C2, e.c2_dtype, ci, va);
       }
     }
+    if constexpr (kBnb) {  // column bn_n of the slab, rows in order; values as stored (bf16)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + i * 16 + r;
+        if (!bn_ok || m >= e.M) continue;
+        const float q = __uint_as_float((uint32_t)f2bf(slab[r * EPI_LD + l]) << 16);
+        const float g = fmaf(bn_a, bn_y[r] - bn_mu, bn_be) > 0.f ? q : 0.f;
+        bn_s1 += g;
+        bn_s2 = fmaf(g, (bn_y[r] - bn_mu) * bn_rs, bn_s2);
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  if constexpr (kBnb) {  // the group's partial row [mb/64][2][N]: one writer per column
+    if (bn_ok && mb < e.M) {
+      float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N + bn_n;
+      P[0] = bn_s1;
+      P[e.N] = bn_s2;
+    }
   }
   if constexpr (kStats) {
     // lanes l, l+8, ..., l+56 hold the same 8 columns over the group's 64 rows: fold them (fixed

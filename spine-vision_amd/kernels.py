@@ -121,6 +121,7 @@ def gemm(
     a_scale_k: torch.Tensor | None = None,
     split_k: int = 1,
     compute_bf16: bool = True,
+    bn: "nv.BnRef | None" = None,
 ) -> torch.Tensor:
     """C = epilogue(A(m,k) . B(k,n)); see sv_gemm in include/sv_kernels.h for the layouts."""
     _check(C is not None, "gemm: output tensor C is required")
@@ -150,6 +151,8 @@ def gemm(
         d.aux, d.aux_dtype, d.ld_aux = ptr(aux), dt(aux), ld_aux if ld_aux is not None else N
     d.split_k = split_k
     d.compute = _cdt(compute_bf16)
+    if bn is not None:
+        d.bn = ctypes.pointer(bn)
     probes = [p_ for p_ in (PROBES + ([PROBE] if PROBE is not None else [])) if p_.matches(a_kmajor, b_kmajor,
                                                                                       compute_bf16, epilogue)]
     if probes:
@@ -883,6 +886,57 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
     return dx
 
 
+def _al16(*ts) -> bool:
+    return all(t.data_ptr() % 16 == 0 for t in ts)
+
+
+def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: torch.Tensor, mean: torch.Tensor,
+                     rstd: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, *, unsplit: bool = True):
+    """conv_bwd_data (bf16 dx, no accumulate) fused with the backward statistics of the BatchNorm + ReLU that
+    produced the conv's input: y [B,H,W,Cs] is that BatchNorm's input (bf16), mean / rstd its batch statistics,
+    gamma / beta its affine parameters.  -> (dx, part), part = f32 [ceil(B*H*W/64)][2][Cs] partial sums of g
+    and g*xhat (g = dx * relu mask) for bn_bwd(part=...), summed by the GEMM epilogue (SV_EPI_STORE_BN_BWD)
+    or, for split-K shapes, by the finish that reads the slabs anyway (sv_gemm_slab_finish_bn_bwd): no
+    statistics pass over dx and y.  ``unsplit=False`` fuses the split-K shapes only.  None when the shape is
+    not on these paths (stride 2, fp32, unaligned parameters): use conv_bwd_data + bn_bwd."""
+    if wp.dtype != torch.bfloat16 or y.dtype != torch.bfloat16 or s.Cs % 8 or s.stride != 1:
+        return None
+    M = s.B * s.H * s.W
+    T = s.KH * s.KW
+    pw = _pointwise(s, wp.dtype)
+    if pw:
+        split = _conv_split(M, s.Cs, s.Cout)
+    elif _is_pow2(s.Cout) and s.Cout >= 32 and (T * s.Cout) % 32 == 0:
+        split = _conv_split(M, s.Cs, T * s.Cout)
+    else:
+        return None
+    if split < 2 and not unsplit:
+        return None
+    OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
+    _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout) and dy.dtype == wp.dtype,
+           "conv_bwd_data_bn: dy must be contiguous [B,OH,OW,Cout] bf16")
+    _check(y.is_contiguous() and y.numel() == M * s.Cs, "conv_bwd_data_bn: y shape")
+    prm = [p_.detach() for p_ in (mean, rstd, gamma, beta)]
+    if not _al16(y, *prm) or any(p_.dtype != torch.float32 or not p_.is_contiguous() for p_ in prm):
+        return None
+    ref = nv.BnRef(ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(prm[3]))
+    dx = torch.empty(s.B, s.H, s.W, s.Cs, device=dy.device, dtype=torch.bfloat16)
+    part = torch.empty((M + 63) // 64, 2, s.Cs, device=dy.device, dtype=torch.float32)
+    work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32) if split > 1 else None
+    if pw and split > 1:
+        gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
+             lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+        call("sv_gemm_slab_finish_bn_bwd", ptr(work), split, M, s.Cs, ptr(dx), ptr(y), ctypes.byref(ref), ptr(part))
+    elif pw:
+        gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
+             lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), C2=part, epilogue=nv.SV_EPI_STORE_BN_BWD,
+             aux=y.view(M, s.Cs), compute_bf16=True, bn=ref)
+    else:
+        call("sv_conv_bwd_data_bn", ptr(dy), ptr(wp), ptr(dx), dt(wp), ctypes.byref(s), ptr(y), ctypes.byref(ref),
+             ptr(part), ptr(work), split)
+    return dx, part
+
+
 def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: torch.Tensor,
                     accumulate: bool = True) -> torch.Tensor:
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
@@ -967,7 +1021,8 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
 
 
 def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=None, dbeta=None,
-           dx_dtype=torch.float32, gmask=None, mask_inplace: bool = False, batch_stats: bool = True) -> torch.Tensor:
+           dx_dtype=torch.float32, gmask=None, mask_inplace: bool = False, batch_stats: bool = True,
+           part: torch.Tensor | None = None) -> torch.Tensor:
     """BatchNorm backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
     act > 0, or -- ``relu_beta`` = the BN's beta, for a BN followed by its own ReLU -- recomputed from y
     like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again).
@@ -976,7 +1031,9 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     shortcut's gradient; ``gmask`` instead writes it to a separate f32 buffer from the apply pass.
     ``batch_stats``: train mode (mean / rstd are the batch's own, so dx carries the two mean corrections);
     False: eval mode (running statistics, an affine map: dx = gamma * rstd * dout, the apply kernel reading
-    zero correction sums)."""
+    zero correction sums).
+    ``part`` (relu_beta form): the backward statistics' partials [P][2][C] already summed by the producer of
+    dout (conv_bwd_data_bn), so the statistics pass is skipped."""
     rows, C = y2d.shape
     _check(_bn_c_ok(C) and dout2d.numel() == rows * C and dout2d.is_contiguous(), "bn_bwd: bad shapes")
     _check(act is None or relu_beta is None, "bn_bwd: act and relu_beta are exclusive")
@@ -988,9 +1045,17 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     if mask_inplace:
         _check(act is not None and gmask is None and dout2d.dtype == torch.float32,
                "bn_bwd: mask_inplace needs act, an f32 dout and no gmask")
-    P = value("sv_bn_nparts", rows, C)
-    part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
-    if relu_beta is not None:
+    given = part is not None
+    if given:
+        _check(relu_beta is not None and part.dtype == torch.float32 and part.is_contiguous() and part.dim() == 3
+               and tuple(part.shape[1:]) == (2, C), "bn_bwd: part must be f32 [P][2][C] (relu_beta form)")
+        P = part.shape[0]
+    else:
+        P = value("sv_bn_nparts", rows, C)
+        part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
+    if given:
+        pass  # summed by dout's producer (conv_bwd_data_bn)
+    elif relu_beta is not None:
         call("sv_bn_relu_bwd_stats", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),
              ptr(relu_beta), rows, C, ptr(part))
     elif mask_inplace:

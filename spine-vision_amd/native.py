@@ -21,12 +21,17 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 SV_F32, SV_BF16 = 0, 1
 SV_IMG_F32_NCHW, SV_IMG_U8_GRAY = 0, 1
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
- SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS) = range(9)
+ SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS, SV_EPI_STORE_BN_BWD) = range(10)
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
+
+
+class BnRef(ctypes.Structure):
+    """sv_bn_ref (include/sv_kernels.h): the BatchNorm of SV_EPI_STORE_BN_BWD / sv_gemm_slab_finish_bn_bwd."""
+    _fields_ = [("mean", _p), ("rstd", _p), ("gamma", _p), ("beta", _p)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -43,6 +48,7 @@ class GemmDesc(ctypes.Structure):
         ("aux", _p), ("aux_dtype", _i32), ("ld_aux", _i64),
         ("split_k", _i32),
         ("compute", _i32),
+        ("bn", ctypes.POINTER(BnRef)),
     ]
 
 
@@ -80,6 +86,7 @@ _SIGS = {
     "sv_gemm_set_impl": [_i32],
     "sv_gemm_set_priority": [_i32],
     "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
+    "sv_gemm_slab_finish_bn_bwd": [_p, _i32, _i32, _i32, _p, _p, ctypes.POINTER(BnRef), _p, _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
     "sv_layernorm_bwd_nparts": [_i64, _i32],
     "sv_layernorm_bwd": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _i64, _i32, _p],
@@ -123,6 +130,7 @@ _SIGS = {
     "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],
     "sv_conv_fwd_split": [_p, _p, _p, _i32, _i32, _CS, _p, _p, _i32, _p],
     "sv_conv_bwd_data_split": [_p, _p, _p, _i32, _i32, _i32, _CS, _p, _i32, _p],
+    "sv_conv_bwd_data_bn": [_p, _p, _p, _i32, _CS, _p, ctypes.POINTER(BnRef), _p, _p, _i32, _p],
     "sv_conv_bwd_weight_work_floats": [_CS],
     "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],
     "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],

@@ -170,6 +170,60 @@ def test_conv_split_k_matches_unsplit(dev, case, monkeypatch):
         assert rel(dx_acc_s - 1.0, dx_s) < 1e-6
 
 
+BN_EPI_CASES = [
+    # B, H, W, Cs (the BN's channels = the dgrad's N), Cout, k: the four producers of the fused statistics
+    (2, 32, 32, 64, 256, 1),    # 1x1, SV_EPI_STORE_BN_BWD epilogue (ResNet-50 layer1 conv3 dgrad)
+    (2, 32, 32, 64, 64, 3),     # 3x3 gathered, epilogue (layer1 conv2 dgrad)
+    (3, 9, 7, 64, 64, 3),       # epilogue, ragged pixel count: a partial 64-row group
+    (4, 32, 32, 64, 64, 3),     # epilogue, 256 64-row groups over 64-column halves of the tile
+    (2, 16, 16, 256, 1024, 1),  # 1x1, split-K + sv_gemm_slab_finish_bn_bwd (layer3 conv3 dgrad)
+    (2, 8, 8, 512, 2048, 1),    # 1x1 (layer4 conv3 dgrad)
+    (2, 16, 16, 128, 128, 3),   # 3x3 gathered (layer2 conv2 dgrad)
+    (2, 8, 8, 512, 512, 3),     # 3x3 gathered (layer4 conv2 dgrad)
+    (3, 7, 5, 128, 128, 3),     # ragged pixel count: a partial 64-row group
+]
+
+
+@pytest.mark.parametrize("case", BN_EPI_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_bwd_data_bn_matches_separate_stats(dev, case):
+    """conv_bwd_data_bn (the data gradient with the next BatchNorm + ReLU's backward statistics from its GEMM
+    epilogue or split-K finish) against conv_bwd_data + bn_bwd's own statistics pass on the same operands:
+    dx bit for bit, the partials' column sums within f32 reordering (1e-5) of the separate pass and of a
+    float64 recomputation from dx and y, and the BatchNorm backward (dx, dgamma, dbeta) within the same."""
+    B, H, W, Cs, Cout, k = case
+    pad = k // 2
+    g = torch.Generator().manual_seed(Cs + k)
+    s = K.conv_shape(B, H, W, Cs, Cout, k, 1, pad)
+    w = torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5
+    wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
+    dy = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(dev)
+    rows = B * H * W
+    y = (torch.randn(rows, Cs, generator=g) * 2 + 0.3).to(torch.bfloat16).to(dev)
+    gam = (torch.rand(Cs, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(Cs, generator=g) * 0.3).to(dev)
+    mean, rstd = K.bn_stats(y)
+    fused = K.conv_bwd_data_bn(dy, wp, s, y.view(B, H, W, Cs), mean, rstd, gam, bet)
+    assert fused is not None, "case must take a fused path"
+    dx_f, part = fused
+    dx_r = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.bfloat16)
+    dg1, db1, dg2, db2 = (torch.zeros(Cs, device=dev) for _ in range(4))
+    o_f = K.bn_bwd(dx_f.view(rows, Cs), y, mean, rstd, gam, relu_beta=bet, dgamma=dg1, dbeta=db1,
+                   dx_dtype=torch.float32, part=part)
+    o_r = K.bn_bwd(dx_r.view(rows, Cs), y, mean, rstd, gam, relu_beta=bet, dgamma=dg2, dbeta=db2,
+                   dx_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert part.shape == ((rows + 63) // 64, 2, Cs)
+    assert torch.equal(dx_f, dx_r)
+    # float64 recomputation of sum g and sum g * xhat from the stored dx and y
+    yd, dd = y.double().cpu(), dx_r.view(rows, Cs).double().cpu()
+    mu, rs = mean.double().cpu(), rstd.double().cpu()
+    gd = torch.where(torch.addcmul(bet.double().cpu(), gam.double().cpu() * rs, yd - mu) > 0, dd, torch.zeros_like(dd))
+    sums = part.double().cpu().sum(0)
+    assert rel(sums[0], gd.sum(0)) < 1e-5 and rel(sums[1], (gd * (yd - mu) * rs).sum(0)) < 1e-5
+    assert rel(db1, db2) < 1e-5 and rel(dg1, dg2) < 1e-5
+    assert rel(o_f, o_r) < 1e-5
+
+
 @pytest.mark.parametrize("C", [64, 256, 2048])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_batchnorm_train_fwd_bwd(dev, C, precision):
