@@ -440,6 +440,20 @@ int sv_bn_bwd_stats_mask(float* dout, const void* act, int32_t act_dtype, const 
                          sv_stream_t stream);
 int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
                      sv_stream_t stream);
+/* A residual block with a projection shortcut (timm Bottleneck's downsample): the block output's gradient
+ * dout feeds the main path's last BatchNorm (y, mean, rstd) and the shortcut's (y2, mean2, rstd2) through
+ * one ReLU mask.  One statistics pass writes g = dout * (act > 0) over dout and both BatchNorms' partials
+ * (part: sums of g and g*xhat; part2: sums of g and g*xhat2) -- bit for bit sv_bn_bwd_stats_mask then
+ * sv_bn_bwd_stats(g) of the shortcut -- reading dout once; one apply pass writes both data gradients from g
+ * (bit for bit two sv_bn_bwd_apply calls).  Both BatchNorms have rows x C; dx, dx2 share dx_dtype.     */
+int sv_bn_bwd_stats_mask_dual(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
+                              const float* mean, const float* rstd, const void* y2, int32_t y2_dtype,
+                              const float* mean2, const float* rstd2, int64_t rows, int32_t C, float* part,
+                              float* part2, sv_stream_t stream);
+int sv_bn_bwd_apply_dual(const float* g, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                         const float* gamma, const float* sums, const void* y2, int32_t y2_dtype, const float* mean2,
+                         const float* rstd2, const float* gamma2, const float* sums2, void* dx, void* dx2,
+                         int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
 int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                     int32_t y_dtype, const float* mean, const float* rstd, const float* gamma, const float* sums,
                     void* dx, int32_t dx_dtype, float* gmask, int64_t rows, int32_t C, sv_stream_t stream);

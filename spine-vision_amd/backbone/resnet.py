@@ -41,6 +41,8 @@ _FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
 # (split, default: +2.2 %), also from the unsplit GEMMs' epilogue (1: no faster than a separate pass, the
 # layer1/2 epilogues absorb what the pass saved), or from their own pass everywhere (0) -- r6e A/B
 _BN_BWD_EPI = os.environ.get("SV_BN_BWD_EPI", "split")
+# SV_BN_DUAL=0: a projection-shortcut block's two output BatchNorm backwards as separate passes (A/B runs)
+_BN_DUAL = os.environ.get("SV_BN_DUAL", "1") != "0"
 
 RESNET_CFGS = {"resnet18": ("basic", (2, 2, 2, 2)), "resnet50": ("bottleneck", (3, 4, 6, 3))}
 _MAX_FORWARD_GRAPHS = 8  # captured forward graphs per model (input signatures beyond that run eagerly)
@@ -433,9 +435,19 @@ class ResNetHip(nn.Module):
         gm = d.reshape(rows, Cq)
         conv, bn, _, _, _, _ = convs[-1]
         cur_in, y, mean, rstd, _, wp, s = saved[-1]
-        dy = K.bn_bwd(gm, y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
-                      dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, mask_inplace=True,
-                      batch_stats=batch_stats)
+        dyd = None
+        if ds_saved is not None and _BN_DUAL:
+            # the shortcut's BatchNorm from the same masked gradient, in the same two passes (gm read once)
+            yd, md, rd, _, _ = ds_saved
+            dbn = blk.downsample[1]
+            dy, dyd = K.bn_bwd_dual(gm, y.view(rows, Cq), mean, rstd, bn.weight, out.view(rows, Cq),
+                                    yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(bn.weight), dbeta=g(bn.bias),
+                                    dgamma2=g(dbn.weight), dbeta2=g(dbn.bias), dx_dtype=act,
+                                    batch_stats=batch_stats)
+        else:
+            dy = K.bn_bwd(gm, y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
+                          dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, mask_inplace=True,
+                          batch_stats=batch_stats)
         params = [bn.weight, bn.bias]
         for ci in range(len(convs) - 1, -1, -1):
             conv, bn, _, _, _, _ = convs[ci]
@@ -464,8 +476,9 @@ class ResNetHip(nn.Module):
         if ds_saved is not None:
             yd, md, rd, wpd, sd = ds_saved
             dconv, dbn = blk.downsample[0], blk.downsample[1]
-            dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
-                           dx_dtype=act, batch_stats=batch_stats)
+            if dyd is None:
+                dyd = K.bn_bwd(gm, yd.view(rows, Cq), md, rd, dbn.weight, dgamma=g(dbn.weight), dbeta=g(dbn.bias),
+                               dx_dtype=act, batch_stats=batch_stats)
             dyd4 = dyd.view(yd.shape)
             jobs.append((dyd4, x_in, sd, g(dconv.weight)))
             # conv1's data gradient first (a plain store), then the strided shortcut's added onto the

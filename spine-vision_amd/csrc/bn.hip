@@ -452,6 +452,77 @@ __global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float*
   if (dbeta) dbeta[c] += s1;
 }
 
+// A residual block with a projection shortcut: its output gradient d feeds two BatchNorms (the main path's
+// last, y, and the shortcut's, y2) through the same ReLU mask.  One pass: g = d * (act > 0) written over d,
+// the main BN's sums (g, g * xhat) and the shortcut BN's g * xhat2 (its sum of g is the same), in the order of
+// bwd_stats_kernel (bit for bit its partials for either BatchNorm), reading d once instead of twice.
+template <int V>
+__global__ void __launch_bounds__(kThreads) bwd_stats_dual_kernel(float* __restrict__ dout, const void* __restrict__ act,
+                                                                  int adt, const void* __restrict__ y, int ydt,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd,
+                                                                  const void* __restrict__ y2, int y2dt,
+                                                                  const float* __restrict__ mean2,
+                                                                  const float* __restrict__ rstd2, int64_t rows, int C,
+                                                                  int tpr, int rp, int64_t rpp, float* __restrict__ part,
+                                                                  float* __restrict__ part2) {
+  const int t = threadIdx.x;
+  const int c = (blockIdx.x * tpr + t % tpr) * V;
+  const int rsub = t / tpr;
+  float mu[V], rs[V], mu2[V], rs2[V], s1[V], s2[V], s3[V];
+  ldp<V>(mean, c, mu);
+  ldp<V>(rstd, c, rs);
+  ldp<V>(mean2, c, mu2);
+  ldp<V>(rstd2, c, rs2);
+#pragma unroll
+  for (int q = 0; q < V; ++q) s1[q] = s2[q] = s3[q] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.y * rpp;
+  int64_t r1 = r0 + rpp;
+  if (r1 > rows) r1 = rows;
+  int64_t r = r0 + rsub;
+  for (; r + rp < r1; r += 2 * rp) {
+    const size_t e0 = (size_t)r * C + c, e1 = e0 + (size_t)rp * C;
+    float v0[V], g0[V], v1[V], g1[V], w0[V], w1[V];
+    ldv<V>(y, ydt, e0, v0);
+    ldv<V>(y, ydt, e1, v1);
+    ldv<V>(y2, y2dt, e0, w0);
+    ldv<V>(y2, y2dt, e1, w1);
+    grad_masked<V, false>(dout, SV_F32, act, adt, e0, v0, mu, rs, nullptr, nullptr, c, g0);
+    grad_masked<V, false>(dout, SV_F32, act, adt, e1, v1, mu, rs, nullptr, nullptr, c, g1);
+    stv<V>(dout, SV_F32, e0, g0);
+    stv<V>(dout, SV_F32, e1, g1);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s1[q] += g0[q];
+      s2[q] = fmaf(g0[q], (v0[q] - mu[q]) * rs[q], s2[q]);
+      s3[q] = fmaf(g0[q], (w0[q] - mu2[q]) * rs2[q], s3[q]);
+      s1[q] += g1[q];
+      s2[q] = fmaf(g1[q], (v1[q] - mu[q]) * rs[q], s2[q]);
+      s3[q] = fmaf(g1[q], (w1[q] - mu2[q]) * rs2[q], s3[q]);
+    }
+  }
+  for (; r < r1; r += rp) {
+    const size_t e = (size_t)r * C + c;
+    float v[V], g[V], w[V];
+    ldv<V>(y, ydt, e, v);
+    ldv<V>(y2, y2dt, e, w);
+    grad_masked<V, false>(dout, SV_F32, act, adt, e, v, mu, rs, nullptr, nullptr, c, g);
+    stv<V>(dout, SV_F32, e, g);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s1[q] += g[q];
+      s2[q] = fmaf(g[q], (v[q] - mu[q]) * rs[q], s2[q]);
+      s3[q] = fmaf(g[q], (w[q] - mu2[q]) * rs2[q], s3[q]);
+    }
+  }
+  float s1b[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) s1b[q] = s1[q];
+  reduce_write<V>(s1, s2, tpr, rp, c, C, part);
+  __syncthreads();  // reduce_write's LDS is reused
+  reduce_write<V>(s1b, s3, tpr, rp, c, C, part2);
+}
+
 struct BwdArgs {
   const void* dout; int ddt;
   const void* act; int adt;
@@ -484,6 +555,50 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
       o[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (v[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
     stv<V>(a.dx, a.xdt, e, o);
     if (a.gmask) stv<V>(a.gmask, SV_F32, e, g);
+  }
+}
+
+// both BatchNorms' data gradients from the shared masked gradient g (bwd_apply_kernel's formula for each)
+struct BwdDualArgs {
+  const float* g;
+  const void* y; int ydt;
+  const float *mean, *rstd, *gamma, *sums;
+  const void* y2; int y2dt;
+  const float *mean2, *rstd2, *gamma2, *sums2;
+  void* dx; void* dx2; int xdt;
+  int64_t rows; int C;
+};
+
+template <int V>
+__global__ void __launch_bounds__(kThreads) bwd_apply_dual_kernel(const BwdDualArgs a) {
+  const int64_t nv = a.rows * a.C / V;
+  const float inv_n = 1.0f / (float)a.rows;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const size_t e = (size_t)i * V;
+    const int c = (int)(e % a.C);
+    float g[V], v[V], w[V], o[V], o2[V], mu[V], rs[V], ga[V], sg[V], sgx[V];
+    ldv<V>(a.g, SV_F32, e, g);
+    ldv<V>(a.y, a.ydt, e, v);
+    ldv<V>(a.y2, a.y2dt, e, w);
+    ldp<V>(a.mean, c, mu);
+    ldp<V>(a.rstd, c, rs);
+    ldp<V>(a.gamma, c, ga);
+    ldp<V>(a.sums, c, sg);
+    ldp<V>(a.sums + a.C, c, sgx);
+#pragma unroll
+    for (int q = 0; q < V; ++q)
+      o[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (v[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+    ldp<V>(a.mean2, c, mu);
+    ldp<V>(a.rstd2, c, rs);
+    ldp<V>(a.gamma2, c, ga);
+    ldp<V>(a.sums2, c, sg);
+    ldp<V>(a.sums2 + a.C, c, sgx);
+#pragma unroll
+    for (int q = 0; q < V; ++q)
+      o2[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (w[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+    stv<V>(a.dx, a.xdt, e, o);
+    stv<V>(a.dx2, a.xdt, e, o2);
   }
 }
 
@@ -846,4 +961,44 @@ extern "C" int sv_avgpool_bwd(const float* dfeat, float* dx, int32_t B, int32_t 
   SV_REQUIRE(dfeat && dx && B > 0 && HW > 0 && C % 4 == 0 && C > 0, "sv_avgpool_bwd: bad arguments");
   avgpool_bwd_kernel<<<grid_for((int64_t)B * HW * C / 4), kThreads, 0, (hipStream_t)stream>>>(dfeat, dx, B, HW, C);
   return check_launch("sv_avgpool_bwd");
+}
+
+extern "C" int sv_bn_bwd_stats_mask_dual(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
+                                         const float* mean, const float* rstd, const void* y2, int32_t y2_dtype,
+                                         const float* mean2, const float* rstd2, int64_t rows, int32_t C, float* part,
+                                         float* part2, sv_stream_t stream) {
+  BN_REQUIRE_C(C, "sv_bn_bwd_stats_mask_dual");
+  SV_REQUIRE(dout && act && y && mean && rstd && y2 && mean2 && rstd2 && part && part2 && rows > 0 && dt_ok(act_dtype) &&
+                 dt_ok(y_dtype) && dt_ok(y2_dtype),
+             "sv_bn_bwd_stats_mask_dual: bad arguments");
+  const RedGeo g = red_geo(C);
+  const int P = nparts_for(rows, C);
+  const int64_t rpp = (rows + P - 1) / P;
+  const dim3 grid(g.cslices, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (g.vec == 8)
+    bwd_stats_dual_kernel<8><<<grid, kThreads, 0, st>>>(dout, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
+                                                        rstd2, rows, C, g.tpr, g.rp, rpp, part, part2);
+  else
+    bwd_stats_dual_kernel<4><<<grid, kThreads, 0, st>>>(dout, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
+                                                        rstd2, rows, C, g.tpr, g.rp, rpp, part, part2);
+  return check_launch("sv_bn_bwd_stats_mask_dual");
+}
+
+extern "C" int sv_bn_bwd_apply_dual(const float* g, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                                    const float* gamma, const float* sums, const void* y2, int32_t y2_dtype,
+                                    const float* mean2, const float* rstd2, const float* gamma2, const float* sums2,
+                                    void* dx, void* dx2, int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(C % 4 == 0 && C > 0 && rows > 0, "sv_bn_bwd_apply_dual: C must be a multiple of 4");
+  SV_REQUIRE(g && y && mean && rstd && gamma && sums && y2 && mean2 && rstd2 && gamma2 && sums2 && dx && dx2 &&
+                 dt_ok(y_dtype) && dt_ok(y2_dtype) && dt_ok(dx_dtype),
+             "sv_bn_bwd_apply_dual: bad arguments");
+  BwdDualArgs a{g, y, y_dtype, mean, rstd, gamma, sums, y2, y2_dtype, mean2, rstd2, gamma2, sums2, dx, dx2, dx_dtype,
+                rows, C};
+  hipStream_t st = (hipStream_t)stream;
+  if (vec_for(C) == 8)
+    bwd_apply_dual_kernel<8><<<grid_for(rows * C / 8), kThreads, 0, st>>>(a);
+  else
+    bwd_apply_dual_kernel<4><<<grid_for(rows * C / 4), kThreads, 0, st>>>(a);
+  return check_launch("sv_bn_bwd_apply_dual");
 }

@@ -1079,6 +1079,32 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     return dx
 
 
+def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dgamma=None, dbeta=None,
+                dgamma2=None, dbeta2=None, dx_dtype=torch.float32, batch_stats: bool = True):
+    """A projection-shortcut block's two output BatchNorms from one masked gradient: equals
+    ``bn_bwd(gm, y2d, ..., act=act, mask_inplace=True)`` followed by ``bn_bwd(gm, y2, mean2, rstd2, gamma2)``
+    bit for bit (gm, f32, is overwritten with the masked gradient the same way), with gm read once per pass
+    instead of twice (sv_bn_bwd_stats_mask_dual / sv_bn_bwd_apply_dual). -> (dx, dx2)."""
+    rows, C = y2d.shape
+    _check(_bn_c_ok(C) and gm.dtype == torch.float32 and gm.numel() == rows * C and gm.is_contiguous()
+           and act.numel() == rows * C and act.is_contiguous() and y2.numel() == rows * C and y2.is_contiguous(),
+           "bn_bwd_dual: bad shapes")
+    P = value("sv_bn_nparts", rows, C)
+    part = torch.empty(2, P, 2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_bwd_stats_mask_dual", ptr(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(y2),
+         dt(y2), ptr(mean2), ptr(rstd2), rows, C, ptr(part[0]), ptr(part[1]))
+    sums = torch.empty(2, 2, C, device=y2d.device, dtype=torch.float32)
+    call("sv_bn_bwd_finish", ptr(part[0]), P, C, ptr(sums[0]), ptr(dgamma), ptr(dbeta))
+    call("sv_bn_bwd_finish", ptr(part[1]), P, C, ptr(sums[1]), ptr(dgamma2), ptr(dbeta2))
+    if not batch_stats:
+        sums.zero_()
+    dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+    dx2 = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+    call("sv_bn_bwd_apply_dual", ptr(gm), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums[0]), ptr(y2),
+         dt(y2), ptr(mean2), ptr(rstd2), ptr(gamma2), ptr(sums[1]), ptr(dx), ptr(dx2), dt(dx), rows, C)
+    return dx, dx2
+
+
 def bn_relu_bwd_pooled(dpool4d: torch.Tensor, idx: torch.Tensor, H: int, W: int, y2d, mean, rstd, gamma, beta, *,
                        dgamma=None, dbeta=None, dx_dtype=torch.float32, batch_stats: bool = True) -> torch.Tensor:
     """bn_bwd(maxpool_bwd(dpool, idx, H, W), y, ..., relu_beta=beta) without materialising the max-pool

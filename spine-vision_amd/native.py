@@ -143,6 +143,8 @@ _SIGS = {
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_stats_mask": [_p, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
+    "sv_bn_bwd_stats_mask_dual": [_p, _p, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p, _p, _p],
+    "sv_bn_bwd_apply_dual": [_p, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
     "sv_bn_relu_bwd_stats": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_relu_bwd_apply": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
     "sv_bn_relu_bwd_stats_pool": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _i32, _p, _p],

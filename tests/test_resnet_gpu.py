@@ -360,6 +360,35 @@ def test_bn_bwd_mask_inplace_matches_gmask(dev, rows, C):
     assert rel(db1, g64.sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("rows,C,dt_", [(4099, 256, torch.bfloat16), (2 * 64 * 64, 256, torch.bfloat16),
+                                        (1000, 2048, torch.bfloat16), (515, 12, torch.float32)])
+def test_bn_bwd_dual_matches_two_passes(dev, rows, C, dt_):
+    """bn_bwd_dual (a projection-shortcut block's main and shortcut output BatchNorms from one masked gradient,
+    one statistics and one apply pass) is bit for bit bn_bwd(mask_inplace) then bn_bwd of the shortcut: the
+    masked gradient written over gm, both data gradients, dgamma / dbeta of both.  C = 12 takes the 4-channel
+    kernels; 2048 the widest layer4 row."""
+    g = torch.Generator().manual_seed(rows + C)
+    y = torch.randn(rows, C, generator=g).to(dev, dt_)
+    yd = (torch.randn(rows, C, generator=g) * 1.5 - 0.2).to(dev, dt_)
+    gam, bet = (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.3).to(dev)
+    gd, bd = (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.3).to(dev)
+    m1, r1 = K.bn_stats(y)
+    m2, r2 = K.bn_stats(yd)
+    out = K.bn_act(y, m1, r1, gam, bet, res=yd, res_bn=(m2, r2, gd, bd), relu=True, out_dtype=dt_)
+    d0 = torch.randn(rows, C, generator=g).to(dev)
+    grads = [torch.zeros(C, device=dev) for _ in range(8)]
+    ga = d0.clone()
+    dx1 = K.bn_bwd(ga, y, m1, r1, gam, act=out, dgamma=grads[0], dbeta=grads[1], dx_dtype=dt_, mask_inplace=True)
+    dx2 = K.bn_bwd(ga, yd, m2, r2, gd, dgamma=grads[2], dbeta=grads[3], dx_dtype=dt_)
+    gb = d0.clone()
+    ex1, ex2 = K.bn_bwd_dual(gb, y, m1, r1, gam, out, yd, m2, r2, gd, dgamma=grads[4], dbeta=grads[5],
+                             dgamma2=grads[6], dbeta2=grads[7], dx_dtype=dt_)
+    torch.cuda.synchronize()
+    assert torch.equal(ga, gb) and torch.equal(dx1, ex1) and torch.equal(dx2, ex2)
+    for a, b in zip(grads[:4], grads[4:]):
+        assert torch.equal(a, b)
+
+
 def test_bn_act_downsample_residual(dev):
     rows, C = 64, 256
     y, r = _rand((rows, C), 11), _rand((rows, C), 12)
