@@ -764,6 +764,27 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
   a.C = y;
   a.c_dtype = y_dtype;
   a.kper = ceil_div(a.K, BKT) * BKT;
+  // SV_STEM_GATHER=0: the register-staged kernel instead (A/B runs)
+  static const bool stem8 = !getenv("SV_STEM_GATHER") || atoi(getenv("SV_STEM_GATHER")) != 0;
+  if (stem8 && dtype == SV_BF16 && s->Cs == 8 && !slab && s->KH == s->KW && s->KH <= 7 && a.ntaps <= CONV_MAX_TAPS &&
+      a.N % 8 == 0) {
+    // 8-channel pixels (the ResNet stem over its zero-padded RGB operand): one tap per 16-B chunk, gathered
+    // per lane (mode 6); K padded to whole 32-deep k-steps with zero-page chunks
+    ConvG g = make_convg(s->H, s->W, 8, OH, OW, s->stride);
+    g.kw = s->KW;
+    g.pad = s->pad;
+    g.ntaps = a.ntaps;
+    g.kw_mul = (65536u + (uint32_t)s->KW - 1) / (uint32_t)s->KW;
+    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, ceil_div(a.K, 32) * 32, 1, a.K, y, y_dtype);
+    if (stats) {
+      SV_REQUIRE(((uintptr_t)stats & 15) == 0, "sv_conv_fwd_stats: stats alignment");
+      d.epilogue = SV_EPI_STORE_STATS;
+      d.C2 = stats;
+      d.c2_dtype = SV_F32;
+    }
+    const int rc = launch_gemm3_conv(&d, g, 6, (hipStream_t)stream);
+    if (rc != SV_ERR_UNSUPPORTED) return rc;
+  }
   if (dtype == SV_BF16 && s->Cs >= 32 && pow2(s->Cs) && a.K % 32 == 0) {
     ConvG g = make_convg(s->H, s->W, s->Cs, OH, OW, s->stride);
     for (int j = 0; j < a.ntaps; ++j) {

@@ -100,6 +100,50 @@ __device__ __forceinline__ void issue_gather(const uint16_t* __restrict__ X, con
   }
 }
 
+// implicit-GEMM A operand over 8-channel pixels (CONV 6, the ResNet stem's Cs = 8): each lane's 16-B chunk
+// is one whole tap of its pixel, so the tap is decoded per lane (taps past ntaps read the zero page)
+template <int BKT, int PER_WAVE>
+__device__ __forceinline__ void issue_gather8(const uint16_t* __restrict__ X, const ConvG& g, const int (&gb)[PER_WAVE],
+                                              const int (&gy)[PER_WAVE], const int (&gx)[PER_WAVE], int k0,
+                                              char* lds_tile, int wid) {
+  const int lane = threadIdx.x & 63;
+  constexpr int RB = BKT * 2;
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int piece = wid + NW * j;
+    const int byte = piece * 1024 + lane * 16;
+    const int row = byte / RB, ch = (byte % RB) >> 4;
+    const int t = (k0 >> 3) + (ch ^ kswz<BKT>(row));
+    const uint16_t* src = g_conv_zero;
+    if (t < g.ntaps && gb[j] >= 0) {
+      const int q = (int)(((uint32_t)t * g.kw_mul) >> 16);
+      const int iy = gy[j] + q - g.pad, ix = gx[j] + (t - q * g.kw) - g.pad;
+      if ((unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW)
+        src = X + ((size_t)(gb[j] + iy) * g.SW + ix) * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+// its B operand: the packed weight [N][ntaps * 8] k-major, columns past ntaps * 8 (the K padding to a whole
+// k-step) read the zero page instead of the next row
+template <int BKT, int PER_WAVE>
+__device__ __forceinline__ void issue_tile_kclamp(const uint16_t* __restrict__ X, int64_t ld, int row0, int k0, int R,
+                                                  int kreal, char* lds_tile, int wid) {
+  const int lane = threadIdx.x & 63;
+  constexpr int RB = BKT * 2;
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int piece = wid + NW * j;
+    const int byte = piece * 1024 + lane * 16;
+    const int row = byte / RB, ch = (byte % RB) >> 4;
+    const int k = k0 + (ch ^ kswz<BKT>(row)) * 8;
+    int grow = row0 + row;
+    if (grow >= R) grow = 0;
+    const uint16_t* src = k < kreal ? X + (size_t)grow * ld + k : g_conv_zero;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
 __device__ __forceinline__ uint32_t cg_div(uint32_t n, uint32_t mul, uint32_t shift) {
   return (uint32_t)(((uint64_t)__umulhi(n, mul) + n) >> shift);
 }
@@ -319,6 +363,9 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       } else if constexpr (CONV == 0) {
         issue_tile<AK, BM, BKT, C::A_PER_WAVE>(A, lda, m0, k0, e.M, st, wid);
         issue_tile<BKM, BN, BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, st + C::A_BYTES, wid);
+      } else if constexpr (CONV == 6) {
+        issue_gather8<BKT, C::A_PER_WAVE>(A, cg, gb, gy, gx, k0, st, wid);
+        issue_tile_kclamp<BKT, C::B_PER_WAVE>(B, ldb, n0, k0, e.N, cg.ntaps * 8, st + C::A_BYTES, wid);
       } else {
         const int jt = (CONV == 5 ? (int)cg.ctap0[split] : 0) + (k0 >> cg.lsc);  // wave-uniform tap
         const int cb = k0 & ((1 << cg.lsc) - 1);                                  // and channel base
@@ -479,6 +526,10 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   if (mode == 2 && d->epilogue == SV_EPI_SLAB)
     return launch<true, false, SV_EPI_SLAB, 32, S, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, S, 5>(d, 4, s, &g);
+  // 8-channel pixels (the ResNet stem), plain store or with the BatchNorm statistics
+  if (mode == 6 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, S, 6>(d, 1, s, &g);
+  if (mode == 6 && d->epilogue == SV_EPI_STORE_STATS)
+    return launch<true, true, SV_EPI_STORE_STATS, 32, S, 6>(d, 1, s, &g);
   return SV_ERR_UNSUPPORTED;
 }
 // gathered weight gradients (modes 3, 4) at S ring stages
@@ -494,7 +545,8 @@ static int conv_w(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s
 
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
-  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 || (mode != 3 && mode != 4 && g.lsc < 5))
+  if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 ||
+      (mode != 3 && mode != 4 && mode != 6 && g.lsc < 5) || (mode == 6 && (g.lsc != 3 || g.ntaps * 8 > d->K)))
     return SV_ERR_UNSUPPORTED;
   // ring depth: 3 stages (fprop / dgrad, two workgroups per CU) and 4 (wgrads); 6 stages (144 KiB, five
   // tiles in flight) measured no faster for any ResNet-50 conv pass (profiles/round3/r6b_conv_ring_depth.txt)

@@ -401,6 +401,10 @@ struct ConvG {
   int8_t tdy[CONV_MAX_TAPS], tdx[CONV_MAX_TAPS];
   uint8_t twt[CONV_MAX_TAPS];
   uint8_t ctap0[4], ctaps[4];  // mode 5: each output parity class's run of taps in tdy/tdx/twt
+  // mode 6 (fprop over 8-channel pixels, the ResNet stem): every 16-B chunk of a k-step is its own tap
+  // t = k >> 3, (ty, tx) = (t / kw - pad, t % kw - pad) decoded per lane, t / kw = (t * kw_mul) >> 16
+  uint32_t kw_mul;
+  int kw, pad, ntaps;
 };
 // d = n / D for n < 2^31: (umulhi(n, mul) + n) >> shift
 inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {

@@ -741,6 +741,17 @@ def _gathered(s: nv.ConvShape, dtype: torch.dtype) -> bool:
     return dtype == torch.bfloat16 and s.Cs >= 32 and _is_pow2(s.Cs) and (s.KH * s.KW * s.Cs) % 32 == 0
 
 
+def _stem8(s: nv.ConvShape, dtype: torch.dtype) -> bool:
+    """the bf16 8-channel gathered path of sv_conv_fwd (conv.hip mode 6: the ResNet stem over its zero-padded
+    RGB operand, one tap per 16-B chunk)"""
+    return (_STEM_GATHER and dtype == torch.bfloat16 and s.Cs == 8 and s.KH == s.KW and s.KH <= 7
+            and s.Cout % 8 == 0)
+
+
+# SV_STEM_GATHER=0: the stem forward on the register-staged conv kernel plus a BatchNorm statistics pass (A/B runs)
+_STEM_GATHER = os.environ.get("SV_STEM_GATHER", "1") != "0"
+
+
 def _slab_finish(work: torch.Tensor, split: int, M: int, N: int, C: torch.Tensor, *, accumulate: bool = False,
                  stats: torch.Tensor | None = None) -> None:
     _timed_call("fold", 4.0 * M * N * (split + 1 + int(bool(accumulate))), "sv_gemm_slab_finish", ptr(work), split, M,
@@ -809,13 +820,13 @@ def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dt
         part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
         _pointwise_fwd(x, wp, s, y, M, stats=part)
         return y, part
-    if not _gathered(s, wp.dtype):
+    if not (_gathered(s, wp.dtype) or _stem8(s, wp.dtype)):
         return conv_fwd(x, wp, s, out_dtype), None
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
     part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
-    split = _conv_split(M, s.Cout, s.KH * s.KW * s.Cs)
+    split = 1 if _stem8(s, wp.dtype) else _conv_split(M, s.Cout, s.KH * s.KW * s.Cs)
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
         call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), ptr(work), split)

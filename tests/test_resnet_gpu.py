@@ -90,13 +90,14 @@ def test_conv_fwd_dgrad_wgrad(dev, case, precision):
 
 @pytest.mark.parametrize("case", [(2, 16, 16, 64, 128, 1, 1), (1, 9, 9, 64, 64, 3, 1), (2, 14, 10, 64, 256, 3, 1),
                                   (2, 16, 16, 256, 512, 1, 2), (3, 7, 5, 128, 64, 3, 2), (4, 64, 64, 256, 1024, 1, 1),
-                                  (4, 67, 67, 128, 1024, 1, 1)])
+                                  (4, 67, 67, 128, 1024, 1, 1), (2, 33, 30, 8, 64, 7, 2), (4, 64, 64, 8, 64, 7, 2)])
 def test_conv_fwd_bn_stats_epilogue(dev, case):
     """SV_EPI_STORE_STATS: the conv GEMM's epilogue emits the BatchNorm statistics of its stored bf16
     output.  Same y as conv_fwd (bitwise), and mean / rstd / running stats as bn_stats over that y
     (f32 rounding only).  Cases: pointwise GEMM, gathered 3x3 / stride 2, M not a multiple of 64
-    (81 rows: a partial row group), M below one 256-row tile, and two pointwise grids of >= 256
-    256x256 tiles that take the persistent v9 kernel (the second with a ragged last row group)."""
+    (81 rows: a partial row group), M below one 256-row tile, two pointwise grids of >= 256
+    256x256 tiles that take the persistent v9 kernel (the second with a ragged last row group), and the
+    ResNet stem's 7x7 / 2 over 8-channel pixels (per-lane tap gather, mode 6; the first ragged)."""
     B, H, W, Cs, Cout, k, st = case
     pad = k // 2
     g = torch.Generator().manual_seed(11)
