@@ -89,6 +89,21 @@ typedef struct {
   const float* beta;
 } sv_bn_ref;
 
+/* Launch policy of the GEMM kernels behind ONE call (sv_gemm, the sv_conv_* entry points).  It travels
+ * with the call -- there is no process-wide GEMM state -- so launches from other streams, models, threads
+ * or devices of the same process are never affected.  A zero-initialised policy is the default schedule.  */
+typedef struct {
+  int32_t impl;      /* 0 = the measured per-shape dispatch; 2 / 3 / 8 / 9 = force that kernel family where its
+                      * contract holds (tests/test_gemm_family_gpu.py compares the families bit for bit)      */
+  int32_t grid_cap;  /* > 0: the persistent v3 / v9 grids run on at most this many workgroups (the ResNet side
+                      * stream's weight gradients; CUs left to RCCL under data parallelism); 0 = every CU of
+                      * the stream's device.  Persistent over their tiles, so the results are bitwise unchanged */
+  int32_t wg_per_cu; /* 0 = one workgroup per output tile; 1..2 = persistent grids of n workgroups per CU, so
+                      * GEMMs issued on two streams at once (data + weight gradients) share every CU         */
+  int32_t priority;  /* 1 = the v3 K loop's waves at raised s_setprio (critical-path GEMM beside another
+                      * stream's kernels); 0 = normal.  Bitwise neutral                                    */
+} sv_gemm_policy;
+
 typedef struct {
   int32_t M, N, K;
   const void* A; int32_t a_dtype; int32_t a_kmajor; int64_t lda;
@@ -103,27 +118,10 @@ typedef struct {
   int32_t split_k;           /* SV_EPI_SLAB: number of K slices (>= 1); slab stride = M*N floats  */
   int32_t compute;           /* SV_BF16: bf16 MFMA (operands rounded to bf16); SV_F32: f32 MFMA    */
   const sv_bn_ref* bn;       /* SV_EPI_STORE_BN_BWD: the BatchNorm (NULL otherwise)                */
+  sv_gemm_policy policy;     /* launch policy of THIS call (zero-initialised = the defaults)      */
 } sv_gemm_desc;
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
-/* Process-wide cap on the workgroup count of subsequent v3 / v9 GEMM launches (persistent over their
- * tiles; 0 = off); returns the previous value.  The ResNet backward issues its side-stream weight
- * gradients under a cap so part of the chip stays free for the data-gradient / BatchNorm chain.       */
-int sv_gemm_set_grid_cap(int32_t n);
-/* Residency policy for the bf16 GEMMs launched after this call (host-side, process-wide):
- * 0 (default) = one workgroup per output tile; n > 0 = persistent grids of n workgroups per CU, so
- * that GEMMs issued concurrently on two streams (data gradients + weight gradients) are co-resident
- * on every CU instead of the first one filling the chip.  Returns the previous value.               */
-int sv_gemm_set_workgroups_per_cu(int32_t n);
-/* Wave priority of the v3 GEMMs launched after this call (host-side, process-wide): 1 = their waves
- * run at raised s_setprio, so a critical-path GEMM sharing CUs with a concurrent stream's kernels
- * issues first; 0 (default) = normal.  Returns the previous value.                                  */
-int sv_gemm_set_priority(int32_t p);
-/* Kernel family for the bf16 GEMMs launched after this call (host-side, process-wide, initially 0):
- * 0 = the measured per-shape dispatch, 2 / 3 / 8 / 9 = force that family where its contract holds
- * (tests/test_gemm_family_gpu.py compares the families bit for bit; tools/gemm_bench.py times them).
- * Returns the previous value.                                                                      */
-int sv_gemm_set_impl(int32_t impl);
 /* Finish of a split-K GEMM (SV_EPI_SLAB): C[m, n] = (accumulate ? C[m, n] : 0) + sum_s slab[s][m][n],
  * slices summed in order (deterministic); c_dtype f32 or bf16 (accumulate: f32 only).  stats != NULL
  * (bf16 C): also the SV_EPI_STORE_STATS partials [ceil(M/64)][2][N] of the values as stored.
@@ -337,7 +335,8 @@ int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream)
  *   x   [B][H][W][Cs]    input, Cs = stored channels (power of two; >= the real Cin, zero padded)
  *   y   [B][OH][OW][Cout]  OH = (H + 2 pad - KH)/stride + 1
  *   wp  [Cout][KH*KW][Cs]  packed weight (sv_conv_weight_pack), dtype
- * Cout must be a multiple of 8 (bf16) / 4 (f32).                                                   */
+ * Cout must be a multiple of 8 (bf16) / 4 (f32).  `policy` (NULL = defaults): the launch policy of the
+ * convolution's GEMMs (sv_gemm_policy; the f32 register-staged kernel ignores it).                  */
 typedef struct sv_conv_shape {
   int32_t B, H, W, Cs;  /* input                                      */
   int32_t Cout;         /* output channels                            */
@@ -357,16 +356,16 @@ typedef struct {
 int sv_conv_weight_pack_multi(const sv_pack_seg* segs, int32_t nseg, int32_t dtype, sv_stream_t stream);
 /* y = conv(x, w).  y_dtype may differ from dtype (f32 or bf16 store).                             */
 int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
-                sv_stream_t stream);
+                const sv_gemm_policy* policy, sv_stream_t stream);
 /* dx (+)= conv_transpose(dy, w): dy [B][OH][OW][Cout] (dtype), dx [B][H][W][Cs] (dx_dtype). Stride-2
  * convolutions run as four stride-1 sub-convolutions, one per output parity class.                 */
 int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                     int32_t dtype, const sv_conv_shape* s, sv_stream_t stream);
+                     int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* policy, sv_stream_t stream);
 /* dw (+)= dy^T * im2col(x) into torch layout [Cout][Cin][KH][KW] f32, through split-K f32 slabs in
  * `work` (sv_conv_bwd_weight_work_floats(s) floats).                                              */
 int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s);
 int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate, int32_t dtype,
-                       const sv_conv_shape* s, sv_stream_t stream);
+                       const sv_conv_shape* s, const sv_gemm_policy* policy, sv_stream_t stream);
 /* Row f1, classification side: the collated uint8 HWC crops [B][H][W][3] -- the output of the
  * reference's construct_3channel ([T2,T1,T2], or one plane replicated; spine_vision/training/
  * datasets/classification.py:40-68) before ToTensor/Normalize (:247-278) -- straight into the ResNet
@@ -380,7 +379,7 @@ int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mean, const fl
  * Only the bf16 gathered-operand path (Cs >= 32, power of two, Cout % 8 == 0) carries it: other
  * shapes return SV_ERR_UNSUPPORTED (use sv_conv_fwd + sv_bn_stats).                                */
 int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
-                      float* stats, sv_stream_t stream);
+                      float* stats, const sv_gemm_policy* policy, sv_stream_t stream);
 /* Split-K forms for grids smaller than the chip (the deep ResNet stages: few 256x128 output tiles,
  * long K = taps x channels): the gathered GEMM writes `split` f32 slabs [split][M][N] into `work`
  * (split * M * N floats), then sv_gemm_slab_finish sums them into y (+ the STORE_STATS partials when
@@ -390,9 +389,10 @@ int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, i
  * compact slabs into `work` (split * B*H*W*Cs floats in all), one pass scatters them into dx (+= when
  * accumulate; dx f32 or bf16).                                                                       */
 int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
-                      float* stats, float* work, int32_t split, sv_stream_t stream);
+                      float* stats, float* work, int32_t split, const sv_gemm_policy* policy, sv_stream_t stream);
 int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                           int32_t dtype, const sv_conv_shape* s, float* work, int32_t split, sv_stream_t stream);
+                           int32_t dtype, const sv_conv_shape* s, float* work, int32_t split,
+                           const sv_gemm_policy* policy, sv_stream_t stream);
 /* Stride-1 data gradient dx (bf16) of the gathered bf16 path (as sv_conv_bwd_data, no accumulate) plus
  * the backward statistics partials [ceil(B*H*W/64)][2][Cs] of the BatchNorm + ReLU that produced the
  * conv's input (y = that BatchNorm's input [B][H][W][Cs] bf16): split == 1 from the GEMM epilogue
@@ -400,7 +400,7 @@ int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_
  * sv_gemm_slab_finish_bn_bwd.  Other shapes are an error.                                            */
 int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int32_t dtype, const sv_conv_shape* s,
                         const void* y, const sv_bn_ref* bn, float* part, float* work, int32_t split,
-                        sv_stream_t stream);
+                        const sv_gemm_policy* policy, sv_stream_t stream);
 /* NCHW f32 image [B][C][H][W] -> NHWC [B][H][W][Cs] (dtype), channels >= C zero.                  */
 int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int32_t C, int32_t H, int32_t W,
                      int32_t Cs, sv_stream_t stream);

@@ -326,14 +326,12 @@ class ConvNeXtHip(nn.Module):
         hn = self.head.norm
         main = torch.cuda.current_stream()
         side = self._side_stream(main.device) if self.overlap_wgrad else None
-        # block GEMMs of the two streams: one persistent workgroup per CU each, so they share every CU
-        prev_res = nv.value("sv_gemm_set_workgroups_per_cu", self.side_wg_per_cu if side is not None else 0)
-        prev_cap = nv.value("sv_gemm_set_grid_cap", _comm_cap(main.device, self.comm_reserve_cus))
+        # the backward's GEMM launch policy, passed with every call (no process-wide state): block GEMMs of
+        # the two streams on one persistent workgroup per CU each, so they share every CU; under data
+        # parallelism every grid leaves comm_reserve_cus CUs to RCCL
+        comm_cap = _comm_cap(main.device, self.comm_reserve_cus)
+        pol = nv.policy(grid_cap=comm_cap, wg_per_cu=self.side_wg_per_cu if side is not None else 0)
         lean = side is not None and bf and self.lean_sync
-        # lean mode: the side stream's weight-gradient GEMMs run at raised wave priority where they share a
-        # CU with the main stream's data-gradient GEMMs (+1.0% step, interleaved A/B gpurun_out prio2;
-        # raising the main stream's instead cost 0.7%, prio1)
-        prev_prio = nv.value("sv_gemm_set_priority", 0)
         # lean mode: per block (side-stream event, the operands the side stream reads), oldest first;
         # released in batches once the side stream has passed them (_release_side)
         pending: list = []
@@ -356,7 +354,7 @@ class ConvNeXtHip(nn.Module):
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 dsrc = db.view(M, C) if bf else d2
                 if lean:
-                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending)
+                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol)
                     self._release_side(main, pending)
                     continue
                 # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
@@ -370,7 +368,7 @@ class ConvNeXtHip(nn.Module):
                     # dW2 = gamma (.) d^T a, dgamma = rowdot(W2, d^T a) + b2 (.) colsum(d), db2 = gamma (.) colsum(d)
                     K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(),
                                        blk.mlp.fc2.bias.detach(), dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma),
-                                       db2=g(blk.mlp.fc2.bias), compute_bf16=bf)
+                                       db2=g(blk.mlp.fc2.bias), compute_bf16=bf, policy=pol)
                 ev_w2 = side.record_event() if side is not None else None
                 # fc2: dh = ((d * gamma) @ W2) * GELU'(h).  bf16 mode folds gamma into a bf16 copy of W2;
                 # GELU'(h) was stored by the forward epilogue
@@ -379,10 +377,10 @@ class ConvNeXtHip(nn.Module):
                     w2g = tape.w2g.pop(id(blk), None)
                     if w2g is None:
                         w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
-                    K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
+                    K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True, policy=pol)
                 else:
                     K.linear_dgrad(d2, blk.mlp.fc2.weight.detach(), out=dh, epilogue=nv.SV_EPI_MUL_AUX,
-                                   a_scale_k=blk.gamma, aux=gh, compute_bf16=False)
+                                   a_scale_k=blk.gamma, aux=gh, compute_bf16=False, policy=pol)
                 # fc1: dy = dh @ W1 (main) ; dW1 = dh^T y, db1 = colsum(dh) (side, fused in the wgrad GEMM).
                 # bf16 mode: dy and dz travel as bf16 (the depthwise backward reads dz through its LDS-DMA
                 # ring, where 2-byte columns cost no more than 4-byte ones)
@@ -393,9 +391,9 @@ class ConvNeXtHip(nn.Module):
                 folds: list | None = [] if self.merge_folds else None  # one fold launch for the block
                 with torch.cuda.stream(side) if side is not None else _nullctx():
                     K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True,
-                                   bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf, defer=folds)
+                                   bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf, defer=folds, policy=pol)
                 dy = torch.empty(M, C, device=d.device, dtype=act)
-                K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf)
+                K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf, policy=pol)
                 # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
                 # the LN weight/bias partials are folded on the side stream (off the data-gradient chain)
                 dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight,
@@ -433,9 +431,9 @@ class ConvNeXtHip(nn.Module):
                 dsrc = db.view(Mo, Cout) if bf else d.view(Mo, Cout)
                 wds = self._w(conv.weight, cache).reshape(Cout, 4 * C)
                 dpatch = torch.empty(Mo, 4 * C, device=d.device, dtype=torch.float32)
-                K.linear_dgrad(dsrc, wds, out=dpatch, compute_bf16=bf)
+                K.linear_dgrad(dsrc, wds, out=dpatch, compute_bf16=bf, policy=pol)
                 K.linear_wgrad(dsrc, patches, out=g(conv.weight), accumulate=True, bias_out=g(conv.bias),
-                               compute_bf16=bf)
+                               compute_bf16=bf, policy=pol)
                 d, db = K.downsample_bwd(dpatch, x_prev, d_mean, d_rstd, ln.weight, dlnw=g(ln.weight),
                                          dlnb=g(ln.bias), with_bf16=bf)
                 self._ready([ln.weight, ln.bias, conv.weight, conv.bias])
@@ -448,14 +446,11 @@ class ConvNeXtHip(nn.Module):
             dz0 = K.layernorm_bwd(d.view(-1, C0), z0, s_mean, s_rstd, ln.weight, dw=g(ln.weight), db=g(ln.bias),
                                   out_dtype=torch.bfloat16)
             K.linear_wgrad(dz0, patches, out=g(conv.weight).view(C0, 48), accumulate=True, bias_out=g(conv.bias),
-                           compute_bf16=True, cols=48)
+                           compute_bf16=True, cols=48, policy=pol)
         else:
             s_mean, s_rstd = tape.stem
             K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
                        db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
-        nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
-        nv.value("sv_gemm_set_priority", prev_prio)
-        nv.value("sv_gemm_set_grid_cap", prev_cap)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
             pending.clear()  # safe: later main-stream allocations are ordered after the join
@@ -477,11 +472,14 @@ class ConvNeXtHip(nn.Module):
             main.wait_event(pending[cls._RELEASE_BATCH - 1][0])
             del pending[:cls._RELEASE_BATCH]
 
-    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, pending):
+    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol):
         """bf16 block backward with one main->side hand-off.  Main: fc2 dgrad (x GELU'), fc1 dgrad,
         LayerNorm backward, depthwise backward-data.  Side, after the LayerNorm backward: fc2 wgrad
         (+ gamma, bias), fc1 wgrad (+ bias), the LayerNorm weight/bias fold and the depthwise wgrad of
-        the block, beside the main stream's next block.  Returns the new (d, db)."""
+        the block, beside the main stream's next block.  ``pol``: the main stream's GEMM policy; the side
+        stream's GEMMs run at raised wave priority where they share a CU with the main stream's data-gradient
+        GEMMs (+1.0% step, interleaved A/B gpurun_out prio2; raising the main stream's instead cost 0.7%,
+        prio1), under side_grid_cap when set.  Returns the new (d, db)."""
         g = self._grad
         x, z, y, mean, rstd, gh, a = saved
         B, H, W, C = x.shape
@@ -491,27 +489,26 @@ class ConvNeXtHip(nn.Module):
         if w2g is None:
             w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
         dh = torch.empty(M, 4 * C, device=d.device, dtype=torch.bfloat16)
-        K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True)
+        K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True, policy=pol)
         dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
-        K.linear_dgrad(dh, w1, out=dy, compute_bf16=True)
+        K.linear_dgrad(dh, w1, out=dy, compute_bf16=True, policy=pol)
         dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
                                         db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
-        nv.value("sv_gemm_set_priority", 1)
-        side_cap = self.side_grid_cap
-        if side_cap is not None and self.comm_reserve_cus > 0:
-            side_cap = min(side_cap, _comm_cap(main.device, self.comm_reserve_cus))
-        prev_cap = nv.value("sv_gemm_set_grid_cap", side_cap) if side_cap is not None else None
+        side_cap = pol.grid_cap
+        if self.side_grid_cap is not None:
+            side_cap = min(self.side_grid_cap, side_cap) if side_cap > 0 else self.side_grid_cap
+        spol = nv.policy(grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=1)
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
-                               compute_bf16=True)
+                               compute_bf16=True, policy=spol)
             # the block's remaining folds (fc1 wgrad slab + bias, LayerNorm and depthwise weight / bias
             # partials) in ONE launch instead of four
             folds: list | None = [] if self.merge_folds else None
             K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
-                           compute_bf16=True, defer=folds)
+                           compute_bf16=True, defer=folds, policy=spol)
             ln_finish(record=False, defer=folds)
             K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias), defer=folds)
             if folds is not None:
@@ -519,9 +516,6 @@ class ConvNeXtHip(nn.Module):
             self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias, blk.mlp.fc1.weight,
                          blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
             pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a, folds)))
-        nv.value("sv_gemm_set_priority", 0)
-        if prev_cap is not None:
-            nv.value("sv_gemm_set_grid_cap", prev_cap)
         # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
         db = torch.empty_like(db)
         K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)

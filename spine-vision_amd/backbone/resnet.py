@@ -390,14 +390,15 @@ class ResNetHip(nn.Module):
             self._side[device] = torch.cuda.Stream(device=device)
         return self._side[device]
 
-    def _flush_wgrads(self, jobs: list, params: list, side, keep: list, deferred: list | None = None) -> None:
+    def _flush_wgrads(self, jobs: list, params: list, side, keep: list, deferred: list | None = None,
+                      pol: "nv.GemmPolicy | None" = None) -> None:
         """Run the block's weight gradients (conv_bwd_weight jobs) and report its parameters ready.  With a
         side stream: one hand-off (the side stream waits for everything the main stream has issued, so the
         grad-ready event it records also covers the BatchNorm gradients), and the operands stay referenced
         in ``keep`` until the streams join (the main stream's allocator may not reuse them earlier)."""
         if side is None:
             for dy4, x, s, dw in jobs:
-                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
+                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True, policy=pol)
             if deferred is not None:  # reported after the streams join (a bucket may hold side-stream grads)
                 deferred.extend(params)
             else:
@@ -410,17 +411,16 @@ class ResNetHip(nn.Module):
         cap = self.side_grid_cap
         if self.comm_reserve_cus > 0:
             cap = min(cap, max(1, ncu - self.comm_reserve_cus))
-        prev = nv.value("sv_gemm_set_grid_cap", cap)
+        spol = nv.policy(grid_cap=cap)  # the side stream's own policy, passed with each call
         with torch.cuda.stream(side):
             for dy4, x, s, dw in jobs:
-                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True)
+                K.conv_bwd_weight(dy4, x, s, dw=dw, accumulate=True, policy=spol)
             self._ready(params)
-        nv.value("sv_gemm_set_grid_cap", prev)
         keep.append(jobs)
 
     @torch.no_grad()
     def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None,
-                        batch_stats: bool = True) -> torch.Tensor:
+                        batch_stats: bool = True, pol: "nv.GemmPolicy | None" = None) -> torch.Tensor:
         """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
         block's parameter gradients and returns dL/d(block input) (f32)."""
         act = self.act_dtype
@@ -463,9 +463,9 @@ class ResNetHip(nn.Module):
             # the inner BN's backward statistics from the data gradient's GEMM epilogue / split-K finish where
             # that path carries them (stride 1, bf16), else from bn_bwd's own statistics pass
             fused = (K.conv_bwd_data_bn(dy4, wp, s, py, pmean, prstd, pbn.weight, pbn.bias,
-                                        unsplit=_BN_BWD_EPI != "split")
+                                        unsplit=_BN_BWD_EPI != "split", policy=pol)
                      if _BN_BWD_EPI != "0" and act == torch.bfloat16 else None)
-            da, bpart = fused if fused is not None else (K.conv_bwd_data(dy4, wp, s, dx_dtype=act), None)
+            da, bpart = fused if fused is not None else (K.conv_bwd_data(dy4, wp, s, dx_dtype=act, policy=pol), None)
             # the inner BN's own ReLU: mask recomputed from y (the activation pa is not read again)
             dy = K.bn_bwd(da.view(-1, Cp), py.view(-1, Cp), pmean, prstd, pbn.weight, relu_beta=pbn.bias.detach(),
                           dgamma=g(pbn.weight), dbeta=g(pbn.bias), dx_dtype=act,
@@ -483,13 +483,13 @@ class ResNetHip(nn.Module):
             jobs.append((dyd4, x_in, sd, g(dconv.weight)))
             # conv1's data gradient first (a plain store), then the strided shortcut's added onto the
             # one output parity class its 1x1 taps reach (the other three are skipped, not rewritten)
-            dx = K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx_dtype=torch.float32)
-            K.conv_bwd_data(dyd4, wpd, sd, dx=dx, accumulate=True)
+            dx = K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx_dtype=torch.float32, policy=pol)
+            K.conv_bwd_data(dyd4, wpd, sd, dx=dx, accumulate=True, policy=pol)
             params += [dconv.weight, dbn.weight, dbn.bias]
         else:
             dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
-            K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True)
-        self._flush_wgrads(jobs, params, side, keep, deferred)
+            K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True, policy=pol)
+        self._flush_wgrads(jobs, params, side, keep, deferred, pol)
         return dx
 
     @torch.no_grad()
@@ -501,7 +501,7 @@ class ResNetHip(nn.Module):
         main_cap = 0
         if self.comm_reserve_cus > 0:
             main_cap = max(1, torch.cuda.get_device_properties(main.device).multi_processor_count - self.comm_reserve_cus)
-        prev_cap = nv.value("sv_gemm_set_grid_cap", main_cap)
+        pol = nv.policy(grid_cap=main_cap)  # the main stream's GEMM policy, passed with each call
         keep: list = []
         deferred: list | None = [] if side is not None else None
         d = K.avgpool_bwd(dfeat, tape.out_shape)  # f32 gradient of the last block output
@@ -512,8 +512,7 @@ class ResNetHip(nn.Module):
             # weight gradient, which stays on the main stream as the last producer); the side queue is
             # empty by then (r4k trace), so they no longer wait behind a backlog: +0.5 % (r4s A/B)
             d = self._block_backward(blk, saved_block, d, side if (i > 0 or _FIRST_BLOCK_SIDE) else None, keep,
-                                     deferred,
-                                     batch_stats=tape.batch_stats)
+                                     deferred, batch_stats=tape.batch_stats, pol=pol)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
@@ -527,11 +526,10 @@ class ResNetHip(nn.Module):
                            dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
                            batch_stats=tape.batch_stats)
         self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
-                           [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred)
+                           [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred, pol)
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
             self._ready(deferred)
-        nv.value("sv_gemm_set_grid_cap", prev_cap)
         keep.clear()
 
 

@@ -18,6 +18,16 @@ namespace sv {
 int set_error(int code, const char* fmt, ...);
 int check_launch(const char* what);
 
+// ---- per-device facts (abi.cpp): keyed by the device of the launch's stream, cached per device under a
+// mutex -- no launch inherits another device's CU count, and the library is reentrant across devices ----
+int stream_device(hipStream_t s);   // the device a stream belongs to (the null stream: the current device)
+int device_cus(hipStream_t s);      // compute units of that device
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device) before its first launch there
+void ensure_lds_attr(const void* kernel, int bytes, hipStream_t s);
+// the grid of a persistent launch of `total` tiles under `pol` (nullable): one workgroup per tile, or
+// wg_per_cu x CUs, then at most pol->grid_cap
+int policy_grid(const sv_gemm_policy* pol, int total, int per_cu_default, hipStream_t s);
+
 #define SV_REQUIRE(cond, ...)                                                       \
   do {                                                                              \
     if (!(cond)) return ::sv::set_error(SV_ERR_INVALID_ARG, __VA_ARGS__);           \

@@ -382,14 +382,7 @@ static int launch(const Args& a, int split, hipStream_t s) {
   constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
   static_assert(lds <= 160 * 1024, "conv kernel LDS");
-  if (lds > 65536) {
-    static bool attr_set = false;  // per template instantiation
-    if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel<BF16, MODE>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_set = true;
-    }
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&conv_kernel<BF16, MODE>), (int)lds, s);
   dim3 grid(tilesM * tilesN, 1, split);
   conv_kernel<BF16, MODE><<<grid, kGemmThreads, lds, s>>>(a, tilesM, tilesN);
   return check_launch(MODE == FPROP ? "sv_conv_fwd" : MODE == DGRAD ? "sv_conv_bwd_data" : "sv_conv_bwd_weight");
@@ -606,8 +599,9 @@ static ConvG make_convg(int SH, int SW, int SC, int GH, int GW, int si) {
   return g;
 }
 static sv_gemm_desc conv_desc(const void* A, const void* B, int M, int N, int K, int b_kmajor, int64_t ldb, void* C,
-                              int c_dtype) {
+                              int c_dtype, const sv_gemm_policy* pol) {
   sv_gemm_desc d{};
+  if (pol) d.policy = *pol;
   d.M = M;
   d.N = N;
   d.K = K;
@@ -736,8 +730,8 @@ extern "C" int sv_image_u8_hwc_to_nhwc(const uint8_t* img, const float* norm_mea
 }
 
 static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                         const sv_conv_shape* s, float* stats, sv_stream_t stream, float* slab = nullptr,
-                         int split = 1) {
+                         const sv_conv_shape* s, float* stats, const sv_gemm_policy* pol, sv_stream_t stream,
+                         float* slab = nullptr, int split = 1) {
   if (int rc = check_shape(s, dtype, "sv_conv_fwd")) return rc;
   SV_REQUIRE(x && wp && y, "sv_conv_fwd: null pointer");
   SV_REQUIRE(y_dtype == SV_BF16 || y_dtype == SV_F32, "sv_conv_fwd: bad y dtype");
@@ -775,7 +769,7 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
     g.pad = s->pad;
     g.ntaps = a.ntaps;
     g.kw_mul = (65536u + (uint32_t)s->KW - 1) / (uint32_t)s->KW;
-    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, ceil_div(a.K, 32) * 32, 1, a.K, y, y_dtype);
+    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, ceil_div(a.K, 32) * 32, 1, a.K, y, y_dtype, pol);
     if (stats) {
       SV_REQUIRE(((uintptr_t)stats & 15) == 0, "sv_conv_fwd_stats: stats alignment");
       d.epilogue = SV_EPI_STORE_STATS;
@@ -791,7 +785,7 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
       g.tdy[j] = a.tdy[j];
       g.tdx[j] = a.tdx[j];
     }
-    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype);
+    sv_gemm_desc d = conv_desc(x, wp, a.M, a.N, a.K, 1, a.K, y, y_dtype, pol);
     if (slab) {
       d.epilogue = SV_EPI_SLAB;
       d.C = slab;
@@ -816,27 +810,29 @@ static int conv_fwd_impl(const void* x, const void* wp, void* y, int32_t y_dtype
 }
 
 extern "C" int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                           const sv_conv_shape* s, sv_stream_t stream) {
-  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, nullptr, stream);
+                           const sv_conv_shape* s, const sv_gemm_policy* policy, sv_stream_t stream) {
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, nullptr, policy, stream);
 }
 
 extern "C" int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                                 const sv_conv_shape* s, float* stats, sv_stream_t stream) {
+                                 const sv_conv_shape* s, float* stats, const sv_gemm_policy* policy,
+                                 sv_stream_t stream) {
   SV_REQUIRE(stats, "sv_conv_fwd_stats: null stats");
-  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream);
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, policy, stream);
 }
 
 extern "C" int sv_conv_fwd_split(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype,
-                                 const sv_conv_shape* s, float* stats, float* work, int32_t split, sv_stream_t stream) {
+                                 const sv_conv_shape* s, float* stats, float* work, int32_t split,
+                                 const sv_gemm_policy* policy, sv_stream_t stream) {
   SV_REQUIRE(work && split >= 1, "sv_conv_fwd_split: need a workspace and split >= 1");
-  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, stream, work, split);
+  return conv_fwd_impl(x, wp, y, y_dtype, dtype, s, stats, policy, stream, work, split);
 }
 
 // bn != NULL (sv_conv_bwd_data_bn): bf16 dx of the stride-1 gathered path plus the backward statistics of the
 // BatchNorm + ReLU whose output the conv read (y = that BatchNorm's input), from the epilogue or the finish
 static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                              int32_t dtype, const sv_conv_shape* s, sv_stream_t stream, float* slab, int split,
-                              const void* bny = nullptr, const sv_bn_ref* bn = nullptr, float* bnpart = nullptr) {
+                              int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* pol, sv_stream_t stream,
+                              float* slab, int split, const void* bny = nullptr, const sv_bn_ref* bn = nullptr, float* bnpart = nullptr) {
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_data")) return rc;
   SV_REQUIRE(dy && wp && dx, "sv_conv_bwd_data: null pointer");
   SV_REQUIRE(dx_dtype == SV_BF16 || dx_dtype == SV_F32, "sv_conv_bwd_data: bad dx dtype");
@@ -857,7 +853,8 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
         g.tdx[kh * s->KW + kw] = (int8_t)(s->pad - kw);
         g.twt[kh * s->KW + kw] = (uint8_t)(kh * s->KW + kw);
       }
-    sv_gemm_desc d = conv_desc(dy, wp, s->B * s->H * s->W, s->Cs, T_ * s->Cout, 0, (int64_t)T_ * s->Cs, dx, dx_dtype);
+    sv_gemm_desc d =
+        conv_desc(dy, wp, s->B * s->H * s->W, s->Cs, T_ * s->Cout, 0, (int64_t)T_ * s->Cs, dx, dx_dtype, pol);
     if (slab) {
       d.epilogue = SV_EPI_SLAB;
       d.C = slab;
@@ -920,7 +917,7 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
         cs.GW[cls] = GW;
         cs.base[cls] = g.ctaps[cls] ? slab + (size_t)cls * M * s->Cs : nullptr;
       }
-      sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, slab, SV_F32);
+      sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, slab, SV_F32, pol);
       d.epilogue = SV_EPI_SLAB;
       if (int rc = launch_gemm3_conv(&d, g, 5, (hipStream_t)stream)) return rc;
     } else {
@@ -952,7 +949,7 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
           }
           if (nt == 0) continue;
           const int M = s->B * GH * GW;
-          sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, nt * s->Cout, 0, (int64_t)T_ * s->Cs, next, SV_F32);
+          sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, nt * s->Cout, 0, (int64_t)T_ * s->Cs, next, SV_F32, pol);
           d.epilogue = SV_EPI_SLAB;
           d.split_k = split;
           if (int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream)) return rc;
@@ -1018,27 +1015,29 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
 }
 
 extern "C" int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
-                                int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
-  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, nullptr, 1);
+                                int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* policy,
+                                sv_stream_t stream) {
+  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, policy, stream, nullptr, 1);
 }
 
 extern "C" int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
                                       int32_t dtype, const sv_conv_shape* s, float* work, int32_t split,
-                                      sv_stream_t stream) {
+                                      const sv_gemm_policy* policy, sv_stream_t stream) {
   SV_REQUIRE(work && split >= 1, "sv_conv_bwd_data_split: need a workspace and split >= 1");
-  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, stream, work, split);
+  return conv_bwd_data_impl(dy, wp, dx, dx_dtype, accumulate, dtype, s, policy, stream, work, split);
 }
 
 extern "C" int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int32_t dtype, const sv_conv_shape* s,
                                    const void* y, const sv_bn_ref* bn, float* part, float* work, int32_t split,
-                                   sv_stream_t stream) {
+                                   const sv_gemm_policy* policy, sv_stream_t stream) {
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_data_bn")) return rc;
   SV_REQUIRE(y && bn && part && bn->mean && bn->rstd && bn->gamma && bn->beta && split >= 1 && (split == 1 || work),
              "sv_conv_bwd_data_bn: null pointer / split > 1 without a workspace");
   SV_REQUIRE(dtype == SV_BF16 && s->stride == 1 && s->Cout >= 32 && pow2(s->Cout) && s->Cs % 8 == 0 &&
                  ((int64_t)s->KH * s->KW * s->Cout) % 32 == 0,
              "sv_conv_bwd_data_bn: only the bf16 stride-1 gathered path (Cout >= 32, power of two; Cs %% 8 == 0)");
-  return conv_bwd_data_impl(dy, wp, dx, SV_BF16, 0, dtype, s, stream, split > 1 ? work : nullptr, split, y, bn, part);
+  return conv_bwd_data_impl(dy, wp, dx, SV_BF16, 0, dtype, s, policy, stream, split > 1 ? work : nullptr, split, y, bn,
+                            part);
 }
 
 // the transposed wgrad (mode 4: taps*channels on the 256-row side, Cout on the 128-column side) when
@@ -1084,7 +1083,9 @@ extern "C" int64_t sv_conv_bwd_weight_work_floats(const sv_conv_shape* s) {
 }
 
 extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, float* dw, int32_t accumulate,
-                                  int32_t dtype, const sv_conv_shape* s, sv_stream_t stream) {
+                                  int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* policy,
+                                  sv_stream_t stream) {
+  const sv_gemm_policy* pol = policy;
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_weight")) return rc;
   SV_REQUIRE(dy && x && work && dw, "sv_conv_bwd_weight: null pointer");
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
@@ -1101,8 +1102,8 @@ extern "C" int sv_conv_bwd_weight(const void* dy, const void* x, float* work, fl
         g.tdx[kh * s->KW + kw] = (int8_t)(kw - s->pad);
       }
     const bool tr = wgrad_transposed(s);
-    sv_gemm_desc d = tr ? conv_desc(x, dy, T_ * s->Cs, s->Cout, (int)npix, 0, s->Cout, work, SV_F32)
-                        : conv_desc(dy, x, s->Cout, T_ * s->Cs, (int)npix, 0, T_ * s->Cs, work, SV_F32);
+    sv_gemm_desc d = tr ? conv_desc(x, dy, T_ * s->Cs, s->Cout, (int)npix, 0, s->Cout, work, SV_F32, pol)
+                        : conv_desc(dy, x, s->Cout, T_ * s->Cs, (int)npix, 0, T_ * s->Cs, work, SV_F32, pol);
     d.a_kmajor = 0;
     d.lda = tr ? T_ * s->Cs : s->Cout;
     d.epilogue = SV_EPI_SLAB;

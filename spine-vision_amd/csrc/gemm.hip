@@ -264,14 +264,7 @@ static int launch(const sv_gemm_desc* d, hipStream_t s) {
   constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
   dim3 grid(tilesM * tilesN, 1, split);
-  if (lds > 65536) {
-    static bool attr_set = false;  // per template instantiation
-    if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BF16, TA, TB, AK, BKM>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_set = true;
-    }
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&gemm_kernel<BF16, TA, TB, AK, BKM>), (int)lds, s);
   gemm_kernel<BF16, TA, TB, AK, BKM><<<grid, kGemmThreads, lds, s>>>(
       reinterpret_cast<const TA*>(d->A), d->lda, reinterpret_cast<const TB*>(d->B), d->ldb, d->a_scale_k, d->K,
       kper, tilesM, tilesN, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);
@@ -292,43 +285,16 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace sv;
 
-namespace sv {
-int g_gemm_wg_per_cu = 0;  // sv_gemm_set_workgroups_per_cu
-int g_gemm_prio = 0;       // sv_gemm_set_priority
-int g_gemm_grid_cap = 0;   // sv_gemm_set_grid_cap
-}
-
-static int g_gemm_impl = 0;  // sv_gemm_set_impl: 0 = measured per-shape dispatch, 2/3/8 = force a family
-
-extern "C" int sv_gemm_set_impl(int32_t impl) {
-  const int prev = g_gemm_impl;
-  g_gemm_impl = impl;
-  return prev;
-}
-
-extern "C" int sv_gemm_set_priority(int32_t p) {
-  const int prev = g_gemm_prio;
-  g_gemm_prio = p ? 1 : 0;
-  return prev;
-}
-
-extern "C" int sv_gemm_set_grid_cap(int32_t n) {
-  const int prev = g_gemm_grid_cap;
-  g_gemm_grid_cap = n < 0 ? 0 : n;
-  return prev;
-}
-
-extern "C" int sv_gemm_set_workgroups_per_cu(int32_t n) {
-  const int prev = g_gemm_wg_per_cu;
-  g_gemm_wg_per_cu = n < 0 ? 0 : (n > 2 ? 2 : n);
-  return prev;
-}
-
 extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
   SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_STORE_BN_BWD, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->policy.impl == 0 || d->policy.impl == 2 || d->policy.impl == 3 || d->policy.impl == 8 || d->policy.impl == 9,
+             "sv_gemm: policy.impl must be 0, 2, 3, 8 or 9 (got %d)", d->policy.impl);
+  SV_REQUIRE(d->policy.grid_cap >= 0 && d->policy.wg_per_cu >= 0 && d->policy.wg_per_cu <= 2 &&
+                 (d->policy.priority == 0 || d->policy.priority == 1),
+             "sv_gemm: bad policy (grid_cap >= 0, wg_per_cu 0..2, priority 0/1)");
   if (d->M == 0 || d->N == 0) return SV_OK;
   const bool bf = d->compute == SV_BF16;
   SV_REQUIRE(bf || d->compute == SV_F32, "sv_gemm: bad compute type");
@@ -361,7 +327,8 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!bf) return launch_layout<false, float, float>(d, s);
   // bf16 operands: the LDS-DMA pipelined v2 kernel when the shape fits its contract (K % 64 == 0)
-  const int impl = g_gemm_impl;
+  const int impl = d->policy.impl;
+  const int wpc = d->policy.wg_per_cu;
   if (d->epilogue == SV_EPI_STORE_BN_BWD) {  // the v3 kernels carry the BatchNorm-backward epilogue
     const int rc = launch_gemm3(d, s);
     SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_BN_BWD needs K %% 32 == 0, bf16 operands, k-major A, m-major B");
@@ -406,13 +373,13 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     int rc = SV_ERR_UNSUPPORTED;
     if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below
     if (rc != SV_ERR_UNSUPPORTED) return rc;
-    if ((impl == 0 || impl == 9) && !g_gemm_wg_per_cu && v8_shape) rc = launch_gemm8(d, s);
+    if ((impl == 0 || impl == 9) && !wpc && v8_shape) rc = launch_gemm8(d, s);
     else if (impl == 8) rc = launch_gemm8(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);
     else if (impl == 3) rc = launch_gemm3(d, s);
-    else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, g_gemm_wg_per_cu ? "32x3" : "32x4");
+    else if (d->epilogue == SV_EPI_SLAB) rc = launch_gemm3(d, s, wpc ? "32x3" : "32x4");
     else if (heavy_epi || (d->epilogue == SV_EPI_STORE && d->K <= 2048)) rc = launch_gemm3(d, s);
-    else if (g_gemm_wg_per_cu) rc = launch_gemm3(d, s);  // v2's 144 KiB would not share a CU
+    else if (wpc) rc = launch_gemm3(d, s);  // v2's 144 KiB would not share a CU
     else rc = launch_gemm2(d, s);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }

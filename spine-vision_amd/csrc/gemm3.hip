@@ -22,9 +22,6 @@
 #include <string.h>
 
 namespace sv {
-extern int g_gemm_wg_per_cu;
-extern int g_gemm_grid_cap;
-extern int g_gemm_prio;
 namespace g3 {
 
 constexpr int BM = 256, BN = 128, THREADS = 512, NW = 8;
@@ -427,16 +424,6 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
 template <bool AK, bool BKM, int EPI, int BKT, int S, int CONV = 0>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* cg = nullptr) {
   using C = Cfg<BKT, S>;
@@ -449,27 +436,18 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  e.prio = g_gemm_prio;
+  e.prio = d->policy.priority;
   if (EPI == SV_EPI_STORE_BN_BWD) {
     e.bn_mu = d->bn->mean;
     e.bn_rs = d->bn->rstd;
     e.bn_be = d->bn->beta;
     e.gamma = d->bn->gamma;
   }
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-    attr_set = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>), (int)C::LDS, s);
   // one workgroup per tile, which lets kernels of the side stream take CUs as tiles retire
   const int total = tilesM * tilesN * split;
-  int grid = total;
-  if (g_gemm_wg_per_cu > 0) {  // co-residency with a concurrent GEMM (sv_gemm_set_workgroups_per_cu)
-    const int slots = g_gemm_wg_per_cu * num_cus();
-    grid = total > slots ? slots : total;
-  }
-  if (g_gemm_grid_cap > 0 && grid > g_gemm_grid_cap) grid = g_gemm_grid_cap;  // persistent over the rest
+  // (policy.wg_per_cu: co-residency with a concurrent GEMM; policy.grid_cap: persistent over the rest)
+  const int grid = policy_grid(&d->policy, total, 0, s);
   gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
       tilesM, tilesN, split, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,

@@ -25,7 +25,6 @@
 #include <stdlib.h>
 
 namespace sv {
-extern int g_gemm_grid_cap;
 namespace g9 {
 
 #ifdef SV_CLOCK_STAMPS
@@ -645,16 +644,6 @@ constexpr int lds_total() {
                                    EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS)) ? 4096 : 0);
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
 template <bool AK, bool BKM, int EPI, bool P8>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int nk = d->K / split / BK;
@@ -672,16 +661,9 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   x.aux = d->aux ? (uint32_t)(((size_t)(d->M - 1) * d->ld_aux + d->N) * (d->aux_dtype == SV_F32 ? 4 : 2)) : 0u;
   x.a = (uint32_t)((AK ? (size_t)(d->M - 1) * d->lda + d->K : (size_t)(d->K - 1) * d->lda + d->M) * 2);
   x.b = (uint32_t)((BKM ? (size_t)(d->N - 1) * d->ldb + d->K : (size_t)(d->K - 1) * d->ldb + d->N) * 2);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_total<AK, EPI>());
-    attr_set = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8>), lds_total<AK, EPI>(), s);
   const int total = tilesM * tilesN * split;
-  int grid = num_cus();
-  if (g_gemm_grid_cap > 0 && grid > g_gemm_grid_cap) grid = g_gemm_grid_cap;
-  if (grid > total) grid = total;
+  const int grid = policy_grid(&d->policy, total, 1, s);  // persistent: one workgroup per CU (or the cap)
   gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_total<AK, EPI>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
                                                                   reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
                                                                   tilesM, tilesN, split, e, x);

@@ -122,8 +122,10 @@ def gemm(
     split_k: int = 1,
     compute_bf16: bool = True,
     bn: "nv.BnRef | None" = None,
+    policy: "nv.GemmPolicy | None" = None,
 ) -> torch.Tensor:
-    """C = epilogue(A(m,k) . B(k,n)); see sv_gemm in include/sv_kernels.h for the layouts."""
+    """C = epilogue(A(m,k) . B(k,n)); see sv_gemm in include/sv_kernels.h for the layouts.  ``policy``: the
+    launch policy of this call (nv.policy(...): kernel family, grid cap, residency, priority); None = defaults."""
     _check(C is not None, "gemm: output tensor C is required")
     need_a = (M - 1) * lda + K if a_kmajor else (K - 1) * lda + M
     need_b = (N - 1) * ldb + K if b_kmajor else (K - 1) * ldb + N
@@ -153,6 +155,8 @@ def gemm(
     d.compute = _cdt(compute_bf16)
     if bn is not None:
         d.bn = ctypes.pointer(bn)
+    if policy is not None:
+        d.policy = policy
     probes = [p_ for p_ in (PROBES + ([PROBE] if PROBE is not None else [])) if p_.matches(a_kmajor, b_kmajor,
                                                                                       compute_bf16, epilogue)]
     if probes:
@@ -184,20 +188,20 @@ def gemm(
 
 
 def linear_fwd(x2d, w, *, out, bias=None, epilogue=nv.SV_EPI_STORE, out2=None, gamma=None, residual=None,
-               compute_bf16=True):
+               compute_bf16=True, policy=None):
     """out[M,N] = epilogue(x2d[M,K] @ w[N,K]^T)  (torch Linear weight layout)."""
     M, K = x2d.shape
     N = w.shape[0]
     return gemm(x2d, w, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=K, ldb=K, epilogue=epilogue, C=out,
-                C2=out2, bias=bias, gamma=gamma, aux=residual, compute_bf16=compute_bf16)
+                C2=out2, bias=bias, gamma=gamma, aux=residual, compute_bf16=compute_bf16, policy=policy)
 
 
-def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=None, compute_bf16=True):
+def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=None, compute_bf16=True, policy=None):
     """out[M,K] = epilogue((dy2d[M,N] * a_scale_k[N]) @ w[N,K])."""
     M, N = dy2d.shape
     K = w.shape[1]
     return gemm(dy2d, w, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=N, ldb=K, epilogue=epilogue, C=out,
-                a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16)
+                a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16, policy=policy)
 
 
 _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
@@ -227,7 +231,7 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
 
 
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
-                 compute_bf16=True, cols=None, defer: list | None = None) -> torch.Tensor:
+                 compute_bf16=True, cols=None, defer: list | None = None, policy=None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
     writes -- or, with ``accumulate``, adds -- into ``out``).  With ``bias_out`` the column sums of
     dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum).  ``cols``: use only the
@@ -240,7 +244,7 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
     gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
-         C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
+         C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy)
     if out is None:
         if split == 1 and not accumulate:
             if cs is not None:
@@ -263,7 +267,7 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     return out
 
 
-def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf16=True):
+def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf16=True, policy=None):
     """fc2 weight / bias / layer-scale gradients of out = x + gamma * (a W2^T + b2) from d_out:
     dW2 += gamma (.) d^T a, dgamma += rowdot(W2, d^T a) + b2 (.) colsum(d), db2 += gamma (.) colsum(d).
     The wgrad GEMM writes split-K slabs (+ colsum partials); ONE fused pass (a workgroup per row)
@@ -275,7 +279,7 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     slab = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.float32)
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
     gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
-         C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16)
+         C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy)
     _timed_call("fold", 4.0 * ((split + 2) * C * K4 + (split + 4) * C),
                 "sv_layerscale_wgrad_reduce", ptr(slab), ptr(cs), split, ptr(w2), ptr(gamma), ptr(b2), ptr(dw2),
                 ptr(dgamma), ptr(db2), None, C, K4)
@@ -758,37 +762,40 @@ def _slab_finish(work: torch.Tensor, split: int, M: int, N: int, C: torch.Tensor
                 N, ptr(C), dt(C), N, int(accumulate), ptr(stats))
 
 
-def _pointwise_fwd(x, wp, s, y, M, stats=None):
+def _pointwise_fwd(x, wp, s, y, M, stats=None, policy=None):
     """1x1 conv forward as a GEMM over [M, Cs] rows; split-K + slab finish when the grid is small."""
     split = _conv_split(M, s.Cout, s.Cs)
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
         gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
-             ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+             ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True, policy=policy)
         _slab_finish(work, split, M, s.Cout, y, stats=stats)
     elif stats is not None:
         gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
-             ldb=s.Cs, C=y.view(M, s.Cout), C2=stats, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True)
+             ldb=s.Cs, C=y.view(M, s.Cout), C2=stats, epilogue=nv.SV_EPI_STORE_STATS, compute_bf16=True,
+             policy=policy)
     else:
         gemm(x.view(M, s.Cs), wp.view(s.Cout, s.Cs), M=M, N=s.Cout, K=s.Cs, a_kmajor=True, b_kmajor=True, lda=s.Cs,
-             ldb=s.Cs, C=y.view(M, s.Cout), compute_bf16=True)
+             ldb=s.Cs, C=y.view(M, s.Cout), compute_bf16=True, policy=policy)
 
 
-def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype) -> torch.Tensor:
+def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype,
+             policy: "nv.GemmPolicy | None" = None) -> torch.Tensor:
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
     if _pointwise(s, wp.dtype):
-        _pointwise_fwd(x, wp, s, y, s.B * s.H * s.W)
+        _pointwise_fwd(x, wp, s, y, s.B * s.H * s.W, policy=policy)
         return y
     M, K = s.B * OH * OW, s.KH * s.KW * s.Cs
     split = _conv_split(M, s.Cout, K) if _gathered(s, wp.dtype) else 1
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
-        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), None, ptr(work), split)
+        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), None, ptr(work), split,
+             nv.pol_ref(policy))
         return y
-    call("sv_conv_fwd", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s))
+    call("sv_conv_fwd", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), nv.pol_ref(policy))
     return y
 
 
@@ -804,24 +811,25 @@ def _ones(n: int, device: torch.device) -> torch.Tensor:
     return t
 
 
-def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype):
+def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torch.dtype,
+                      policy: "nv.GemmPolicy | None" = None):
     """conv_fwd plus the train-mode BatchNorm statistics of y straight from the GEMM epilogue
     (SV_EPI_STORE_STATS: no separate read pass over y) -> (y, partials [ceil(M/64)][2][Cout] f32), or
     (y, None) when the conv runs on a path without that epilogue (then use bn_stats(y))."""
     if wp.dtype != torch.bfloat16 or out_dtype != torch.bfloat16 or s.Cout % 8:
-        return conv_fwd(x, wp, s, out_dtype), None
+        return conv_fwd(x, wp, s, out_dtype, policy), None
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     M = s.B * OH * OW
     if _pointwise(s, wp.dtype):
         if s.Cs % 32:
-            return conv_fwd(x, wp, s, out_dtype), None
+            return conv_fwd(x, wp, s, out_dtype, policy), None
         _conv_check_x(x, s, wp.dtype, "conv_fwd")
         y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
         part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
-        _pointwise_fwd(x, wp, s, y, M, stats=part)
+        _pointwise_fwd(x, wp, s, y, M, stats=part, policy=policy)
         return y, part
     if not (_gathered(s, wp.dtype) or _stem8(s, wp.dtype)):
-        return conv_fwd(x, wp, s, out_dtype), None
+        return conv_fwd(x, wp, s, out_dtype, policy), None
     _conv_check_x(x, s, wp.dtype, "conv_fwd")
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
@@ -829,9 +837,10 @@ def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dt
     split = 1 if _stem8(s, wp.dtype) else _conv_split(M, s.Cout, s.KH * s.KW * s.Cs)
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
-        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), ptr(work), split)
+        call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), ptr(work), split,
+             nv.pol_ref(policy))
     else:
-        call("sv_conv_fwd_stats", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part))
+        call("sv_conv_fwd_stats", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), nv.pol_ref(policy))
     return y, part
 
 
@@ -848,7 +857,8 @@ def bn_stats_from_partials(part: torch.Tensor, rows: int, *, eps: float = EPS_BN
 
 
 def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: torch.Tensor | None = None,
-                  accumulate: bool = False, dx_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+                  accumulate: bool = False, dx_dtype: torch.dtype = torch.float32,
+                  policy: "nv.GemmPolicy | None" = None) -> torch.Tensor:
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout) and dy.dtype == wp.dtype,
            "conv_bwd_data: dy must be contiguous [B,OH,OW,Cout] in the compute dtype")
@@ -863,16 +873,16 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
         if split > 1:
             work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
-                 lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+                 lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True, policy=policy)
             _slab_finish(work, split, M, s.Cs, dx, accumulate=accumulate)
         elif accumulate:  # dx += dy W: the layer-scale/residual epilogue with gamma = 1, residual = dx (in place)
             ones = _ones(s.Cs, dy.device)
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
                  lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), epilogue=nv.SV_EPI_BIAS_GAMMA_RES, gamma=ones,
-                 aux=dx.view(M, s.Cs), compute_bf16=True)
+                 aux=dx.view(M, s.Cs), compute_bf16=True, policy=policy)
         else:
             gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
-                 lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), compute_bf16=True)
+                 lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), compute_bf16=True, policy=policy)
         return dx
     T = s.KH * s.KW
     if (wp.dtype == torch.bfloat16 and s.stride == 1 and s.Cout >= 32 and s.Cs % 8 == 0
@@ -882,7 +892,7 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
         if split > 1:
             work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
             call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
-                 ctypes.byref(s), ptr(work), split)
+                 ctypes.byref(s), ptr(work), split, nv.pol_ref(policy))
             return dx
     if wp.dtype == torch.bfloat16 and s.stride == 2 and s.Cout >= 32 and s.Cs % 8 == 0:
         # stride 2: one gathered GEMM per output parity class into compact f32 slabs + one scatter pass
@@ -891,9 +901,10 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
         split = _conv_split(M // 4, s.Cs, max(32, (T * s.Cout) // 4))
         work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
         call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
-             ctypes.byref(s), ptr(work), split)
+             ctypes.byref(s), ptr(work), split, nv.pol_ref(policy))
         return dx
-    call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s))
+    call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s),
+         nv.pol_ref(policy))
     return dx
 
 
@@ -902,7 +913,8 @@ def _al16(*ts) -> bool:
 
 
 def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: torch.Tensor, mean: torch.Tensor,
-                     rstd: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, *, unsplit: bool = True):
+                     rstd: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, *, unsplit: bool = True,
+                     policy: "nv.GemmPolicy | None" = None):
     """conv_bwd_data (bf16 dx, no accumulate) fused with the backward statistics of the BatchNorm + ReLU that
     produced the conv's input: y [B,H,W,Cs] is that BatchNorm's input (bf16), mean / rstd its batch statistics,
     gamma / beta its affine parameters.  -> (dx, part), part = f32 [ceil(B*H*W/64)][2][Cs] partial sums of g
@@ -936,20 +948,20 @@ def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: tor
     work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32) if split > 1 else None
     if pw and split > 1:
         gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
-             lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True)
+             lda=s.Cout, ldb=s.Cs, C=work, epilogue=nv.SV_EPI_SLAB, split_k=split, compute_bf16=True, policy=policy)
         call("sv_gemm_slab_finish_bn_bwd", ptr(work), split, M, s.Cs, ptr(dx), ptr(y), ctypes.byref(ref), ptr(part))
     elif pw:
         gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,
              lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), C2=part, epilogue=nv.SV_EPI_STORE_BN_BWD,
-             aux=y.view(M, s.Cs), compute_bf16=True, bn=ref)
+             aux=y.view(M, s.Cs), compute_bf16=True, bn=ref, policy=policy)
     else:
         call("sv_conv_bwd_data_bn", ptr(dy), ptr(wp), ptr(dx), dt(wp), ctypes.byref(s), ptr(y), ctypes.byref(ref),
-             ptr(part), ptr(work), split)
+             ptr(part), ptr(work), split, nv.pol_ref(policy))
     return dx, part
 
 
 def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: torch.Tensor,
-                    accumulate: bool = True) -> torch.Tensor:
+                    accumulate: bool = True, policy: "nv.GemmPolicy | None" = None) -> torch.Tensor:
     OH, OW = conv_out_hw(s.H, s.W, s.KH, s.stride, s.pad)
     _conv_check_x(x, s, dy.dtype, "conv_bwd_weight")
     _check(dy.is_contiguous() and tuple(dy.shape) == (s.B, OH, OW, s.Cout), "conv_bwd_weight: dy shape")
@@ -958,11 +970,12 @@ def conv_bwd_weight(dy: torch.Tensor, x: torch.Tensor, s: nv.ConvShape, *, dw: t
     if _pointwise(s, dy.dtype):
         M = s.B * s.H * s.W
         linear_wgrad(dy.view(M, s.Cout), x.view(M, s.Cs), out=dw.view(s.Cout, s.Cs), accumulate=accumulate,
-                     compute_bf16=True)
+                     compute_bf16=True, policy=policy)
         return dw
     nwork = value("sv_conv_bwd_weight_work_floats", ctypes.byref(s))
     work = torch.empty(nwork, device=dy.device, dtype=torch.float32)
-    call("sv_conv_bwd_weight", ptr(dy), ptr(x), ptr(work), ptr(dw), int(accumulate), dt(dy), ctypes.byref(s))
+    call("sv_conv_bwd_weight", ptr(dy), ptr(x), ptr(work), ptr(dw), int(accumulate), dt(dy), ctypes.byref(s),
+         nv.pol_ref(policy))
     return dw
 
 

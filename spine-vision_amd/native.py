@@ -34,6 +34,20 @@ class BnRef(ctypes.Structure):
     _fields_ = [("mean", _p), ("rstd", _p), ("gamma", _p), ("beta", _p)]
 
 
+class GemmPolicy(ctypes.Structure):
+    """sv_gemm_policy (include/sv_kernels.h): the launch policy of ONE GEMM / convolution call (no process-wide
+    GEMM state).  All zero = the measured per-shape dispatch on every CU."""
+    _fields_ = [("impl", _i32), ("grid_cap", _i32), ("wg_per_cu", _i32), ("priority", _i32)]
+
+    def __repr__(self) -> str:
+        return (f"GemmPolicy(impl={self.impl}, grid_cap={self.grid_cap}, wg_per_cu={self.wg_per_cu}, "
+                f"priority={self.priority})")
+
+
+def policy(impl: int = 0, grid_cap: int = 0, wg_per_cu: int = 0, priority: int = 0) -> GemmPolicy:
+    return GemmPolicy(int(impl), int(grid_cap or 0), int(wg_per_cu), int(priority))
+
+
 class GemmDesc(ctypes.Structure):
     _fields_ = [
         ("M", _i32), ("N", _i32), ("K", _i32),
@@ -49,6 +63,7 @@ class GemmDesc(ctypes.Structure):
         ("split_k", _i32),
         ("compute", _i32),
         ("bn", ctypes.POINTER(BnRef)),
+        ("policy", GemmPolicy),
     ]
 
 
@@ -74,6 +89,7 @@ class ConvShape(ctypes.Structure):
 
 
 _CS = ctypes.POINTER(ConvShape)
+_POL = ctypes.POINTER(GemmPolicy)
 
 # name -> argtypes (restype is int for all entry points unless listed in _RESTYPES)
 _SIGS = {
@@ -81,10 +97,6 @@ _SIGS = {
     "sv_last_error_string": [],
     "sv_build_target": [],
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
-    "sv_gemm_set_workgroups_per_cu": [_i32],
-    "sv_gemm_set_grid_cap": [_i32],
-    "sv_gemm_set_impl": [_i32],
-    "sv_gemm_set_priority": [_i32],
     "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
     "sv_gemm_slab_finish_bn_bwd": [_p, _i32, _i32, _i32, _p, _p, ctypes.POINTER(BnRef), _p, _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
@@ -125,14 +137,14 @@ _SIGS = {
     # ResNet
     "sv_conv_weight_pack": [_p, _p, _i32, _CS, _p],
     "sv_conv_weight_pack_multi": [ctypes.POINTER(PackSeg), _i32, _i32, _p],
-    "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _p],
-    "sv_conv_fwd_stats": [_p, _p, _p, _i32, _i32, _CS, _p, _p],
-    "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _p],
-    "sv_conv_fwd_split": [_p, _p, _p, _i32, _i32, _CS, _p, _p, _i32, _p],
-    "sv_conv_bwd_data_split": [_p, _p, _p, _i32, _i32, _i32, _CS, _p, _i32, _p],
-    "sv_conv_bwd_data_bn": [_p, _p, _p, _i32, _CS, _p, ctypes.POINTER(BnRef), _p, _p, _i32, _p],
+    "sv_conv_fwd": [_p, _p, _p, _i32, _i32, _CS, _POL, _p],
+    "sv_conv_fwd_stats": [_p, _p, _p, _i32, _i32, _CS, _p, _POL, _p],
+    "sv_conv_bwd_data": [_p, _p, _p, _i32, _i32, _i32, _CS, _POL, _p],
+    "sv_conv_fwd_split": [_p, _p, _p, _i32, _i32, _CS, _p, _p, _i32, _POL, _p],
+    "sv_conv_bwd_data_split": [_p, _p, _p, _i32, _i32, _i32, _CS, _p, _i32, _POL, _p],
+    "sv_conv_bwd_data_bn": [_p, _p, _p, _i32, _CS, _p, ctypes.POINTER(BnRef), _p, _p, _i32, _POL, _p],
     "sv_conv_bwd_weight_work_floats": [_CS],
-    "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _p],
+    "sv_conv_bwd_weight": [_p, _p, _p, _p, _i32, _i32, _CS, _POL, _p],
     "sv_image_to_nhwc": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_image_u8_hwc_to_nhwc": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_bn_nparts": [_i64, _i32],
@@ -159,9 +171,7 @@ _SIGS = {
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
-                                                                     "sv_gemm_set_workgroups_per_cu", "sv_gemm_set_impl",
-                                                                     "sv_gemm_set_priority", "sv_gemm_set_grid_cap"}
+_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats"}
 
 _lib = None
 _lock = threading.Lock()
@@ -224,6 +234,11 @@ def call(name: str, *args):
 
 def value(name: str, *args) -> int:
     return getattr(lib(), name)(*args)
+
+
+def pol_ref(p: GemmPolicy | None):
+    """ctypes argument for a nullable ``const sv_gemm_policy*`` (None -> NULL = the defaults)."""
+    return None if p is None else ctypes.byref(p)
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

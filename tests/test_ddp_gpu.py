@@ -26,11 +26,11 @@ def _batch():
     return img, coords, torch.ones_like(mask)
 
 
-def _model(dev):
+def _model(dev, precision="fp32"):
     from oracle import weights as ow
     from spine_vision_amd.training import CoordinateRegressor
 
-    m = CoordinateRegressor("convnext_base", pretrained=False, dropout=0.0, precision="fp32")
+    m = CoordinateRegressor("convnext_base", pretrained=False, dropout=0.0, precision=precision)
     ow.fill_module(m)
     return m.to(dev).train()
 
@@ -221,3 +221,89 @@ def test_two_rank_resnet_graph_forward(dev):
     assert torch.equal(g0[1], g1[1]) and torch.equal(e0[1], e1[1])  # replicas in sync
     assert g0[0] == e0[0] and g1[0] == e1[0]  # per-rank losses: graph == eager
     assert torch.equal(g0[1], e0[1])
+
+
+# the bf16 data-parallel ConvNeXt path: 512x512, 4 images per rank, so the backward's GEMM
+# grids exceed the 224 CUs the comm reserve leaves them (S1 fc1: 512 tiles) and the cap is exercised
+B16, S16 = 4, 512
+
+
+def _bf16_batch():
+    from oracle import weights as ow
+
+    img, coords, mask = ow.localization_batch(2 * B16, S16, S16)
+    return img, coords, torch.ones_like(mask)
+
+
+def _bf16_rank(rank, world, port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    import torch.distributed as dist
+
+    from spine_vision_amd.training import StepEngine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.pop("SV_COMM_RESERVE_CUS", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    m = _model(dev, "bf16")
+    if rank == 1:  # the broadcast must overwrite a diverged replica
+        with torch.no_grad():
+            m.backbone.stages[2].blocks[5].mlp.fc1.bias.add_(1.0)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=16.0)
+    bb = m.backbone
+    setup = (bb.comm_reserve_cus, bb.lean_sync, bb.overlap_wgrad, bb.precision)
+    img, coords, mask = _bf16_batch()
+    sl = slice(rank * B16, (rank + 1) * B16)
+    loss = eng.step_localization(img[sl].to(dev), coords[sl].to(dev), mask[sl].to(dev))
+    torch.cuda.synchronize()
+    out[rank] = (float(loss), eng.arena.grad_flat.cpu().clone(), eng.arena.param_flat.cpu().clone(),
+                 len(eng.bucketer.buckets), setup)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_bf16_lean_step_equals_half_batch_average(dev):
+    """Two ranks (gloo, the box's one GPU) run the bf16 ConvNeXt-base step exactly as StepEngine sets it up under
+    data parallelism: the lean side-stream backward with per-block grad-ready events launching the bucketed
+    all-reduce, every backward GEMM grid capped by the 32-CU comm reserve.  The replicas end bit-identical, and
+    the all-reduced gradient equals, bit for bit, the average of two single-process half-batch gradients
+    ((g0 + g1) / 2 in f32: a 2-rank SUM is order-free and the halving exact).  Reference: accelerate DDP
+    (spine_vision/training/trainers/base.py:253-266), LocalizationTrainer._train_step (localization.py:186-209)."""
+    from spine_vision_amd.training import StepEngine
+
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_bf16_rank, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=500)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    (l0, g0, p0, nb, setup0), (l1, g1, p1, _, setup1) = out[0], out[1]
+    assert setup0 == setup1 == (32, True, True, "bf16"), setup0
+    assert nb > 1
+    assert torch.equal(g0, g1) and torch.equal(p0, p1)
+    img, coords, mask = _bf16_batch()
+    halves = []
+    for r in range(2):
+        m = _model(dev, "bf16")
+        eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=False)
+        sl = slice(r * B16, (r + 1) * B16)
+        lr_ = float(eng.step_localization(img[sl].to(dev), coords[sl].to(dev), mask[sl].to(dev)))
+        torch.cuda.synchronize()
+        assert lr_ == (l0, l1)[r]  # each rank's loss is its half-batch loss
+        halves.append(eng.arena.grad_flat.cpu().clone())
+        del eng, m
+    avg = (halves[0] + halves[1]) / 2
+    diff = (g0 - avg).abs().max()
+    print(f"[ddp] bf16 world 2: {nb} buckets, max |allreduced - half-batch average| = {float(diff):.3e}")
+    assert torch.equal(g0, avg)

@@ -1,8 +1,16 @@
-"""GPU: every bf16 GEMM family forced through sv_gemm_set_impl (2 = gemm2.hip BK64x3, 3 = gemm3.hip
-BK32x3, 8 = gemm8.hip 256x256, 9 = gemm9.hip persistent 256x256 BK64) against the measured per-shape dispatch (impl 0), on every operand
-layout and epilogue the ConvNeXt step uses, ragged M/N included -- the knob is tested, not dormant.
-Every family accumulates each 16x16 output fragment over k in the same order with the same MFMA, so the
-outputs must be BIT-identical; a torch fp32 product on the same bf16 operands checks the values."""
+"""GPU: every bf16 GEMM family forced through the per-call policy (sv_gemm_policy.impl: 2 = gemm2.hip BK64x3,
+3 = gemm3.hip BK32x3, 8 = gemm8.hip 256x256, 9 = gemm9.hip persistent 256x256 BK64) against the measured
+per-shape dispatch (impl 0), on every operand layout and epilogue the ConvNeXt step uses, ragged M/N included
+-- the knob is tested, not dormant.  Every family accumulates each 16x16 output fragment over k in the same
+order with the same MFMA, so the outputs must be BIT-identical; a torch fp32 product on the same bf16 operands
+checks the values.
+
+The bs32 cases run the production schedule the bench times: at ConvNeXt-base 512x512
+bs32 the persistent v9 kernel processes SEVERAL 256x256 tiles per workgroup (S1 fc1: 4096 tiles on 256 CUs),
+with the fused GELU-dual, gamma-residual and x GELU' epilogues keeping stores and operand loads in flight
+across tiles; they are checked bit for bit against v3 (one workgroup per tile) and against torch fp32, under
+the forward's default policy and the backward's (one persistent workgroup per CU, raised priority, the
+data-parallel grid cap)."""
 
 import pytest
 import torch
@@ -13,109 +21,170 @@ from spine_vision_amd import native as nv
 pytestmark = pytest.mark.gpu
 
 
-def _impl(i):
-    return nv.value("sv_gemm_set_impl", i)
+def _ops(dev, M, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    bf = torch.bfloat16
+    t = {
+        "y": torch.randn(M, C, generator=g).to(bf).to(dev),
+        "w1": (torch.randn(4 * C, C, generator=g) * 0.05).to(bf).to(dev),
+        "w2": (torch.randn(C, 4 * C, generator=g) * 0.05).to(bf).to(dev),
+        "b1": (torch.randn(4 * C, generator=g) * 0.1).to(dev),
+        "b2": (torch.randn(C, generator=g) * 0.1).to(dev),
+        "gam": (torch.rand(C, generator=g) * 0.25 + 0.05).to(dev),
+        "x": torch.randn(M, C, generator=g).to(dev),
+        "a": torch.randn(M, 4 * C, generator=g).to(bf).to(dev),
+        "gh": torch.randn(M, 4 * C, generator=g).to(bf).to(dev),
+        "dy": torch.randn(M, C, generator=g).to(bf).to(dev),
+        "dh": torch.randn(M, 4 * C, generator=g).to(bf).to(dev),
+    }
+    return t
 
 
-def _run_both(fn, impl):
-    prev = _impl(0)
-    try:
-        a = fn()
-        torch.cuda.synchronize()
-        _impl(impl)
-        b = fn()
-        torch.cuda.synchronize()
-    finally:
-        _impl(prev)
-    return a, b
+def _funcs(t, dev, M, C):
+    bf = torch.bfloat16
+
+    def fc1_fwd(pol):
+        o, o2 = torch.empty(M, 4 * C, device=dev, dtype=bf), torch.empty(M, 4 * C, device=dev, dtype=bf)
+        K.linear_fwd(t["y"], t["w1"], out=o, out2=o2, bias=t["b1"], epilogue=nv.SV_EPI_BIAS_GELU_DUAL, policy=pol)
+        return torch.cat([o, o2])
+
+    def fc2_fwd(pol):
+        o = torch.empty(M, C, device=dev)
+        K.linear_fwd(t["a"], t["w2"], out=o, bias=t["b2"], gamma=t["gam"], residual=t["x"],
+                     epilogue=nv.SV_EPI_BIAS_GAMMA_RES, policy=pol)
+        return o
+
+    def fc2_dgrad(pol):
+        o = torch.empty(M, 4 * C, device=dev, dtype=bf)
+        K.linear_dgrad(t["dy"], t["w2"], out=o, epilogue=nv.SV_EPI_MUL_AUX, aux=t["gh"], policy=pol)
+        return o
+
+    def fc1_dgrad(pol):
+        o = torch.empty(M, C, device=dev, dtype=bf)
+        K.linear_dgrad(t["dh"], t["w1"], out=o, policy=pol)
+        return o
+
+    def wgrad(pol):  # the fc2 weight gradient d^T a with its fused bias column sum (split-K slabs + fold)
+        bo = torch.zeros(C, device=dev)
+        o = K.linear_wgrad(t["dy"], t["a"], bias_out=bo, bias_accumulate=False, policy=pol)
+        return torch.cat([o.reshape(-1), bo])
+
+    def wgrad1(pol):  # the fc1 weight gradient dh^T y
+        return K.linear_wgrad(t["dh"], t["y"], policy=pol).reshape(-1)
+
+    return [("fc1_fwd", fc1_fwd), ("fc2_fwd", fc2_fwd), ("fc2_dgrad", fc2_dgrad), ("fc1_dgrad", fc1_dgrad),
+            ("wgrad", wgrad), ("wgrad1", wgrad1)]
+
+
+def _same(name, ref, got, C, tag):
+    if name == "wgrad":
+        # the families fold the fused bias column sum in different f32 orders (v2 per BK-64 chunk, v3 per
+        # BK-32 step, v9 per lane group of its A fragments): the weight gradient is bit-identical, db within ~1 ulp
+        nw = ref.numel() - C
+        assert torch.equal(ref[:nw], got[:nw]), (tag, name, float((ref[:nw] - got[:nw]).abs().max()))
+        r = float((ref[nw:] - got[nw:]).norm() / ref[nw:].norm())
+        assert r < 1e-6, (tag, name, r)
+        return
+    assert torch.equal(ref, got), (tag, name, float((ref.float() - got.float()).abs().max()))
 
 
 @pytest.mark.parametrize("impl", [2, 3, 8, 9])
 @pytest.mark.parametrize("M,C", [(3000, 128), (8192, 256), (2048 + 96, 512)])
 def test_gemm_family_bitwise_vs_dispatch(dev, impl, M, C):
-    g = torch.Generator().manual_seed(M + C)
-    bf = torch.bfloat16
-    y = (torch.randn(M, C, generator=g)).to(bf).to(dev)
-    w1 = (torch.randn(4 * C, C, generator=g) * 0.05).to(bf).to(dev)
-    w2 = (torch.randn(C, 4 * C, generator=g) * 0.05).to(bf).to(dev)
-    b1 = (torch.randn(4 * C, generator=g) * 0.1).to(dev)
-    b2 = (torch.randn(C, generator=g) * 0.1).to(dev)
-    gam = (torch.rand(C, generator=g) * 0.25 + 0.05).to(dev)
-    x = torch.randn(M, C, generator=g).to(dev)
-    a = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
-    gh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
-    dy = torch.randn(M, C, generator=g).to(bf).to(dev)
-    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
-
-    def fc1_fwd():
-        o, o2 = torch.empty(M, 4 * C, device=dev, dtype=bf), torch.empty(M, 4 * C, device=dev, dtype=bf)
-        K.linear_fwd(y, w1, out=o, out2=o2, bias=b1, epilogue=nv.SV_EPI_BIAS_GELU_DUAL)
-        return torch.cat([o, o2])
-
-    def fc2_fwd():
-        o = torch.empty(M, C, device=dev)
-        K.linear_fwd(a, w2, out=o, bias=b2, gamma=gam, residual=x, epilogue=nv.SV_EPI_BIAS_GAMMA_RES)
-        return o
-
-    def fc2_dgrad():
-        o = torch.empty(M, 4 * C, device=dev, dtype=bf)
-        K.linear_dgrad(dy, w2, out=o, epilogue=nv.SV_EPI_MUL_AUX, aux=gh)
-        return o
-
-    def fc1_dgrad():
-        o = torch.empty(M, C, device=dev, dtype=bf)
-        K.linear_dgrad(dh, w1, out=o)
-        return o
-
-    def wgrad():
-        bo = torch.zeros(C, device=dev)
-        o = K.linear_wgrad(dy, a, bias_out=bo, bias_accumulate=False)
-        return torch.cat([o.reshape(-1), bo])
-
-    for name, fn in [("fc1_fwd", fc1_fwd), ("fc2_fwd", fc2_fwd), ("fc2_dgrad", fc2_dgrad), ("fc1_dgrad", fc1_dgrad),
-                     ("wgrad", wgrad)]:
-        ref, got = _run_both(fn, impl)
-        if name == "wgrad":
-            # the families fold the fused bias column sum in different f32 orders (v2 per BK-64 chunk,
-            # v3 per BK-32 step, v9 per lane group of its A fragments): the weight gradient is
-            # bit-identical, db within ~1 ulp
-            nw = ref.numel() - C
-            assert torch.equal(ref[:nw], got[:nw]), (impl, name, float((ref[:nw] - got[:nw]).abs().max()))
-            r = float((ref[nw:] - got[nw:]).norm() / ref[nw:].norm())
-            assert r < 1e-6, (impl, name, r)
-            continue
-        assert torch.equal(ref, got), (impl, name, float((ref.float() - got.float()).abs().max()))
+    t = _ops(dev, M, C, M + C)
+    for name, fn in _funcs(t, dev, M, C):
+        ref = fn(None)
+        got = fn(nv.policy(impl=impl))
+        torch.cuda.synchronize()
+        _same(name, ref, got, C, f"impl{impl}")
     # values: fc1 dgrad against torch fp32 on the same bf16 operands
-    o = fc1_dgrad()
-    r = dh.float() @ w1.float()
+    o = dict(_funcs(t, dev, M, C))["fc1_dgrad"](None)
+    r = t["dh"].float() @ t["w1"].float()
     assert float((o.float() - r).norm() / r.norm()) < 5e-3
 
 
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _torch_refs(t, M, C):
+    """fp32 products of the same bf16 operands (torch on the GPU; GELU in erf form, its derivative Phi + x phi)."""
+    y, w1, w2 = t["y"].float(), t["w1"].float(), t["w2"].float()
+    h = y @ w1.t() + t["b1"]
+    phi = torch.exp(-0.5 * h * h) * 0.3989422804014327
+    Phi = 0.5 * (1.0 + torch.erf(h * 0.7071067811865476))
+    ref = {"fc1_fwd": (Phi + h * phi, h * Phi)}
+    del phi, Phi, h
+    ref["fc2_fwd"] = t["gam"] * (t["a"].float() @ w2.t() + t["b2"])  # the delta over the residual
+    ref["fc2_dgrad"] = (t["dy"].float() @ w2) * t["gh"].float()
+    ref["fc1_dgrad"] = t["dh"].float() @ w1
+    ref["wgrad"] = (t["dy"].float().t() @ t["a"].float(), t["dy"].float().sum(0))
+    ref["wgrad1"] = t["dh"].float().t() @ y
+    return ref
+
+
+# ConvNeXt-base 512x512 bs32: S1 (M = 32*128^2, C = 128), S3 (32*32^2, 512), S4 (32*16^2, 1024)
+_BS32 = [(524288, 128), (32768, 512), (8192, 1024)]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("M,C", _BS32, ids=["S1", "S3", "S4"])
+def test_gemm_bs32_production_schedule(dev, M, C):
+    """The bs32 shapes the bench runs: the dispatch's schedule (v9 with several tiles per persistent workgroup
+    where it picks v9) under the forward's default policy AND the lean backward's (one persistent workgroup per
+    CU, raised priority, grid capped at 224 as under data parallelism) equals v3 (one workgroup per tile) bit for
+    bit on every epilogue, and v3's values match torch fp32 on the same bf16 operands."""
+    t = _ops(dev, M, C, 7 + C)
+    funcs = _funcs(t, dev, M, C)
+    bwd = nv.policy(wg_per_cu=1, priority=1, grid_cap=224)
+    outs = {}
+    for name, fn in funcs:
+        ref = fn(nv.policy(impl=3))
+        for tag, pol in (("default", None), ("backward", bwd)):
+            got = fn(pol)
+            torch.cuda.synchronize()
+            _same(name, ref, got, C, tag)
+            del got
+        outs[name] = ref
+    ref = _torch_refs(t, M, C)
+    n = M * 4 * C
+    r = {
+        "fc1_fwd GELU'": _rel(outs["fc1_fwd"][:M].float(), ref["fc1_fwd"][0]),
+        "fc1_fwd GELU": _rel(outs["fc1_fwd"][M:].float(), ref["fc1_fwd"][1]),
+        "fc2_fwd": _rel(outs["fc2_fwd"] - t["x"], ref["fc2_fwd"]),
+        "fc2_dgrad": _rel(outs["fc2_dgrad"].float(), ref["fc2_dgrad"]),
+        "fc1_dgrad": _rel(outs["fc1_dgrad"].float(), ref["fc1_dgrad"]),
+        "wgrad": _rel(outs["wgrad"][:C * 4 * C], ref["wgrad"][0].reshape(-1)),
+        "wgrad bias": _rel(outs["wgrad"][C * 4 * C:], ref["wgrad"][1]),
+        "wgrad1": _rel(outs["wgrad1"], ref["wgrad1"].reshape(-1)),
+    }
+    print(f"[bs32] M={M} C={C} rel vs torch fp32: " + ", ".join(f"{k} {v:.2e}" for k, v in r.items()))
+    assert n > 0
+    # bf16 outputs: the store's rounding (2^-9 relative at most, ~1e-3 RMS); f32 outputs: accumulation order
+    for k in ("fc1_fwd GELU'", "fc1_fwd GELU", "fc2_dgrad", "fc1_dgrad"):
+        assert r[k] < 4e-3, (k, r[k])
+    for k in ("fc2_fwd", "wgrad", "wgrad bias", "wgrad1"):
+        assert r[k] < 1e-4, (k, r[k])
+
+
 def test_gemm_priority_is_bitwise_neutral(dev):
-    """sv_gemm_set_priority only raises the waves' issue priority (the lean backward's side-stream
-    wgrads): the split-K weight gradient is bit-identical either way."""
+    """policy.priority only raises the waves' issue priority (the lean backward's side-stream wgrads): the
+    split-K weight gradient is bit-identical either way."""
     g = torch.Generator().manual_seed(3)
     bf = torch.bfloat16
     dy = torch.randn(8192, 256, generator=g).to(bf).to(dev)
     a = torch.randn(8192, 1024, generator=g).to(bf).to(dev)
-    prev_res = nv.value("sv_gemm_set_workgroups_per_cu", 1)  # the backward's residency policy
-    try:
-        ref = K.linear_wgrad(dy, a)
-        prev = nv.value("sv_gemm_set_priority", 1)
-        try:
-            got = K.linear_wgrad(dy, a)
-        finally:
-            nv.value("sv_gemm_set_priority", prev)
-        torch.cuda.synchronize()
-    finally:
-        nv.value("sv_gemm_set_workgroups_per_cu", prev_res)
+    ref = K.linear_wgrad(dy, a, policy=nv.policy(wg_per_cu=1))  # the backward's residency policy
+    got = K.linear_wgrad(dy, a, policy=nv.policy(wg_per_cu=1, priority=1))
+    torch.cuda.synchronize()
     assert torch.equal(ref, got)
 
 
 @pytest.mark.parametrize("impl", [0, 3, 9])
 def test_gemm_grid_cap_bitwise(dev, impl):
-    """sv_gemm_set_grid_cap (the ResNet side stream's weight gradients run under a cap): the kernels are
-    persistent over their tiles, so a capped grid computes every tile exactly as the full grid does --
+    """policy.grid_cap (the ResNet side stream's weight gradients, the data-parallel comm reserve): the kernels
+    are persistent over their tiles, so a capped grid computes every tile exactly as the full grid does --
     forward, data-gradient and split-K weight-gradient GEMMs equal bit for bit at caps of 37 and 96."""
     g = torch.Generator().manual_seed(5)
     bf = torch.bfloat16
@@ -124,25 +193,39 @@ def test_gemm_grid_cap_bitwise(dev, impl):
     w1 = (torch.randn(4 * C, C, generator=g) * 0.05).to(bf).to(dev)
     dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
 
-    def run():
+    def run(cap):
+        pol = nv.policy(impl=impl, grid_cap=cap)
         o = torch.empty(M, 4 * C, device=dev, dtype=bf)
-        K.linear_fwd(y, w1, out=o)
+        K.linear_fwd(y, w1, out=o, policy=pol)
         d = torch.empty(M, C, device=dev, dtype=bf)
-        K.linear_dgrad(dh, w1, out=d, compute_bf16=True)
-        wg = K.linear_wgrad(dh, y, compute_bf16=True)
+        K.linear_dgrad(dh, w1, out=d, compute_bf16=True, policy=pol)
+        wg = K.linear_wgrad(dh, y, compute_bf16=True, policy=pol)
         torch.cuda.synchronize()
         return o.float(), d.float(), wg
 
-    prev_impl = _impl(impl)
-    try:
-        ref = run()
-        for cap in (37, 96):
-            prev = nv.value("sv_gemm_set_grid_cap", cap)
-            try:
-                out = run()
-            finally:
-                nv.value("sv_gemm_set_grid_cap", prev)
-            for a, b in zip(ref, out):
-                assert torch.equal(a, b)
-    finally:
-        _impl(prev_impl)
+    ref = run(0)
+    for cap in (37, 96):
+        for a, b in zip(ref, run(cap)):
+            assert torch.equal(a, b)
+
+
+def test_gemm_policy_is_per_call(dev):
+    """A policy travels with its call only: a capped launch on a side stream leaves an uncapped launch issued
+    meanwhile on the default stream untouched (both bitwise the reference), and an invalid policy is refused
+    with an error rather than applied."""
+    g = torch.Generator().manual_seed(6)
+    bf = torch.bfloat16
+    M, C = 8192, 512
+    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    y = torch.randn(M, C, generator=g).to(bf).to(dev)
+    ref = K.linear_wgrad(dh, y)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        capped = K.linear_wgrad(dh, y, policy=nv.policy(grid_cap=17, priority=1, wg_per_cu=1))
+    plain = K.linear_wgrad(dh, y)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, capped) and torch.equal(ref, plain)
+    with pytest.raises(RuntimeError, match="policy"):
+        K.linear_wgrad(dh, y, policy=nv.policy(impl=5))

@@ -15,8 +15,14 @@ via models/backbone.py:29.
   5.5e-3 off float64 on this fixture, measured on CPU; a ReLU-mask flip at fp32 rounding moves whole
   gradient rows), so each HIP gradient is held against float64 within max(1e-3, 3x the fp32 oracle's own
   error), as in test_resnet_fp32_forward_backward.
-* bf16: bounds ~2x the error measured on MI355X for exactly these cases (values beside BF16_BOUNDS and in
-  DESIGN.md "Oracle and parity").
+* bf16: against ``oracle.bf16emu`` -- the same model in float64 with a bf16
+  rounding at exactly the HIP path's store points, forward and backward -- relative to the bf16 NOISE FLOOR,
+  the distance between that emulation in float64 and in float32 (two valid roundings-at-the-same-points
+  computations; see oracle/bf16emu.py floor_check).  Measured on CPU: the floor is 0.24-0.26 (train) and
+  0.03 (eval) median per gradient tensor at B=2..32, so no fixed bound below it can hold for ANY bf16
+  implementation; the HIP distance is held to a small multiple of it per tensor, with a cosine / norm guard
+  that a dropped or zeroed gradient cannot pass.  The fp32-oracle distances are printed as
+  measurements only.
 """
 
 import copy
@@ -32,17 +38,9 @@ from oracle import weights as ow
 pytestmark = pytest.mark.gpu
 
 LABELS = ["pfirrmann", "modic", "herniation"]
-# (logits rel-L2 bound, worst-gradient bound, median-gradient bound) for bf16, ~2x measured on MI355X
-# (gpurun_out/r4a, round 3): eval 1.57e-2 / 8.7e-2 (conv1.weight) / 2.14e-2; train 1.06e-2 / 0.517 / 0.369.
-# The train-mode gradients are ill-conditioned in ANY reduced precision: torch's CPU bf16 autocast of the
-# same model is 0.35-0.37 (median) / 0.48-0.52 (worst) off fp32 at B=2 and at B=8 (measured in the build
-# container), and even the fp32 oracle is 1.6e-3 (median) off float64: a train-mode BatchNorm projects its
-# input gradient to zero mean per channel, so the BN scale / shift gradients upstream are small
-# differences of large sums.
-BF16_BOUNDS = {
-    "eval": (3.2e-2, 0.18, 4.5e-2),
-    "train": (2.2e-2, 1.05, 0.75),
-}
+# floor_check parameters: median / worst ratio of the HIP distance to the bf16 noise floor, the floor's lower
+# clamp, and the cosine guard
+FLOOR = {"ratio_median": 2.0, "ratio_max": 4.0, "min_floor": 1e-2, "min_cos": 0.5}
 
 
 def rel(a, b):
@@ -120,10 +118,69 @@ def test_resnet50_256_fp32(dev, mode):
     assert all(v < 1e-5 for v in buf.values()), buf
 
 
+def bf16_vs_emulation(dev, mode, B, engine=False):
+    """HIP bf16 (whole model, optionally through StepEngine's flat buffers / bf16 shadow as the bench runs it)
+    against oracle.bf16emu in float64 and float32; -> (logit errors, floor_check table)."""
+    from oracle import bf16emu as be
+    from spine_vision_amd.training import Classifier, StepEngine
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    tasks = _create_tasks_for_training(target_labels=LABELS, label_smoothing=0.1)
+    ref = oh.Classifier(orn.create("resnet50"), 2048, dropout=0.0)
+    ow.fill_module(ref, conditioned=True)
+    train = mode == "train"
+    img, targets = ow.classification_batch(B, 256, 256)
+    o64, g64, b64 = be.classifier_grads(ref, img, targets, torch.float64, train)
+    o32, g32, _ = be.classifier_grads(ref, img, targets, torch.float32, train)
+    hip = Classifier(backbone="resnet50", tasks=tasks, pretrained=False, dropout=0.0, precision="bf16")
+    hip.load_state_dict(ref.state_dict(), strict=True)
+    hip = hip.to(dev).train(train)
+    tg = {k: v.to(dev) for k, v in targets.items()}
+    if engine:  # lr 0: the step's AdamW leaves the weights (and the compared gradients) as the forward saw them
+        eng = StepEngine(hip, dev, lr=0.0, weight_decay=0.0, grad_clip=1.0)
+        logits = {}
+        eng.step(lambda m: _keep(logits, m(img.to(dev))) and m.get_loss(logits, tg))
+    else:
+        logits = hip(img.to(dev))
+        hip.get_loss(logits, tg).backward()
+    torch.cuda.synchronize()
+    lerr = {k: (rel(logits[k], o64[k]), rel(o32[k], o64[k])) for k in LABELS}
+    table = be.floor_check({n: p.grad for n, p in hip.named_parameters()}, g64, g32, **FLOOR)
+    if train:
+        hb = dict(hip.named_buffers())
+        berr = {n: rel(hb[n], b) for n, b in b64.items()}
+        assert all(v < 1e-2 for v in berr.values()), berr
+    return lerr, table
+
+
+def _keep(d, out):
+    d.update(out)
+    return True
+
+
+def report_floor(tag, lerr, table):
+    ratios = {n: v[2] for n, v in table.items()}
+    worst = max(ratios, key=ratios.get)
+    errs = [v[0] for v in table.values()]
+    floors = [v[1] for v in table.values()]
+    print(f"[parity] {tag}: logits rel vs emu64 {max(v[0] for v in lerr.values()):.3e} (floor "
+          f"{max(v[1] for v in lerr.values()):.3e}); grad vs emu64 median {np.median(errs):.3e} (floor median "
+          f"{np.median(floors):.3e}); ratio median {np.median(list(ratios.values())):.2f}, worst {ratios[worst]:.2f} "
+          f"({worst}); min cosine {min(v[3] for v in table.values()):.3f}")
+    for k, (e, f) in lerr.items():
+        assert e <= 4.0 * max(f, 1e-3), (k, e, f)
+
+
 @pytest.mark.parametrize("mode", ["eval", "train"])
-def test_resnet50_256_bf16(dev, mode):
+def test_resnet50_256_bf16_vs_emulation(dev, mode):
+    lerr, table = bf16_vs_emulation(dev, mode, 2)
+    report_floor(f"resnet50@256 B2 bf16 {mode}", lerr, table)
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_resnet50_256_bf16_vs_fp32_reported(dev, mode):
+    """The bf16 path against the fp32 oracle: reported for DESIGN.md, not bounded -- that distance is the bf16
+    noise itself (test_resnet50_256_bf16_vs_emulation carries the bound)."""
     logit, grads, buf = _case(dev, "bf16", mode)
-    lw, worst, med = _report(f"resnet50@256 B2 bf16 {mode}", logit, grads)
-    bl, bw, bm = BF16_BOUNDS[mode]
-    assert lw < bl and worst < bw and med < bm, (lw, worst, med)
+    _report(f"resnet50@256 B2 bf16 {mode} (vs fp32 oracle)", logit, grads)
     assert all(v < 1e-2 for v in buf.values()), buf
