@@ -61,6 +61,12 @@ PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsam
                "adamw": "fused AdamW over the flat buffers (+ bf16 shadow refresh)",
                "fold": "split-K / partial-sum folds (reduce_multi, reduce_pair, layer-scale fold): bytes = the slab "
                        "bytes they move, overhead of split-K rather than algorithmic work"}
+# step-time cost of the data-parallel CU reserve (SV_COMM_RESERVE_CUS, default 0 = none) measured at world 1
+# (SV_BENCH_RESERVE A/B, interleaved on one box; DESIGN.md "Multi-GPU": 32 CUs by grid caps 2.2 %, by CU masks
+# 12-24 %), and the measured worst start latency of a comm-stream kernel behind the backward's GEMMs without a
+# reserve (tests/test_comm_reserve_gpu.py: 0.2-0.41 ms): both folded into dp_rehearsal's predicted scaling
+RESERVE_COST = float(os.environ.get("SV_RESERVE_COST", "0.0"))
+COMM_DELAY_MS = float(os.environ.get("SV_COMM_DELAY_MS", "0.41"))
 # HBM-bound kernel classes timed by kernels.OpProbe (reported separately against 8 TB/s)
 OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "fold")
 
@@ -514,13 +520,12 @@ def main():
     else:
         model = CoordinateRegressor(args.backbone, pretrained=False, precision=args.precision)
     model = model.to(device).train()
-    if os.environ.get("SV_BENCH_RESERVE"):  # A/B at world 1: the CU reservation a multi-GPU run applies
-        for m in model.modules():
-            if hasattr(m, "comm_reserve_cus"):
-                m.comm_reserve_cus = int(os.environ["SV_BENCH_RESERVE"])
+    # SV_BENCH_RESERVE (A/B at world 1): the CU reserve a multi-GPU run applies (CU-masked step streams + capped
+    # GEMM grids, training/cumask.py); world > 1 takes SV_COMM_RESERVE_CUS (default 32)
+    reserve = int(os.environ["SV_BENCH_RESERVE"]) if os.environ.get("SV_BENCH_RESERVE") else None
     graphed = args.graph == "on" and cls and world == 1
     engine = StepEngine(model, device, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
-                        cuda_graph=graphed and not args.inference)
+                        cuda_graph=graphed and not args.inference, comm_reserve_cus=reserve)
     if cls:
         img, targets = synthetic_cls_batch(args.batch, args.image_size, args.image_size, device, 1234 + rank)
 
@@ -709,10 +714,15 @@ def main():
         result["dp_rehearsal"] = {
             "buckets_mb_ready_ms": ready,
             "backward_end_ms": round(bwd_end, 3), "step_ms_last": round(step_last, 3),
-            "predictions": [timeline.predict(ready, bwd_end, ms, 8, bw) for bw in (200.0, 300.0, 400.0)],
+            # the reserve's own cost (32 of 256 CUs masked from the step under data parallelism), measured at
+            # world 1 as an interleaved A/B (SV_BENCH_RESERVE, DESIGN.md "Multi-GPU"), stretches every time
+            "reserve_cost_frac": RESERVE_COST,
+            "comm_launch_delay_ms": COMM_DELAY_MS,
+            "predictions": [timeline.predict(ready, bwd_end, ms, 8, bw, reserve_cost=RESERVE_COST,
+                                             launch_delay_ms=COMM_DELAY_MS) for bw in (200.0, 300.0, 400.0)],
         }
     if world > 1:
-        result["config"]["comm_reserve_cus"] = int(os.environ.get("SV_COMM_RESERVE_CUS", "32"))
+        result["config"]["comm_reserve_cus"] = engine.comm_reserve_cus
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
         if not cls and not args.inference:

@@ -49,6 +49,15 @@ int sv_version(void);                        /* ABI version, bumped on any signa
 const char* sv_last_error_string(void);      /* thread-local message of the last failing call    */
 const char* sv_build_target(void);           /* offload arch the device code was compiled for     */
 
+/* ---- data-parallel CU reserve ---------------------------------------------------------------
+ * A stream of `device` whose kernels never occupy the CUs listed in `reserved` (n_reserved CU indices in the
+ * numbering of hipExtStreamCreateWithCUMask's bit vector), so RCCL's all-reduce kernels -- on streams of their
+ * own -- always find free CUs while the backward runs on this one (accelerate DDP's overlap of the gradient
+ * exchange with the backward, spine_vision/training/trainers/base.py:253-266).  The stream lives until the
+ * process ends (the host wraps it as a torch ExternalStream).  The GEMMs launched on it should cap their
+ * persistent grids (sv_gemm_policy.grid_cap) at the unmasked CU count, or their last workgroups queue.  */
+int sv_stream_create_cu_reserved(int32_t device, const int32_t* reserved, int32_t n_reserved, sv_stream_t* out);
+
 /* ---- GEMM on MFMA (bf16 in / f32 accumulate, or exact f32 in / f32 accumulate) --------------
  * C[m,n] = epilogue( sum_k A(m,k) * B(k,n) ),  m < M, n < N, k < K.
  *   A(m,k) = A[m*lda + k]  if a_kmajor  else  A[k*lda + m]

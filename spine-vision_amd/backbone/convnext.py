@@ -143,6 +143,7 @@ class ConvNeXtHip(nn.Module):
         # CUs free so RCCL's all-reduce kernels on the comm stream find a CU (a v9 workgroup holds its CU's
         # LDS for the whole launch); 0 = every CU
         self.comm_reserve_cus = 0
+        self.comm_cu_mask = False  # StepEngine: also mask the side stream's CUs (opt-in, see engine.py)
         # a block's fc1 wgrad slab / bias, LayerNorm and depthwise partials folded by ONE launch
         # (sv_reduce_partials_multi) instead of four (SV_MERGED_FOLDS=0: one launch per fold, A/B only)
         self.merge_folds = os.environ.get("SV_MERGED_FOLDS", "1") != "0"
@@ -303,9 +304,17 @@ class ConvNeXtHip(nn.Module):
 
     # -- backward ----------------------------------------------------------------------------------
     def _side_stream(self, device) -> torch.cuda.Stream:
-        if device not in self._side:
-            self._side[device] = torch.cuda.Stream(device=device)
-        return self._side[device]
+        """The weight-gradient side stream; CU-masked (never on the CUs reserved for RCCL, training/cumask.py) when
+        StepEngine asks for it (comm_reserve_cus > 0 and SV_COMM_CU_MASK=1)."""
+        key = (device, self.comm_reserve_cus, self.comm_cu_mask)
+        if key not in self._side:
+            if self.comm_reserve_cus > 0 and self.comm_cu_mask:
+                from ..training.cumask import reserved_stream
+
+                self._side[key] = reserved_stream(device, self.comm_reserve_cus, "side")
+            else:
+                self._side[key] = torch.cuda.Stream(device=device)
+        return self._side[key]
 
     @staticmethod
     def _grad(p: torch.Tensor) -> torch.Tensor:

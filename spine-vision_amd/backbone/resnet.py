@@ -162,6 +162,7 @@ class ResNetHip(nn.Module):
         # data-parallel runs: the backward's GEMM grids (both streams) leave this many CUs to RCCL (see
         # ConvNeXtHip.comm_reserve_cus); 0 = every CU
         self.comm_reserve_cus = 0
+        self.comm_cu_mask = False  # StepEngine: also mask the side stream's CUs (opt-in, see engine.py)
         self._init_weights()
 
     def set_weight_shadow(self, shadow: dict[int, torch.Tensor] | None) -> None:
@@ -386,9 +387,17 @@ class ResNetHip(nn.Module):
             self.grad_ready_hook(params)
 
     def _side_stream(self, device) -> torch.cuda.Stream:
-        if device not in self._side:
-            self._side[device] = torch.cuda.Stream(device=device)
-        return self._side[device]
+        """The weight-gradient side stream; CU-masked (never on the CUs reserved for RCCL, training/cumask.py) when
+        StepEngine asks for it (comm_reserve_cus > 0 and SV_COMM_CU_MASK=1)."""
+        key = (device, self.comm_reserve_cus, self.comm_cu_mask)
+        if key not in self._side:
+            if self.comm_reserve_cus > 0 and self.comm_cu_mask:
+                from ..training.cumask import reserved_stream
+
+                self._side[key] = reserved_stream(device, self.comm_reserve_cus, "side")
+            else:
+                self._side[key] = torch.cuda.Stream(device=device)
+        return self._side[key]
 
     def _flush_wgrads(self, jobs: list, params: list, side, keep: list, deferred: list | None = None,
                       pol: "nv.GemmPolicy | None" = None) -> None:

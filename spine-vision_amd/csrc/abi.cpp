@@ -84,6 +84,33 @@ int sv_version(void) { return 3; }
 
 const char* sv_last_error_string(void) { return sv::g_err; }
 
+int sv_stream_create_cu_reserved(int32_t device, const int32_t* reserved, int32_t n_reserved, sv_stream_t* out) {
+  SV_REQUIRE(out && (n_reserved == 0 || reserved) && n_reserved >= 0, "sv_stream_create_cu_reserved: bad arguments");
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+    return sv::set_error(SV_ERR_INVALID_ARG, "sv_stream_create_cu_reserved: no device %d", device);
+  SV_REQUIRE(n_reserved < ncu, "sv_stream_create_cu_reserved: reserving %d of %d CUs", n_reserved, ncu);
+  const int words = (ncu + 31) / 32;
+  uint32_t mask[64];
+  SV_REQUIRE(words <= 64, "sv_stream_create_cu_reserved: %d CUs", ncu);
+  for (int w = 0; w < words; ++w) mask[w] = 0xffffffffu;
+  if (ncu % 32) mask[words - 1] = (1u << (ncu % 32)) - 1u;
+  for (int i = 0; i < n_reserved; ++i) {
+    SV_REQUIRE(reserved[i] >= 0 && reserved[i] < ncu, "sv_stream_create_cu_reserved: CU %d out of range", reserved[i]);
+    mask[reserved[i] / 32] &= ~(1u << (reserved[i] % 32));
+  }
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != device) hipSetDevice(device);
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (cur != device) hipSetDevice(cur);
+  if (e != hipSuccess)
+    return sv::set_error(SV_ERR_LAUNCH, "sv_stream_create_cu_reserved: %s", hipGetErrorString(e));
+  *out = (sv_stream_t)s;
+  return SV_OK;
+}
+
 const char* sv_build_target(void) {
 #ifdef SV_OFFLOAD_ARCH
   return SV_OFFLOAD_ARCH;

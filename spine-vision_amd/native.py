@@ -97,6 +97,7 @@ _SIGS = {
     "sv_last_error_string": [],
     "sv_build_target": [],
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
+    "sv_stream_create_cu_reserved": [_i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_p)],
     "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
     "sv_gemm_slab_finish_bn_bwd": [_p, _i32, _i32, _i32, _p, _p, ctypes.POINTER(BnRef), _p, _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
@@ -171,7 +172,8 @@ _SIGS = {
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats"}
+_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
+                                                                     "sv_stream_create_cu_reserved"}
 
 _lib = None
 _lock = threading.Lock()

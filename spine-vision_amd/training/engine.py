@@ -99,7 +99,7 @@ class StepEngine:
     def __init__(self, model: torch.nn.Module, device: torch.device | str, *, lr: float = 1e-4,
                  weight_decay: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  grad_clip: float | None = 1.0, distributed: bool | None = None, bucket_mb: float = 64.0,
-                 cuda_graph: bool = False) -> None:
+                 cuda_graph: bool = False, comm_reserve_cus: int | None = None) -> None:
         # a backbone whose backward queries events (ConvNeXt's lean side-stream release) declares
         # graph_safe = False and cannot be captured: asking for it is an error, not a silent fallback.
         if cuda_graph:
@@ -116,13 +116,27 @@ class StepEngine:
         self.distributed = distributed
         self.bucketer = None
         self.buffer_sync = None
+        # CUs kept free for RCCL's all-reduce kernels while the backward runs (SV_COMM_RESERVE_CUS; default 0): the
+        # backward's persistent GEMM grids are capped at CUs - reserve, and with SV_COMM_CU_MASK=1 the step and the
+        # side streams also run on CU-masked streams (training/cumask.py).  Measured on MI355X (DESIGN.md
+        # "Multi-GPU", tests/test_comm_reserve_gpu.py, tools/cu_mask_probe.py): neither bounds a comm kernel's
+        # start latency -- the data- and weight-gradient GEMMs of the two streams together still cover every CU --
+        # and they cost 2.2 % (caps) and 12-24 % (masks) of the step, so the default reserves nothing
+        if comm_reserve_cus is None:
+            comm_reserve_cus = int(os.environ.get("SV_COMM_RESERVE_CUS", "0")) if distributed else 0
+        self.comm_reserve_cus = comm_reserve_cus if self.device.type == "cuda" else 0
+        self._stream = None
+        if self.comm_reserve_cus > 0:
+            mask = os.environ.get("SV_COMM_CU_MASK", "0") != "0"
+            if mask:
+                from .cumask import reserved_stream
+
+                self._stream = reserved_stream(self.device, self.comm_reserve_cus, "main")
+            for m in model.modules():
+                if hasattr(m, "comm_reserve_cus"):
+                    m.comm_reserve_cus = self.comm_reserve_cus
+                    m.comm_cu_mask = mask
         if distributed:
-            if self.device.type == "cuda":
-                # RCCL's kernels need free CUs during the backward (SV_COMM_RESERVE_CUS, default 32 of 256)
-                reserve = int(os.environ.get("SV_COMM_RESERVE_CUS", "32"))
-                for m in model.modules():
-                    if hasattr(m, "comm_reserve_cus"):
-                        m.comm_reserve_cus = reserve
             broadcast_parameters(self.arena, model)
             self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb)
             self.bucketer.attach(model)
@@ -139,6 +153,17 @@ class StepEngine:
 
     def step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
         """Run one optimisation step; returns the (device) loss tensor."""
+        if self._stream is None:
+            return self._step(loss_fn)
+        # the CU-reserved stream: ordered after the caller's stream (the inputs), and the caller's stream after it
+        cur = torch.cuda.current_stream(self.device)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            loss = self._step(loss_fn)
+        cur.wait_stream(self._stream)
+        return loss
+
+    def _step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
         self.optimizer.zero_grad()
         if self.buffer_sync is not None:
             self.buffer_sync.sync()

@@ -1,14 +1,20 @@
-"""Data-parallel readiness on one GPU: RCCL's all-reduce kernels run on a comm stream
-beside the backward, whose persistent v9 GEMM workgroups hold a whole CU's LDS for the entire launch.  With
-world > 1 StepEngine sets ``comm_reserve_cus`` (SV_COMM_RESERVE_CUS, default 32) and the backward's GEMM
-grids leave that many CUs free.
+"""Data-parallel readiness on one GPU: RCCL's all-reduce kernels run on a comm
+stream beside the backward, whose persistent v9 GEMM workgroups hold a whole CU's LDS for the entire launch, on
+TWO streams at once (data gradients on the main stream, weight gradients on the side stream).
 
 The test stands in for RCCL with a proxy kernel (a torch reduction, which needs LDS like RCCL's kernels) on a
 high-priority comm stream, launched the moment each block's gradients are reported ready in the ConvNeXt-base
 bs32 512x512 backward.  It records, per launch, the time from the ready event to the proxy's completion minus
-the proxy's standalone duration (its start latency), with every CU available to the GEMMs and with 32
-reserved, and asserts the reserved schedule's p90 latency stays within the bound below.  Reference path:
-accelerate DDP (spine_vision/training/trainers/base.py:253-266), NCCL/RCCL kernels on their own stream."""
+the proxy's standalone duration (its start latency), for the default data-parallel setup (no CU reserve) and
+for a 32-CU reserve by grid caps (round 3's mechanism), and bounds the default's median AND maximum.
+
+Measured (profiles/round4/r7b_*, r7c_*, r7d_*; rocprofv3 trace of this test): the worst waits follow the
+downsample gradients, reported on the main stream while the side stream's weight-gradient GEMMs run; there the
+two streams' persistent grids cover every CU whether or not each is capped, so the caps do not bound the tail
+(0.4-0.7 ms either way) and cost 2.2 % of the step; CU-masked step streams (training/cumask.py) made it worse
+(0.5-2.8 ms, and -12..-24 % step).  The default therefore reserves nothing, the tail is bounded here, and
+bench.py's data-parallel prediction charges every bucket that start latency.  Reference path: accelerate DDP
+(spine_vision/training/trainers/base.py:253-266), NCCL/RCCL kernels on their own stream."""
 
 import numpy as np
 import pytest
@@ -16,7 +22,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-RESERVED_P90_US = 60.0  # measured on MI355X: see DESIGN.md "Multi-GPU" (the print below)
+# bounds on the default (no reserve) schedule; measured on MI355X over three boxes: median 36.7-41.8 us,
+# p90 49.5-55.2 us, max 203-414 us (the print below)
+DEFAULT_MEDIAN_US = 80.0
+DEFAULT_MAX_US = 1000.0
 
 
 def _latencies(dev, reserve):
@@ -24,8 +33,8 @@ def _latencies(dev, reserve):
 
     torch.manual_seed(0)
     model = CoordinateRegressor("convnext_base", pretrained=False, precision="bf16").to(dev).train()
-    eng = StepEngine(model, dev)
-    model.backbone.comm_reserve_cus = reserve
+    eng = StepEngine(model, dev, comm_reserve_cus=reserve)  # world 1, with the data-parallel CU reserve
+    assert model.backbone.comm_reserve_cus == reserve
     comm = torch.cuda.Stream(device=dev, priority=-1)
     buf = torch.randn(1024, 1024, device=dev)
     out = torch.empty(1024, device=dev)
@@ -41,6 +50,8 @@ def _latencies(dev, reserve):
     alone_us = e0.elapsed_time(e1) * 1e3 / 20
     marks = []
 
+    names = {id(p): n for n, p in model.named_parameters()}
+
     def hook(params):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()  # on the stream that made the gradients final
@@ -50,7 +61,7 @@ def _latencies(dev, reserve):
             a.record()
             torch.sum(buf, dim=0, out=out)
             b.record()
-        marks.append((ev, b))
+        marks.append((ev, b, names.get(id(params[0]), "?")))
 
     img = torch.randn(32, 3, 512, 512, device=dev)
     coords = torch.rand(32, 5, 2, device=dev)
@@ -59,7 +70,9 @@ def _latencies(dev, reserve):
         model.backbone.grad_ready_hook = hook if step == 2 else None
         eng.step_localization(img, coords, mask)
     torch.cuda.synchronize()
-    lat = np.array([ev.elapsed_time(b) * 1e3 - alone_us for ev, b in marks])
+    lat = np.array([ev.elapsed_time(b) * 1e3 - alone_us for ev, b, _ in marks])
+    worst = sorted(range(len(lat)), key=lambda i: -lat[i])[:3]
+    print(f"[comm] reserve {reserve}: worst launches " + ", ".join(f"#{i} {marks[i][2]} {lat[i]:.0f} us" for i in worst))
     return alone_us, lat
 
 
@@ -70,5 +83,6 @@ def test_comm_stream_kernel_starts_with_reserved_cus(dev):
         res[reserve] = (alone, lat)
         print(f"[comm] reserve {reserve:2d} CUs: proxy alone {alone:.1f} us; start latency over {len(lat)} "
               f"launches: median {np.median(lat):.1f} us, p90 {np.percentile(lat, 90):.1f} us, max {lat.max():.1f} us")
-    assert len(res[32][1]) > 30
-    assert np.percentile(res[32][1], 90) < RESERVED_P90_US
+    lat0 = res[0][1]
+    assert len(lat0) > 30
+    assert np.median(lat0) < DEFAULT_MEDIAN_US and lat0.max() < DEFAULT_MAX_US, (np.median(lat0), lat0.max())

@@ -247,8 +247,10 @@ def _bf16_rank(rank, world, port, out):
 
     from spine_vision_amd.training import StepEngine
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    os.environ.pop("SV_COMM_RESERVE_CUS", None)
+    # the optional 32-CU comm reserve (grid caps on every backward GEMM; the default reserves nothing): caps are
+    # bitwise neutral, so the reference below runs without them
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SV_COMM_RESERVE_CUS="32")
+    os.environ.pop("SV_COMM_CU_MASK", None)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     m = _model(dev, "bf16")
@@ -272,7 +274,7 @@ def _bf16_rank(rank, world, port, out):
 def test_two_rank_bf16_lean_step_equals_half_batch_average(dev):
     """Two ranks (gloo, the box's one GPU) run the bf16 ConvNeXt-base step exactly as StepEngine sets it up under
     data parallelism: the lean side-stream backward with per-block grad-ready events launching the bucketed
-    all-reduce, every backward GEMM grid capped by the 32-CU comm reserve.  The replicas end bit-identical, and
+    all-reduce, here with every backward GEMM grid capped by the optional 32-CU comm reserve.  The replicas end bit-identical, and
     the all-reduced gradient equals, bit for bit, the average of two single-process half-batch gradients
     ((g0 + g1) / 2 in f32: a 2-rank SUM is order-free and the halving exact).  Reference: accelerate DDP
     (spine_vision/training/trainers/base.py:253-266), LocalizationTrainer._train_step (localization.py:186-209)."""

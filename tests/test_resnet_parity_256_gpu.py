@@ -39,8 +39,10 @@ pytestmark = pytest.mark.gpu
 
 LABELS = ["pfirrmann", "modic", "herniation"]
 # floor_check parameters: median / worst ratio of the HIP distance to the bf16 noise floor, the floor's lower
-# clamp, and the cosine guard
-FLOOR = {"ratio_median": 2.0, "ratio_max": 4.0, "min_floor": 1e-2, "min_cos": 0.5}
+# clamp, and the cosine guard.  Measured on MI355X (profiles/round4/r7c_tests.log): ratio median 0.97-1.02,
+# worst 1.24-1.53, min cosine 0.934-0.999 (B=2 eval / train, B=32 train) -- the HIP path is as far from the
+# float64 emulation as the float32 emulation is
+FLOOR = {"ratio_median": 1.5, "ratio_max": 2.5, "min_floor": 1e-2, "min_cos": 0.5}
 
 
 def rel(a, b):
