@@ -176,25 +176,28 @@ def cpu_baseline(args):
         def one():
             ostep.train_step_localization(model, opt, img, coords, mask)
     model.train()
-    one()  # warmup
-    n, t0 = 0, time.perf_counter()
+    # at least 3 timed steps (the median: the first carries the allocator's warm-up), more while the budget lasts
+    times = []
+    t0 = time.perf_counter()
     while True:
+        t1 = time.perf_counter()
         one()
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or n >= 8:
+        times.append(time.perf_counter() - t1)
+        if len(times) >= 3 and (time.perf_counter() - t0 >= args.cpu_seconds or len(times) >= 8):
             break
+    med = sorted(times)[len(times) // 2]
     try:
         cpu_name = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:  # pragma: no cover
         cpu_name = "unknown"
     return {
-        "value": round(B * n / el, 4),
+        "value": round(B / med, 4),
         "unit": "images/sec",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} timed fp32 train steps (after 1 warmup) of {args.backbone} {args.image_size}x"
-                  f"{args.image_size} bs{B} on {cpu_name}, torch eager CPU, oracle/ restatement",
+        "sample": f"median of {len(times)} timed fp32 train steps ({', '.join(f'{t:.1f}' for t in times)} s) of "
+                  f"{args.backbone} {args.image_size}x{args.image_size} bs{B} on {cpu_name}, torch eager CPU, "
+                  "oracle/ restatement",
     }
 
 

@@ -128,6 +128,13 @@ typedef struct {
   int32_t compute;           /* SV_BF16: bf16 MFMA (operands rounded to bf16); SV_F32: f32 MFMA    */
   const sv_bn_ref* bn;       /* SV_EPI_STORE_BN_BWD: the BatchNorm (NULL otherwise)                */
   sv_gemm_policy policy;     /* launch policy of THIS call (zero-initialised = the defaults)      */
+  /* SV_EPI_SLAB with fold_out != NULL: the split-K fold as well, fold_out[m][n] (row stride fold_ld, f32) =  */
+  /* (fold_accumulate ? fold_out : 0) + sum_s C[s][m][n], slices in order s = 0, 1, ... (bitwise the         */
+  /* sv_reduce_partials fold of the slabs).  The persistent v9 kernel folds in place: the last workgroup to  */
+  /* finish a tile's slice sums that tile (no launch, no waiting); fold_counters = int32 [ceil(M/256) *      */
+  /* ceil(N/256)], all zero on entry and left zero (one buffer per stream).  Other kernels fold with a      */
+  /* separate pass.  C2 (the column sums) is not folded.                                                    */
+  float* fold_out; int64_t fold_ld; int32_t fold_accumulate; int32_t* fold_counters;
 } sv_gemm_desc;
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
@@ -302,6 +309,11 @@ int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4);
 int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t P, const float* W2,
                                const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2,
                                float* ws, int32_t C, int32_t K4, sv_stream_t stream);
+/* The same finish over the ALREADY FOLDED G[C][K4] (the wgrad GEMM's in-kernel fold, sv_gemm_desc.fold_out) and
+ * the P column-sum partials cs_part[P][C]: bitwise sv_layerscale_wgrad_reduce of the P slabs whose sum is G.  */
+int sv_layerscale_wgrad_fold_finish(const float* G, const float* cs_part, int32_t P, const float* W2, const float* gamma,
+                                    const float* b2, float* dW2, float* dgamma, float* db2, int32_t C, int32_t K4,
+                                    sv_stream_t stream);
 
 /* ---- optimizer step on flat buffers (all params of the model live in one f32 buffer) ----------
  * Replaces accelerator.clip_grad_norm_ (torch.nn.utils.clip_grad_norm_) + torch.optim.AdamW.step.

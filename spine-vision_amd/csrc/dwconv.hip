@@ -32,6 +32,7 @@ constexpr int kDwThreads = 256;  // 4 independent waves per workgroup
 
 struct DwGeo {
   int B, H, W, C, tw, tilesW, tilesH, ntiles;  // tw = strip width (output columns per lane)
+  int xcd;                                      // XCD-contiguous block order (xcd_block)
 };
 
 __device__ __forceinline__ void dw_tile(const DwGeo& g, int tile, int& b, int& h0, int& w0) {
@@ -74,6 +75,15 @@ __device__ __forceinline__ void wait_rows(int younger) {
 }
 
 __device__ __forceinline__ int wave_id_uniform() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// XCD-contiguous block order: blocks are dealt round-robin over the 8 XCDs (b, b + 8, ... share one), so
+// consecutive block indices -- neighbouring strips, whose 3-pixel halos overlap -- would land on different XCDs
+// and each XCD's L2 would fetch the shared halo rows / columns again.  Block b works on logical block
+// (b % 8) * (G / 8) + b / 8 instead: each XCD walks a contiguous range of strips and the halo re-reads hit its
+// own L2 (G % 8 == 0; otherwise the identity).  `xcd` = 0 disables it (A/B).
+__device__ __forceinline__ int xcd_block(int b, int G, int xcd) {
+  return (xcd && (G & 7) == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
 
 // LDS image of one input row: NCOL columns x the wave's 64 channels, packed ([column][channel], 64 *
 // sizeof(T) bytes per column).  DMA'd 16 B per lane (global_load_lds_dwordx4): one instruction moves
@@ -133,7 +143,7 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_ring_kernel(const TIN* __r
   constexpr int ROWB = DwRow<TIN>::template bytes<TC>();
   constexpr int NL = DwRow<TIN>::template nd<TC>();  // DMA instructions per row
   const int lane = threadIdx.x & 63, wv = wave_id_uniform();
-  const int gw = blockIdx.x * (kDwThreads / 64) + wv;
+  const int gw = xcd_block(blockIdx.x, gridDim.x, g.xcd) * (kDwThreads / 64) + wv;
   const int ncg = g.C / 64;
   if (gw >= g.ntiles * ncg) return;  // whole wave; no barriers below
   char* ring = dw_smem + wv * PF * ROWB;
@@ -243,7 +253,8 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
 #pragma unroll
   for (int i = 0; i < 49; ++i) acc[i] = 0.f;
   float dbacc = 0.f;
-  for (int tile = blockIdx.x * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
+  const int lb = xcd_block(blockIdx.x, gridDim.x, g.xcd);  // logical block: its tiles AND its partial row
+  for (int tile = lb * 4 + wv; tile < g.ntiles; tile += gridDim.x * 4) {
     int b, h0, w0;
     dw_tile(g, tile, b, h0, w0);
     auto issue = [&](int ir) {
@@ -307,9 +318,9 @@ __global__ void __launch_bounds__(kDwThreads) dwconv7_wgrad_ring_kernel(const TD
   }
   for (int i = threadIdx.x; i < 64 * 49; i += kDwThreads) {
     const int ch = i / 49, tap = i - ch * 49;
-    dw_part[(size_t)blockIdx.x * g.C * 49 + (size_t)(c0 + ch) * 49 + tap] = red[tap * 64 + ch];
+    dw_part[(size_t)lb * g.C * 49 + (size_t)(c0 + ch) * 49 + tap] = red[tap * 64 + ch];
   }
-  if (threadIdx.x < 64) db_part[(size_t)blockIdx.x * g.C + c0 + threadIdx.x] = redb[threadIdx.x];
+  if (threadIdx.x < 64) db_part[(size_t)lb * g.C + c0 + threadIdx.x] = redb[threadIdx.x];
 }
 
 // ring depths: f32 input rows (3 KiB for a 4-wide strip) 3 deep, so four workgroups fit a CU as with bf16
@@ -322,7 +333,8 @@ template <typename T>
 constexpr int dw_pf() { return sizeof(T) == 4 ? DW_PF_F32 : DW_PF_BF16; }
 
 static DwGeo dw_geo(int B, int H, int W, int C) {
-  DwGeo g{B, H, W, C, DW_TW, (W + DW_TW - 1) / DW_TW, (H + TH - 1) / TH, 0};
+  static const int xcd = getenv("SV_DW_XCD") ? atoi(getenv("SV_DW_XCD")) : 1;  // A/B runs: 0 = dispatch order
+  DwGeo g{B, H, W, C, DW_TW, (W + DW_TW - 1) / DW_TW, (H + TH - 1) / TH, 0, xcd};
   g.ntiles = B * g.tilesW * g.tilesH;
   return g;
 }

@@ -323,6 +323,9 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
                    d->bn && d->bn->mean && d->bn->rstd && d->bn->gamma && d->bn->beta,
                "sv_gemm: STORE_BN_BWD needs bf16 C and aux, C2, N %% 8 == 0, no bias and the bn parameters");
   if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
+  if (d->fold_out)
+    SV_REQUIRE(d->epilogue == SV_EPI_SLAB && bf && d->fold_counters && d->fold_ld == d->N && al16(d->fold_out),
+               "sv_gemm: fold_out needs SV_EPI_SLAB (bf16), fold_counters, fold_ld == N and a 16-byte aligned output");
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
   hipStream_t s = (hipStream_t)stream;
   if (!bf) return launch_layout<false, float, float>(d, s);
@@ -373,6 +376,15 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     int rc = SV_ERR_UNSUPPORTED;
     if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below
     if (rc != SV_ERR_UNSUPPORTED) return rc;
+    if (d->fold_out) {  // another family: the slabs, then the fold as its own pass (bitwise v9's in-kernel fold)
+      sv_gemm_desc dd = *d;
+      dd.fold_out = nullptr;
+      dd.fold_counters = nullptr;
+      if (int r = sv_gemm(&dd, stream)) return r;
+      const int split = d->split_k < 1 ? 1 : d->split_k;
+      return sv_reduce_partials(reinterpret_cast<const float*>(d->C), split, split, (int64_t)d->M * d->N, d->fold_out,
+                                1.0f, d->fold_accumulate, stream);
+    }
     if ((impl == 0 || impl == 9) && !wpc && v8_shape) rc = launch_gemm8(d, s);
     else if (impl == 8) rc = launch_gemm8(d, s);
     else if (impl == 2) rc = launch_gemm2(d, s);

@@ -149,6 +149,19 @@ struct Ext {
   uint32_t c, c2, aux, a, b;
 };
 
+// in-kernel split-K fold (SV_EPI_SLAB with sv_gemm_desc.fold_out): the slices of a tile are summed by the last
+// workgroup to finish one (arrival ticket per tile), with write-through (sc1) slab stores and sc1 loads -- the
+// hand-off of MI355X_MICROARCH.md's inter-workgroup table, row 1 (every storing wave vmcnt(0), a workgroup
+// barrier, ONE agent-scope atomic add per workgroup; the workgroup whose add returns split - 1 loads).  No
+// workgroup ever waits for another, so any grid, cap or co-scheduling is deadlock-free.
+struct Fold {
+  float* out;
+  int64_t ld;
+  int acc;
+  int* cnt;
+};
+constexpr int kSC1 = 16;  // buffer instruction cache policy: sc1 (write-through store / L1-bypassing load)
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
   // built from kernel arguments only: wave-uniform, so no waterfall loop around the buffer ops
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -189,7 +202,7 @@ struct EpiCount {
 //   P8: n_w + 32c + 8(l >> 4) .. +7  (acc[i][2c][0..3], acc[i][2c+1][0..3]),
 //   P4: n_w + 16c + 4(l >> 4) .. +3  (acc[i][c][0..3]).
 // Arithmetic identical to wave_group_epilogue (gemm_common.h).
-template <int EPI, bool P8, bool AK>
+template <int EPI, bool P8, bool AK, bool FOLD = false>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
                                          int split, const float* lbias) {
 #ifdef SV_DIAG_NOSTORE
@@ -358,7 +371,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
           }
         } else {
           const u32x4 d = {__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(d, rc, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(d, rc, off, 0, FOLD ? kSC1 : 0);  // fold: write-through slab
           if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) {
             const u32x4 d2 = {__float_as_uint(o2[0]), __float_as_uint(o2[1]), __float_as_uint(o2[2]),
                               __float_as_uint(o2[3])};
@@ -395,10 +408,73 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
   }
 }
 
-template <bool AK, bool BKM, int EPI, bool P8>
+// The last-arriving workgroup's fold of tile (m0, n0): out[m][n] = (acc ? out : 0) + sum_s slab_s[m][n], the
+// slices added in order s = 0, 1, ... exactly as sv_reduce_partials' wide body (bitwise its result).  Every
+// lane owns whole 16-B column chunks; FB chunks at a time, each with its 8 slice loads in flight (sc1: the
+// slabs of other XCDs were written through and are read past this CU's L1).
+template <int FB>
+__device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const Fold& f, int m0, int n0, int nsplit) {
+  const int rows = e.M - m0 < BM ? e.M - m0 : BM;
+  const int c4 = (e.N - n0 < BN ? e.N - n0 : BN) / 4;
+  const auto rs = rsrc(e.C, (uint32_t)((size_t)nsplit * e.M * e.N * 4 > 0x7fffffffu ? 0x7fffffffu
+                                                                                    : (size_t)nsplit * e.M * e.N * 4));
+  const uint32_t sstride = (uint32_t)((size_t)e.M * e.N * 4);
+  const int nq = rows * 64;
+  for (int q0 = threadIdx.x; q0 < nq; q0 += THREADS * FB) {
+    float4 acc[FB];
+    uint32_t off[FB];
+    bool ok[FB];
+#pragma unroll
+    for (int b = 0; b < FB; ++b) {
+      const int q = q0 + b * THREADS, r = q >> 6, c = q & 63;
+      ok[b] = q < nq && c < c4;
+      off[b] = ok[b] ? (uint32_t)(((size_t)(m0 + r) * e.N + n0 + 4 * c) * 4) : OOB;
+      acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    int sl = 0;
+    for (; sl + 8 <= nsplit; sl += 8) {
+      u32x4 v[FB][8];
+#pragma unroll
+      for (int b = 0; b < FB; ++b)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[b], (sl + u) * sstride, kSC1);
+#pragma unroll
+      for (int b = 0; b < FB; ++b)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc[b].x += __uint_as_float(v[b][u].x); acc[b].y += __uint_as_float(v[b][u].y);
+          acc[b].z += __uint_as_float(v[b][u].z); acc[b].w += __uint_as_float(v[b][u].w);
+        }
+    }
+    for (; sl < nsplit; ++sl) {
+#pragma unroll
+      for (int b = 0; b < FB; ++b) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off[b], sl * sstride, kSC1);
+        acc[b].x += __uint_as_float(v.x); acc[b].y += __uint_as_float(v.y);
+        acc[b].z += __uint_as_float(v.z); acc[b].w += __uint_as_float(v.w);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < FB; ++b) {
+      if (!ok[b]) continue;
+      const int q = q0 + b * THREADS, r = q >> 6, c = q & 63;
+      float4* o = reinterpret_cast<float4*>(f.out + (size_t)(m0 + r) * f.ld + n0 + 4 * c);
+      float4 a = acc[b];
+      if (f.acc) {
+        const float4 p = *o;
+        a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+      }
+      *o = a;
+    }
+  }
+  (void)x;
+}
+
+template <bool AK, bool BKM, int EPI, bool P8, bool FOLD = false>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int nk, int tilesM,
-             int tilesN, int nsplit, EpiArgs e, Ext x) {
+             int tilesN, int nsplit, EpiArgs e, Ext x, Fold fold) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 2, wn = wid & 3;
   const int nwg = tilesM * tilesN, total = nwg * nsplit;
@@ -630,21 +706,46 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       vm_wait<0>();
       bar();
     }
-    epilogue<EPI, P8, AK>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
+    if constexpr (FOLD) {
+      if (wm == 0) bar();  // align the two wave halves (waves 4-7 run one barrier behind in the K loop)
+    }
+    epilogue<EPI, P8, AK, FOLD>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
                       LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
+    if constexpr (FOLD) {
+      // arrival: every wave's slab stores complete (this also drains the next tile's first DMAs: the K loop's
+      // counted waits then find fewer in flight, which they allow), one ticket per workgroup
+      vm_wait<0>();
+      bar();
+      // the flag word: the A slot of the tile's last K-tile, g - 1 (N/M-major A is triple-buffered: every wave
+      // has read it -- the barrier above -- and the next DMA into it is K-tile g + 2's, issued in the next
+      // tile's first K-tile, after the barriers below)
+      static_assert(!AK, "the in-kernel fold is for the weight-gradient layout (N/M-major A)");
+      volatile int* flag = reinterpret_cast<volatile int*>(smem + a_off<AK>(g - 1));
+      const int tile = (cg.m0 / BM) * tilesN + cg.n0 / BN;
+      if (threadIdx.x == 0)
+        *flag = __hip_atomic_fetch_add(fold.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+      lgkm0();  // the flag's LDS write before the barrier (s_barrier waits for no memory operation on gfx950)
+      bar();
+      if (*flag) {  // workgroup-uniform: the last slice of this tile landed -- fold it
+        fold_tile<2>(e, x, fold, cg.m0, cg.n0, nsplit);
+        if (threadIdx.x == 0) __hip_atomic_store(fold.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      bar();  // the flag word is rewritten by the next tile
+      if (wm == 1) bar();  // re-stagger for the next tile's K loop
+    }
   }
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
   if (wm == 0) bar();
   stamp(1);
 }
 
-template <bool AK, int EPI>
+template <bool AK, int EPI, bool FOLD = false>
 constexpr int lds_total() {
   return lds_bytes<AK>() + ((AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
                                    EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS)) ? 4096 : 0);
 }
 
-template <bool AK, bool BKM, int EPI, bool P8>
+template <bool AK, bool BKM, int EPI, bool P8, bool FOLD = false>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int nk = d->K / split / BK;
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
@@ -661,12 +762,14 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   x.aux = d->aux ? (uint32_t)(((size_t)(d->M - 1) * d->ld_aux + d->N) * (d->aux_dtype == SV_F32 ? 4 : 2)) : 0u;
   x.a = (uint32_t)((AK ? (size_t)(d->M - 1) * d->lda + d->K : (size_t)(d->K - 1) * d->lda + d->M) * 2);
   x.b = (uint32_t)((BKM ? (size_t)(d->N - 1) * d->ldb + d->K : (size_t)(d->K - 1) * d->ldb + d->N) * 2);
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8>), lds_total<AK, EPI>(), s);
+  constexpr int LDS = lds_total<AK, EPI, FOLD>();
+  ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, FOLD>), LDS, s);
   const int total = tilesM * tilesN * split;
   const int grid = policy_grid(&d->policy, total, 1, s);  // persistent: one workgroup per CU (or the cap)
-  gemm9_kernel<AK, BKM, EPI, P8><<<grid, THREADS, lds_total<AK, EPI>(), s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
-                                                                  reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
-                                                                  tilesM, tilesN, split, e, x);
+  const Fold fold{d->fold_out, d->fold_ld, d->fold_accumulate, d->fold_counters};
+  gemm9_kernel<AK, BKM, EPI, P8, FOLD><<<grid, THREADS, LDS, s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
+                                                                 reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
+                                                                 tilesM, tilesN, split, e, x, fold);
   return check_launch("sv_gemm(v9)");
 }
 
@@ -699,6 +802,10 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
       return launch<AK, BKM, SV_EPI_STORE_STATS, true>(d, split, s);
     case SV_EPI_SLAB:
       if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
+      if (d->fold_out) {  // (the weight-gradient layout only: N/M-major A; others fold in a separate pass)
+        if constexpr (AK) return SV_ERR_UNSUPPORTED;
+        else return launch<AK, BKM, SV_EPI_SLAB, false, true>(d, split, s);
+      }
       return launch<AK, BKM, SV_EPI_SLAB, false>(d, split, s);
     default:
       return SV_ERR_UNSUPPORTED;

@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(kThreads) layerscale_finish_kernel(
 // one workgroup per row c of G = sum_p slab[p][c][:]: thread t owns the float4 column groups
 // t, t + 256, ...; dW2[c] += gamma_c G[c], the row dot sum(W2[c] G[c]) and the colsum
 // cs[c] = sum_p cs_part[p][c] are block sums (fixed order), so one kernel finishes dgamma / db2 too.
-__global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float* __restrict__ slab,
+__global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float* __restrict__ slab, int Ps,
                                                                      const float* __restrict__ cs_part, int P,
                                                                      const float* __restrict__ W2,
                                                                      const float* __restrict__ gamma,
@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float
     const size_t off = rowoff + (size_t)gi * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int p = 0;
-    for (; p + 8 <= P; p += 8) {
+    for (; p + 8 <= Ps; p += 8) {
       float4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (size_t)(p + u) * pstride + off);
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
-    for (; p < P; ++p) {
+    for (; p < Ps; ++p) {
       const float4 v = *reinterpret_cast<const float4*>(slab + (size_t)p * pstride + off);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
@@ -583,9 +583,22 @@ int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t 
   SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_reduce: K4=%d must be a multiple of 4", K4);
   SV_REQUIRE((((uintptr_t)slab | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
              "sv_layerscale_wgrad_reduce: buffers must be 16-B aligned");
-  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(slab, cs_part, P, W2, gamma, b2, dW2, dgamma,
+  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(slab, P, cs_part, P, W2, gamma, b2, dW2, dgamma,
                                                                    db2, C, K4);
   return check_launch("sv_layerscale_wgrad_reduce");
+}
+
+int sv_layerscale_wgrad_fold_finish(const float* G, const float* cs_part, int32_t P, const float* W2, const float* gamma,
+                                    const float* b2, float* dW2, float* dgamma, float* db2, int32_t C, int32_t K4,
+                                    sv_stream_t stream) {
+  SV_REQUIRE(G && cs_part && W2 && gamma && b2 && dW2 && dgamma && db2 && P >= 1,
+             "sv_layerscale_wgrad_fold_finish: bad arguments");
+  SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_fold_finish: K4=%d must be a multiple of 4", K4);
+  SV_REQUIRE((((uintptr_t)G | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
+             "sv_layerscale_wgrad_fold_finish: buffers must be 16-B aligned");
+  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(G, 1, cs_part, P, W2, gamma, b2, dW2, dgamma, db2,
+                                                                   C, K4);
+  return check_launch("sv_layerscale_wgrad_fold_finish");
 }
 
 int sv_sqnorm_nparts(int64_t n) {

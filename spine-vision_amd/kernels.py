@@ -123,6 +123,7 @@ def gemm(
     compute_bf16: bool = True,
     bn: "nv.BnRef | None" = None,
     policy: "nv.GemmPolicy | None" = None,
+    fold: tuple | None = None,
 ) -> torch.Tensor:
     """C = epilogue(A(m,k) . B(k,n)); see sv_gemm in include/sv_kernels.h for the layouts.  ``policy``: the
     launch policy of this call (nv.policy(...): kernel family, grid cap, residency, priority); None = defaults."""
@@ -157,6 +158,9 @@ def gemm(
         d.bn = ctypes.pointer(bn)
     if policy is not None:
         d.policy = policy
+    if fold is not None:  # (out, accumulate, counters): the split-K fold inside the GEMM (SV_EPI_SLAB)
+        fo, facc, fcnt = fold
+        d.fold_out, d.fold_ld, d.fold_accumulate, d.fold_counters = ptr(fo), N, int(bool(facc)), ptr(fcnt)
     probes = [p_ for p_ in (PROBES + ([PROBE] if PROBE is not None else [])) if p_.matches(a_kmajor, b_kmajor,
                                                                                       compute_bf16, epilogue)]
     if probes:
@@ -205,8 +209,12 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
 
 
 _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
-# persistent 256x256 wgrads: tiles x split ~ this many workgroups (one per CU; SV_WGRAD9_WGS for A/B runs)
-_WGRAD9_TARGET = int(os.environ.get("SV_WGRAD9_WGS", "256"))
+# persistent 256x256 wgrads: tiles x split ~ this many workgroups (SV_WGRAD9_WGS for A/B runs).  Half the chip
+# (128): the side-stream weight gradients share it with the main stream's data gradients anyway, and half the
+# split depth halves the f32 slabs written and folded -- round 4 on the final kernels: 1072.6-1075.6 vs
+# 1065.7-1067.9 img/s interleaved, fold 4.0 -> 2.5 ms/step (profiles/round4/r7f_fold_ab.txt; round 3 had
+# measured 128 and 256 equal)
+_WGRAD9_TARGET = int(os.environ.get("SV_WGRAD9_WGS", "128"))
 
 
 def _wgrad_split(tiles: int, K: int) -> int:
@@ -230,6 +238,30 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
     return _wgrad_split(-(-N // 128) * -(-K // 128), M)
 
 
+# In-kernel split-K fold of the weight gradients (gemm9.hip: the last workgroup to finish a tile's slice sums the
+# tile; sv_gemm_desc.fold_out), where the separate fold would take sv_reduce_partials' sequential wide body (bitwise
+# the same result) and the slices are few enough for one workgroup to read them.  Opt-in (SV_INKERNEL_FOLD=1):
+# measured slower in the step (1009-1051 vs 1066-1068 img/s interleaved; the one-workgroup fold tail holds up the
+# side stream, profiles/round4/r7f_fold_ab.txt), where halving the split depth instead gains 0.7 %
+_INKERNEL_FOLD = os.environ.get("SV_INKERNEL_FOLD", "0") != "0"
+_FOLD_MAX_SPLIT = int(os.environ.get("SV_FOLD_MAX_SPLIT", "16"))
+_FOLD_COUNTERS: dict = {}
+
+
+def _fold_counters(device, tiles: int) -> torch.Tensor:
+    """Zeroed int32 arrival tickets for in-kernel folds on the current stream (the kernel leaves them zero)."""
+    key = (device, nv._stream())
+    t = _FOLD_COUNTERS.get(key)
+    if t is None or t.numel() < tiles:
+        t = _FOLD_COUNTERS[key] = torch.zeros(max(tiles, 4096), device=device, dtype=torch.int32)
+    return t
+
+
+def _fold_ok(split: int, n: int, out: torch.Tensor, compute_bf16: bool) -> bool:
+    return (_INKERNEL_FOLD and compute_bf16 and 1 < split <= _FOLD_MAX_SPLIT and n >= 65536 and n % 4 == 0
+            and out.dtype == torch.float32 and out.is_contiguous() and out.data_ptr() % 16 == 0)
+
+
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
                  compute_bf16=True, cols=None, defer: list | None = None, policy=None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
@@ -243,6 +275,17 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     split = _wgrad_split_for(N, K, M)
     slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
+    if out is not None and _fold_ok(split, N * K, out, compute_bf16):
+        _check(out.numel() == N * K, "linear_wgrad: bad out")
+        gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
+             C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy,
+             fold=(out, accumulate, _fold_counters(dy2d.device, -(-N // 256) * -(-K // 256))))
+        if cs is not None:
+            if defer is not None:
+                defer.append((cs, bias_out, split, bias_accumulate))
+            else:
+                reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
+        return out
     gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy)
     if out is None:
@@ -278,6 +321,15 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     split = _wgrad_split_for(C, K4, M)
     slab = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.float32)
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
+    G = torch.empty(C * K4, device=dsrc2d.device, dtype=torch.float32)
+    if _fold_ok(split, C * K4, G, compute_bf16):
+        # G = d^T a folded inside the wgrad GEMM; the finish then reads one G instead of `split` slabs
+        gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
+             C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy,
+             fold=(G, False, _fold_counters(dsrc2d.device, -(-C // 256) * -(-K4 // 256))))
+        _timed_call("fold", 4.0 * (3 * C * K4 + (split + 4) * C), "sv_layerscale_wgrad_fold_finish", ptr(G), ptr(cs),
+                    split, ptr(w2), ptr(gamma), ptr(b2), ptr(dw2), ptr(dgamma), ptr(db2), C, K4)
+        return
     gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
          C=slab, C2=cs, split_k=split, compute_bf16=compute_bf16, policy=policy)
     _timed_call("fold", 4.0 * ((split + 2) * C * K4 + (split + 4) * C),

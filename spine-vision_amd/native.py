@@ -64,6 +64,7 @@ class GemmDesc(ctypes.Structure):
         ("compute", _i32),
         ("bn", ctypes.POINTER(BnRef)),
         ("policy", GemmPolicy),
+        ("fold_out", _p), ("fold_ld", _i64), ("fold_accumulate", _i32), ("fold_counters", _p),
     ]
 
 
@@ -128,6 +129,7 @@ _SIGS = {
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_layerscale_wgrad_reduce_ws": [_i32, _i32],
     "sv_layerscale_wgrad_reduce": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
+    "sv_layerscale_wgrad_fold_finish": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_sqnorm_nparts": [_i64],
     "sv_sqnorm_partial": [_p, _i64, _p, _p],
     "sv_clip_coef": [_p, _i32, _f32, _p, _p],

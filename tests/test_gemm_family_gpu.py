@@ -229,3 +229,49 @@ def test_gemm_policy_is_per_call(dev):
     assert torch.equal(ref, capped) and torch.equal(ref, plain)
     with pytest.raises(RuntimeError, match="policy"):
         K.linear_wgrad(dh, y, policy=nv.policy(impl=5))
+
+
+@pytest.mark.parametrize("M,C", [(4096, 128), (131072, 256), (32768, 512), (8192, 1024), (2048 + 512, 512)],
+                         ids=["half-tiles", "S2", "S3", "S4", "ragged-split"])
+def test_wgrad_inkernel_fold_bitwise(dev, M, C):
+    """The split-K fold inside the persistent v9 weight-gradient GEMM (the last workgroup to finish a tile's slice
+    sums it: sv_gemm_desc.fold_out) equals the slabs + separate fold bit for bit -- written or accumulated, under
+    the default grid, a grid cap that makes every workgroup fold several tiles (37), the backward's policy, and the
+    v3 family (slabs + fold pass) -- and so does the layer-scale fc2 finish over the folded G."""
+    g = torch.Generator().manual_seed(M + C)
+    bf = torch.bfloat16
+    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    y = torch.randn(M, C, generator=g).to(bf).to(dev)
+    d = torch.randn(M, C, generator=g).to(bf).to(dev)
+    a = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    w2 = (torch.randn(C, 4 * C, generator=g) * 0.05).to(dev)
+    gam = (torch.rand(C, generator=g) * 0.25 + 0.05).to(dev)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(dev)
+    base = torch.randn(4 * C, C, generator=g).to(dev)
+    base_b = torch.randn(4 * C, generator=g).to(dev)
+
+    saved = (K._INKERNEL_FOLD, K._FOLD_MAX_SPLIT)
+
+    def run(fold, pol):
+        K._INKERNEL_FOLD = fold
+        K._FOLD_MAX_SPLIT = 64  # also the deeper splits (C = 128: 64 slices of half-empty 256x256 tiles)
+        try:
+            o1, b1 = base.clone(), base_b.clone()
+            K.linear_wgrad(dh, y, out=o1, accumulate=True, bias_out=b1, policy=pol)
+            o2 = torch.empty(4 * C, C, device=dev)
+            K.linear_wgrad(dh, y, out=o2, accumulate=False, policy=pol)
+            dw2, dga, db = base.t().contiguous().clone(), gam.clone() * 0.5, b2.clone() * 0.5
+            K.layerscale_wgrad(d, a, w2, gam, b2, dw2=dw2, dgamma=dga, db2=db, policy=pol)
+            torch.cuda.synchronize()
+            return o1, b1, o2, dw2, dga, db
+        finally:
+            K._INKERNEL_FOLD, K._FOLD_MAX_SPLIT = saved
+
+    split = K._wgrad_split_for(4 * C, C, M)
+    ref = run(False, None)
+    for pol in (None, nv.policy(grid_cap=37), nv.policy(wg_per_cu=1, priority=1, grid_cap=224), nv.policy(impl=3)):
+        # (v3 sums the fused bias column in its own order: its reference is its own slabs + fold)
+        r_ = run(False, pol) if pol is not None and pol.impl == 3 else ref
+        got = run(True, pol)
+        for i, (r, o) in enumerate(zip(r_, got)):
+            assert torch.equal(r, o), (pol, i, split, float((r - o).abs().max()))
