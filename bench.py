@@ -62,11 +62,12 @@ PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsam
                "fold": "split-K / partial-sum folds (reduce_multi, reduce_pair, layer-scale fold): bytes = the slab "
                        "bytes they move, overhead of split-K rather than algorithmic work"}
 # step-time cost of the data-parallel CU reserve (SV_COMM_RESERVE_CUS, default 0 = none) measured at world 1
-# (SV_BENCH_RESERVE A/B, interleaved on one box; DESIGN.md "Multi-GPU": 32 CUs by grid caps 2.2 %, by CU masks
-# 12-24 %), and the measured worst start latency of a comm-stream kernel behind the backward's GEMMs without a
-# reserve (tests/test_comm_reserve_gpu.py: 0.2-0.41 ms): both folded into dp_rehearsal's predicted scaling
+# (SV_BENCH_RESERVE A/B, interleaved on one box; DESIGN.md "Multi-GPU": 32 CUs by grid caps 0.6-0.7 %, by CU masks
+# 12-24 %), and the start latency of a comm-stream kernel after a readiness report (tests/test_comm_reserve_gpu.py
+# over five boxes: worst 0.2-2.9 ms during the backward; at its end, with nothing else queued, the 14-19 us of an
+# idle wake-up, tools/event_wake_probe.py -- charged as 0.05 ms): folded into dp_rehearsal's predicted scaling
 RESERVE_COST = float(os.environ.get("SV_RESERVE_COST", "0.0"))
-COMM_DELAY_MS = float(os.environ.get("SV_COMM_DELAY_MS", "0.41"))
+COMM_DELAY_MS = (float(os.environ.get("SV_COMM_DELAY_MS", "2.9")), float(os.environ.get("SV_COMM_DELAY_END_MS", "0.05")))
 # HBM-bound kernel classes timed by kernels.OpProbe (reported separately against 8 TB/s)
 OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "fold")
 
@@ -720,7 +721,7 @@ def main():
             # the reserve's own cost (32 of 256 CUs masked from the step under data parallelism), measured at
             # world 1 as an interleaved A/B (SV_BENCH_RESERVE, DESIGN.md "Multi-GPU"), stretches every time
             "reserve_cost_frac": RESERVE_COST,
-            "comm_launch_delay_ms": COMM_DELAY_MS,
+            "comm_launch_delay_ms": list(COMM_DELAY_MS),
             "predictions": [timeline.predict(ready, bwd_end, ms, 8, bw, reserve_cost=RESERVE_COST,
                                              launch_delay_ms=COMM_DELAY_MS) for bw in (200.0, 300.0, 400.0)],
         }

@@ -242,23 +242,26 @@ class BucketTimeline:
 
     @staticmethod
     def predict(ready: list, bwd_end_ms: float, step_ms: float, world: int, busbw_gbs: float,
-                reserve_cost: float = 0.0, launch_delay_ms: float = 0.0) -> dict:
+                reserve_cost: float = 0.0, launch_delay_ms=0.0) -> dict:
         """Exposed exchange and scaling at ``world`` ranks if every bucket's ring all-reduce takes
         2 (n-1)/n x bytes / busbw on one comm stream, launched at its ready time (a bucket never ready in the
         backward launches at its end); the step grows by what finishes after the backward's end.
         ``reserve_cost``: the measured fractional slowdown of the step under the data-parallel CU reserve,
         which stretches the whole timeline (ready times, backward end, step) before the exchange is added;
-        ``launch_delay_ms``: how long a comm kernel may wait for a CU behind the backward's GEMMs (every bucket
-        is assumed to start that late after its ready time)."""
+        ``launch_delay_ms``: how long a comm kernel may wait behind the backward's kernels after its ready event,
+        (during the backward, the end of the backward): a bucket ready before the backward's end starts that late;
+        one a scalar applies to both."""
         f = 1.0 + reserve_cost
         bwd_end_ms, step_dp = bwd_end_ms * f, step_ms * f
+        d_mid, d_end = launch_delay_ms if isinstance(launch_delay_ms, (tuple, list)) else (launch_delay_ms,) * 2
         t = 0.0
         for mb, r in sorted(ready, key=lambda x: (x[1] is None, x[1] if x[1] is not None else 0.0)):
-            start = max(t, (r * f if r is not None else bwd_end_ms) + launch_delay_ms)
+            rr = r * f if r is not None else bwd_end_ms
+            start = max(t, rr + (d_mid if rr < bwd_end_ms - 1e-6 else d_end))
             t = start + 2.0 * (world - 1) / world * mb * 2**20 / (busbw_gbs * 1e9) * 1e3
         exposed = max(0.0, t - bwd_end_ms)
         return {"world": world, "busbw_gbs": busbw_gbs, "reserve_cost_frac": reserve_cost,
-                "launch_delay_ms": launch_delay_ms,
+                "launch_delay_ms": [d_mid, d_end],
                 "comm_end_ms": round(t, 3), "exposed_ms": round(exposed, 3),
                 "predicted_step_ms": round(step_dp + exposed, 3),
                 "predicted_scaling": round(world * step_ms / (step_dp + exposed), 3)}
