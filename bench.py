@@ -456,6 +456,11 @@ def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: d
         "hbm_gbs": round(gbs, 1),
         "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
     }
+    shares = getattr(probe, "shares", None)
+    if shares and len(shares) == len(probe.events):
+        durs = [a.elapsed_time(b) for a, b in probe.events]
+        share = sum(d * s for d, s in zip(durs, shares)) / max(sum(durs), 1e-30)
+        out.update({"granted_cu_share": round(share, 3), "frac_of_granted_cus": round(ach / (pk * share), 4)})
     if fma:
         out.update({"valu_gfma_per_launch": round(fma / 1e9, 3), "valu_tfma": round(tfma, 2),
                     "valu_frac": round(tfma / PEAK_VALU_TFMA, 4)})

@@ -34,6 +34,10 @@ class GemmProbe:
         self.flops = 0.0
         self.bytes = 0.0
         self.launches = 0
+        # per launch: the fraction of the chip's CUs its grid is sized for (256x256 tiles x split-K slices, capped
+        # by the policy's grid cap), so a class that runs on part of the chip by design can be read against the
+        # peak of the CUs it was given (bench.py: frac_of_granted_cus)
+        self.shares: list[float] = []
 
     def matches(self, a_kmajor: bool, b_kmajor: bool, bf: bool, epilogue: int) -> bool:
         k = (bool(a_kmajor), bool(b_kmajor), bool(bf))
@@ -86,6 +90,16 @@ def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0) -> None:
     pr.bytes += nbytes
     pr.fma += fma
     pr.launches += 1
+
+
+_CUS: dict = {}
+
+
+def _device_cus(device) -> int:
+    n = _CUS.get(device)
+    if n is None:
+        n = _CUS[device] = torch.cuda.get_device_properties(device).multi_processor_count
+    return n
 
 
 def _check(cond: bool, msg: str) -> None:
@@ -181,8 +195,12 @@ def gemm(
                 nbytes += M * N * C2.element_size()
         if aux is not None:
             nbytes += M * N * aux.element_size()
+        cus = _device_cus(C.device)
+        cap = policy.grid_cap if policy is not None and policy.grid_cap > 0 else cus
+        share = min(-(-M // 256) * -(-N // 256) * max(split_k, 1), cap, cus) / cus
         for p_ in probes:
             p_.events.append((ev0, ev1))
+            p_.shares.append(share)
             p_.flops += 2.0 * M * N * K
             p_.bytes += nbytes
             p_.launches += 1
