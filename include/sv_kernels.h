@@ -499,6 +499,37 @@ int sv_bn_relu_bwd_apply_pool(const float* dpool, const uint8_t* idx, int32_t B,
                               int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
                               const float* beta, const float* sums, void* dx, int32_t dx_dtype, int32_t C,
                               sv_stream_t stream);
+/* One launch per BatchNorm for small row counts (rows <= SV_BN_SMALL_MAX_ROWS and the geometry
+ * sv_bn_small_ok accepts: ResNet layers 3-4 at 256 px).  One workgroup owns 8 channels over all rows, so
+ * the statistics and the pass that uses them share the launch; the sums are taken in the multi-launch
+ * path's order, so every output is bit for bit what that path writes:
+ *   sv_bn_bwd_small  mode SV_BN_SMALL_MASK  = sv_bn_bwd_stats_mask + sv_bn_bwd_finish + sv_bn_bwd_apply (act == NULL)
+ *                    mode SV_BN_SMALL_RELU  = sv_bn_relu_bwd_stats + finish + sv_bn_relu_bwd_apply; with `part`
+ *                                             (nparts, e.g. from sv_conv_bwd_data_bn) the statistics pass is skipped
+ *                    mode SV_BN_SMALL_DUAL  = sv_bn_bwd_stats_mask_dual + two finishes + sv_bn_bwd_apply_dual
+ *                    batch_stats == 0: eval-mode apply (zero correction sums; dgamma / dbeta still accumulate)
+ *   sv_bn_act_small  = sv_bn_stats_finish(y = NULL, part) + sv_bn_act_fwd, and with res_part the shortcut
+ *                      BatchNorm's finish too (res = its conv output).  All pointers 16-B aligned.
+ * Replaces: timm Bottleneck bn1/bn2/bn3/downsample BatchNorm2d forward + autograd backward
+ * (spine_vision/training/models/backbone.py:166 -> timm resnet.py).                                  */
+#define SV_BN_SMALL_MAX_ROWS 8192
+#define SV_BN_SMALL_MASK 0
+#define SV_BN_SMALL_RELU 1
+#define SV_BN_SMALL_DUAL 2
+int sv_bn_small_ok(int64_t rows, int32_t C);
+int sv_bn_bwd_small(int32_t mode, void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                    int32_t y_dtype, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                    const void* y2, int32_t y2_dtype, const float* mean2, const float* rstd2, const float* gamma2,
+                    const float* part, int32_t nparts, void* dx, void* dx2, int32_t dx_dtype, float* dgamma,
+                    float* dbeta, float* dgamma2, float* dbeta2, int32_t batch_stats, int64_t rows, int32_t C,
+                    sv_stream_t stream);
+int sv_bn_act_small(const void* y, int32_t y_dtype, const float* part, int32_t nparts, float eps, float momentum,
+                    const float* gamma, const float* beta, float* mean, float* rstd, float* running_mean,
+                    float* running_var, int64_t* num_batches_tracked, const void* res, int32_t res_dtype,
+                    const float* res_part, int32_t res_nparts, float res_eps, float res_momentum,
+                    const float* res_gamma, const float* res_beta, float* res_mean, float* res_rstd,
+                    float* res_running_mean, float* res_running_var, int64_t* res_num_batches_tracked, int32_t relu,
+                    void* out, int32_t out_dtype, int64_t rows, int32_t C, sv_stream_t stream);
 /* g = dout * (act > 0), f32 out (block-output ReLU of the residual join).                         */
 int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g, int64_t n,
                  sv_stream_t stream);

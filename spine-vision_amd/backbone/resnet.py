@@ -240,6 +240,18 @@ class ResNetHip(nn.Module):
             return mean, rstd
         return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
 
+    def _small_bn(self, y4d: torch.Tensor, part: torch.Tensor | None) -> bool:
+        """Train-mode BatchNorm whose statistics partials the conv produced and whose rows are few enough for the
+        one-launch form (K.bn_act_small)."""
+        return (self.training and part is not None and K.bn_small_ok(y4d.numel() // y4d.shape[-1], y4d.shape[-1])
+                and part.data_ptr() % 16 == 0)
+
+    @staticmethod
+    def _bn_params(bn: nn.BatchNorm2d) -> tuple:
+        momentum = 0.1 if bn.momentum is None else bn.momentum
+        return (bn.weight.detach(), bn.bias.detach(), bn.eps, momentum, bn.running_mean, bn.running_var,
+                bn.num_batches_tracked)
+
     def _conv(self, x4d, conv, k, stride, pad, Cin=None, packed=None):
         """conv(x) -> (y, packed weight, shape, BN-statistics partials or None); y in the activation dtype.
         In train mode (bf16) the conv GEMM's epilogue also emits the following BatchNorm's statistics.
@@ -339,33 +351,54 @@ class ResNetHip(nn.Module):
             cur = x
             saved = []
             convs = blk.convs()
+            last_part = None  # the last BatchNorm's partials when its statistics join the residual launch
             for ci, (conv, bn, k, st, pad, relu) in enumerate(convs):
                 y, wp, s, part = self._conv(cur, conv, k, st, pad, packed=packed)
                 Bq, Hq, Wq, Cq = y.shape
-                mean, rstd = self._bn(bn, y.view(-1, Cq), part)
                 last = ci == len(convs) - 1
+                small = self._small_bn(y, part)
                 if not last:
-                    a = K.bn_act(y.view(-1, Cq), mean, rstd, bn.weight, bn.bias, relu=True, out_dtype=act)
+                    if small:  # statistics fold + BatchNorm + ReLU in one launch (bit for bit the two below)
+                        a, mean, rstd = K.bn_act_small(y.view(-1, Cq), part, self._bn_params(bn), relu=True,
+                                                       out_dtype=act)
+                    else:
+                        mean, rstd = self._bn(bn, y.view(-1, Cq), part)
+                        a = K.bn_act(y.view(-1, Cq), mean, rstd, bn.weight, bn.bias, relu=True, out_dtype=act)
                     a = a.view(Bq, Hq, Wq, Cq)
                     saved.append((cur, y, mean, rstd, a, wp, s))
                     cur = a
+                elif small:
+                    last_part = part
+                    saved.append((cur, y, None, None, None, wp, s))
                 else:
+                    mean, rstd = self._bn(bn, y.view(-1, Cq), part)
                     saved.append((cur, y, mean, rstd, None, wp, s))
             # residual join: out = relu(bn_last(y) + shortcut), shortcut = x or BN(conv_ds(x))
-            _, y_last, m_last, r_last, _, _, _ = saved[-1]
+            c_last, y_last, m_last, r_last, _, wp_last, s_last = saved[-1]
             bn_last = convs[-1][1]
             Bq, Hq, Wq, Cq = y_last.shape
             ds_saved = None
             if blk.downsample is not None:
                 dconv, dbn = blk.downsample[0], blk.downsample[1]
                 yd, wpd, sd, pd = self._conv(x_in, dconv, 1, blk.stride, 0)
-                md, rd = self._bn(dbn, yd.view(-1, Cq), pd)
-                out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias, res=yd.view(-1, Cq),
-                               res_bn=(md, rd, dbn.weight, dbn.bias), relu=True, out_dtype=act)
+                if last_part is not None and self._small_bn(yd, pd):
+                    out, m_last, r_last, md, rd = K.bn_act_small(
+                        y_last.view(-1, Cq), last_part, self._bn_params(bn_last), res=yd.view(-1, Cq), res_part=pd,
+                        res_params=self._bn_params(dbn), relu=True, out_dtype=act)
+                else:
+                    if last_part is not None:
+                        m_last, r_last = self._bn(bn_last, y_last.view(-1, Cq), last_part)
+                    md, rd = self._bn(dbn, yd.view(-1, Cq), pd)
+                    out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias,
+                                   res=yd.view(-1, Cq), res_bn=(md, rd, dbn.weight, dbn.bias), relu=True, out_dtype=act)
                 ds_saved = (yd, md, rd, wpd, sd)
+            elif last_part is not None:
+                out, m_last, r_last = K.bn_act_small(y_last.view(-1, Cq), last_part, self._bn_params(bn_last),
+                                                     res=x_in.view(-1, Cq), relu=True, out_dtype=act)
             else:
                 out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias,
                                res=x_in.view(-1, Cq), relu=True, out_dtype=act)
+            saved[-1] = (c_last, y_last, m_last, r_last, None, wp_last, s_last)
             out = out.view(Bq, Hq, Wq, Cq)
             if save:
                 tape.blocks.append((x_in, saved, ds_saved, out))

@@ -69,6 +69,17 @@ __device__ __forceinline__ void stv(void* p, int dt, size_t i, const float (&v)[
     st4d(p, dt, i, make_float4(v[0], v[1], v[2], v[3]));
   }
 }
+// the elementwise forms every pass shares (so the one-launch small-row kernels at the end of this file give
+// the multi-launch path's bits): the affine pre-activation and the train-mode data gradient, every fused
+// multiply-add written out -- hipcc contracts a*b+c by context (a product hoisted out of a loop or shared by two
+// expressions stays unfused), which would let two kernels computing the same formula round differently
+__device__ __forceinline__ float bn_pre(float g, float rs, float v, float mu, float b) { return fmaf(g * rs, v - mu, b); }
+__device__ __forceinline__ float bn_dx(float ga, float rs, float g, float sg, float v, float mu, float sgx, float inv_n) {
+  const float a1 = fmaf(-sg, inv_n, g);                 // g - sum g / n
+  const float xs = ((v - mu) * rs) * sgx;               // xhat * sum g xhat
+  return (ga * rs) * fmaf(-xs, inv_n, a1);              // gamma rstd (g - sum g / n - xhat sum g xhat / n)
+}
+
 template <int V>
 __device__ __forceinline__ void ldp(const float* p, int c, float (&o)[V]) {
 #pragma unroll
@@ -218,6 +229,21 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, in
   return true;
 }
 
+// batch statistics of channel c from its (shifted by k) sums; running statistics updated torch's way
+__device__ __forceinline__ float bn_finish_channel(float s1, float s2, float k, int64_t rows, float eps, float momentum,
+                                                   int c, float* mean, float* rstd, float* rmean, float* rvar) {
+  const float n = (float)rows;
+  const float m1 = s1 / n;
+  const float var = fmaxf(fmaf(-m1, m1, s2 / n), 0.f);
+  const float mu = k + m1;
+  const float r = 1.0f / sqrtf(var + eps);
+  mean[c] = mu;
+  rstd[c] = r;
+  if (rmean) rmean[c] = fmaf(momentum, mu, (1.f - momentum) * rmean[c]);
+  if (rvar) rvar[c] = fmaf(momentum, rows > 1 ? (var * n) / (n - 1.f) : var, (1.f - momentum) * rvar[c]);
+  return r;
+}
+
 __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
     const void* __restrict__ y, int ydt, const float* __restrict__ part, int P, int64_t rows, int C, float eps,
     float momentum, float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rmean,
@@ -229,14 +255,7 @@ __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
   // shift k: row 0 of y (sv_bn_stats partials); y == NULL: unshifted partials (SV_EPI_STORE_STATS)
   const float k = y == nullptr ? 0.f
                   : ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
-  const float n = (float)rows;
-  const float m1 = s1 / n;
-  const float var = fmaxf(s2 / n - m1 * m1, 0.f);
-  const float mu = k + m1;
-  mean[c] = mu;
-  rstd[c] = 1.0f / sqrtf(var + eps);
-  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
-  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (rows > 1 ? var * n / (n - 1.f) : var);
+  bn_finish_channel(s1, s2, k, rows, eps, momentum, c, mean, rstd, rmean, rvar);
 }
 
 __global__ void eval_params_kernel(const float* __restrict__ rm, const float* __restrict__ rv, float eps,
@@ -270,7 +289,7 @@ __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
     ldp<V>(a.gamma, c, g);
     ldp<V>(a.beta, c, b);
 #pragma unroll
-    for (int q = 0; q < V; ++q) o[q] = fmaf(g[q] * rs[q], v[q] - mu[q], b[q]);
+    for (int q = 0; q < V; ++q) o[q] = bn_pre(g[q], rs[q], v[q], mu[q], b[q]);
     if (a.res) {
       float r[V];
       ldv<V>(a.res, a.rdt, e, r);
@@ -281,7 +300,7 @@ __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
         ldp<V>(a.rgamma, c, rg);
         ldp<V>(a.rbeta, c, rb);
 #pragma unroll
-        for (int q = 0; q < V; ++q) r[q] = fmaf(rg[q] * rr[q], r[q] - rm[q], rb[q]);
+        for (int q = 0; q < V; ++q) r[q] = bn_pre(rg[q], rr[q], r[q], rm[q], rb[q]);
       }
 #pragma unroll
       for (int q = 0; q < V; ++q) o[q] += r[q];
@@ -367,7 +386,7 @@ __device__ __forceinline__ void grad_masked(const void* dout, int ddt, const voi
     ldp<V>(gamma, c, ga);
     ldp<V>(beta, c, be);
 #pragma unroll
-    for (int q = 0; q < V; ++q) g[q] = fmaf(ga[q] * rs[q], v[q] - mu[q], be[q]) > 0.f ? g[q] : 0.f;
+    for (int q = 0; q < V; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
   } else {
     if (act) {
       float m[V];
@@ -552,7 +571,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
     ldp<V>(a.sums + a.C, c, sgx);
 #pragma unroll
     for (int q = 0; q < V; ++q)
-      o[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (v[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+      o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
     stv<V>(a.dx, a.xdt, e, o);
     if (a.gmask) stv<V>(a.gmask, SV_F32, e, g);
   }
@@ -588,7 +607,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_dual_kernel(const BwdDualA
     ldp<V>(a.sums + a.C, c, sgx);
 #pragma unroll
     for (int q = 0; q < V; ++q)
-      o[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (v[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+      o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
     ldp<V>(a.mean2, c, mu);
     ldp<V>(a.rstd2, c, rs);
     ldp<V>(a.gamma2, c, ga);
@@ -596,7 +615,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_dual_kernel(const BwdDualA
     ldp<V>(a.sums2 + a.C, c, sgx);
 #pragma unroll
     for (int q = 0; q < V; ++q)
-      o2[q] = ga[q] * rs[q] * (g[q] - sg[q] * inv_n - (w[q] - mu[q]) * rs[q] * sgx[q] * inv_n);
+      o2[q] = bn_dx(ga[q], rs[q], g[q], sg[q], w[q], mu[q], sgx[q], inv_n);
     stv<V>(a.dx, a.xdt, e, o);
     stv<V>(a.dx2, a.xdt, e, o2);
   }
@@ -706,6 +725,288 @@ __global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const float* __re
     const int64_t b = e / ((int64_t)HW * C);
     const float4 g = *reinterpret_cast<const float4*>(dfeat + b * C + c);
     *reinterpret_cast<float4*>(dx + e) = make_float4(g.x * inv, g.y * inv, g.z * inv, g.w * inv);
+  }
+}
+
+
+// ---- one launch per BatchNorm for small row counts (ResNet layers 3-4 at 256 px: rows <= 8192) ------------
+// Every BatchNorm backward above is three launches (statistics partials, their fold, the apply) and every
+// train-mode forward two (the fold of the conv epilogue's partials, the activation).  At layers 3-4 each of
+// those kernels costs 4-7 us of launch and fill whatever its bytes.  Here ONE workgroup
+// of 1024 threads owns 8 channels over ALL rows, so the statistics need no other workgroup and the pass that
+// uses them follows in the same launch.  The arithmetic is the multi-launch path's, in its order:
+//   * thread t is "cell" (p, rsub) of bwd_stats_kernel's geometry (nparts_for: P parts of rpp rows, rp row
+//     groups per part): it sums rows p*rpp + rsub, + rp, .. in ascending order, as that kernel's thread does;
+//   * the rp cells of a part are added in rsub order (reduce_write), and the P part sums are folded in
+//     fold_partials' order (128 streams of 4 accumulators, then the streams in order);
+// so sums, gamma / beta gradients, data gradients (and the forward's mean, rstd, running statistics and
+// activation) are bit for bit the multi-launch results (tests/test_bn_small_gpu.py).  Channel slices are dealt
+// XCD-contiguously (blocks b and b + 8 share an XCD under round-robin placement and get neighbouring slices),
+// so the 8 slices of one 128-B bf16 line read it through one L2.
+constexpr int kSmallThreads = 1024, kSmallStreams = 128;
+
+__device__ __forceinline__ int small_slice(int G) {
+  const int b = blockIdx.x;
+  return (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
+
+// fold_partials' order for channel c + q of one sum: stream j (0..127) over parts j, j + 128, ..; -> stream sum
+template <typename F>
+__device__ __forceinline__ float stream_fold(F&& part_at, int j, int P) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int p = j;
+  for (; p + 3 * kSmallStreams < P; p += 4 * kSmallStreams) {
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = part_at(p + u * kSmallStreams);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += x[u];
+  }
+  for (; p < P; p += kSmallStreams) a[0] += part_at(p);
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+struct SmallBwdArgs {
+  void* dout; int ddt;             // MODE 0 / 2: f32, overwritten with g = dout * (act > 0)
+  const void* act; int adt;
+  const void* y; int ydt;
+  const float *mean, *rstd, *gamma, *beta;  // beta: MODE 1 (the BN's own ReLU, recomputed from y)
+  const void* y2; int y2dt;                 // MODE 2: the projection shortcut's BatchNorm
+  const float *mean2, *rstd2, *gamma2;
+  const float* part; int npart;             // GIVEN: the statistics partials [npart][2][C] its producer summed
+  void* dx; void* dx2; int xdt;
+  float *dgamma, *dbeta, *dgamma2, *dbeta2;
+  int batch_stats;
+  int rows, C, P, rp, rpp;                  // nparts_for geometry
+};
+
+// MODE 0: act-mask form in place (sv_bn_bwd_stats_mask + finish + apply); 1: ReLU recomputed from y
+// (sv_bn_relu_bwd_stats + finish + apply; GIVEN: the statistics pass skipped, `part` folded); 2: dual
+// (sv_bn_bwd_stats_mask_dual + two finishes + sv_bn_bwd_apply_dual)
+template <int MODE, bool GIVEN>
+__global__ void __launch_bounds__(kSmallThreads) bwd_small_kernel(const SmallBwdArgs a) {
+  constexpr int NS = MODE == 2 ? 3 : 2;
+  __shared__ float cell[GIVEN ? 1 : kSmallThreads][NS][8];
+  __shared__ float fold[NS][kSmallStreams][8];
+  __shared__ float tot[NS][8];
+  const int t = threadIdx.x;
+  const int c = small_slice(a.C >> 3) * 8;
+  float mu[8], rs[8], be[8], mu2[8], rs2[8];
+  ldp<8>(a.mean, c, mu);
+  ldp<8>(a.rstd, c, rs);
+  if constexpr (MODE == 1) ldp<8>(a.beta, c, be);
+  if constexpr (MODE == 2) {
+    ldp<8>(a.mean2, c, mu2);
+    ldp<8>(a.rstd2, c, rs2);
+  }
+  const int cells = a.P * a.rp;
+  const int p = t / a.rp, rsub = t - p * a.rp;
+  const int r0 = p * a.rpp + rsub;
+  const int r1 = min((p + 1) * a.rpp, a.rows);
+  float ga[8];
+  ldp<8>(a.gamma, c, ga);
+  if constexpr (!GIVEN) {
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s1[q] = s2[q] = s3[q] = 0.f;
+    if (t < cells) {
+      for (int r = r0; r < r1; r += a.rp) {
+        const size_t e = (size_t)r * a.C + c;
+        float v[8], g[8];
+        ldv<8>(a.y, a.ydt, e, v);
+        ldv<8>(a.dout, a.ddt, e, g);
+        if constexpr (MODE == 1) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
+        } else {
+          float m[8];
+          ldv<8>(a.act, a.adt, e, m);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) g[q] = m[q] > 0.f ? g[q] : 0.f;
+          stv<8>(a.dout, SV_F32, e, g);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          s1[q] += g[q];
+          s2[q] = fmaf(g[q], (v[q] - mu[q]) * rs[q], s2[q]);
+        }
+        if constexpr (MODE == 2) {
+          float w[8];
+          ldv<8>(a.y2, a.y2dt, e, w);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) s3[q] = fmaf(g[q], (w[q] - mu2[q]) * rs2[q], s3[q]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      cell[t][0][q] = s1[q];
+      cell[t][1][q] = s2[q];
+      if constexpr (MODE == 2) cell[t][2][q] = s3[q];
+    }
+    __syncthreads();
+    // part sums in reduce_write's order, written over the part's first cell (its own)
+    for (int i = t; i < a.P * 8; i += kSmallThreads) {
+      const int pp = i >> 3, q = i & 7;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        float acc = cell[pp * a.rp][k][q];
+        for (int r = 1; r < a.rp; ++r) acc += cell[pp * a.rp + r][k][q];
+        cell[pp * a.rp][k][q] = acc;
+      }
+    }
+    __syncthreads();
+  }
+  {
+    const int j = t >> 3, q = t & 7;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      if constexpr (GIVEN)
+        fold[k][j][q] = stream_fold([&](int pp) { return a.part[(size_t)pp * 2 * a.C + (size_t)k * a.C + c + q]; }, j,
+                                    a.npart);
+      else
+        fold[k][j][q] = stream_fold([&](int pp) { return cell[pp * a.rp][k][q]; }, j, a.P);
+    }
+  }
+  __syncthreads();
+  if (t < NS * 8) {
+    const int k = t >> 3, q = t & 7;
+    float sum = 0.f;
+    for (int i = 0; i < kSmallStreams; ++i) sum += fold[k][i][q];
+    tot[k][q] = sum;
+    if (k == 0) {
+      if (a.dbeta) a.dbeta[c + q] += sum;
+      if (MODE == 2 && a.dbeta2) a.dbeta2[c + q] += sum;
+    } else if (k == 1) {
+      if (a.dgamma) a.dgamma[c + q] += sum;
+    } else {
+      if (a.dgamma2) a.dgamma2[c + q] += sum;
+    }
+  }
+  __syncthreads();
+  float sg[8], sgx[8], sgx2[8], ga2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    sg[q] = a.batch_stats ? tot[0][q] : 0.f;
+    sgx[q] = a.batch_stats ? tot[1][q] : 0.f;
+    sgx2[q] = (MODE == 2 && a.batch_stats) ? tot[NS - 1][q] : 0.f;
+  }
+  if constexpr (MODE == 2) ldp<8>(a.gamma2, c, ga2);
+  const float inv_n = 1.0f / (float)a.rows;
+  // the apply over this thread's own cell rows (MODE 0 / 2 read back the g they wrote)
+  if (t < cells) {
+    for (int r = r0; r < r1; r += a.rp) {
+      const size_t e = (size_t)r * a.C + c;
+      float v[8], g[8], o[8];
+      ldv<8>(a.y, a.ydt, e, v);
+      if constexpr (MODE == 1) {
+        ldv<8>(a.dout, a.ddt, e, g);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
+      } else {
+        ldv<8>(a.dout, SV_F32, e, g);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
+      stv<8>(a.dx, a.xdt, e, o);
+      if constexpr (MODE == 2) {
+        float w[8], o2[8];
+        ldv<8>(a.y2, a.y2dt, e, w);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o2[q] = bn_dx(ga2[q], rs2[q], g[q], sg[q], w[q], mu2[q], sgx2[q], inv_n);
+        stv<8>(a.dx2, a.xdt, e, o2);
+      }
+    }
+  }
+}
+
+// The train-mode forward from the conv epilogue's UNSHIFTED partials [P][2][C]: fold (sv_bn_stats_finish with
+// y == NULL, same order), mean / rstd / running statistics, then out = act(BN(y) + res) as act_kernel computes it,
+// res = the identity shortcut or (RBN) the projection shortcut's BN from its own partials.
+struct SmallActArgs {
+  const void* y; int ydt;
+  const float* part; int P; float eps, momentum;
+  const float *gamma, *beta;
+  float *mean, *rstd, *rmean, *rvar; int64_t* nbt;
+  const void* res; int rdt;
+  const float* rpart; int rP; float reps, rmomentum;
+  const float *rgamma, *rbeta;
+  float *rmean_o, *rrstd_o, *rrmean, *rrvar; int64_t* rnbt;
+  int relu; void* out; int odt;
+  int rows, C;
+};
+
+template <bool RES, bool RBN>
+__global__ void __launch_bounds__(kSmallThreads) act_small_kernel(const SmallActArgs a) {
+  constexpr int NB = RBN ? 2 : 1;
+  __shared__ float fold[NB][2][kSmallStreams][8];
+  __shared__ float stat[NB][2][8];
+  const int t = threadIdx.x;
+  const int c = small_slice(a.C >> 3) * 8;
+  if (blockIdx.x == 0 && t == 0) {
+    if (a.nbt) a.nbt[0] += 1;
+    if (RBN && a.rnbt) a.rnbt[0] += 1;
+  }
+  {
+    const int j = t >> 3, q = t & 7;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const float* part = nb ? a.rpart : a.part;
+      const int P = nb ? a.rP : a.P;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        fold[nb][k][j][q] = stream_fold([&](int pp) { return part[(size_t)pp * 2 * a.C + (size_t)k * a.C + c + q]; }, j, P);
+    }
+  }
+  __syncthreads();
+  if (t < NB * 8) {
+    const int nb = t >> 3, q = t & 7;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < kSmallStreams; ++i) s1 += fold[nb][0][i][q];
+    for (int i = 0; i < kSmallStreams; ++i) s2 += fold[nb][1][i][q];
+    if (nb == 0)
+      bn_finish_channel(s1, s2, 0.f, a.rows, a.eps, a.momentum, c + q, a.mean, a.rstd, a.rmean, a.rvar);
+    else
+      bn_finish_channel(s1, s2, 0.f, a.rows, a.reps, a.rmomentum, c + q, a.rmean_o, a.rrstd_o, a.rrmean, a.rrvar);
+    stat[nb][0][q] = nb ? a.rmean_o[c + q] : a.mean[c + q];
+    stat[nb][1][q] = nb ? a.rrstd_o[c + q] : a.rstd[c + q];
+  }
+  __syncthreads();
+  float mu[8], rs[8], g[8], b[8], rm[8], rr[8], rg[8], rb[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    mu[q] = stat[0][0][q];
+    rs[q] = stat[0][1][q];
+    rm[q] = stat[NB - 1][0][q];
+    rr[q] = stat[NB - 1][1][q];
+  }
+  ldp<8>(a.gamma, c, g);
+  ldp<8>(a.beta, c, b);
+  if constexpr (RBN) {
+    ldp<8>(a.rgamma, c, rg);
+    ldp<8>(a.rbeta, c, rb);
+  }
+  for (int r = t; r < a.rows; r += kSmallThreads) {
+    const size_t e = (size_t)r * a.C + c;
+    float v[8], o[8];
+    ldv<8>(a.y, a.ydt, e, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = bn_pre(g[q], rs[q], v[q], mu[q], b[q]);
+    if constexpr (RES) {
+      float x[8];
+      ldv<8>(a.res, a.rdt, e, x);
+      if constexpr (RBN) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = bn_pre(rg[q], rr[q], x[q], rm[q], rb[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] += x[q];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = fmaxf(o[q], 0.f);
+    }
+    stv<8>(a.out, a.odt, e, o);
   }
 }
 
@@ -1001,4 +1302,85 @@ extern "C" int sv_bn_bwd_apply_dual(const float* g, const void* y, int32_t y_dty
   else
     bwd_apply_dual_kernel<4><<<grid_for(rows * C / 4), kThreads, 0, st>>>(a);
   return check_launch("sv_bn_bwd_apply_dual");
+}
+
+// ---- one-launch small-row BatchNorm (see bwd_small_kernel) --------------------------------------------------
+static bool small_geo(int64_t rows, int32_t C, RedGeo& g, int& P, int& rpp) {
+  if (rows <= 0 || rows > SV_BN_SMALL_MAX_ROWS || C < 8 || C % 8) return false;
+  g = red_geo(C);
+  if (g.vec != 8) return false;
+  P = nparts_for(rows, C);
+  rpp = (int)((rows + P - 1) / P);
+  return (int64_t)P * g.rp <= kSmallThreads;
+}
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int sv_bn_small_ok(int64_t rows, int32_t C) {
+  RedGeo g;
+  int P, rpp;
+  return small_geo(rows, C, g, P, rpp) ? 1 : 0;
+}
+
+extern "C" int sv_bn_bwd_small(int32_t mode, void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype,
+                               const void* y, int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
+                               const float* beta, const void* y2, int32_t y2_dtype, const float* mean2,
+                               const float* rstd2, const float* gamma2, const float* part, int32_t nparts, void* dx,
+                               void* dx2, int32_t dx_dtype, float* dgamma, float* dbeta, float* dgamma2, float* dbeta2,
+                               int32_t batch_stats, int64_t rows, int32_t C, sv_stream_t stream) {
+  RedGeo g;
+  int P, rpp;
+  SV_REQUIRE(small_geo(rows, C, g, P, rpp), "sv_bn_bwd_small: rows=%lld C=%d outside the one-launch geometry",
+             (long long)rows, (int)C);
+  SV_REQUIRE(mode >= SV_BN_SMALL_MASK && mode <= SV_BN_SMALL_DUAL, "sv_bn_bwd_small: bad mode %d", (int)mode);
+  SV_REQUIRE(dout && y && mean && rstd && gamma && dx && dt_ok(dout_dtype) && dt_ok(y_dtype) && dt_ok(dx_dtype) &&
+                 al16(dout) && al16(y) && al16(dx) && al16(mean) && al16(rstd) && al16(gamma),
+             "sv_bn_bwd_small: bad arguments");
+  SV_REQUIRE(mode == SV_BN_SMALL_RELU || (dout_dtype == SV_F32 && act && dt_ok(act_dtype) && al16(act) && !part),
+             "sv_bn_bwd_small: the mask modes need an f32 dout, act and no given partials");
+  SV_REQUIRE(mode != SV_BN_SMALL_RELU || (beta && al16(beta)), "sv_bn_bwd_small: the ReLU mode needs beta");
+  SV_REQUIRE(mode != SV_BN_SMALL_DUAL || (y2 && mean2 && rstd2 && gamma2 && dx2 && dt_ok(y2_dtype) && al16(y2) &&
+                                          al16(dx2) && al16(mean2) && al16(rstd2) && al16(gamma2)),
+             "sv_bn_bwd_small: the dual mode needs y2, mean2, rstd2, gamma2 and dx2");
+  SV_REQUIRE(!part || (nparts > 0 && al16(part)), "sv_bn_bwd_small: bad partials");
+  SmallBwdArgs a{dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, beta, y2, y2_dtype, mean2, rstd2,
+                 gamma2, part, nparts, dx, dx2, dx_dtype, dgamma, dbeta, dgamma2, dbeta2, batch_stats ? 1 : 0,
+                 (int)rows, C, P, g.rp, rpp};
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = C / 8;
+  if (mode == SV_BN_SMALL_MASK) bwd_small_kernel<0, false><<<grid, kSmallThreads, 0, st>>>(a);
+  else if (mode == SV_BN_SMALL_DUAL) bwd_small_kernel<2, false><<<grid, kSmallThreads, 0, st>>>(a);
+  else if (part) bwd_small_kernel<1, true><<<grid, kSmallThreads, 0, st>>>(a);
+  else bwd_small_kernel<1, false><<<grid, kSmallThreads, 0, st>>>(a);
+  return check_launch("sv_bn_bwd_small");
+}
+
+extern "C" int sv_bn_act_small(const void* y, int32_t y_dtype, const float* part, int32_t nparts, float eps,
+                               float momentum, const float* gamma, const float* beta, float* mean, float* rstd,
+                               float* running_mean, float* running_var, int64_t* num_batches_tracked, const void* res,
+                               int32_t res_dtype, const float* res_part, int32_t res_nparts, float res_eps,
+                               float res_momentum, const float* res_gamma, const float* res_beta, float* res_mean,
+                               float* res_rstd, float* res_running_mean, float* res_running_var,
+                               int64_t* res_num_batches_tracked, int32_t relu, void* out, int32_t out_dtype,
+                               int64_t rows, int32_t C, sv_stream_t stream) {
+  RedGeo g;
+  int P, rpp;
+  SV_REQUIRE(small_geo(rows, C, g, P, rpp), "sv_bn_act_small: rows=%lld C=%d outside the one-launch geometry",
+             (long long)rows, (int)C);
+  SV_REQUIRE(y && part && nparts > 0 && gamma && beta && mean && rstd && out && dt_ok(y_dtype) && dt_ok(out_dtype) &&
+                 al16(y) && al16(part) && al16(gamma) && al16(beta) && al16(out),
+             "sv_bn_act_small: bad arguments");
+  SV_REQUIRE(!res || (dt_ok(res_dtype) && al16(res)), "sv_bn_act_small: bad residual");
+  SV_REQUIRE(!res_part || (res && res_nparts > 0 && al16(res_part) && res_gamma && res_beta && res_mean && res_rstd &&
+                           al16(res_gamma) && al16(res_beta)),
+             "sv_bn_act_small: incomplete residual BatchNorm");
+  SmallActArgs a{y, y_dtype, part, nparts, eps, momentum, gamma, beta, mean, rstd, running_mean, running_var,
+                 num_batches_tracked, res, res_dtype, res_part, res_nparts, res_eps, res_momentum, res_gamma, res_beta,
+                 res_mean, res_rstd, res_running_mean, res_running_var, res_num_batches_tracked, relu ? 1 : 0, out,
+                 out_dtype, (int)rows, C};
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = C / 8;
+  if (res_part) act_small_kernel<true, true><<<grid, kSmallThreads, 0, st>>>(a);
+  else if (res) act_small_kernel<true, false><<<grid, kSmallThreads, 0, st>>>(a);
+  else act_small_kernel<false, false><<<grid, kSmallThreads, 0, st>>>(a);
+  return check_launch("sv_bn_act_small");
 }

@@ -1114,6 +1114,55 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
     return out
 
 
+# One launch per BatchNorm where the rows are few (sv_bn_*_small: ResNet layers 3-4 at 256 px), bit for bit the
+# multi-launch path.  Opt-in (SV_BN_SMALL=1): measured slower (classification 3524-3542 vs 3779-3806 img/s
+# interleaved, profiles/round4/r8c_bn_small_ab.txt).  A workgroup that owns 8 channels over all rows reads 16 B per
+# row, one cache line per lane, so it streams at the L1's line rate: layer3's output BatchNorm backward took 86 us
+# in one launch against ~45 us in three; at layer4 the two forms are equal (r8d trace)
+_BN_SMALL = os.environ.get("SV_BN_SMALL", "0") != "0"
+_SMALL_OK: dict = {}
+
+
+def bn_small_ok(rows: int, C: int) -> bool:
+    """Whether (rows, C) has the one-launch BatchNorm geometry (sv_bn_small_ok)."""
+    key = (rows, C)
+    ok = _SMALL_OK.get(key)
+    if ok is None:
+        ok = _SMALL_OK[key] = bool(value("sv_bn_small_ok", rows, C))
+    return _BN_SMALL and ok
+
+
+def _bn_small_args_ok(*ts) -> bool:
+    return all(t is None or (t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0) for t in ts)
+
+
+def bn_act_small(y2d, part, bn_params: tuple, *, res=None, res_part=None, res_params: tuple | None = None,
+                 relu=True, out_dtype=torch.float32):
+    """Train-mode BatchNorm (+ residual, + its own ReLU) from the conv epilogue's unshifted statistics partials in
+    ONE launch (sv_bn_act_small): bit for bit ``bn_stats_from_partials`` + ``bn_act``.  ``bn_params`` =
+    (gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked); with ``res_part`` the residual is
+    the projection shortcut's conv output and ``res_params`` its BatchNorm's.  -> (out, mean, rstd[, mean2, rstd2])."""
+    rows, C = y2d.shape
+    g, b, eps, mom, rm, rv, nbt = bn_params
+    dev = y2d.device
+    mean = torch.empty(C, device=dev, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    out = torch.empty(rows, C, device=dev, dtype=out_dtype)
+    if res_part is not None:
+        g2, b2, eps2, mom2, rm2, rv2, nbt2 = res_params
+        mean2, rstd2 = torch.empty_like(mean), torch.empty_like(mean)
+    else:
+        g2 = b2 = rm2 = rv2 = nbt2 = mean2 = rstd2 = None
+        eps2, mom2 = 0.0, 0.0
+    call("sv_bn_act_small", ptr(y2d), dt(y2d), ptr(part), part.shape[0], float(eps), float(mom), ptr(g), ptr(b),
+         ptr(mean), ptr(rstd), ptr(rm), ptr(rv), ptr(nbt), ptr(res), nv.dt_none(res), ptr(res_part),
+         res_part.shape[0] if res_part is not None else 0, float(eps2), float(mom2), ptr(g2), ptr(b2), ptr(mean2),
+         ptr(rstd2), ptr(rm2), ptr(rv2), ptr(nbt2), int(relu), ptr(out), dt(out), rows, C)
+    if res_part is not None:
+        return out, mean, rstd, mean2, rstd2
+    return out, mean, rstd
+
+
 def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=None, dbeta=None,
            dx_dtype=torch.float32, gmask=None, mask_inplace: bool = False, batch_stats: bool = True,
            part: torch.Tensor | None = None) -> torch.Tensor:
@@ -1143,6 +1192,16 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     if given:
         _check(relu_beta is not None and part.dtype == torch.float32 and part.is_contiguous() and part.dim() == 3
                and tuple(part.shape[1:]) == (2, C), "bn_bwd: part must be f32 [P][2][C] (relu_beta form)")
+    small_mode = (nv.SV_BN_SMALL_RELU if relu_beta is not None else nv.SV_BN_SMALL_MASK if mask_inplace else None)
+    if (small_mode is not None and gmask is None and bn_small_ok(rows, C)
+            and _bn_small_args_ok(dout2d, y2d, mean, rstd, gamma, act, relu_beta, part, dgamma, dbeta)):
+        dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        call("sv_bn_bwd_small", small_mode, ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d),
+             ptr(mean), ptr(rstd), ptr(gamma), ptr(relu_beta), None, 0, None, None, None, ptr(part),
+             part.shape[0] if given else 0, ptr(dx), None, dt(dx), ptr(dgamma), ptr(dbeta), None, None,
+             int(batch_stats), rows, C)
+        return dx
+    if given:
         P = part.shape[0]
     else:
         P = value("sv_bn_nparts", rows, C)
@@ -1183,6 +1242,14 @@ def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dg
     _check(_bn_c_ok(C) and gm.dtype == torch.float32 and gm.numel() == rows * C and gm.is_contiguous()
            and act.numel() == rows * C and act.is_contiguous() and y2.numel() == rows * C and y2.is_contiguous(),
            "bn_bwd_dual: bad shapes")
+    if bn_small_ok(rows, C) and _bn_small_args_ok(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, dgamma,
+                                                   dbeta, dgamma2, dbeta2):
+        dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        dx2 = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        call("sv_bn_bwd_small", nv.SV_BN_SMALL_DUAL, ptr(gm), dt(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), ptr(gamma), None, ptr(y2), dt(y2), ptr(mean2), ptr(rstd2), ptr(gamma2), None, 0, ptr(dx),
+             ptr(dx2), dt(dx), ptr(dgamma), ptr(dbeta), ptr(dgamma2), ptr(dbeta2), int(batch_stats), rows, C)
+        return dx, dx2
     P = value("sv_bn_nparts", rows, C)
     part = torch.empty(2, P, 2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_stats_mask_dual", ptr(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(y2),
