@@ -463,8 +463,14 @@ class ResNetHip(nn.Module):
     @torch.no_grad()
     def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None,
                         batch_stats: bool = True, pol: "nv.GemmPolicy | None" = None) -> torch.Tensor:
-        """Backward of one residual block given d = dL/d(block output) (f32, NHWC); accumulates the
-        block's parameter gradients and returns dL/d(block input) (f32)."""
+        """Backward of one residual block given d = dL/d(block output) (f32, NHWC, contiguous); accumulates the
+        block's parameter gradients and returns dL/d(block input) (f32).
+
+        ``d`` is CLOBBERED: the block-output BatchNorm's statistics pass writes the ReLU-masked gradient over it
+        (it is the shortcut's gradient), and an identity block returns that same buffer with the main path's data
+        gradient added.  Callers pass a buffer they own (the next block's dx, or the pooling gradient)."""
+        assert d.is_contiguous() and d.dtype == torch.float32, \
+            "_block_backward: d must be a contiguous f32 buffer the caller owns (it is overwritten)"
         act = self.act_dtype
         g = self._grad
         jobs = []

@@ -399,7 +399,8 @@ __device__ __forceinline__ void grad_masked(const void* dout, int ddt, const voi
 
 // backward statistics: sum g and sum g * xhat
 template <int V, bool RELU_Y, bool POOL = false>
-__global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* __restrict__ dout, int ddt,
+// (dout is not __restrict__: sv_bn_bwd_stats_mask passes it as gout too and writes g back over it)
+__global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, int ddt,
                                                              const void* __restrict__ act, int adt,
                                                              const void* __restrict__ y, int ydt,
                                                              const float* __restrict__ mean,

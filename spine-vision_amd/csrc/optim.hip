@@ -507,7 +507,9 @@ int sv_reduce_partials_multi(const sv_red_seg* segs, int32_t nseg, float alpha, 
     if (g.n == 0) continue;
     // the wide body needs whole 16-B column groups; sv_reduce_partials_pair's choice of body
     const bool wide = g.P <= 64 && g.n >= 65536 && g.n % 4 == 0 && (((uintptr_t)g.out) & 15) == 0;
-    if (g.n % 4 == 0) SV_REQUIRE((((uintptr_t)g.part) & 15) == 0, "sv_reduce_partials_multi: partials must be 16-B aligned");
+    // both bodies read 16-B column groups of every partial row: rows must start 16-B aligned, so n % 4 == 0
+    SV_REQUIRE(g.n % 4 == 0 && (((uintptr_t)g.part) & 15) == 0,
+               "sv_reduce_partials_multi: segment %d needs n %% 4 == 0 and 16-B aligned partials", i);
     const int64_t nb = wide ? (g.n / 4 + kThreads - 1) / kThreads : (g.n + 63) / 64;
     m.s[k] = MultiSeg{g.part, g.out, g.n, blocks, g.P, wide ? 1 : 0, g.accumulate ? 1 : 0};
     blocks += nb;

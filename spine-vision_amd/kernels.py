@@ -797,15 +797,21 @@ def _pointwise(s: nv.ConvShape, dtype: torch.dtype) -> bool:
             and s.Cs % 32 == 0 and s.Cout % 32 == 0)
 
 
-def _conv_split(M: int, N: int, K: int) -> int:
+# gathered forward convolutions split K only from this many 32-deep k-steps (round 4, profiles/round4/
+# r8e_conv_split_sweep.txt: layer2's 3x3 forward, K = 1152, 128 tiles, runs in 30 us unsplit against 35 + a 7 us
+# finish at split 2; layer3 / 4, K = 2304 / 4608, are fastest at split 4 / 8 as before)
+_CONV_FWD_MIN_KSTEPS = int(os.environ.get("SV_CONV_FWD_MIN_KSTEPS", "64"))
+
+
+def _conv_split(M: int, N: int, K: int, min_ksteps: int = 32) -> int:
     """split-K depth of a bf16 conv GEMM whose grid of 256x128 tiles would not give every CU a workgroup
     (ResNet layer3/4 at 256 px: 32-128 tiles, each a long latency-bound chain of 32-deep k-steps):
     about one workgroup per CU, >= 16 k-steps per slice, <= 32 MiB of f32 slabs (written by the GEMM,
-    read back by sv_gemm_slab_finish), at most 16 slices.  1 = no split (also for K < 1024, where the
-    slab round trip costs more than the chain it shortens)."""
+    read back by sv_gemm_slab_finish), at most 16 slices.  1 = no split (also below ``min_ksteps`` k-steps, where
+    the slab round trip costs more than the chain it shortens)."""
     tiles = -(-M // 256) * -(-N // 128)
     ksteps = K // 32
-    if tiles >= 192 or ksteps < 32:
+    if tiles >= 192 or ksteps < min_ksteps:
         return 1
     return max(1, min(-(-256 // tiles), ksteps // 16, (32 << 20) // (M * N * 4), 16))
 
@@ -859,7 +865,7 @@ def conv_fwd(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dtype: torc
         _pointwise_fwd(x, wp, s, y, s.B * s.H * s.W, policy=policy)
         return y
     M, K = s.B * OH * OW, s.KH * s.KW * s.Cs
-    split = _conv_split(M, s.Cout, K) if _gathered(s, wp.dtype) else 1
+    split = _conv_split(M, s.Cout, K, _CONV_FWD_MIN_KSTEPS) if _gathered(s, wp.dtype) else 1
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
         call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), None, ptr(work), split,
@@ -904,7 +910,7 @@ def conv_fwd_bn_stats(x: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, out_dt
     _check(tuple(wp.shape) == (s.Cout, s.KH * s.KW, s.Cs), "conv_fwd: packed weight shape")
     y = torch.empty(s.B, OH, OW, s.Cout, device=x.device, dtype=out_dtype)
     part = torch.empty((M + 63) // 64, 2, s.Cout, device=x.device, dtype=torch.float32)
-    split = 1 if _stem8(s, wp.dtype) else _conv_split(M, s.Cout, s.KH * s.KW * s.Cs)
+    split = 1 if _stem8(s, wp.dtype) else _conv_split(M, s.Cout, s.KH * s.KW * s.Cs, _CONV_FWD_MIN_KSTEPS)
     if split > 1:
         work = torch.empty(split * M * s.Cout, device=x.device, dtype=torch.float32)
         call("sv_conv_fwd_split", ptr(x), ptr(wp), ptr(y), dt(y), dt(wp), ctypes.byref(s), ptr(part), ptr(work), split,

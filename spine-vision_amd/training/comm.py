@@ -125,16 +125,17 @@ class GradBucketer:
                     # buckets, the timing event and the compute stream's join are ordered after it
                     w.wait()
                     w = None
-                if e0 is not None:
+                if e0 is not None and w is None:
                     e1 = torch.cuda.Event(enable_timing=True)
                     e1.record()
                     self._bucket_ev.append((e0, e1, view.numel() * view.element_size()))
             # gloo on device tensors: wait() blocks the host until the reduce is done, so it is deferred
-            # to finish() (the backward keeps being enqueued meanwhile)
-            self.works.append((w, view, op))
+            # to finish() (the backward keeps being enqueued meanwhile); its timing event is recorded there,
+            # after the wait, so the bucket's time covers the exchange and not only its enqueue
+            self.works.append((w, view, op, e0))
         else:
             w = dist.all_reduce(view, op=op, group=self.group, async_op=True)
-            self.works.append((w, view, op))
+            self.works.append((w, view, op, None))
         self.launched[b] = True
 
     def finish(self) -> None:
@@ -142,12 +143,16 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for w, view, op in self.works:
+        for w, view, op, e0 in self.works:
             if w is None:
                 continue
             if self.use_streams:
                 with torch.cuda.stream(self.comm_stream):
                     w.wait()
+                    if e0 is not None:
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e1.record()
+                        self._bucket_ev.append((e0, e1, view.numel() * view.element_size()))
                     if op == dist.ReduceOp.SUM and self.world > 1:
                         view.div_(self.world)
                 continue

@@ -42,9 +42,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--split", type=int, default=0, help="force the fwd / stride-1 dgrad split-K depth (0: dispatch's)")
     args = ap.parse_args()
+    if args.split:
+        K._conv_split = lambda M, N, Kd: args.split
     dev = torch.device("cuda:0")
-    tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("SV_"))
+    tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("SV_")) + (f" split={args.split}" if args.split else "")
     for name, (B, H, W, Cs, Cin, Cout, k, s, p) in SHAPES.items():
         if args.only and args.only not in name:
             continue
