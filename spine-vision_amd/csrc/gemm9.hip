@@ -161,6 +161,13 @@ struct Fold {
   int* cnt;
 };
 constexpr int kSC1 = 16;  // buffer instruction cache policy: sc1 (write-through store / L1-bypassing load)
+// cache policy of the GELU'(h) store of the dual epilogue: nt (2).  That tensor is read only by the backward,
+// ~20 ms and tens of GB of traffic later, so keeping its lines in L2 / the Infinity Cache only evicts the GELU(h)
+// the next GEMM reads at once: step 1072.9-1073.7 -> 1083.4-1084.2 img/s interleaved (profiles/round4/
+// r8g_gelu_grad_nt_ab.txt).  -DSV_G9_GRAD_CPOL=0 restores the default policy (tools/build_ab.sh)
+#ifndef SV_G9_GRAD_CPOL
+#define SV_G9_GRAD_CPOL 2
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
   // built from kernel arguments only: wave-uniform, so no waterfall loop around the buffer ops
@@ -355,7 +362,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
         }
         if constexpr (P8) {
           const u32x4 pk = pack8(o);
-          __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0,
+                                                 EPI == SV_EPI_BIAS_GELU_DUAL ? SV_G9_GRAD_CPOL : 0);
           if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) __builtin_amdgcn_raw_buffer_store_b128(pack8(o2), rc2, off, 0, 0);
           if constexpr (EPI == SV_EPI_STORE_STATS) {
             // statistics of the values AS STORED (bf16), rows past M excluded
