@@ -82,9 +82,19 @@ __device__ __forceinline__ int perm8(int rho) {
 // LDS-DMA by buffer_load ... lds: the per-lane byte offset of each of a wave's pieces is computed
 // once per tile (voffset), the K position is the uniform soffset, rows / columns past the matrix get
 // an offset past the descriptor's range and land as zeros (their results are never stored)
+template <int CPOL = 0>
 __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* dst) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, CPOL);
 }
+// A/B switches (tools/build_ab.sh): cache policy of the epilogue's bf16 operand loads (GELU'(h): its last read) and
+// of a weight gradient's B operand DMA (the saved activation: its last read).  nt on either measured no better
+// (profiles/round4/r8h_nt_loads_rejected.txt: the wgrad's B panel is re-read by every M tile of its K slice)
+#ifndef SV_G9_AUXBF_CPOL
+#define SV_G9_AUXBF_CPOL 0
+#endif
+#ifndef SV_G9_SLAB_B_CPOL
+#define SV_G9_SLAB_B_CPOL 0
+#endif
 // A wave's DMA pieces of one operand differ only by whole rows (K-major: 64 rows; N/M-major: 16 k-rows)
 // and the source swizzle does not depend on the piece, so each operand needs ONE per-lane byte offset
 // (per tile) plus a uniform piece offset in soffset.  Rows / columns past the matrix read past the
@@ -295,9 +305,9 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
         for (int c = 0; c < CH; ++c) {
           const uint32_t base = okn[c] && m < e.M ? (uint32_t)((m * e.ld_aux + n[c]) * (AUXF ? 4 : 2)) : OOB;
           if constexpr (AUXBF && P8) {
-            raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 0);
+            raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, SV_G9_AUXBF_CPOL);
           } else if constexpr (AUXBF) {
-            const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(ra, base, 0, 0);
+            const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(ra, base, 0, SV_G9_AUXBF_CPOL);
             raw[ii][c][0] = u32x4{t.x, t.y, 0u, 0u};
           } else if constexpr (P8) {
             raw[ii][c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 0);
@@ -524,7 +534,8 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       const uint32_t so = BKM ? (uint32_t)k0 * 2 : (uint32_t)((int64_t)k0 * ldb * 2);
       const uint32_t step = (uint32_t)((BKM ? 64 : 16) * ldb * 2);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dma(rb, vb, so + j * step, bb + (wid + 8 * j) * 1024);
+      for (int j = 0; j < 4; ++j)
+        dma<EPI == SV_EPI_SLAB ? SV_G9_SLAB_B_CPOL : 0>(rb, vb, so + j * step, bb + (wid + 8 * j) * 1024);
     } else if constexpr (AK) {
       char* ab = smem + a_off<AK>(l_g);
       const int h = part == 1 ? 0 : 1;  // pieces h*8 + wid (rows 64h + ..) and h*8 + 16 + wid (+128 rows)
