@@ -130,10 +130,12 @@ typedef struct {
   sv_gemm_policy policy;     /* launch policy of THIS call (zero-initialised = the defaults)      */
   /* SV_EPI_SLAB with fold_out != NULL: the split-K fold as well, fold_out[m][n] (row stride fold_ld, f32) =  */
   /* (fold_accumulate ? fold_out : 0) + sum_s C[s][m][n], slices in order s = 0, 1, ... (bitwise the         */
-  /* sv_reduce_partials fold of the slabs).  The persistent v9 kernel folds in place: the last workgroup to  */
-  /* finish a tile's slice sums that tile (no launch, no waiting); fold_counters = int32 [ceil(M/256) *      */
-  /* ceil(N/256)], all zero on entry and left zero (one buffer per stream).  Other kernels fold with a      */
-  /* separate pass.  C2 (the column sums) is not folded.                                                    */
+  /* sv_reduce_partials fold of the slabs).  The persistent v9 kernel folds in place: when every (tile,      */
+  /* slice) unit has a workgroup and the grid is at most half the CUs, each slice's workgroup waits for its  */
+  /* tile's other slices and sums 1/split of the tile's rows; otherwise the last workgroup to finish a       */
+  /* tile's slice sums that tile (no waiting).  fold_counters = int32 [2 * ceil(M/256) * ceil(N/256)], all   */
+  /* zero on entry and left zero (one buffer per stream).  Other kernels fold with a separate pass.  C2      */
+  /* (the column sums) is not folded.  ABI version 3.                                                        */
   float* fold_out; int64_t fold_ld; int32_t fold_accumulate; int32_t* fold_counters;
 } sv_gemm_desc;
 

@@ -159,17 +159,24 @@ struct Ext {
   uint32_t c, c2, aux, a, b;
 };
 
-// in-kernel split-K fold (SV_EPI_SLAB with sv_gemm_desc.fold_out): the slices of a tile are summed by the last
-// workgroup to finish one (arrival ticket per tile), with write-through (sc1) slab stores and sc1 loads -- the
-// hand-off of MI355X_MICROARCH.md's inter-workgroup table, row 1 (every storing wave vmcnt(0), a workgroup
-// barrier, ONE agent-scope atomic add per workgroup; the workgroup whose add returns split - 1 loads).  No
-// workgroup ever waits for another, so any grid, cap or co-scheduling is deadlock-free.
+// in-kernel split-K fold (SV_EPI_SLAB with sv_gemm_desc.fold_out), write-through (sc1) slab stores and sc1 loads --
+// the hand-off of MI355X_MICROARCH.md's inter-workgroup table, row 1 (every storing wave vmcnt(0), a workgroup
+// barrier, ONE agent-scope atomic add per workgroup).  Two forms, two int32 counters per tile (arrivals,
+// departures), zero between launches:
+//   kFoldLast   the workgroup whose add returns split - 1 sums the whole tile.  No workgroup waits for another,
+//               so any grid, cap or co-scheduling is deadlock-free; but one CU then streams split x 256 KiB
+//               (round 4: the one-CU tail cost the step 1-6 %).
+//   kFoldSpread every workgroup of the tile polls the arrival counter (sc1 loads) until all split slices have
+//               landed, then sums its own 1/split of the tile's rows; the last to leave re-arms both counters.
+//               Needs every slice of a tile resident at once: the host picks it only when the grid holds every
+//               (tile, slice) unit, one per workgroup, within the chip's CUs.
 struct Fold {
   float* out;
   int64_t ld;
   int acc;
   int* cnt;
 };
+constexpr int kFoldNone = 0, kFoldLast = 1, kFoldSpread = 2;
 constexpr int kSC1 = 16;  // buffer instruction cache policy: sc1 (write-through store / L1-bypassing load)
 // cache policy of the GELU'(h) store of the dual epilogue: nt (2).  That tensor is read only by the backward,
 // ~20 ms and tens of GB of traffic later, so keeping its lines in L2 / the Infinity Cache only evicts the GELU(h)
@@ -219,7 +226,7 @@ struct EpiCount {
 //   P8: n_w + 32c + 8(l >> 4) .. +7  (acc[i][2c][0..3], acc[i][2c+1][0..3]),
 //   P4: n_w + 16c + 4(l >> 4) .. +3  (acc[i][c][0..3]).
 // Arithmetic identical to wave_group_epilogue (gemm_common.h).
-template <int EPI, bool P8, bool AK, bool FOLD = false>
+template <int EPI, bool P8, bool AK, int FOLD = kFoldNone>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x, int m_w, int n_w,
                                          int split, const float* lbias) {
 #ifdef SV_DIAG_NOSTORE
@@ -431,8 +438,12 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
 // lane owns whole 16-B column chunks; FB chunks at a time, each with its 8 slice loads in flight (sc1: the
 // slabs of other XCDs were written through and are read past this CU's L1).
 template <int FB>
-__device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const Fold& f, int m0, int n0, int nsplit) {
-  const int rows = e.M - m0 < BM ? e.M - m0 : BM;
+__device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const Fold& f, int m0, int n0, int nsplit,
+                                          int r_lo = 0, int r_hi = BM) {
+  if (e.M - m0 < r_hi) r_hi = e.M - m0;
+  m0 += r_lo;
+  const int rows = r_hi - r_lo;
+  if (rows <= 0) return;
   const int c4 = (e.N - n0 < BN ? e.N - n0 : BN) / 4;
   const auto rs = rsrc(e.C, (uint32_t)((size_t)nsplit * e.M * e.N * 4 > 0x7fffffffu ? 0x7fffffffu
                                                                                     : (size_t)nsplit * e.M * e.N * 4));
@@ -489,7 +500,7 @@ __device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const 
   (void)x;
 }
 
-template <bool AK, bool BKM, int EPI, bool P8, bool FOLD = false>
+template <bool AK, bool BKM, int EPI, bool P8, int FOLD = kFoldNone>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int nk, int tilesM,
              int tilesN, int nsplit, EpiArgs e, Ext x, Fold fold) {
@@ -741,13 +752,34 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       static_assert(!AK, "the in-kernel fold is for the weight-gradient layout (N/M-major A)");
       volatile int* flag = reinterpret_cast<volatile int*>(smem + a_off<AK>(g - 1));
       const int tile = (cg.m0 / BM) * tilesN + cg.n0 / BN;
-      if (threadIdx.x == 0)
-        *flag = __hip_atomic_fetch_add(fold.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
-      lgkm0();  // the flag's LDS write before the barrier (s_barrier waits for no memory operation on gfx950)
-      bar();
-      if (*flag) {  // workgroup-uniform: the last slice of this tile landed -- fold it
-        fold_tile<2>(e, x, fold, cg.m0, cg.n0, nsplit);
-        if (threadIdx.x == 0) __hip_atomic_store(fold.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int* arrive = fold.cnt + 2 * tile;
+      int* depart = arrive + 1;
+      if constexpr (FOLD == kFoldLast) {
+        if (threadIdx.x == 0)
+          *flag = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+        lgkm0();  // the flag's LDS write before the barrier (s_barrier waits for no memory operation on gfx950)
+        bar();
+        if (*flag) {  // workgroup-uniform: the last slice of this tile landed -- fold it
+          fold_tile<2>(e, x, fold, cg.m0, cg.n0, nsplit);
+          if (threadIdx.x == 0) __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        // arrive, then poll (one lane, sc1 loads, s_sleep between) until every slice of the tile has landed;
+        // the other waves load after the barrier the polling wave joins
+        if (threadIdx.x == 0) {
+          __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsplit)
+            __builtin_amdgcn_s_sleep(4);
+        }
+        bar();
+        const int per = (BM + nsplit - 1) / nsplit;
+        fold_tile<2>(e, x, fold, cg.m0, cg.n0, nsplit, cg.split * per, cg.split * per + per);
+        // departure: the last workgroup out re-arms both counters (nobody polls them any more)
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1) {
+          __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       bar();  // the flag word is rewritten by the next tile
       if (wm == 1) bar();  // re-stagger for the next tile's K loop
@@ -758,13 +790,13 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   stamp(1);
 }
 
-template <bool AK, int EPI, bool FOLD = false>
+template <bool AK, int EPI, int FOLD = kFoldNone>
 constexpr int lds_total() {
   return lds_bytes<AK>() + ((AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
                                    EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS)) ? 4096 : 0);
 }
 
-template <bool AK, bool BKM, int EPI, bool P8, bool FOLD = false>
+template <bool AK, bool BKM, int EPI, bool P8, int FOLD = kFoldNone>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int nk = d->K / split / BK;
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
@@ -786,6 +818,20 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int total = tilesM * tilesN * split;
   const int grid = policy_grid(&d->policy, total, 1, s);  // persistent: one workgroup per CU (or the cap)
   const Fold fold{d->fold_out, d->fold_ld, d->fold_accumulate, d->fold_counters};
+  if constexpr (FOLD != kFoldNone) {
+    // the spread fold waits for a tile's other slices: only when every (tile, slice) unit has a workgroup of its
+    // own and the grid is at most half the chip (one workgroup per CU): then two such launches on two streams
+    // can never hold every CU with partly-resident grids, so a waiting workgroup's peers always find a CU.
+    // Otherwise the wait-free last-arriver form.
+    if (grid == total && 2 * total <= device_cus(s)) {
+      constexpr int LDS2 = lds_total<AK, EPI, kFoldSpread>();
+      ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, kFoldSpread>), LDS2, s);
+      gemm9_kernel<AK, BKM, EPI, P8, kFoldSpread><<<grid, THREADS, LDS2, s>>>(
+          reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk, tilesM,
+          tilesN, split, e, x, fold);
+      return check_launch("sv_gemm(v9, spread fold)");
+    }
+  }
   gemm9_kernel<AK, BKM, EPI, P8, FOLD><<<grid, THREADS, LDS, s>>>(reinterpret_cast<const uint16_t*>(d->A), d->lda,
                                                                  reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk,
                                                                  tilesM, tilesN, split, e, x, fold);
@@ -823,7 +869,7 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
       if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
       if (d->fold_out) {  // (the weight-gradient layout only: N/M-major A; others fold in a separate pass)
         if constexpr (AK) return SV_ERR_UNSUPPORTED;
-        else return launch<AK, BKM, SV_EPI_SLAB, false, true>(d, split, s);
+        else return launch<AK, BKM, SV_EPI_SLAB, false, kFoldLast>(d, split, s);
       }
       return launch<AK, BKM, SV_EPI_SLAB, false>(d, split, s);
     default:

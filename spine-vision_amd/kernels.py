@@ -256,22 +256,23 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
     return _wgrad_split(-(-N // 128) * -(-K // 128), M)
 
 
-# In-kernel split-K fold of the weight gradients (gemm9.hip: the last workgroup to finish a tile's slice sums the
-# tile; sv_gemm_desc.fold_out), where the separate fold would take sv_reduce_partials' sequential wide body (bitwise
-# the same result) and the slices are few enough for one workgroup to read them.  Opt-in (SV_INKERNEL_FOLD=1):
-# measured slower in the step (1009-1051 vs 1066-1068 img/s interleaved; the one-workgroup fold tail holds up the
-# side stream, profiles/round4/r7f_fold_ab.txt), where halving the split depth instead gains 0.7 %
+# In-kernel split-K fold of the weight gradients (gemm9.hip, sv_gemm_desc.fold_out), where the separate fold would
+# take sv_reduce_partials' sequential wide body (bitwise the same result).  The kernel spreads each tile's fold over
+# the tile's own slices when the grid allows it (every slice resident: one unit per workgroup, at most half the
+# CUs), else the last workgroup to finish a slice sums the tile.  SV_INKERNEL_FOLD=1 turns it on; round 4's
+# last-arriver form alone measured slower (1009-1051 vs 1066-1068 img/s; profiles/round4/r7f_fold_ab.txt)
 _INKERNEL_FOLD = os.environ.get("SV_INKERNEL_FOLD", "0") != "0"
-_FOLD_MAX_SPLIT = int(os.environ.get("SV_FOLD_MAX_SPLIT", "16"))
+_FOLD_MAX_SPLIT = int(os.environ.get("SV_FOLD_MAX_SPLIT", "64"))
 _FOLD_COUNTERS: dict = {}
 
 
 def _fold_counters(device, tiles: int) -> torch.Tensor:
-    """Zeroed int32 arrival tickets for in-kernel folds on the current stream (the kernel leaves them zero)."""
+    """Zeroed int32 counters (arrivals, departures) per tile for in-kernel folds on the current stream (the kernel
+    leaves them zero)."""
     key = (device, nv._stream())
     t = _FOLD_COUNTERS.get(key)
-    if t is None or t.numel() < tiles:
-        t = _FOLD_COUNTERS[key] = torch.zeros(max(tiles, 4096), device=device, dtype=torch.int32)
+    if t is None or t.numel() < 2 * tiles:
+        t = _FOLD_COUNTERS[key] = torch.zeros(max(2 * tiles, 4096), device=device, dtype=torch.int32)
     return t
 
 

@@ -234,10 +234,11 @@ def test_gemm_policy_is_per_call(dev):
 @pytest.mark.parametrize("M,C", [(4096, 128), (131072, 256), (32768, 512), (8192, 1024), (2048 + 512, 512)],
                          ids=["half-tiles", "S2", "S3", "S4", "ragged-split"])
 def test_wgrad_inkernel_fold_bitwise(dev, M, C):
-    """The split-K fold inside the persistent v9 weight-gradient GEMM (the last workgroup to finish a tile's slice
-    sums it: sv_gemm_desc.fold_out) equals the slabs + separate fold bit for bit -- written or accumulated, under
-    the default grid, a grid cap that makes every workgroup fold several tiles (37), the backward's policy, and the
-    v3 family (slabs + fold pass) -- and so does the layer-scale fc2 finish over the folded G."""
+    """The split-K fold inside the persistent v9 weight-gradient GEMM (sv_gemm_desc.fold_out) equals the slabs +
+    separate fold bit for bit -- written or accumulated, under the default grid (every slice its own workgroup: the
+    spread form, each slice's workgroup summing 1/split of its tile's rows), a grid cap that makes every workgroup
+    fold several tiles (37: the last-arriver form), the backward's policy, and the v3 family (slabs + fold pass) --
+    and so does the layer-scale fc2 finish over the folded G."""
     g = torch.Generator().manual_seed(M + C)
     bf = torch.bfloat16
     dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
@@ -275,3 +276,37 @@ def test_wgrad_inkernel_fold_bitwise(dev, M, C):
         got = run(True, pol)
         for i, (r, o) in enumerate(zip(r_, got)):
             assert torch.equal(r, o), (pol, i, split, float((r - o).abs().max()))
+
+
+@pytest.mark.timeout(300)
+def test_wgrad_spread_fold_under_uneven_load(dev):
+    """The spread fold's hand-off (write-through slabs, one agent-scope add per workgroup, an sc1 poll, sc1 loads)
+    under uneven load: each fold GEMM is launched while a persistent GEMM on a second stream holds part of the chip,
+    so a tile's slices land at different times and their workgroups wait on one another.  Every word of every
+    repetition must equal the separate fold's result (MI355X_MICROARCH.md: test hand-offs under uneven load)."""
+    g = torch.Generator().manual_seed(11)
+    bf = torch.bfloat16
+    M, C = 32768, 512
+    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    y = torch.randn(M, C, generator=g).to(bf).to(dev)
+    xa = torch.randn(65536, 1024, generator=g).to(bf).to(dev)
+    wb = torch.randn(2048, 1024, generator=g).to(bf).to(dev)
+    busy = torch.empty(65536, 2048, device=dev, dtype=bf)
+    saved = K._INKERNEL_FOLD
+    try:
+        K._INKERNEL_FOLD = False
+        ref = K.linear_wgrad(dh, y, out=torch.empty(4 * C, C, device=dev))
+        K._INKERNEL_FOLD = True
+        side = torch.cuda.Stream(device=dev)
+        outs = []
+        for rep in range(6):
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # a 2-tile-per-CU persistent GEMM beside the fold (cap varies the skew)
+                K.linear_fwd(xa, wb, out=busy, policy=nv.policy(grid_cap=64 + 32 * rep))
+            outs.append(K.linear_wgrad(dh, y, out=torch.empty(4 * C, C, device=dev)))
+            torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+    finally:
+        K._INKERNEL_FOLD = saved
+    for i, o in enumerate(outs):
+        assert torch.equal(o, ref), (i, float((o - ref).abs().max()))
