@@ -259,8 +259,10 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
 # In-kernel split-K fold of the weight gradients (gemm9.hip, sv_gemm_desc.fold_out), where the separate fold would
 # take sv_reduce_partials' sequential wide body (bitwise the same result).  The kernel spreads each tile's fold over
 # the tile's own slices when the grid allows it (every slice resident: one unit per workgroup, at most half the
-# CUs), else the last workgroup to finish a slice sums the tile.  SV_INKERNEL_FOLD=1 turns it on; round 4's
-# last-arriver form alone measured slower (1009-1051 vs 1066-1068 img/s; profiles/round4/r7f_fold_ab.txt)
+# CUs), else the last workgroup to finish a slice sums the tile.  Opt-in (SV_INKERNEL_FOLD=1), both forms measured
+# slower in the step: the last-arriver form 1009-1051 vs 1066-1068 img/s (r7f_fold_ab.txt: one CU streams the
+# tile), the spread form 1037-1039 vs 1056-1057 (r8j_spread_fold_ab.txt: the fold passes drop 2.4 -> 1.7 ms/step
+# but each wgrad launch grows 170 -> 195 us in-step, its slices waiting on one another beside the main stream)
 _INKERNEL_FOLD = os.environ.get("SV_INKERNEL_FOLD", "0") != "0"
 _FOLD_MAX_SPLIT = int(os.environ.get("SV_FOLD_MAX_SPLIT", "64"))
 _FOLD_COUNTERS: dict = {}
