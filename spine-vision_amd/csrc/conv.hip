@@ -1054,6 +1054,10 @@ static bool wgrad_transposed(const sv_conv_shape* s) {
 // per slice.  Mode 4 (few output tiles, Cout < 256): 192-256 workgroups with >= 2048 pixels per slice
 // where the pixel count allows -- fewer, longer slices halve the slab round trip of the layer1 3x3
 // (76 -> 60 us) and the stem (131 -> 119 us) against the 512-workgroup split (tools/conv_bench.py)
+// A/B switches (tools/build_ab.sh): the transposed wgrad's workgroup target (and gemm3.hip's SV_CONVW4_STAGES)
+#ifndef SV_CONVW4_WGS
+#define SV_CONVW4_WGS 256
+#endif
 static int wgrad_split3(const sv_conv_shape* s) {
   const int OH = out_dim(s->H, s->KH, s->stride, s->pad), OW = out_dim(s->W, s->KW, s->stride, s->pad);
   const int64_t K = (int64_t)s->B * OH * OW;
@@ -1061,7 +1065,7 @@ static int wgrad_split3(const sv_conv_shape* s) {
   int64_t split;
   if (wgrad_transposed(s)) {
     const int64_t tiles = ceil_div(tc, 256) * ceil_div(s->Cout, 128);
-    const int64_t lo = ceil_div(192, tiles), hi = ceil_div(256, tiles);
+    const int64_t lo = ceil_div(SV_CONVW4_WGS * 3 / 4, tiles), hi = ceil_div(SV_CONVW4_WGS, tiles);
     split = K / 2048 > lo ? K / 2048 : lo;
     if (split > hi) split = hi;
     const int64_t maxs = K / 512 > 0 ? K / 512 : 1;

@@ -521,6 +521,11 @@ static int conv_w(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s
 }
 }  // namespace g3
 
+// ring depth of the transposed gather wgrad (mode 4): 4 stages (96 KiB, one workgroup per CU); A/B builds try 3
+// (72 KiB, two per CU) with conv.hip's SV_CONVW4_WGS doubled
+#ifndef SV_CONVW4_STAGES
+#define SV_CONVW4_STAGES 4
+#endif
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s) {
   using namespace g3;
   if (d->compute != SV_BF16 || d->a_dtype != SV_BF16 || d->b_dtype != SV_BF16 || d->K % 32 ||
@@ -528,7 +533,8 @@ int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream
     return SV_ERR_UNSUPPORTED;
   // ring depth: 3 stages (fprop / dgrad, two workgroups per CU) and 4 (wgrads); 6 stages (144 KiB, five
   // tiles in flight) measured no faster for any ResNet-50 conv pass (profiles/round3/r6b_conv_ring_depth.txt)
-  if (mode == 3 || mode == 4) return conv_w<4>(d, g, mode, s);
+  if (mode == 4) return conv_w<SV_CONVW4_STAGES>(d, g, mode, s);
+  if (mode == 3) return conv_w<4>(d, g, mode, s);
   return conv_fd<3>(d, g, mode, s);
 }
 
