@@ -253,16 +253,17 @@ class BucketTimeline:
         backward launches at its end); the step grows by what finishes after the backward's end.
         ``reserve_cost``: the measured fractional slowdown of the step under the data-parallel CU reserve,
         which stretches the whole timeline (ready times, backward end, step) before the exchange is added;
-        ``launch_delay_ms``: how long a comm kernel may wait behind the backward's kernels after its ready event,
-        (during the backward, the end of the backward): a bucket ready before the backward's end starts that late;
-        one a scalar applies to both."""
+        ``launch_delay_ms``: (mid, end) -- how long a comm kernel may wait behind the backward's kernels after its
+        ready event while the backward runs (mid), and its start latency once the compute queues are idle (end).  A
+        bucket that becomes ready shortly before the backward's end waits at most for the rest of the backward:
+        delay = min(mid, time left in the backward + end).  A scalar applies to both."""
         f = 1.0 + reserve_cost
         bwd_end_ms, step_dp = bwd_end_ms * f, step_ms * f
         d_mid, d_end = launch_delay_ms if isinstance(launch_delay_ms, (tuple, list)) else (launch_delay_ms,) * 2
         t = 0.0
         for mb, r in sorted(ready, key=lambda x: (x[1] is None, x[1] if x[1] is not None else 0.0)):
             rr = r * f if r is not None else bwd_end_ms
-            start = max(t, rr + (d_mid if rr < bwd_end_ms - 1e-6 else d_end))
+            start = max(t, rr + min(d_mid, max(0.0, bwd_end_ms - rr) + d_end))
             t = start + 2.0 * (world - 1) / world * mb * 2**20 / (busbw_gbs * 1e9) * 1e3
         exposed = max(0.0, t - bwd_end_ms)
         return {"world": world, "busbw_gbs": busbw_gbs, "reserve_cost_frac": reserve_cost,
