@@ -88,7 +88,9 @@ __global__ void __launch_bounds__(kThreads) reduce_pair_kernel(RedSeg a, RedSeg 
   const int c4 = threadIdx.x % C4, pg = threadIdx.x / C4;
   const int64_t col = blk * (4 * C4) + c4 * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col + 4 <= sg.n) {
+  // 16-B loads only where every partial row starts 16-B aligned (n % 4 == 0; the host checks the base); otherwise
+  // the scalar form, which adds the same partials in the same order
+  if (col + 4 <= sg.n && (sg.n & 3) == 0) {
     int p = pg;
     for (; p + 3 * PG < P; p += 4 * PG) {
       float4 v[4];
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(kThreads) reduce_multi_kernel(MultiSegs segs, 
   const int64_t col = blk * (4 * C4) + c4 * 4;
   const int P = sg.P;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col + 4 <= sg.n) {
+  if (col + 4 <= sg.n && (sg.n & 3) == 0) {  // (as reduce_pair_kernel: 16-B loads only for 16-B aligned rows)
     int p = pg;
     for (; p + 3 * PG < P; p += 4 * PG) {
       float4 v[4];
@@ -507,9 +509,8 @@ int sv_reduce_partials_multi(const sv_red_seg* segs, int32_t nseg, float alpha, 
     if (g.n == 0) continue;
     // the wide body needs whole 16-B column groups; sv_reduce_partials_pair's choice of body
     const bool wide = g.P <= 64 && g.n >= 65536 && g.n % 4 == 0 && (((uintptr_t)g.out) & 15) == 0;
-    // both bodies read 16-B column groups of every partial row: rows must start 16-B aligned, so n % 4 == 0
-    SV_REQUIRE(g.n % 4 == 0 && (((uintptr_t)g.part) & 15) == 0,
-               "sv_reduce_partials_multi: segment %d needs n %% 4 == 0 and 16-B aligned partials", i);
+    // the 16-B bodies (wide; deep with n % 4 == 0) read every partial row from a 16-B aligned start
+    if (g.n % 4 == 0) SV_REQUIRE((((uintptr_t)g.part) & 15) == 0, "sv_reduce_partials_multi: partials must be 16-B aligned");
     const int64_t nb = wide ? (g.n / 4 + kThreads - 1) / kThreads : (g.n + 63) / 64;
     m.s[k] = MultiSeg{g.part, g.out, g.n, blocks, g.P, wide ? 1 : 0, g.accumulate ? 1 : 0};
     blocks += nb;
