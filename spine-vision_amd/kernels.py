@@ -233,6 +233,9 @@ _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
 # 1065.7-1067.9 img/s interleaved, fold 4.0 -> 2.5 ms/step (profiles/round4/r7f_fold_ab.txt; round 3 had
 # measured 128 and 256 equal)
 _WGRAD9_TARGET = int(os.environ.get("SV_WGRAD9_WGS", "128"))
+# ...but the whole chip for long weight gradients: ConvNeXt-large bs64's (309 GFLOP each) on half the chip made the
+# side stream the long pole (590 vs 598 img/s at 256, profiles/round4/r9c_large_wgrad_target.txt)
+_WGRAD9_LONG_GFLOP = float(os.environ.get("SV_WGRAD9_LONG_GFLOP", "150"))
 
 
 def _wgrad_split(tiles: int, K: int) -> int:
@@ -248,11 +251,13 @@ def _wgrad_split_for(N: int, K: int, M: int) -> int:
     64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
     if min(N, K) >= 128 and max(N, K) >= 256:
         tiles9 = -(-N // 256) * -(-K // 256)
-        split = max(1, _WGRAD9_TARGET // tiles9)
-        while split > 1 and M % (split * 64):
-            split -= 1
-        if M % (split * 64) == 0:
-            return split
+        target = _WGRAD9_TARGET if 2.0 * M * N * K <= _WGRAD9_LONG_GFLOP * 1e9 else 256
+        # the slice count whose grid is nearest the target, among those that cut M into whole 64-row K-tiles and
+        # keep one workgroup per CU (rounding down alone left ConvNeXt-large's S3 wgrads, 36 tiles, at split 2:
+        # 72 workgroups, 47 % longer launches, the large bs64 step 16 % slower, profiles/round4/r9b_configs/)
+        ok = [s_ for s_ in range(1, max(2, 2 * target // tiles9 + 1)) if M % (s_ * 64) == 0 and tiles9 * s_ <= 256]
+        if ok:
+            return min(ok, key=lambda s_: (abs(tiles9 * s_ - target), s_))
     return _wgrad_split(-(-N // 128) * -(-K // 128), M)
 
 
