@@ -229,15 +229,19 @@ def _stream() -> int:
     return _raw_stream(_cur_device())
 
 
+_FNS: dict = {}  # name -> bound ctypes function (ctypes attribute lookup is a dict miss + a getattr per call)
+
+
 def call(name: str, *args):
     """Invoke an sv_* entry point on the current stream; raise RuntimeError on a non-zero status."""
-    L = _lib if _lib is not None else lib()
-    fn = getattr(L, name)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(_lib if _lib is not None else lib(), name)
     if name in _VALUE_FNS:
         return fn(*args)
     rc = fn(*args, _stream())
     if rc != 0:
-        msg = L.sv_last_error_string().decode()
+        msg = lib().sv_last_error_string().decode()
         raise RuntimeError(f"{name} failed (status {rc}): {msg}")
     return rc
 
