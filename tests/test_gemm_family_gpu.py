@@ -124,12 +124,14 @@ def _torch_refs(t, M, C):
     return ref
 
 
-# ConvNeXt-base 512x512 bs32: S1 (M = 32*128^2, C = 128), S3 (32*32^2, 512), S4 (32*16^2, 1024)
-_BS32 = [(524288, 128), (32768, 512), (8192, 1024)]
+# ConvNeXt-base 512x512 bs32: S1 (M = 32*128^2, C = 128), S3 (32*32^2, 512), S4 (32*16^2, 1024); ConvNeXt-large
+# 512x512 bs64 (BASELINE configs[4]): S1 (64*128^2, 192, partial 256-column tiles) and S3 (64*32^2, 768, the stage
+# of 27 of its 36 blocks; its weight gradients at split 4 = 144 workgroups)
+_BS32 = [(524288, 128), (32768, 512), (8192, 1024), (1048576, 192), (65536, 768)]
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("M,C", _BS32, ids=["S1", "S3", "S4"])
+@pytest.mark.parametrize("M,C", _BS32, ids=["S1", "S3", "S4", "large-S1", "large-S3"])
 def test_gemm_bs32_production_schedule(dev, M, C):
     """The bs32 shapes the bench runs: the dispatch's schedule (v9 with several tiles per persistent workgroup
     where it picks v9) under the forward's default policy AND the lean backward's (one persistent workgroup per
