@@ -29,6 +29,11 @@ __device__ __forceinline__ void st4d(void* p, int dt, size_t i, float4 v) {
   else st4(reinterpret_cast<uint16_t*>(p), i, v);
 }
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+// channel of flat element e: 32-bit division where the tensor fits (64-bit division is a long software sequence
+// on the GPU and these passes run it once per element group); `n` = the tensor's element count
+__device__ __forceinline__ int chan_of(size_t e, int C, int64_t n) {
+  return n <= 0xffffffffll ? (int)((uint32_t)e % (uint32_t)C) : (int)(e % (size_t)C);
+}
 __device__ __forceinline__ float4 ld4f(const float* p, int c) { return *reinterpret_cast<const float4*>(p + c); }
 
 // V consecutive channels per thread: 8 (one 16-B bf16 access, two 16-B f32 accesses) when C % 8 == 0,
@@ -281,7 +286,7 @@ __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
   const int64_t nv = a.rows * a.C / V;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
     const size_t e = (size_t)i * V;
-    const int c = (int)(e % a.C);
+    const int c = chan_of(e, a.C, a.rows * a.C);
     float v[V], mu[V], rs[V], g[V], b[V], o[V];
     ldv<V>(a.y, a.ydt, e, v);
     ldp<V>(a.mean, c, mu);
@@ -339,10 +344,15 @@ struct PoolSrc {
 template <int V>
 __device__ __forceinline__ void pool_grad(const PoolSrc& p, int C, size_t e, float (&g)[V]) {
   const int OH = pool_out(p.H), OW = pool_out(p.W);
-  const int c = (int)(e % C);
-  const int64_t pix = (int64_t)(e / C);
-  const int ix = (int)(pix % p.W), iy = (int)((pix / p.W) % p.H);
-  const int64_t b = pix / ((int64_t)p.W * p.H);
+  // pixel coordinates in 32-bit arithmetic (the host guarantees B*H*W*C < 2^31): 64-bit division is a long
+  // software sequence on the GPU, and this runs once per element group in both BatchNorm passes
+  const uint32_t ee = (uint32_t)e, uC = (uint32_t)C;
+  const int c = (int)(ee % uC);
+  const uint32_t pix = ee / uC, rowi = pix / (uint32_t)p.W;
+  const int ix = (int)(pix - rowi * (uint32_t)p.W);
+  const uint32_t bq = rowi / (uint32_t)p.H;
+  const int iy = (int)(rowi - bq * (uint32_t)p.H);
+  const int64_t b = (int64_t)bq;
 #pragma unroll
   for (int q = 0; q < V; ++q) g[q] = 0.f;
   const int oy0 = iy / 2, oy1 = (iy + 1) / 2;
@@ -561,7 +571,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     const size_t e = (size_t)i * V;
-    const int c = (int)(e % a.C);
+    const int c = chan_of(e, a.C, a.rows * a.C);
     float v[V], mu[V], rs[V], ga[V], sg[V], sgx[V], g[V], o[V];
     ldv<V>(a.y, a.ydt, e, v);
     ldp<V>(a.mean, c, mu);
@@ -596,7 +606,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_dual_kernel(const BwdDualA
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     const size_t e = (size_t)i * V;
-    const int c = (int)(e % a.C);
+    const int c = chan_of(e, a.C, a.rows * a.C);
     float g[V], v[V], w[V], o[V], o2[V], mu[V], rs[V], ga[V], sg[V], sgx[V];
     ldv<V>(a.g, SV_F32, e, g);
     ldv<V>(a.y, a.ydt, e, v);
@@ -639,10 +649,21 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const void* __res
   const int64_t n4 = (int64_t)B * OH * OW * C / 4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = i * 4;
-    const int c = (int)(e % C);
-    const int64_t pix = e / C;
-    const int ox = (int)(pix % OW), oy = (int)((pix / OW) % OH);
-    const int64_t b = pix / ((int64_t)OW * OH);
+    int c, ox, oy;
+    int64_t b;
+    if (n4 * 4 <= 0xffffffffll) {  // 32-bit index arithmetic (see chan_of)
+      const uint32_t ee = (uint32_t)e, pix = ee / (uint32_t)C, r = pix / (uint32_t)OW, bq = r / (uint32_t)OH;
+      c = (int)(ee - pix * (uint32_t)C);
+      ox = (int)(pix - r * (uint32_t)OW);
+      oy = (int)(r - bq * (uint32_t)OH);
+      b = bq;
+    } else {
+      const int64_t pix = e / C;
+      c = (int)(e % C);
+      ox = (int)(pix % OW);
+      oy = (int)((pix / OW) % OH);
+      b = pix / ((int64_t)OW * OH);
+    }
     float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int arg[4] = {-1, -1, -1, -1};
     for (int kh = 0; kh < 3; ++kh) {
@@ -1195,7 +1216,7 @@ extern "C" int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const 
 // dpool [B][OH][OW][C] (f32) through idx, gathered inside both passes instead of materialised
 static bool pool_args_ok(const float* dpool, const uint8_t* idx, int B, int H, int W, int C) {
   return dpool && idx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && ((uintptr_t)dpool & 15) == 0 &&
-         ((uintptr_t)idx & 3) == 0;
+         ((uintptr_t)idx & 3) == 0 && (int64_t)B * H * W * C < (1ll << 31);  // pool_grad's 32-bit indexing
 }
 
 extern "C" int sv_bn_relu_bwd_stats_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W,
