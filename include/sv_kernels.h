@@ -49,6 +49,28 @@ int sv_version(void);                        /* ABI version, bumped on any signa
 const char* sv_last_error_string(void);      /* thread-local message of the last failing call    */
 const char* sv_build_target(void);           /* offload arch the device code was compiled for     */
 
+/* ---- per-device context (sv_ctx_create / sv_ctx_destroy) ---------------------------------
+ * The library keeps, per device, the properties its launches are sized by (CU count, LDS per workgroup) and the
+ * set of kernels whose dynamic-LDS limit it has raised on that device; every entry point finds its device from the
+ * stream it is given, under one mutex, so the library is reentrant across devices and threads.  sv_ctx is the
+ * handle to that per-device state: sv_ctx_create(device) queries it now (instead of at the first launch) and
+ * returns the device's context (the same handle for the same device, reference-counted); sv_ctx_destroy drops a
+ * reference and, at zero, forgets the device's cached state (the next launch queries it again).  Entry points do
+ * not take the handle: they work with or without one.                                                          */
+typedef struct sv_ctx sv_ctx;
+typedef struct sv_ctx_info {
+  int32_t device;              /* HIP device ordinal                                                            */
+  int32_t compute_units;       /* CUs the persistent grids are sized for                                        */
+  int32_t lds_bytes_per_wg;    /* the device's per-workgroup LDS limit (160 KiB on gfx950)                      */
+  int32_t xcds;                /* L2 domains the block order is dealt over (8 on MI355X)                         */
+  int32_t lds_raised_kernels;  /* kernels whose dynamic-LDS limit the library has raised on this device so far   */
+  int32_t refs;                /* live sv_ctx_create references                                                 */
+  char arch[32];               /* gcnArchName                                                                   */
+} sv_ctx_info;
+int sv_ctx_create(int32_t device, sv_ctx** out);
+int sv_ctx_destroy(sv_ctx* ctx);
+int sv_ctx_get_info(const sv_ctx* ctx, sv_ctx_info* out);
+
 /* ---- data-parallel CU reserve ---------------------------------------------------------------
  * A stream of `device` whose kernels never occupy the CUs listed in `reserved` (n_reserved CU indices in the
  * numbering of hipExtStreamCreateWithCUMask's bit vector), so RCCL's all-reduce kernels -- on streams of their

@@ -27,11 +27,41 @@ int check_launch(const char* what) {
   return SV_OK;
 }
 
+}  // namespace sv
+
+// The per-device context (sv_ctx): everything the launches are sized by, queried once per device, under one mutex.
+struct sv_ctx {
+  int device = -1;
+  int cus = 0;  // 0 = not queried yet
+  int lds = 0;
+  int refs = 0;
+  char arch[32] = "";
+  std::set<const void*> lds_raised;  // kernels whose dynamic-LDS limit is raised on this device
+};
+
+namespace sv {
+
 namespace {
 constexpr int kMaxDevices = 64;
 std::mutex g_dev_mu;
-int g_cus[kMaxDevices] = {};                       // 0 = not queried yet
-std::set<std::pair<const void*, int>> g_lds_attr;  // (kernel, device) pairs whose LDS limit is raised
+sv_ctx g_ctx[kMaxDevices];
+
+// the device's context with its properties queried (caller holds g_dev_mu)
+sv_ctx& ctx_locked(int dev) {
+  sv_ctx& c = g_ctx[dev];
+  if (!c.cus) {
+    c.device = dev;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    c.cus = n;
+    int l = 0;
+    if (hipDeviceGetAttribute(&l, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || l <= 0) l = 163840;
+    c.lds = l;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) snprintf(c.arch, sizeof(c.arch), "%s", prop.gcnArchName);
+  }
+  return c;
+}
 }  // namespace
 
 int stream_device(hipStream_t s) {
@@ -44,19 +74,15 @@ int device_cus(hipStream_t s) {
   const int dev = stream_device(s);
   if (dev < 0 || dev >= kMaxDevices) return 256;
   std::lock_guard<std::mutex> lk(g_dev_mu);
-  if (!g_cus[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    g_cus[dev] = n;
-  }
-  return g_cus[dev];
+  return ctx_locked(dev).cus;
 }
 
 void ensure_lds_attr(const void* kernel, int bytes, hipStream_t s) {
   if (bytes <= 65536) return;
   const int dev = stream_device(s);
+  if (dev < 0 || dev >= kMaxDevices) return;
   std::lock_guard<std::mutex> lk(g_dev_mu);
-  if (g_lds_attr.insert({kernel, dev}).second) {
+  if (ctx_locked(dev).lds_raised.insert(kernel).second) {
     int cur = -1;
     hipGetDevice(&cur);
     if (cur != dev) hipSetDevice(dev);
@@ -80,7 +106,46 @@ int policy_grid(const sv_gemm_policy* pol, int total, int per_cu_default, hipStr
 
 extern "C" {
 
-int sv_version(void) { return 3; }
+int sv_version(void) { return 4; }
+
+int sv_ctx_create(int32_t device, sv_ctx** out) {
+  SV_REQUIRE(out, "sv_ctx_create: null out");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  SV_REQUIRE(device >= 0 && device < n && device < sv::kMaxDevices, "sv_ctx_create: no device %d (%d visible)",
+             (int)device, n);
+  std::lock_guard<std::mutex> lk(sv::g_dev_mu);
+  sv_ctx& c = sv::ctx_locked(device);
+  ++c.refs;
+  *out = &c;
+  return SV_OK;
+}
+
+int sv_ctx_destroy(sv_ctx* ctx) {
+  SV_REQUIRE(ctx && ctx >= sv::g_ctx && ctx < sv::g_ctx + sv::kMaxDevices, "sv_ctx_destroy: not a context");
+  std::lock_guard<std::mutex> lk(sv::g_dev_mu);
+  SV_REQUIRE(ctx->refs > 0, "sv_ctx_destroy: context of device %d already released", ctx->device);
+  if (--ctx->refs == 0) {  // forget the cached state; the LDS limits stay raised in the runtime (harmless)
+    const int dev = ctx->device;
+    *ctx = sv_ctx{};
+    ctx->device = dev;
+  }
+  return SV_OK;
+}
+
+int sv_ctx_get_info(const sv_ctx* ctx, sv_ctx_info* out) {
+  SV_REQUIRE(ctx && out && ctx >= sv::g_ctx && ctx < sv::g_ctx + sv::kMaxDevices, "sv_ctx_get_info: bad arguments");
+  std::lock_guard<std::mutex> lk(sv::g_dev_mu);
+  sv_ctx& c = sv::ctx_locked((int)(ctx - sv::g_ctx));
+  out->device = c.device;
+  out->compute_units = c.cus;
+  out->lds_bytes_per_wg = c.lds;
+  out->xcds = c.cus % 8 == 0 ? 8 : 1;
+  out->lds_raised_kernels = (int32_t)c.lds_raised.size();
+  out->refs = c.refs;
+  snprintf(out->arch, sizeof(out->arch), "%s", c.arch);
+  return SV_OK;
+}
 
 const char* sv_last_error_string(void) { return sv::g_err; }
 

@@ -45,6 +45,12 @@ class GemmPolicy(ctypes.Structure):
                 f"priority={self.priority})")
 
 
+class CtxInfo(ctypes.Structure):
+    """sv_ctx_info (include/sv_kernels.h): the per-device state the library sizes its launches by."""
+    _fields_ = [("device", _i32), ("compute_units", _i32), ("lds_bytes_per_wg", _i32), ("xcds", _i32),
+                ("lds_raised_kernels", _i32), ("refs", _i32), ("arch", ctypes.c_char * 32)]
+
+
 def policy(impl: int = 0, grid_cap: int = 0, wg_per_cu: int = 0, priority: int = 0) -> GemmPolicy:
     return GemmPolicy(int(impl), int(grid_cap or 0), int(wg_per_cu), int(priority))
 
@@ -96,6 +102,9 @@ _POL = ctypes.POINTER(GemmPolicy)
 # name -> argtypes (restype is int for all entry points unless listed in _RESTYPES)
 _SIGS = {
     "sv_version": [],
+    "sv_ctx_create": [_i32, ctypes.POINTER(_p)],
+    "sv_ctx_destroy": [_p],
+    "sv_ctx_get_info": [_p, ctypes.POINTER(CtxInfo)],
     "sv_last_error_string": [],
     "sv_build_target": [],
     "sv_gemm": [ctypes.POINTER(GemmDesc), _p],
@@ -183,6 +192,9 @@ _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.
 _VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
                                                                      "sv_stream_create_cu_reserved", "sv_bn_small_ok"}
 
+# entry points that take no stream (call() appends none) but return an sv_status
+_NOSTREAM_FNS = {"sv_ctx_create", "sv_ctx_destroy", "sv_ctx_get_info"}
+
 _lib = None
 _lock = threading.Lock()
 
@@ -239,7 +251,7 @@ def call(name: str, *args):
         fn = _FNS[name] = getattr(_lib if _lib is not None else lib(), name)
     if name in _VALUE_FNS:
         return fn(*args)
-    rc = fn(*args, _stream())
+    rc = fn(*args) if name in _NOSTREAM_FNS else fn(*args, _stream())
     if rc != 0:
         msg = lib().sv_last_error_string().decode()
         raise RuntimeError(f"{name} failed (status {rc}): {msg}")
@@ -274,3 +286,39 @@ def dt(t: torch.Tensor) -> int:
     if t.dtype == torch.bfloat16:
         return SV_BF16
     raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+class DeviceContext:
+    """The library's per-device context (sv_ctx): created once per device by the host (StepEngine,
+    the trainers), it queries the device's properties up front and holds a reference until ``close()``.  Entry
+    points find their device from the stream, so launches work with or without one."""
+
+    def __init__(self, device: int) -> None:
+        h = _p()
+        call("sv_ctx_create", int(device), ctypes.byref(h))
+        self._h = h
+
+    def info(self) -> CtxInfo:
+        out = CtxInfo()
+        call("sv_ctx_get_info", self._h, ctypes.byref(out))
+        return out
+
+    @property
+    def handle(self) -> int:
+        return int(self._h.value or 0)
+
+    def close(self) -> None:
+        if self._h is not None:
+            call("sv_ctx_destroy", self._h)
+            self._h = None
+
+
+_CONTEXTS: dict = {}
+
+
+def device_context(device: int) -> DeviceContext:
+    """The process's context of ``device`` (created on first use, kept for the process's lifetime)."""
+    c = _CONTEXTS.get(device)
+    if c is None:
+        c = _CONTEXTS[device] = DeviceContext(device)
+    return c

@@ -108,6 +108,11 @@ class StepEngine:
                 raise ValueError(f"cuda_graph=True: {unsafe[0]} is not capture-safe (graph_safe = False)")
         self.model = model
         self.device = torch.device(device)
+        if self.device.type == "cuda":  # the kernel library's per-device context (sv_ctx), queried up front
+            from .. import native as nv
+
+            self.ctx = nv.device_context(self.device.index if self.device.index is not None else
+                                         torch.cuda.current_device())
         self.grad_clip = grad_clip
         self.arena = FlatArena(model, self.device, with_shadow=self.device.type == "cuda")
         self.optimizer = FlatAdamW(self.arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)

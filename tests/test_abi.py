@@ -64,7 +64,8 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
 
     structs = {"sv_gemm_desc": nv.GemmDesc, "sv_gemm_policy": nv.GemmPolicy, "sv_bn_ref": nv.BnRef,
-               "sv_red_seg": nv.RedSeg, "sv_pack_seg": nv.PackSeg, "sv_conv_shape": nv.ConvShape}
+               "sv_red_seg": nv.RedSeg, "sv_pack_seg": nv.PackSeg, "sv_conv_shape": nv.ConvShape,
+               "sv_ctx_info": nv.CtxInfo}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sv_kernels.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
@@ -82,3 +83,16 @@ def test_struct_layouts_match_header(tmp_path):
         assert int(got[cname]) == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def test_ctx_rejects_bad_devices():
+    """sv_ctx_create validates the device ordinal (no GPU in the build container: every ordinal is out of range) and
+    sv_ctx_destroy / sv_ctx_get_info refuse pointers that are not contexts."""
+    L = nv.lib()
+    h = ctypes.c_void_p()
+    assert L.sv_ctx_create(-1, ctypes.byref(h)) == 1
+    assert "no device" in L.sv_last_error_string().decode()
+    assert L.sv_ctx_create(10**6, ctypes.byref(h)) == 1
+    bogus = ctypes.c_void_p(16)
+    assert L.sv_ctx_destroy(bogus) == 1
+    assert L.sv_ctx_get_info(bogus, ctypes.byref(nv.CtxInfo())) == 1

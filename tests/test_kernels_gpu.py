@@ -557,3 +557,26 @@ def test_reduce_multi_matches_pair_and_torch(dev):
         ref = p.double().sum(0) + (r.double() if acc else 0)
         err = float((o.double() - ref).abs().max() / (ref.abs().max() + 1e-30))
         assert err < 1e-5, (P, n, acc, err)
+
+
+def test_device_context(dev):
+    """sv_ctx: one reference-counted context per device holding what the launches are sized
+    by -- the CU count the persistent grids use, the LDS limit, the kernels whose LDS limit was raised there."""
+    from spine_vision_amd import native as nv
+
+    a, b = nv.DeviceContext(dev.index or 0), nv.DeviceContext(dev.index or 0)
+    try:
+        assert a.handle == b.handle != 0
+        i = a.info()
+        props = torch.cuda.get_device_properties(dev)
+        assert i.device == (dev.index or 0) and i.compute_units == props.multi_processor_count
+        assert i.lds_bytes_per_wg >= 65536 and i.arch.decode().startswith("gfx950") and i.refs >= 2
+        x = torch.randn(4096, 512, device=dev).to(torch.bfloat16)
+        w = torch.randn(2048, 512, device=dev).to(torch.bfloat16)
+        K.linear_fwd(x, w, out=torch.empty(4096, 2048, device=dev, dtype=torch.bfloat16))  # a 160 KiB-LDS v9 launch
+        torch.cuda.synchronize()
+        assert a.info().lds_raised_kernels >= 1
+    finally:
+        a.close()
+        b.close()
+    assert nv.device_context(dev.index or 0).info().refs >= 1  # the process's own context stays
