@@ -403,7 +403,9 @@ int sv_conv_weight_pack_multi(const sv_pack_seg* segs, int32_t nseg, int32_t dty
 int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t dtype, const sv_conv_shape* s,
                 const sv_gemm_policy* policy, sv_stream_t stream);
 /* dx (+)= conv_transpose(dy, w): dy [B][OH][OW][Cout] (dtype), dx [B][H][W][Cs] (dx_dtype). Stride-2
- * convolutions run as four stride-1 sub-convolutions, one per output parity class.                 */
+ * convolutions run as four stride-1 sub-convolutions, one per output parity class; bf16 with even H, W,
+ * more than one tap, Cout >= 32 and Cs % 8 == 0 (accumulate: f32 dx) as ONE gathered GEMM launch whose
+ * epilogue stores each class's rows at their dx pixels (no workspace, no scatter pass).              */
 int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
                      int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* policy, sv_stream_t stream);
 /* dw (+)= dy^T * im2col(x) into torch layout [Cout][Cin][KH][KW] f32, through split-K f32 slabs in
@@ -442,7 +444,9 @@ int sv_conv_bwd_data_split(const void* dy, const void* wp, void* dx, int32_t dx_
  * the backward statistics partials [ceil(B*H*W/64)][2][Cs] of the BatchNorm + ReLU that produced the
  * conv's input (y = that BatchNorm's input [B][H][W][Cs] bf16): split == 1 from the GEMM epilogue
  * (SV_EPI_STORE_BN_BWD), split >= 2 through f32 slabs in `work` (split * B*H*W*Cs floats) and
- * sv_gemm_slab_finish_bn_bwd.  Other shapes are an error.                                            */
+ * sv_gemm_slab_finish_bn_bwd.  Stride 2 (even H, W, more than one tap, split == 1): the one-launch
+ * parity-class GEMM (sv_conv_bwd_data) with the same epilogue, partials [4][ceil(B*H*W/256)][2][Cs]
+ * (class c = 2*(y&1) + (x&1) from row c * ceil(B*H*W/256)).  Other shapes are an error.              */
 int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int32_t dtype, const sv_conv_shape* s,
                         const void* y, const sv_bn_ref* bn, float* part, float* work, int32_t split,
                         const sv_gemm_policy* policy, sv_stream_t stream);

@@ -41,6 +41,9 @@ _FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
 # (split, default: +2.2 %), also from the unsplit GEMMs' epilogue (1: no faster than a separate pass, the
 # layer1/2 epilogues absorb what the pass saved), or from their own pass everywhere (0) -- r6e A/B
 _BN_BWD_EPI = os.environ.get("SV_BN_BWD_EPI", "split")
+# SV_S2_BN=1: the strided 3x3s' inner BatchNorm statistics from the one-launch parity-class dgrad's
+# epilogue (SV_EPI_STORE_BN_BWD) instead of their own pass: -0.9 % (r9i, as for stride 1)
+_S2_BN = os.environ.get("SV_S2_BN", "0") == "1"
 # SV_BN_DUAL=0: a projection-shortcut block's two output BatchNorm backwards as separate passes (A/B runs)
 _BN_DUAL = os.environ.get("SV_BN_DUAL", "1") != "0"
 
@@ -509,9 +512,11 @@ class ResNetHip(nn.Module):
             _, py, pmean, prstd, pa, _, _ = saved[ci - 1]
             Cp = py.shape[-1]
             # the inner BN's backward statistics from the data gradient's GEMM epilogue / split-K finish where
-            # that path carries them (stride 1, bf16), else from bn_bwd's own statistics pass
+            # that path carries them (bf16; stride 2 on even grids without a split), else from bn_bwd's own
+            # statistics pass
             fused = (K.conv_bwd_data_bn(dy4, wp, s, py, pmean, prstd, pbn.weight, pbn.bias,
-                                        unsplit=_BN_BWD_EPI != "split", policy=pol)
+                                        unsplit=_BN_BWD_EPI != "split" or (s.stride == 2 and _S2_BN),
+                                        policy=pol)
                      if _BN_BWD_EPI != "0" and act == torch.bfloat16 else None)
             da, bpart = fused if fused is not None else (K.conv_bwd_data(dy4, wp, s, dx_dtype=act, policy=pol), None)
             # the inner BN's own ReLU: mask recomputed from y (the activation pa is not read again)

@@ -884,12 +884,18 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
     const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
-  if (dtype == SV_BF16 && st == 2 && slab && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
+  // stride 2, even H, W, more than one tap: all four output parity classes share one GH x GW grid
+  const bool s2_even = st == 2 && s->H % 2 == 0 && s->W % 2 == 0 && s->KH * s->KW > 1;
+  // ... and without a workspace their rows go straight into dx (plain store, in-place f32 accumulate, or
+  // bf16 with the BatchNorm statistics)
+  const bool s2_direct = s2_even && !slab && (!accumulate || dx_dtype == SV_F32) && (!bn || dx_dtype == SV_BF16);
+  if (dtype == SV_BF16 && st == 2 && (slab || s2_direct) && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
     // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass.  Even H, W
-    // and no split: all four classes share one GH x GW grid and run as ONE launch (mode 5) -- the
-    // per-class launches are each below one wave of workgroups (64-128 tiles for the ResNet-50 3x3s)
+    // and no split: all four classes run as ONE launch (mode 5) -- the per-class launches are each below
+    // one wave of workgroups (64-128 tiles for the ResNet-50 3x3s) -- and with no workspace that launch
+    // stores each class's rows at their dx pixels (no slabs, no scatter pass)
     ClassSlabs cs{};
-    if (split == 1 && s->H % 2 == 0 && s->W % 2 == 0 && s->KH * s->KW > 1) {
+    if (s2_direct || (split == 1 && s2_even)) {
       const int GH = s->H / 2, GW = s->W / 2, M = s->B * GH * GW;
       ConvG g = make_convg(OH, OW, s->Cout, GH, GW, 1);
       g.lcout = ilog2(s->Cout);
@@ -916,6 +922,24 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
         cs.GH[cls] = GH;
         cs.GW[cls] = GW;
         cs.base[cls] = g.ctaps[cls] ? slab + (size_t)cls * M * s->Cs : nullptr;
+      }
+      if (s2_direct) {
+        sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, dx, dx_dtype, pol);
+        if (bn) {  // partial rows [4][ceil(M / 64)][2][Cs]: class c's from row c * ceil(M / 64)
+          d.epilogue = SV_EPI_STORE_BN_BWD;
+          d.aux = bny;
+          d.aux_dtype = SV_BF16;
+          d.ld_aux = s->Cs;
+          d.bn = bn;
+          d.C2 = bnpart;
+          d.c2_dtype = SV_F32;
+        } else if (accumulate) {  // dx += conv^T(dy) in place (gamma = 1)
+          d.epilogue = SV_EPI_BIAS_GAMMA_RES;
+          d.aux = dx;
+          d.aux_dtype = SV_F32;
+          d.ld_aux = s->Cs;
+        }
+        return launch_gemm3_conv(&d, g, 5, (hipStream_t)stream);
       }
       sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, slab, SV_F32, pol);
       d.epilogue = SV_EPI_SLAB;
@@ -1033,9 +1057,12 @@ extern "C" int sv_conv_bwd_data_bn(const void* dy, const void* wp, void* dx, int
   if (int rc = check_shape(s, dtype, "sv_conv_bwd_data_bn")) return rc;
   SV_REQUIRE(y && bn && part && bn->mean && bn->rstd && bn->gamma && bn->beta && split >= 1 && (split == 1 || work),
              "sv_conv_bwd_data_bn: null pointer / split > 1 without a workspace");
-  SV_REQUIRE(dtype == SV_BF16 && s->stride == 1 && s->Cout >= 32 && pow2(s->Cout) && s->Cs % 8 == 0 &&
+  // stride 2: even H, W, more than one tap, no split (mode 5 straight into dx)
+  const bool s2 = s->stride == 2 && s->H % 2 == 0 && s->W % 2 == 0 && s->KH * s->KW > 1 && split == 1;
+  SV_REQUIRE(dtype == SV_BF16 && (s->stride == 1 || s2) && s->Cout >= 32 && pow2(s->Cout) && s->Cs % 8 == 0 &&
                  ((int64_t)s->KH * s->KW * s->Cout) % 32 == 0,
-             "sv_conv_bwd_data_bn: only the bf16 stride-1 gathered path (Cout >= 32, power of two; Cs %% 8 == 0)");
+             "sv_conv_bwd_data_bn: only the bf16 stride-1 gathered path or stride 2 with even H, W and no split "
+             "(Cout >= 32, power of two; Cs %% 8 == 0)");
   return conv_bwd_data_impl(dy, wp, dx, SV_BF16, 0, dtype, s, policy, stream, split > 1 ? work : nullptr, split, y, bn,
                             part);
 }

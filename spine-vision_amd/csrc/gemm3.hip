@@ -419,7 +419,9 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     // the epilogue operand is bf16 (GELU'(h), pre-activation) or the f32 residual stream
     constexpr int AUXT = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD || EPI == SV_EPI_STORE_BN_BWD) ? SV_BF16
                          : EPI == SV_EPI_BIAS_GAMMA_RES ? SV_F32 : -1;
-    wave_tile_epilogue<4, 2, EPI, AUXT>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64,
+    // mode 5 with a non-slab epilogue: each class's rows go straight to their dx pixels
+    constexpr bool REMAP = CONV == 5 && EPI != SV_EPI_SLAB;
+    wave_tile_epilogue<4, 2, EPI, AUXT, REMAP>(acc, reinterpret_cast<float*>(smem) + wid * 16 * EPI_LD, m0 + wm * 64,
                                   n0 + wn * 64, e, split);
   }
 }
@@ -442,6 +444,15 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
     e.bn_rs = d->bn->rstd;
     e.bn_be = d->bn->beta;
     e.gamma = d->bn->gamma;
+  }
+  if constexpr (CONV == 5 && EPI != SV_EPI_SLAB) {  // rows remapped to dx pixels (even H, W: 2GH x 2GW)
+    e.rm_gh = cg->GH;
+    e.rm_gw = cg->GW;
+    e.rm_gw_mul = cg->gw_mul;
+    e.rm_gw_shift = cg->gw_shift;
+    e.rm_ghw_mul = cg->ghw_mul;
+    e.rm_ghw_shift = cg->ghw_shift;
+    e.rm_prow = ceil_div(d->M, 64);
   }
   ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>), (int)C::LDS, s);
   // one workgroup per tile, which lets kernels of the side stream take CUs as tiles retire
@@ -504,6 +515,12 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   if (mode == 2 && d->epilogue == SV_EPI_SLAB)
     return launch<true, false, SV_EPI_SLAB, 32, S, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, S, 5>(d, 4, s, &g);
+  // mode 5 straight into dx (no split): plain store, in-place accumulate, or with the BatchNorm statistics
+  if (mode == 5 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 5>(d, 4, s, &g);
+  if (mode == 5 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
+    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5>(d, 4, s, &g);
+  if (mode == 5 && d->epilogue == SV_EPI_STORE_BN_BWD)
+    return launch<true, false, SV_EPI_STORE_BN_BWD, 32, S, 5>(d, 4, s, &g);
   // 8-channel pixels (the ResNet stem), plain store or with the BatchNorm statistics
   if (mode == 6 && d->epilogue == SV_EPI_STORE) return launch<true, true, SV_EPI_STORE, 32, S, 6>(d, 1, s, &g);
   if (mode == 6 && d->epilogue == SV_EPI_STORE_STATS)

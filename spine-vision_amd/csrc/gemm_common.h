@@ -26,7 +26,23 @@ struct EpiArgs {
   const float* bn_mu = nullptr;
   const float* bn_rs = nullptr;
   const float* bn_be = nullptr;
+  // remapped rows (the v3 kernel's stride-2 dgrad, mode 5, storing straight into dx): GEMM row m of
+  // parity class `split` = (b, gy, gx) on the class's GH x GW grid -> output row
+  // (b * 2GH + 2gy + py) * 2GW + 2gx + px, for the store and the epilogue operand alike; the
+  // STORE_BN_BWD partial rows of class c start at row c * rm_prow
+  int rm_gh = 0, rm_gw = 0, rm_prow = 0;
+  uint32_t rm_gw_mul = 0, rm_gw_shift = 0, rm_ghw_mul = 0, rm_ghw_shift = 0;
 };
+
+__device__ __forceinline__ size_t remap_row(const EpiArgs& e, int m, int cls) {
+  const uint32_t u = (uint32_t)m;
+  const uint32_t b = (__umulhi(u, e.rm_ghw_mul) + u) >> e.rm_ghw_shift;
+  const uint32_t rem = u - b * (uint32_t)(e.rm_gh * e.rm_gw);
+  const uint32_t gy = (__umulhi(rem, e.rm_gw_mul) + rem) >> e.rm_gw_shift;
+  const uint32_t gx = rem - gy * (uint32_t)e.rm_gw;
+  const size_t y = (size_t)b * (2 * e.rm_gh) + 2 * gy + (cls >> 1);
+  return y * (size_t)(2 * e.rm_gw) + 2 * gx + (cls & 1);
+}
 
 __device__ __forceinline__ float4 ld4_any(const void* p, int dt, size_t i) {
   return dt == SV_F32 ? ld4(reinterpret_cast<const float*>(p), i) : ld4(reinterpret_cast<const uint16_t*>(p), i);
@@ -116,12 +132,18 @@ __device__ __forceinline__ void gelu_dual4(float4 v, float4& g, float4& dg) {
 // EPI >= 0: the epilogue kind is a compile-time constant (kernels specialised per epilogue carry
 // only that epilogue's registers); EPI = -1: read e.epi at run time.
 // AUXT: dtype of the epilogue operand when known at compile time (SV_F32 / SV_BF16), -1 = e.aux_dtype
-template <int FM, int PRE = 1, int FN = 4, int J0 = 0, int EPI = -1, int AUXT = -1>
+// REMAP: output / operand rows through remap_row (e.rm_*, `split` = the parity class); not with SLAB
+template <int FM, int PRE = 1, int FN = 4, int J0 = 0, int EPI = -1, int AUXT = -1, bool REMAP = false>
 __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], int i0, float* __restrict__ slab,
                                                     int mb, int nb, const EpiArgs& e_in, int split) {
   EpiArgs e = e_in;
   if constexpr (EPI >= 0) e.epi = EPI;
   if constexpr (AUXT >= 0) e.aux_dtype = AUXT;
+  static_assert(!REMAP || (EPI >= 0 && EPI != SV_EPI_SLAB), "remapped rows: compile-time non-slab epilogues");
+  auto orow = [&](int m) -> size_t {
+    if constexpr (REMAP) return remap_row(e, m, split);
+    else return (size_t)m;
+  };
   const int l = threadIdx.x & 63;
   const int cu = (l & 7) * 8, r0 = l >> 3;
   const int n = nb + cu;
@@ -177,11 +199,11 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       for (int q = 0; q < RW; ++q) r[h][q] = make_uint4(0, 0, 0, 0);
       if (need_aux && okn && m < e.M) {
         if (e.aux_dtype == SV_BF16) {
-          if (okn4) r[h][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n);
-          else r[h][0] = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n),
-                                    *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + (size_t)m * e.ld_aux + n + 2), 0, 0);
+          if (okn4) r[h][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(e.aux) + orow(m) * e.ld_aux + n);
+          else r[h][0] = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + orow(m) * e.ld_aux + n),
+                                    *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(e.aux) + orow(m) * e.ld_aux + n + 2), 0, 0);
         } else if constexpr (RW == 2) {
-          const float* f = reinterpret_cast<const float*>(e.aux) + (size_t)m * e.ld_aux + n;
+          const float* f = reinterpret_cast<const float*>(e.aux) + orow(m) * e.ld_aux + n;
           r[h][0] = *reinterpret_cast<const uint4*>(f);
           if (okn4) r[h][RW - 1] = *reinterpret_cast<const uint4*>(f + 4);
         }
@@ -209,8 +231,8 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
       xa[slot][h] = xb[slot][h] = make_float4(0.f, 0.f, 0.f, 0.f);
       const int m = mb + i * 16 + r0 + 8 * h;
       if (need_aux && okn && m < e.M) {
-        if (okn4) ld8_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n, xa[slot][h], xb[slot][h]);
-        else xa[slot][h] = ld4_any(e.aux, e.aux_dtype, (size_t)m * e.ld_aux + n);
+        if (okn4) ld8_any(e.aux, e.aux_dtype, orow(m) * e.ld_aux + n, xa[slot][h], xb[slot][h]);
+        else xa[slot][h] = ld4_any(e.aux, e.aux_dtype, orow(m) * e.ld_aux + n);
       }
     }
   };
@@ -244,7 +266,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb + i * 16 + r;
-        bn_y[r] = bn_ok && m < e.M ? __uint_as_float((uint32_t)yp[(size_t)m * e.ld_aux + bn_n] << 16) : 0.f;
+        bn_y[r] = bn_ok && m < e.M ? __uint_as_float((uint32_t)yp[orow(m) * e.ld_aux + bn_n] << 16) : 0.f;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -292,7 +314,7 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
         oa = ggrad4(va, xa[si][h]);
         ob = ggrad4(vb, xb[si][h]);
       }
-      const size_t ci = (size_t)m * e.ldc + n;
+      const size_t ci = orow(m) * e.ldc + n;
       if (okn4) st8_any(e.C, e.c_dtype, ci, oa, ob);
       else st4_any(e.C, e.c_dtype, ci, oa);
       if constexpr (kStats) {  // N % 8 == 0: all 8 columns valid
@@ -329,7 +351,8 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
   }
   if constexpr (kBnb) {  // the group's partial row [mb/64][2][N]: one writer per column
     if (bn_ok && mb < e.M) {
-      float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N + bn_n;
+      const int prow = (mb >> 6) + (REMAP ? split * e.rm_prow : 0);
+      float* P = reinterpret_cast<float*>(e.C2) + (size_t)prow * 2 * e.N + bn_n;
       P[0] = bn_s1;
       P[e.N] = bn_s2;
     }
@@ -362,13 +385,13 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
 // writes 8 whole 128-B rows (bf16: 16 B per lane) -- full cache lines instead of 32-B fragments.
 // The epilogue operands of each 64-row group (bias, gamma, residual / pre-activation) are loaded
 // before its first slab.
-template <int FM, int PRE = 1, int EPI = -1, int AUXT = -1>
+template <int FM, int PRE = 1, int EPI = -1, int AUXT = -1, bool REMAP = false>
 __device__ __forceinline__ void wave_tile_epilogue(const f32x4 (&acc)[FM][4], float* __restrict__ slab, int mb,
                                                    int nb, const EpiArgs& e, int split) {
   static_assert(FM % 4 == 0, "64-row groups");
 #pragma unroll
   for (int i0 = 0; i0 < FM; i0 += 4)
-    wave_group_epilogue<FM, PRE, 4, 0, EPI, AUXT>(acc, i0, slab, mb + 16 * i0, nb, e, split);
+    wave_group_epilogue<FM, PRE, 4, 0, EPI, AUXT, REMAP>(acc, i0, slab, mb + 16 * i0, nb, e, split);
 }
 
 // (16 FM) x (16 FN) wave tile, FN a multiple of 4: 64-column groups stored one after the other
@@ -418,7 +441,8 @@ inline void conv_fastdiv(uint32_t D, uint32_t& mul, uint32_t& shift) {
 // Weight gradients, split-K slabs: mode 3 dW = dy^T gather(x) (M = Cout, N = taps * channels), mode 4
 // the transposed product dW^T = gather(x)^T dy (M = taps * channels, N = Cout) for Cout < 256.
 // Mode 5: the stride-2 dgrad of all four output parity classes in one launch (even H, W: every class
-// has the same GH x GW grid; class c takes taps ctap0[c] .. + ctaps[c] and writes slab c, epilogue SLAB)
+// has the same GH x GW grid; class c takes taps ctap0[c] .. + ctaps[c] and writes slab c, epilogue SLAB,
+// or its rows straight into dx [B][2GH][2GW][N] with STORE / BIAS_GAMMA_RES (accumulate) / STORE_BN_BWD)
 int launch_gemm3_conv(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t s);
 
 // v2 entry (gemm2.hip): returns SV_ERR_UNSUPPORTED when the shape/dtypes are outside its contract

@@ -980,9 +980,14 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
             return dx
     if wp.dtype == torch.bfloat16 and s.stride == 2 and s.Cout >= 32 and s.Cs % 8 == 0:
         # stride 2: one gathered GEMM per output parity class into compact f32 slabs + one scatter pass
-        # (csrc/conv.hip dgrad_s2_scatter_kernel); the workspace holds every class's slabs
+        # (csrc/conv.hip dgrad_s2_scatter_kernel); the workspace holds every class's slabs.  Even H, W
+        # without a split: the one-launch form stores each class's rows straight into dx (no workspace)
         M = s.B * s.H * s.W
-        split = _conv_split(M // 4, s.Cs, max(32, (T * s.Cout) // 4))
+        split = _s2_split(s, M, T)
+        if split == 1 and _s2_direct(s) and (not accumulate or dx.dtype == torch.float32):
+            call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s),
+                 nv.pol_ref(policy))
+            return dx
         work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32)
         call("sv_conv_bwd_data_split", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp),
              ctypes.byref(s), ptr(work), split, nv.pol_ref(policy))
@@ -990,6 +995,24 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
     call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s),
          nv.pol_ref(policy))
     return dx
+
+
+# stride-2 data gradients stored straight into dx by the parity-class GEMM's epilogue (csrc/gemm3.hip mode 5
+# with remapped rows); 0 = the compact f32 slabs + scatter pass (A/B and the bitwise cross-check)
+_S2_DIRECT = os.environ.get("SV_S2_DIRECT", "1") != "0"
+# SV_S2_NOSPLIT=1: no split-K for the stride-2 dgrads that the one-launch form can take (A/B runs)
+_S2_NOSPLIT = os.environ.get("SV_S2_NOSPLIT", "0") == "1"
+
+
+def _s2_direct(s: nv.ConvShape) -> bool:
+    return _S2_DIRECT and s.stride == 2 and s.H % 2 == 0 and s.W % 2 == 0 and s.KH * s.KW > 1
+
+
+def _s2_split(s: nv.ConvShape, M: int, T: int) -> int:
+    """split-K depth of a stride-2 dgrad's per-class GEMMs (M = B*H*W dx pixels, T taps)"""
+    if _S2_NOSPLIT and _s2_direct(s):
+        return 1
+    return _conv_split(M // 4, s.Cs, max(32, (T * s.Cout) // 4))
 
 
 def _al16(*ts) -> bool:
@@ -1004,14 +1027,22 @@ def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: tor
     gamma / beta its affine parameters.  -> (dx, part), part = f32 [ceil(B*H*W/64)][2][Cs] partial sums of g
     and g*xhat (g = dx * relu mask) for bn_bwd(part=...), summed by the GEMM epilogue (SV_EPI_STORE_BN_BWD)
     or, for split-K shapes, by the finish that reads the slabs anyway (sv_gemm_slab_finish_bn_bwd): no
-    statistics pass over dx and y.  ``unsplit=False`` fuses the split-K shapes only.  None when the shape is
-    not on these paths (stride 2, fp32, unaligned parameters): use conv_bwd_data + bn_bwd."""
-    if wp.dtype != torch.bfloat16 or y.dtype != torch.bfloat16 or s.Cs % 8 or s.stride != 1:
+    statistics pass over dx and y.  ``unsplit=False`` fuses the split-K shapes only.  Stride 2 (even H, W,
+    no split): the one-launch parity-class GEMM with the same epilogue, 4 * ceil(B*H*W/256) partial rows
+    (one run per class).  None when the shape is not on these paths (odd stride-2 grids, split stride-2
+    shapes, fp32, unaligned parameters): use conv_bwd_data + bn_bwd."""
+    if wp.dtype != torch.bfloat16 or y.dtype != torch.bfloat16 or s.Cs % 8 or s.stride not in (1, 2):
         return None
     M = s.B * s.H * s.W
     T = s.KH * s.KW
     pw = _pointwise(s, wp.dtype)
-    if pw:
+    s2 = s.stride == 2
+    if s2:  # the one-launch parity-class GEMM without a split; partials [4][ceil(M/4/64)][2][Cs]
+        if not (_s2_direct(s) and _is_pow2(s.Cout) and s.Cout >= 32
+                and _s2_split(s, M, T) == 1):
+            return None
+        split = 1
+    elif pw:
         split = _conv_split(M, s.Cs, s.Cout)
     elif _is_pow2(s.Cout) and s.Cout >= 32 and (T * s.Cout) % 32 == 0:
         split = _conv_split(M, s.Cs, T * s.Cout)
@@ -1028,7 +1059,8 @@ def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: tor
         return None
     ref = nv.BnRef(ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(prm[3]))
     dx = torch.empty(s.B, s.H, s.W, s.Cs, device=dy.device, dtype=torch.bfloat16)
-    part = torch.empty((M + 63) // 64, 2, s.Cs, device=dy.device, dtype=torch.float32)
+    prows = 4 * ((M // 4 + 63) // 64) if s2 else (M + 63) // 64
+    part = torch.empty(prows, 2, s.Cs, device=dy.device, dtype=torch.float32)
     work = torch.empty(split * M * s.Cs, device=dy.device, dtype=torch.float32) if split > 1 else None
     if pw and split > 1:
         gemm(dy.view(M, s.Cout), wp.view(s.Cout, s.Cs), M=M, N=s.Cs, K=s.Cout, a_kmajor=True, b_kmajor=False,

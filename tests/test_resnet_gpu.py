@@ -183,6 +183,10 @@ BN_EPI_CASES = [
     (2, 16, 16, 128, 128, 3),   # 3x3 gathered (layer2 conv2 dgrad)
     (2, 8, 8, 512, 512, 3),     # 3x3 gathered (layer4 conv2 dgrad)
     (3, 7, 5, 128, 128, 3),     # ragged pixel count: a partial 64-row group
+    # stride 2 (dx grid H x W): the one-launch parity-class GEMM, rows remapped into dx (layer2-4 conv2 dgrads)
+    (2, 32, 32, 64, 64, 3, 2),
+    (3, 18, 14, 64, 128, 3, 2),  # 189 rows per class: a partial 64-row group in every class's run
+    (2, 64, 64, 128, 128, 3, 2),
 ]
 
 
@@ -192,13 +196,15 @@ def test_conv_bwd_data_bn_matches_separate_stats(dev, case):
     epilogue or split-K finish) against conv_bwd_data + bn_bwd's own statistics pass on the same operands:
     dx bit for bit, the partials' column sums within f32 reordering (1e-5) of the separate pass and of a
     float64 recomputation from dx and y, and the BatchNorm backward (dx, dgamma, dbeta) within the same."""
-    B, H, W, Cs, Cout, k = case
+    B, H, W, Cs, Cout, k = case[:6]
+    st = case[6] if len(case) > 6 else 1
     pad = k // 2
     g = torch.Generator().manual_seed(Cs + k)
-    s = K.conv_shape(B, H, W, Cs, Cout, k, 1, pad)
+    s = K.conv_shape(B, H, W, Cs, Cout, k, st, pad)
+    OH, OW = K.conv_out_hw(H, W, k, st, pad)
     w = torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5
     wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
-    dy = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(dev)
+    dy = torch.randn(B, OH, OW, Cout, generator=g).to(torch.bfloat16).to(dev)
     rows = B * H * W
     y = (torch.randn(rows, Cs, generator=g) * 2 + 0.3).to(torch.bfloat16).to(dev)
     gam = (torch.rand(Cs, generator=g) + 0.5).to(dev)
@@ -207,14 +213,16 @@ def test_conv_bwd_data_bn_matches_separate_stats(dev, case):
     fused = K.conv_bwd_data_bn(dy, wp, s, y.view(B, H, W, Cs), mean, rstd, gam, bet)
     assert fused is not None, "case must take a fused path"
     dx_f, part = fused
-    dx_r = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.bfloat16)
+    with pytest.MonkeyPatch.context() as mp:  # stride 2: the slab + scatter form as the reference
+        mp.setattr(K, "_S2_DIRECT", False)
+        dx_r = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.bfloat16)
     dg1, db1, dg2, db2 = (torch.zeros(Cs, device=dev) for _ in range(4))
     o_f = K.bn_bwd(dx_f.view(rows, Cs), y, mean, rstd, gam, relu_beta=bet, dgamma=dg1, dbeta=db1,
                    dx_dtype=torch.float32, part=part)
     o_r = K.bn_bwd(dx_r.view(rows, Cs), y, mean, rstd, gam, relu_beta=bet, dgamma=dg2, dbeta=db2,
                    dx_dtype=torch.float32)
     torch.cuda.synchronize()
-    assert part.shape == ((rows + 63) // 64, 2, Cs)
+    assert part.shape == ((4 * ((rows // 4 + 63) // 64) if st == 2 else (rows + 63) // 64), 2, Cs)
     assert torch.equal(dx_f, dx_r)
     # float64 recomputation of sum g and sum g * xhat from the stored dx and y
     yd, dd = y.double().cpu(), dx_r.view(rows, Cs).double().cpu()
@@ -224,6 +232,51 @@ def test_conv_bwd_data_bn_matches_separate_stats(dev, case):
     assert rel(sums[0], gd.sum(0)) < 1e-5 and rel(sums[1], (gd * (yd - mu) * rs).sum(0)) < 1e-5
     assert rel(db1, db2) < 1e-5 and rel(dg1, dg2) < 1e-5
     assert rel(o_f, o_r) < 1e-5
+
+
+S2_CASES = [
+    # B, H, W (dx grid), Cs, Cout, k, pad: stride-2 dgrads on the one-launch parity-class GEMM
+    (2, 32, 32, 64, 64, 3, 1),
+    (3, 18, 14, 64, 128, 3, 1),   # 189 rows per class (partial tiles)
+    (2, 64, 64, 128, 128, 3, 1),  # ResNet-50 @256 layer2 conv2 at B = 2
+    (2, 16, 16, 256, 256, 3, 1),  # layer4-like: Cs = 256, one tile column
+    (2, 16, 12, 64, 64, 2, 0),    # 2x2 pad 0: one tap per class
+    (2, 20, 20, 64, 32, 5, 2),    # 5x5: 9 / 6 / 6 / 4 taps per class, Cout 32
+]
+
+
+@pytest.mark.parametrize("case", S2_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_s2_direct_matches_scatter(dev, case):
+    """The stride-2 data gradient stored straight into dx by the parity-class GEMM's epilogue (rows remapped
+    per class) against the compact f32 slabs + scatter pass on the same operands: bit for bit for a bf16 and
+    an f32 store and for the f32 in-place accumulate (the add is the same f32 add either way), and the
+    stored dx against a float64 conv_transpose2d of the same bf16 operands."""
+    B, H, W, Cs, Cout, k, pad = case
+    g = torch.Generator().manual_seed(H * 31 + Cs + k)
+    s = K.conv_shape(B, H, W, Cs, Cout, k, 2, pad)
+    OH, OW = K.conv_out_hw(H, W, k, 2, pad)
+    assert K._conv_split(B * H * W // 4, Cs, max(32, k * k * Cout // 4)) == 1, "case must take the direct path"
+    w = (torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5).to(torch.bfloat16).float()
+    wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
+    dy = torch.randn(B, OH, OW, Cout, generator=g).to(torch.bfloat16).to(dev)
+    base = torch.randn(B, H, W, Cs, generator=g).to(dev)
+    out = {}
+    for direct in (True, False):
+        with pytest.MonkeyPatch.context() as mp:
+            mp.setattr(K, "_S2_DIRECT", direct)
+            d16 = torch.full((B, H, W, Cs), float("nan"), device=dev, dtype=torch.bfloat16)
+            K.conv_bwd_data(dy, wp, s, dx=d16)
+            d32 = K.conv_bwd_data(dy, wp, s, dx_dtype=torch.float32)
+            acc = base.clone()
+            K.conv_bwd_data(dy, wp, s, dx=acc, accumulate=True)
+            out[direct] = (d16, d32, acc)
+    torch.cuda.synchronize()
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+    ref = F.conv_transpose2d(dy.double().cpu().permute(0, 3, 1, 2), w.double(), stride=2, padding=pad,
+                             output_padding=(H - ((OH - 1) * 2 - 2 * pad + k), W - ((OW - 1) * 2 - 2 * pad + k)))
+    assert rel(out[True][1].permute(0, 3, 1, 2), ref) < 1e-5
+    assert rel((out[True][2] - base).permute(0, 3, 1, 2), ref) < 1e-5
 
 
 @pytest.mark.parametrize("C", [64, 256, 2048])

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4: stride-2 dgrad variants -- the inner BatchNorm statistics from the parity-class epilogue (SV_S2_BN)
+# and no split-K for the strided dgrads (SV_S2_NOSPLIT) -- ResNet tests, then classification A/B/C
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/${1:-r9i}
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_resnet_gpu.py tests/test_resnet_parity_256_gpu.py > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+for i in 1 2 3; do
+  for v in a b c; do
+    case $v in a) E="SV_S2_BN=1 SV_S2_NOSPLIT=0";; b) E="SV_S2_BN=0 SV_S2_NOSPLIT=0";; c) E="SV_S2_BN=1 SV_S2_NOSPLIT=1";; esac
+    env $E timeout -k 10 300 python bench.py --workload classification --steps 50 --warmup 10 --no-cpu-baseline > $O/cls_${v}_$i.json 2>>$O/bench.err || exit $?
+    python -c "import json; d=json.loads(open('$O/cls_${v}_$i.json').read().strip().splitlines()[-1]); print('$v $E', d['value'], d['ms_per_step'])"
+  done
+done
