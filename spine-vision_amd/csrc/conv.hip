@@ -885,10 +885,11 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
     if (rc != SV_ERR_UNSUPPORTED) return rc;
   }
   // stride 2, even H, W, more than one tap: all four output parity classes share one GH x GW grid
-  const bool s2_even = st == 2 && s->H % 2 == 0 && s->W % 2 == 0 && s->KH * s->KW > 1;
+  const bool s2_grid = st == 2 && s->H % 2 == 0 && s->W % 2 == 0;
+  const bool s2_even = s2_grid && s->KH * s->KW > 1;
   // ... and without a workspace their rows go straight into dx (plain store, in-place f32 accumulate, or
-  // bf16 with the BatchNorm statistics)
-  const bool s2_direct = s2_even && !slab && (!accumulate || dx_dtype == SV_F32) && (!bn || dx_dtype == SV_BF16);
+  // bf16 with the BatchNorm statistics); any kernel size (1x1: only class (0, 0) has a tap)
+  const bool s2_direct = s2_grid && !slab && (!accumulate || dx_dtype == SV_F32) && (!bn || dx_dtype == SV_BF16);
   if (dtype == SV_BF16 && st == 2 && (slab || s2_direct) && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
     // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass.  Even H, W
     // and no split: all four classes run as ONE launch (mode 5) -- the per-class launches are each below
@@ -939,6 +940,10 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
           d.aux_dtype = SV_F32;
           d.ld_aux = s->Cs;
         }
+        // accumulating: trailing classes without taps would only re-add zero (1x1: one class of four)
+        int ncls = 4;
+        while (accumulate && ncls > 1 && g.ctaps[ncls - 1] == 0) --ncls;
+        d.split_k = ncls;
         return launch_gemm3_conv(&d, g, 5, (hipStream_t)stream);
       }
       sv_gemm_desc d = conv_desc(dy, wp, M, s->Cs, maxt * s->Cout, 0, (int64_t)T_ * s->Cs, slab, SV_F32, pol);

@@ -515,10 +515,13 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   if (mode == 2 && d->epilogue == SV_EPI_SLAB)
     return launch<true, false, SV_EPI_SLAB, 32, S, 2>(d, d->split_k < 1 ? 1 : d->split_k, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_SLAB) return launch<true, false, SV_EPI_SLAB, 32, S, 5>(d, 4, s, &g);
-  // mode 5 straight into dx (no split): plain store, in-place accumulate, or with the BatchNorm statistics
-  if (mode == 5 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 5>(d, 4, s, &g);
+  // mode 5 straight into dx (no split): plain store, in-place accumulate, or with the BatchNorm statistics;
+  // split_k = the number of classes launched (classes 0 .. split_k - 1; an accumulate skips trailing classes
+  // without taps)
+  const int ncls = d->split_k >= 1 && d->split_k <= 4 ? d->split_k : 4;
+  if (mode == 5 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 5>(d, ncls, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
-    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5>(d, 4, s, &g);
+    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5>(d, ncls, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_STORE_BN_BWD)
     return launch<true, false, SV_EPI_STORE_BN_BWD, 32, S, 5>(d, 4, s, &g);
   // 8-channel pixels (the ResNet stem), plain store or with the BatchNorm statistics

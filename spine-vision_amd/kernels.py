@@ -1000,12 +1000,13 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
 # stride-2 data gradients stored straight into dx by the parity-class GEMM's epilogue (csrc/gemm3.hip mode 5
 # with remapped rows); 0 = the compact f32 slabs + scatter pass (A/B and the bitwise cross-check)
 _S2_DIRECT = os.environ.get("SV_S2_DIRECT", "1") != "0"
-# SV_S2_NOSPLIT=1: no split-K for the stride-2 dgrads that the one-launch form can take (A/B runs)
-_S2_NOSPLIT = os.environ.get("SV_S2_NOSPLIT", "0") == "1"
+# no split-K for the stride-2 dgrads that the one-launch form takes: the four classes already give the grid
+# 4x the tiles, and the split's slabs cost more than the longer chains (+0.6 %, r9j); SV_S2_NOSPLIT=0 restores it
+_S2_NOSPLIT = os.environ.get("SV_S2_NOSPLIT", "1") != "0"
 
 
 def _s2_direct(s: nv.ConvShape) -> bool:
-    return _S2_DIRECT and s.stride == 2 and s.H % 2 == 0 and s.W % 2 == 0 and s.KH * s.KW > 1
+    return _S2_DIRECT and s.stride == 2 and s.H % 2 == 0 and s.W % 2 == 0
 
 
 def _s2_split(s: nv.ConvShape, M: int, T: int) -> int:
@@ -1038,7 +1039,7 @@ def conv_bwd_data_bn(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, y: tor
     pw = _pointwise(s, wp.dtype)
     s2 = s.stride == 2
     if s2:  # the one-launch parity-class GEMM without a split; partials [4][ceil(M/4/64)][2][Cs]
-        if not (_s2_direct(s) and _is_pow2(s.Cout) and s.Cout >= 32
+        if not (_s2_direct(s) and T > 1 and _is_pow2(s.Cout) and s.Cout >= 32
                 and _s2_split(s, M, T) == 1):
             return None
         split = 1

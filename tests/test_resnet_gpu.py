@@ -242,6 +242,8 @@ S2_CASES = [
     (2, 16, 16, 256, 256, 3, 1),  # layer4-like: Cs = 256, one tile column
     (2, 16, 12, 64, 64, 2, 0),    # 2x2 pad 0: one tap per class
     (2, 20, 20, 64, 32, 5, 2),    # 5x5: 9 / 6 / 6 / 4 taps per class, Cout 32
+    (2, 16, 16, 256, 512, 1, 0),  # 1x1 (the downsample shortcut): class (0, 0) only; accumulate launches it alone
+    (2, 14, 10, 64, 256, 1, 0),   # 1x1, 35 rows per class
 ]
 
 
@@ -255,7 +257,7 @@ def test_conv_s2_direct_matches_scatter(dev, case):
     g = torch.Generator().manual_seed(H * 31 + Cs + k)
     s = K.conv_shape(B, H, W, Cs, Cout, k, 2, pad)
     OH, OW = K.conv_out_hw(H, W, k, 2, pad)
-    assert K._conv_split(B * H * W // 4, Cs, max(32, k * k * Cout // 4)) == 1, "case must take the direct path"
+    assert K._s2_direct(s) and K._s2_split(s, B * H * W, k * k) == 1, "case must take the direct path"
     w = (torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5).to(torch.bfloat16).float()
     wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
     dy = torch.randn(B, OH, OW, Cout, generator=g).to(torch.bfloat16).to(dev)
