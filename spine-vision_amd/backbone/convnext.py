@@ -150,6 +150,8 @@ class ConvNeXtHip(nn.Module):
         # the lean side stream's GEMMs on at most this many workgroups (None: every CU; SV_SIDE_GRID_CAP)
         cap = os.environ.get("SV_SIDE_GRID_CAP")
         self.side_grid_cap: int | None = int(cap) if cap else None
+        # the side stream's weight-gradient GEMM family (sv_gemm_policy.impl; 0 = the measured dispatch, A/B runs)
+        self.side_impl = int(os.environ.get("SV_WGRAD_IMPL", "0"))
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -508,7 +510,7 @@ class ConvNeXtHip(nn.Module):
         side_cap = pol.grid_cap
         if self.side_grid_cap is not None:
             side_cap = min(self.side_grid_cap, side_cap) if side_cap > 0 else self.side_grid_cap
-        spol = nv.policy(grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=1)
+        spol = nv.policy(impl=self.side_impl, grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=1)
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),

@@ -16,6 +16,8 @@ from spine_vision_amd import kernels as K  # noqa: E402
 SHAPES = {  # name: (B, H, W, Cs, Cin, Cout, k, stride, pad)
     "stem7x7s2": (32, 256, 256, 8, 3, 64, 7, 2, 3),
     "l1_3x3": (32, 64, 64, 64, 64, 64, 3, 1, 1),
+    "l1_1x1in": (32, 64, 64, 256, 256, 64, 1, 1, 0),
+    "l1_1x1out": (32, 64, 64, 64, 64, 256, 1, 1, 0),
     "l2_3x3s2": (32, 64, 64, 128, 128, 128, 3, 2, 1),
     "l2_3x3": (32, 32, 32, 128, 128, 128, 3, 1, 1),
     "l3_3x3s2": (32, 32, 32, 256, 256, 256, 3, 2, 1),
@@ -60,10 +62,12 @@ def main():
         dw = torch.zeros_like(w)
         t_w = timeit(lambda: K.conv_bwd_weight(dy, x, shape, dw=dw, accumulate=True), args.iters)
         t_f = timeit(lambda: K.conv_fwd(x, wp, shape, torch.bfloat16), args.iters)
-        line = f"{name:12s} wgrad {t_w:8.1f} us  fwd {t_f:8.1f} us"
+        gf = 2.0 * B * OH * OW * Cout * Cin * k * k / 1e9
+        line = (f"{name:12s} {gf:6.2f} GF  wgrad {t_w:8.1f} us {gf / t_w * 1e3:6.0f} TF  "
+                f"fwd {t_f:8.1f} us {gf / t_f * 1e3:6.0f} TF")
         if Cin == Cs:
             t_d = timeit(lambda: K.conv_bwd_data(dy, wp, shape, dx_dtype=torch.bfloat16), args.iters)
-            line += f"  dgrad {t_d:8.1f} us"
+            line += f"  dgrad {t_d:8.1f} us {gf / t_d * 1e3:6.0f} TF"
         print(line + f"  [{tag}]", flush=True)
 
 
