@@ -185,6 +185,11 @@ constexpr int kSC1 = 16;  // buffer instruction cache policy: sc1 (write-through
 #ifndef SV_G9_GRAD_CPOL
 #define SV_G9_GRAD_CPOL 2
 #endif
+// ... and of its GELU(h) store (C2, read by the fc2 forward at once and the fc2 weight gradient in the backward);
+// A/B builds only (-DSV_G9_C2_CPOL=2: nt)
+#ifndef SV_G9_C2_CPOL
+#define SV_G9_C2_CPOL 0
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
   // built from kernel arguments only: wave-uniform, so no waterfall loop around the buffer ops
@@ -381,7 +386,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
           const u32x4 pk = pack8(o);
           __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0,
                                                  EPI == SV_EPI_BIAS_GELU_DUAL ? SV_G9_GRAD_CPOL : 0);
-          if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) __builtin_amdgcn_raw_buffer_store_b128(pack8(o2), rc2, off, 0, 0);
+          if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) __builtin_amdgcn_raw_buffer_store_b128(pack8(o2), rc2, off, 0, SV_G9_C2_CPOL);
           if constexpr (EPI == SV_EPI_STORE_STATS) {
             // statistics of the values AS STORED (bf16), rows past M excluded
             if (m < e.M) {
