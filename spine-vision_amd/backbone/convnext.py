@@ -341,6 +341,9 @@ class ConvNeXtHip(nn.Module):
         # the two streams on one persistent workgroup per CU each, so they share every CU; under data
         # parallelism every grid leaves comm_reserve_cus CUs to RCCL
         comm_cap = _comm_cap(main.device, self.comm_reserve_cus)
+        main_cap = int(os.environ.get("SV_MAIN_BWD_CAP", "0"))  # A/B runs: the main stream's backward GEMM grids
+        if main_cap > 0:
+            comm_cap = min(comm_cap, main_cap) if comm_cap > 0 else main_cap
         pol = nv.policy(grid_cap=comm_cap, wg_per_cu=self.side_wg_per_cu if side is not None else 0)
         lean = side is not None and bf and self.lean_sync
         # lean mode: per block (side-stream event, the operands the side stream reads), oldest first;
