@@ -99,6 +99,26 @@ __device__ __forceinline__ GeluParts gelu_parts(float x) {
   const float h = (p * t) * dens;  // 0.5 erfc(|x|/sqrt2)
   return {0.5f + copysignf(0.5f - h, x), dens};
 }
+// two elements at once in packed f32 (v_pk_mul_f32 / v_pk_fma_f32 where the scalar form has one v_mul / v_fma):
+// per component the same operations in the same order as gelu_parts, so the same bits
+typedef float gelu_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_parts2(gelu_f2 x, gelu_f2& phi, gelu_f2& dens) {
+  constexpr float K = 1.2533141373155003f;
+  const gelu_f2 z = __builtin_elementwise_abs(x) * (gelu_f2){0.70710678118654752f, 0.70710678118654752f};
+  const gelu_f2 d = __builtin_elementwise_fma((gelu_f2){0.3275911f, 0.3275911f}, z, (gelu_f2){1.0f, 1.0f});
+  const gelu_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const gelu_f2 ea = __builtin_elementwise_fma(x * x, (gelu_f2){-0.72134752044448170f, -0.72134752044448170f},
+                                               (gelu_f2){-1.3257480647361593f, -1.3257480647361593f});
+  dens = (gelu_f2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  gelu_f2 p = __builtin_elementwise_fma((gelu_f2){1.061405429f * K, 1.061405429f * K}, t,
+                                        (gelu_f2){-1.453152027f * K, -1.453152027f * K});
+  p = __builtin_elementwise_fma(p, t, (gelu_f2){1.421413741f * K, 1.421413741f * K});
+  p = __builtin_elementwise_fma(p, t, (gelu_f2){-0.284496736f * K, -0.284496736f * K});
+  p = __builtin_elementwise_fma(p, t, (gelu_f2){0.254829592f * K, 0.254829592f * K});
+  const gelu_f2 h = (p * t) * dens;
+  const gelu_f2 r = (gelu_f2){0.5f, 0.5f} - h;
+  phi = (gelu_f2){0.5f, 0.5f} + (gelu_f2){copysignf(r.x, x.x), copysignf(r.y, x.y)};
+}
 __device__ __forceinline__ float phi_cdf(float x) { return gelu_parts(x).phi; }
 __device__ __forceinline__ float gelu_f(float x) { return x * gelu_parts(x).phi; }
 // GELU and its derivative from one evaluation (forward epilogue of fc1)

@@ -187,6 +187,10 @@ constexpr int kSC1 = 16;  // buffer instruction cache policy: sc1 (write-through
 #endif
 // ... and of its GELU(h) store (C2, read by the fc2 forward at once and the fc2 weight gradient in the backward);
 // A/B builds only (-DSV_G9_C2_CPOL=2: nt)
+// GELU epilogues two elements at a time in packed f32 (bitwise the scalar form; -DSV_GELU_PK=0: scalar, A/B)
+#ifndef SV_GELU_PK
+#define SV_GELU_PK 1
+#endif
 #ifndef SV_G9_C2_CPOL
 #define SV_G9_C2_CPOL 0
 #endif
@@ -366,6 +370,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
             xa[w] = __uint_as_float(wd);
           }
         }
+#if SV_GELU_PK
+        if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU) {  // pairs in packed f32
+#pragma unroll
+          for (int w = 0; w < CW; w += 2) {
+            const gelu_f2 h = {v[w], v[w + 1]};
+            gelu_f2 ph, de;
+            gelu_parts2(h, ph, de);
+            const gelu_f2 g = h * ph;
+            if constexpr (EPI == SV_EPI_BIAS_GELU_DUAL) {
+              const gelu_f2 dg = __builtin_elementwise_fma(h, de, ph);
+              o[w] = dg.x, o[w + 1] = dg.y, o2[w] = g.x, o2[w + 1] = g.y;  // C = GELU'(h), C2 = GELU(h)
+            } else {
+              o[w] = g.x, o[w + 1] = g.y;
+            }
+          }
+        } else
+#endif
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
           if constexpr (EPI == SV_EPI_SLAB || EPI == SV_EPI_STORE || EPI == SV_EPI_STORE_STATS) {
