@@ -152,6 +152,9 @@ class ConvNeXtHip(nn.Module):
         self.side_grid_cap: int | None = int(cap) if cap else None
         # the side stream's weight-gradient GEMM family (sv_gemm_policy.impl; 0 = the measured dispatch, A/B runs)
         self.side_impl = int(os.environ.get("SV_WGRAD_IMPL", "0"))
+        # a grid cap on the main stream's backward GEMMs (A/B runs; 128 measured equal to none, 192/224 slower:
+        # profiles/round4/r9u_main_cap_and_tile_queue_rejected.txt)
+        self.main_bwd_cap = int(os.environ.get("SV_MAIN_BWD_CAP", "0"))
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -341,9 +344,8 @@ class ConvNeXtHip(nn.Module):
         # the two streams on one persistent workgroup per CU each, so they share every CU; under data
         # parallelism every grid leaves comm_reserve_cus CUs to RCCL
         comm_cap = _comm_cap(main.device, self.comm_reserve_cus)
-        main_cap = int(os.environ.get("SV_MAIN_BWD_CAP", "0"))  # A/B runs: the main stream's backward GEMM grids
-        if main_cap > 0:
-            comm_cap = min(comm_cap, main_cap) if comm_cap > 0 else main_cap
+        if self.main_bwd_cap > 0:
+            comm_cap = min(comm_cap, self.main_bwd_cap) if comm_cap > 0 else self.main_bwd_cap
         pol = nv.policy(grid_cap=comm_cap, wg_per_cu=self.side_wg_per_cu if side is not None else 0)
         lean = side is not None and bf and self.lean_sync
         # lean mode: per block (side-stream event, the operands the side stream reads), oldest first;
