@@ -75,9 +75,16 @@ class OpProbe:
 OP_PROBES: dict[str, OpProbe] = {}  # name -> probe; bench.py fills it for the timed step it probes
 
 
+# SV_DIAG_SKIP=fold,...: skip every launch of those probe classes (an upper bound on what removing them could buy;
+# the step's results are wrong -- never for training or tests)
+_DIAG_SKIP = {x for x in os.environ.get("SV_DIAG_SKIP", "").split(",") if x}
+
+
 def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0) -> None:
     """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed; ``fma``: the
     launch's algorithmic f32 VALU FMAs (its roof when they outlast its bytes)."""
+    if _DIAG_SKIP and op in _DIAG_SKIP:  # diagnostic timing only: the launch is skipped, its results are garbage
+        return
     pr = OP_PROBES.get(op)
     if pr is None:
         call(*args)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4: upper bound of the split-K folds' cost in the ConvNeXt-base step (SV_DIAG_SKIP=fold: folds skipped,
+# timing only)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/${1:-r9zd}
+mkdir -p $O
+for i in 1 2 3; do
+  for v in none fold; do
+    if [ $v = none ]; then E=""; else E=fold; fi
+    SV_DIAG_SKIP=$E timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/b_${v}_$i.json 2>>$O/bench.err || exit $?
+    python -c "import json; d=json.loads(open('$O/b_${v}_$i.json').read().strip().splitlines()[-1]); print('skip=$v', d['value'], d['ms_per_step'])"
+  done
+done
