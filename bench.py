@@ -618,7 +618,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
-    assert final_loss == final_loss, "loss is NaN"
+    # (a diagnostic SV_DIAG_SKIP run skips launches on purpose: its loss is garbage and its line says so)
+    assert final_loss == final_loss or K._DIAG_SKIP, "loss is NaN"
     mstats = torch.cuda.memory_stats(device)
 
     peak = PEAK_BF16_TFLOPS if bf else PEAK_F32_MFMA_TFLOPS
@@ -693,7 +694,8 @@ def main():
             "hip_graph": bool(engine.cuda_graph),
         },
         "roofline": roof,
-        "loss": round(final_loss, 6),
+        "loss": round(final_loss, 6) if final_loss == final_loss else None,
+        **({"diag_skip": sorted(K._DIAG_SKIP)} if K._DIAG_SKIP else {}),
         "hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
         "hbm_peak_allocated_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 1),
         "num_alloc_retries": int(mstats.get("num_alloc_retries", 0) - retries0),
