@@ -91,7 +91,8 @@ typedef enum {
   SV_EPI_BIAS_GELU2 = 1,     /* C = acc + bias[n]  (pre-activation), C2 = GELU_erf(C)             */
   SV_EPI_BIAS_GAMMA_RES = 2, /* C = aux[m,n] + gamma[n] * (acc + bias[n])   (layer-scale residual) */
   SV_EPI_GELU_GRAD = 3,      /* C = acc * GELU_erf'(aux[m,n])                                      */
-  SV_EPI_SLAB = 4,           /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32);      */
+  SV_EPI_SLAB = 4,           /* split-K partial: C[s][m][n] = partial acc of K-slice s (f32, or   */
+                             /* bf16 when c_dtype is SV_BF16: v9 weight-gradient shapes only);     */
                              /* if C2 != NULL also C2[s][m] = sum_{k in slice s} A(m,k) (f32), i.e.  */
                              /* the bias gradient of a wgrad GEMM (A = dY^T) without another pass.   */
   SV_EPI_BIAS_GELU_DUAL = 5, /* h = acc + bias[n]: C = GELU_erf'(h), C2 = GELU_erf(h)  (fc1 forward: */
@@ -313,6 +314,11 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
                             float* out_b, int32_t P, float alpha, int32_t accumulate, sv_stream_t stream);
 int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, float* out, float alpha,
                        int32_t accumulate, sv_stream_t stream);
+/* sv_reduce_partials (one group) over bf16 partial rows part[P][n] (the bf16 split-K slabs of a weight gradient,
+ * sv_gemm SV_EPI_SLAB with c_dtype SV_BF16): out (+)= alpha * sum_p part[p], f32 sums in slice order.
+ * n % 4 == 0: part 8-B and out 16-B aligned.  ABI version 5.                                          */
+int sv_reduce_partials_bf16(const uint16_t* part, int32_t P, int64_t n, float* out, float alpha, int32_t accumulate,
+                            sv_stream_t stream);
 /* column sums of a [rows][C] matrix into partials [nparts][C]; nparts = sv_colsum_nparts(rows,C). */
 int sv_colsum_nparts(int64_t rows, int32_t C);
 int sv_colsum(const void* x, int32_t x_dtype, int64_t rows, int32_t C, float* part,
@@ -333,6 +339,11 @@ int sv_layerscale_wgrad_reduce_ws(int32_t C, int32_t K4);
 int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t P, const float* W2,
                                const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2,
                                float* ws, int32_t C, int32_t K4, sv_stream_t stream);
+/* sv_layerscale_wgrad_reduce over bf16 slabs slab[P][C][K4] (sv_gemm SV_EPI_SLAB with c_dtype SV_BF16); the
+ * column-sum partials stay f32.  slab 8-B aligned.  ABI version 5.                                    */
+int sv_layerscale_wgrad_reduce_bf16(const uint16_t* slab, const float* cs_part, int32_t P, const float* W2,
+                                    const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2, int32_t C,
+                                    int32_t K4, sv_stream_t stream);
 /* The same finish over the ALREADY FOLDED G[C][K4] (the wgrad GEMM's in-kernel fold, sv_gemm_desc.fold_out) and
  * the P column-sum partials cs_part[P][C]: bitwise sv_layerscale_wgrad_reduce of the P slabs whose sum is G.  */
 int sv_layerscale_wgrad_fold_finish(const float* G, const float* cs_part, int32_t P, const float* W2, const float* gamma,

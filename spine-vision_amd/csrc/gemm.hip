@@ -307,7 +307,8 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(al16(d->A) && al16(d->B) && al16(d->C), "sv_gemm: operands must be 16-byte aligned");
   SV_REQUIRE(d->N % 4 == 0, "sv_gemm: N must be a multiple of 4");
   if (d->epilogue == SV_EPI_SLAB) {
-    SV_REQUIRE(d->c_dtype == SV_F32, "sv_gemm: slab epilogue writes f32");
+    SV_REQUIRE(d->c_dtype == SV_F32 || (bf && d->c_dtype == SV_BF16 && !d->fold_out && d->N % 8 == 0),
+               "sv_gemm: slab epilogue writes f32 (bf16 slabs: bf16 compute, N %% 8 == 0, no in-kernel fold)");
     SV_REQUIRE(!d->C2 || d->c2_dtype == SV_F32, "sv_gemm: slab colsum output is f32");
   } else {
     SV_REQUIRE(d->ldc % 4 == 0, "sv_gemm: ldc must be a multiple of 4");
@@ -374,6 +375,11 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
                                       tiles8 >= 256);
     const bool v9_pick = impl == 0 && v9_shape;
     int rc = SV_ERR_UNSUPPORTED;
+    if (d->epilogue == SV_EPI_SLAB && d->c_dtype == SV_BF16) {  // bf16 slabs: the v9 weight-gradient kernel only
+      rc = launch_gemm9(d, s);
+      SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: bf16 slabs need the v9 weight-gradient layout (N/M-major A)");
+      return rc;
+    }
     if (impl == 9 || v9_pick) rc = launch_gemm9(d, s);  // shapes outside v9's contract take the dispatch below
     if (rc != SV_ERR_UNSUPPORTED) return rc;
     if (d->fold_out) {  // another family: the slabs, then the fold as its own pass (bitwise v9's in-kernel fold)

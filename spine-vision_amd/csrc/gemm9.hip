@@ -285,10 +285,10 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
   }
   const int64_t ldc = slab ? e.N : e.ldc;
   const char* cbase = reinterpret_cast<const char*>(e.C);
-  if (slab) cbase += (size_t)split * e.M * e.N * 4;
+  if (slab) cbase += (size_t)split * e.M * e.N * (P8 ? 2 : 4);  // f32 slabs, or bf16 (P8)
   const auto rc = rsrc(cbase, x.c);
   const auto rc2 = rsrc(e.C2 ? e.C2 : e.C, x.c2);
-  constexpr int CS = (EPI == SV_EPI_SLAB || !P8) ? 4 : 2;  // output element bytes: P8 <=> bf16 outputs
+  constexpr int CS = P8 ? 2 : 4;  // output element bytes: P8 <=> bf16 outputs (bf16 slabs included)
   constexpr bool AUXBF = EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD;
   constexpr bool AUXF = EPI == SV_EPI_BIAS_GAMMA_RES;
   const auto ra = rsrc(e.aux ? e.aux : e.C, x.aux);
@@ -831,7 +831,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int cs = d->c_dtype == SV_F32 ? 4 : 2;
   Ext x;
   if (EPI == SV_EPI_SLAB) {
-    x.c = (uint32_t)((size_t)d->M * d->N * 4);
+    x.c = (uint32_t)((size_t)d->M * d->N * (P8 ? 2 : 4));
   } else {
     x.c = (uint32_t)(((size_t)(d->M - 1) * d->ldc + d->N) * cs);
   }
@@ -893,6 +893,14 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
       return launch<AK, BKM, SV_EPI_STORE_STATS, true>(d, split, s);
     case SV_EPI_SLAB:
       if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
+      if (d->c_dtype == SV_BF16) {  // bf16 slabs (the weight-gradient layout, folded in a separate pass)
+        if constexpr (AK) {
+          return SV_ERR_UNSUPPORTED;
+        } else {
+          if (d->fold_out || d->N % 8) return SV_ERR_UNSUPPORTED;
+          return launch<AK, BKM, SV_EPI_SLAB, true>(d, split, s);
+        }
+      }
       if (d->fold_out) {  // (the weight-gradient layout only: N/M-major A; others fold in a separate pass)
         if constexpr (AK) return SV_ERR_UNSUPPORTED;
         else return launch<AK, BKM, SV_EPI_SLAB, false, kFoldLast>(d, split, s);

@@ -14,10 +14,23 @@ namespace sv {
 
 constexpr int kThreads = 256;
 
+// four consecutive slab elements as floats: f32 (one 16-B load) or bf16 (one 8-B load; bf16 weight-gradient slabs)
+template <typename T>
+__device__ __forceinline__ float4 ld_part4(const T* p) {
+  if constexpr (sizeof(T) == 4) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  }
+}
+
 // out[g][i] (+)= alpha * sum_{p in group g} part[p][i].  grid = (column tiles, groups); each thread
 // owns 4 consecutive columns (16-B loads) and keeps 8 independent loads in flight per round, so the
 // reduction of deep split-K slabs is bandwidth- rather than latency-bound.
-__global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* __restrict__ part,
+template <typename T>
+__global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const T* __restrict__ part,
                                                                     int P, int group, int64_t n,
                                                                     float* __restrict__ out,
                                                                     float alpha, int accumulate) {
@@ -34,14 +47,14 @@ __global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* 
     for (; p + 8 <= p1; p += 8) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(part + (size_t)(p + u) * n + i4);
+      for (int u = 0; u < 8; ++u) v[u] = ld_part4(part + (size_t)(p + u) * n + i4);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
     for (; p < p1; ++p) {
-      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * n + i4);
+      const float4 v = ld_part4(part + (size_t)p * n + i4);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     acc.x *= alpha; acc.y *= alpha; acc.z *= alpha; acc.w *= alpha;
@@ -54,7 +67,10 @@ __global__ void __launch_bounds__(kThreads) reduce_partials_kernel(const float* 
   } else {
     for (int64_t i = i4; i < n && i < i4 + 4; ++i) {
       float s = 0.f;
-      for (int p = p0; p < p1; ++p) s += part[(size_t)p * n + i];
+      for (int p = p0; p < p1; ++p) {
+        if constexpr (sizeof(T) == 4) s += part[(size_t)p * n + i];
+        else s += __uint_as_float((uint32_t)part[(size_t)p * n + i] << 16);
+      }
       s *= alpha;
       o[i] = accumulate ? o[i] + s : s;
     }
@@ -307,7 +323,8 @@ __global__ void __launch_bounds__(kThreads) layerscale_finish_kernel(
 // one workgroup per row c of G = sum_p slab[p][c][:]: thread t owns the float4 column groups
 // t, t + 256, ...; dW2[c] += gamma_c G[c], the row dot sum(W2[c] G[c]) and the colsum
 // cs[c] = sum_p cs_part[p][c] are block sums (fixed order), so one kernel finishes dgamma / db2 too.
-__global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float* __restrict__ slab, int Ps,
+template <typename T>
+__global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const T* __restrict__ slab, int Ps,
                                                                      const float* __restrict__ cs_part, int P,
                                                                      const float* __restrict__ W2,
                                                                      const float* __restrict__ gamma,
@@ -327,14 +344,14 @@ __global__ void __launch_bounds__(kThreads) layerscale_reduce_kernel(const float
     for (; p + 8 <= Ps; p += 8) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (size_t)(p + u) * pstride + off);
+      for (int u = 0; u < 8; ++u) v[u] = ld_part4(slab + (size_t)(p + u) * pstride + off);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
     for (; p < Ps; ++p) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (size_t)p * pstride + off);
+      const float4 v = ld_part4(slab + (size_t)p * pstride + off);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     const float4 w = *reinterpret_cast<const float4*>(W2 + off);
@@ -472,7 +489,7 @@ int sv_reduce_partials_pair(const float* part_a, int64_t n_a, float* out_a, cons
     // with 8 loads in flight (the partial-row groups of the kernel below would each issue ONE load
     // per thread before the LDS fold: latency-bound at ~1 TB/s); the narrow b segment follows
     const int64_t t4 = n_a / 4;
-    reduce_partials_kernel<<<dim3((unsigned)((t4 + kThreads - 1) / kThreads), 1), kThreads, 0, s>>>(part_a, P, P, n_a,
+    reduce_partials_kernel<float><<<dim3((unsigned)((t4 + kThreads - 1) / kThreads), 1), kThreads, 0, s>>>(part_a, P, P, n_a,
                                                                                                    out_a, alpha, accumulate);
     const int rc = check_launch("sv_reduce_partials_pair");
     if (rc != SV_OK || !n_b) return rc;
@@ -532,8 +549,21 @@ int sv_reduce_partials(const float* part, int32_t P, int32_t group, int64_t n, f
   const dim3 grid((unsigned)((threads + kThreads - 1) / kThreads), (unsigned)((P + group - 1) / group));
   if ((n & 3) == 0)
     SV_REQUIRE((((uintptr_t)part | (uintptr_t)out) & 15) == 0, "sv_reduce_partials: buffers must be 16-B aligned");
-  reduce_partials_kernel<<<grid, kThreads, 0, (hipStream_t)stream>>>(part, P, group, n, out, alpha, accumulate);
+  reduce_partials_kernel<float><<<grid, kThreads, 0, (hipStream_t)stream>>>(part, P, group, n, out, alpha, accumulate);
   return check_launch("sv_reduce_partials");
+}
+
+int sv_reduce_partials_bf16(const uint16_t* part, int32_t P, int64_t n, float* out, float alpha, int32_t accumulate,
+                            sv_stream_t stream) {
+  SV_REQUIRE(part && out && P >= 1, "sv_reduce_partials_bf16: bad args");
+  if (n <= 0) return SV_OK;
+  if ((n & 3) == 0)
+    SV_REQUIRE(((uintptr_t)part & 7) == 0 && ((uintptr_t)out & 15) == 0,
+               "sv_reduce_partials_bf16: part must be 8-B and out 16-B aligned");
+  const int64_t threads = (n + 3) / 4;
+  const dim3 grid((unsigned)((threads + kThreads - 1) / kThreads), 1);
+  reduce_partials_kernel<uint16_t><<<grid, kThreads, 0, (hipStream_t)stream>>>(part, P, P, n, out, alpha, accumulate);
+  return check_launch("sv_reduce_partials_bf16");
 }
 
 static int64_t colsum_rpb(int64_t rows) {
@@ -586,9 +616,22 @@ int sv_layerscale_wgrad_reduce(const float* slab, const float* cs_part, int32_t 
   SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_reduce: K4=%d must be a multiple of 4", K4);
   SV_REQUIRE((((uintptr_t)slab | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
              "sv_layerscale_wgrad_reduce: buffers must be 16-B aligned");
-  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(slab, P, cs_part, P, W2, gamma, b2, dW2, dgamma,
-                                                                   db2, C, K4);
+  layerscale_reduce_kernel<float><<<C, kThreads, 0, (hipStream_t)stream>>>(slab, P, cs_part, P, W2, gamma, b2, dW2,
+                                                                          dgamma, db2, C, K4);
   return check_launch("sv_layerscale_wgrad_reduce");
+}
+
+int sv_layerscale_wgrad_reduce_bf16(const uint16_t* slab, const float* cs_part, int32_t P, const float* W2,
+                                    const float* gamma, const float* b2, float* dW2, float* dgamma, float* db2, int32_t C,
+                                    int32_t K4, sv_stream_t stream) {
+  SV_REQUIRE(slab && cs_part && W2 && gamma && b2 && dW2 && dgamma && db2 && P >= 1,
+             "sv_layerscale_wgrad_reduce_bf16: bad arguments");
+  SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_reduce_bf16: K4=%d must be a multiple of 4", K4);
+  SV_REQUIRE(((uintptr_t)slab & 7) == 0 && (((uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
+             "sv_layerscale_wgrad_reduce_bf16: slab 8-B, W2 / dW2 16-B aligned");
+  layerscale_reduce_kernel<uint16_t><<<C, kThreads, 0, (hipStream_t)stream>>>(slab, P, cs_part, P, W2, gamma, b2, dW2,
+                                                                             dgamma, db2, C, K4);
+  return check_launch("sv_layerscale_wgrad_reduce_bf16");
 }
 
 int sv_layerscale_wgrad_fold_finish(const float* G, const float* cs_part, int32_t P, const float* W2, const float* gamma,
@@ -599,8 +642,8 @@ int sv_layerscale_wgrad_fold_finish(const float* G, const float* cs_part, int32_
   SV_REQUIRE(K4 % 4 == 0 && C > 0, "sv_layerscale_wgrad_fold_finish: K4=%d must be a multiple of 4", K4);
   SV_REQUIRE((((uintptr_t)G | (uintptr_t)W2 | (uintptr_t)dW2) & 15) == 0,
              "sv_layerscale_wgrad_fold_finish: buffers must be 16-B aligned");
-  layerscale_reduce_kernel<<<C, kThreads, 0, (hipStream_t)stream>>>(G, 1, cs_part, P, W2, gamma, b2, dW2, dgamma, db2,
-                                                                   C, K4);
+  layerscale_reduce_kernel<float><<<C, kThreads, 0, (hipStream_t)stream>>>(G, 1, cs_part, P, W2, gamma, b2, dW2, dgamma,
+                                                                          db2, C, K4);
   return check_launch("sv_layerscale_wgrad_fold_finish");
 }
 

@@ -154,7 +154,7 @@ def gemm(
     _check(A.numel() >= need_a, f"gemm: A too small ({A.numel()} < {need_a})")
     _check(B.numel() >= need_b, f"gemm: B too small ({B.numel()} < {need_b})")
     if epilogue == nv.SV_EPI_SLAB:
-        _check(C.dtype == torch.float32 and C.numel() >= split_k * M * N, "gemm: slab too small")
+        _check(C.dtype in (torch.float32, torch.bfloat16) and C.numel() >= split_k * M * N, "gemm: slab too small")
     else:
         ldc = N if ldc is None else ldc
         _check(C.numel() >= (M - 1) * ldc + N, "gemm: C too small")
@@ -290,6 +290,20 @@ def _fold_counters(device, tiles: int) -> torch.Tensor:
     return t
 
 
+# bf16 split-K slabs for the v9 weight gradients: each slice's f32 partial rounded to bf16 once (the reference's
+# autocast rounds the whole weight gradient to bf16 once), summed in f32 in slice order by the fold -- half the slab
+# bytes written and read.  ConvNeXt-base bs32 +1.5 % (1091-1098 vs 1077-1079 img/s interleaved), its B=32 parity
+# against the fp32 oracle unchanged (worst gradient 7.89e-3 vs 7.9e-3; profiles/round4/r9zh_bf16_slabs_ab.txt).
+# SV_WGRAD_BF16_SLABS=0: f32 slabs.  Only the default / v9 kernel family (policy.impl 0 or 9) takes them.
+_WGRAD_BF16_SLABS = os.environ.get("SV_WGRAD_BF16_SLABS", "1") != "0"
+
+
+def _bf16_slabs(N: int, K: int, M: int, split: int, compute_bf16: bool, policy=None) -> bool:
+    """the v9 weight-gradient shapes (whole 64-row K-tiles per slice: _wgrad_split_for's v9 branch)"""
+    return (_WGRAD_BF16_SLABS and compute_bf16 and split > 1 and min(N, K) >= 128 and max(N, K) >= 256
+            and K % 8 == 0 and M % (split * 64) == 0 and (policy is None or policy.impl in (0, 9)))
+
+
 def _fold_ok(split: int, n: int, out: torch.Tensor, compute_bf16: bool) -> bool:
     return (_INKERNEL_FOLD and compute_bf16 and 1 < split <= _FOLD_MAX_SPLIT and n >= 65536 and n % 4 == 0
             and out.dtype == torch.float32 and out.is_contiguous() and out.data_ptr() % 16 == 0)
@@ -306,8 +320,21 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     ldx = x2d.shape[1]
     K = ldx if cols is None else cols
     split = _wgrad_split_for(N, K, M)
-    slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
+    if (out is not None and _bf16_slabs(N, K, M, split, compute_bf16, policy) and out.is_contiguous()
+            and out.numel() == N * K):
+        slab16 = torch.empty(split * N * K, device=dy2d.device, dtype=torch.bfloat16)
+        gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
+             C=slab16, C2=cs, split_k=split, compute_bf16=True, policy=policy)
+        _timed_call("fold", 2.0 * split * N * K + 4.0 * N * K * (1 + int(bool(accumulate))), "sv_reduce_partials_bf16",
+                    ptr(slab16), split, N * K, ptr(out), 1.0, int(bool(accumulate)))
+        if cs is not None:
+            if defer is not None:
+                defer.append((cs, bias_out, split, bias_accumulate))
+            else:
+                reduce_into(cs, split, bias_out, accumulate=bias_accumulate)
+        return out
+    slab = torch.empty(split * N * K, device=dy2d.device, dtype=torch.float32)
     if out is not None and _fold_ok(split, N * K, out, compute_bf16):
         _check(out.numel() == N * K, "linear_wgrad: bad out")
         gemm(dy2d, x2d, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=N, ldb=ldx, epilogue=nv.SV_EPI_SLAB,
@@ -352,8 +379,16 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     M, C = dsrc2d.shape
     K4 = a2d.shape[1]
     split = _wgrad_split_for(C, K4, M)
-    slab = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.float32)
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
+    if _bf16_slabs(C, K4, M, split, compute_bf16, policy):
+        slab16 = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.bfloat16)
+        gemm(dsrc2d, a2d, M=C, N=K4, K=M, a_kmajor=False, b_kmajor=False, lda=C, ldb=K4, epilogue=nv.SV_EPI_SLAB,
+             C=slab16, C2=cs, split_k=split, compute_bf16=True, policy=policy)
+        _timed_call("fold", 2.0 * split * C * K4 + 8.0 * C * K4 + 4.0 * (split + 4) * C,
+                    "sv_layerscale_wgrad_reduce_bf16", ptr(slab16), ptr(cs), split, ptr(w2), ptr(gamma), ptr(b2),
+                    ptr(dw2), ptr(dgamma), ptr(db2), C, K4)
+        return
+    slab = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.float32)
     G = torch.empty(C * K4, device=dsrc2d.device, dtype=torch.float32)
     if _fold_ok(split, C * K4, G, compute_bf16):
         # G = d^T a folded inside the wgrad GEMM; the finish then reads one G instead of `split` slabs

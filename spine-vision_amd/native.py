@@ -132,6 +132,7 @@ _SIGS = {
     "sv_pool_ln_fwd": [_p, _p, _p, _f32, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_pool_ln_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p],
     "sv_reduce_partials": [_p, _i32, _i32, _i64, _p, _f32, _i32, _p],
+    "sv_reduce_partials_bf16": [_p, _i32, _i64, _p, _f32, _i32, _p],
     "sv_reduce_partials_pair": [_p, _i64, _p, _p, _i64, _p, _i32, _f32, _i32, _p],
     "sv_reduce_partials_multi": [ctypes.POINTER(RedSeg), _i32, _f32, _p],
     "sv_colsum_nparts": [_i64, _i32],
@@ -139,6 +140,7 @@ _SIGS = {
     "sv_layerscale_wgrad_finish": [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_layerscale_wgrad_reduce_ws": [_i32, _i32],
     "sv_layerscale_wgrad_reduce": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
+    "sv_layerscale_wgrad_reduce_bf16": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_layerscale_wgrad_fold_finish": [_p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_sqnorm_nparts": [_i64],
     "sv_sqnorm_partial": [_p, _i64, _p, _p],

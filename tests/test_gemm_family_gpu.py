@@ -21,6 +21,13 @@ from spine_vision_amd import native as nv
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _f32_slabs(monkeypatch):
+    """These tests pin the kernel families against each other on f32 split-K slabs; the bf16 slabs of the production
+    schedule have their own test (test_wgrad_bf16_slabs)."""
+    monkeypatch.setattr(K, "_WGRAD_BF16_SLABS", False)
+
+
 def _ops(dev, M, C, seed):
     g = torch.Generator().manual_seed(seed)
     bf = torch.bfloat16
@@ -312,3 +319,47 @@ def test_wgrad_spread_fold_under_uneven_load(dev):
         K._INKERNEL_FOLD = saved
     for i, o in enumerate(outs):
         assert torch.equal(o, ref), (i, float((o - ref).abs().max()))
+
+
+@pytest.mark.parametrize("M,C", [(32768, 512), (131072, 256), (8192, 1024)])
+def test_wgrad_bf16_slabs(dev, M, C, monkeypatch):
+    """Opt-in bf16 split-K slabs for the v9 weight gradients (SV_WGRAD_BF16_SLABS): the fold equals, bit for bit, the
+    f32 slabs of the same GEMM rounded to bf16 (RNE) and summed in f32 in slice order; the fc2 layer-scale finish
+    over bf16 slabs stays within bf16 rounding of the f32-slab result (a weight gradient the reference's autocast
+    rounds to bf16 once)."""
+    g = torch.Generator().manual_seed(M // 1024 + C)
+    bf = torch.bfloat16
+    dh = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    y = torch.randn(M, C, generator=g).to(bf).to(dev)
+    nw, kw = 4 * C, C
+    split = K._wgrad_split_for(nw, kw, M)
+    assert split > 1
+    slab = torch.empty(split * nw * kw, device=dev)
+    K.gemm(dh, y, M=nw, N=kw, K=M, a_kmajor=False, b_kmajor=False, lda=nw, ldb=kw, epilogue=nv.SV_EPI_SLAB, C=slab,
+           split_k=split)
+    ref = torch.zeros(nw * kw, device=dev)
+    base = torch.randn(nw * kw, generator=g).to(dev)
+    for p in range(split):
+        ref = ref + slab[p * nw * kw:(p + 1) * nw * kw].to(bf).float()
+    ref = ref + base
+    monkeypatch.setattr(K, "_WGRAD_BF16_SLABS", True)
+    out = base.clone().view(nw, kw)
+    K.linear_wgrad(dh, y, out=out, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(-1), ref), float((out.view(-1) - ref).abs().max())
+    # fc2: the layer-scale finish over bf16 slabs against the f32 slabs
+    d = torch.randn(M, C, generator=g).to(bf).to(dev)
+    a = torch.randn(M, 4 * C, generator=g).to(bf).to(dev)
+    w2 = (torch.randn(C, 4 * C, generator=g) * 0.05).to(dev)
+    gam, b2 = (torch.rand(C, generator=g) + 0.1).to(dev), torch.randn(C, generator=g).to(dev)
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(K, "_WGRAD_BF16_SLABS", flag)
+        dw2, dgm, db2 = torch.zeros(C, 4 * C, device=dev), torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        K.layerscale_wgrad(d, a, w2, gam, b2, dw2=dw2, dgamma=dgm, db2=db2)
+        res[flag] = (dw2, dgm, db2)
+    torch.cuda.synchronize()
+    for i, name in enumerate(("dW2", "dgamma", "db2")):
+        r = _rel(res[True][i], res[False][i])
+        assert r < 4e-3, (name, r)
+    assert torch.equal(res[True][2], res[False][2])  # the bias gradient comes from the f32 column sums
