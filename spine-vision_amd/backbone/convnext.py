@@ -155,6 +155,10 @@ class ConvNeXtHip(nn.Module):
         # a grid cap on the main stream's backward GEMMs (A/B runs; 128 measured equal to none, 192/224 slower:
         # profiles/round4/r9u_main_cap_and_tile_queue_rejected.txt)
         self.main_bwd_cap = int(os.environ.get("SV_MAIN_BWD_CAP", "0"))
+        # the block weight gradients' persistent grid target (kernels._wgrad_split_for): with bf16 split-K slabs the
+        # whole chip (256) beats half of it (128) here, +0.8 % (1108-1112 vs 1097-1105 img/s interleaved; ResNet's
+        # stay at 128, where 256 measured -2 %: profiles/round4/r9zn_wgrad_target_bf16_slabs.txt); SV_CNX_WGRAD_WGS
+        self.wgrad_target = int(os.environ.get("SV_CNX_WGRAD_WGS", "256"))
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -519,12 +523,12 @@ class ConvNeXtHip(nn.Module):
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
-                               compute_bf16=True, policy=spol)
+                               compute_bf16=True, policy=spol, wgrad_target=self.wgrad_target)
             # the block's remaining folds (fc1 wgrad slab + bias, LayerNorm and depthwise weight / bias
             # partials) in ONE launch instead of four
             folds: list | None = [] if self.merge_folds else None
             K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
-                           compute_bf16=True, defer=folds, policy=spol)
+                           compute_bf16=True, defer=folds, policy=spol, wgrad_target=self.wgrad_target)
             ln_finish(record=False, defer=folds)
             K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias), defer=folds)
             if folds is not None:

@@ -251,14 +251,14 @@ def _wgrad_split(tiles: int, K: int) -> int:
     return max(1, min(split, K // 512 if K >= 512 else 1))
 
 
-def _wgrad_split_for(N: int, K: int, M: int) -> int:
+def _wgrad_split_for(N: int, K: int, M: int, target: int | None = None) -> int:
     """Split-K factor of a weight gradient G[N,K] = dY[M,N]^T X[M,K].  Outputs of at least 128 x 256 run
     on the persistent 256x256 kernel (gemm9.hip; a 128-row output half-fills its tiles and still beats
     the 256x128 kernel): one tile per CU (tiles * split ~ 256 CUs) with every K slice a whole number of
     64-deep K-tiles; smaller ones on the 256x128 kernel (~512 workgroups)."""
     if min(N, K) >= 128 and max(N, K) >= 256:
         tiles9 = -(-N // 256) * -(-K // 256)
-        target = _WGRAD9_TARGET if 2.0 * M * N * K <= _WGRAD9_LONG_GFLOP * 1e9 else 256
+        target = (target or _WGRAD9_TARGET) if 2.0 * M * N * K <= _WGRAD9_LONG_GFLOP * 1e9 else 256
         # the slice count whose grid is nearest the target, among those that cut M into whole 64-row K-tiles and
         # keep one workgroup per CU (rounding down alone left ConvNeXt-large's S3 wgrads, 36 tiles, at split 2:
         # 72 workgroups, 47 % longer launches, the large bs64 step 16 % slower, profiles/round4/r9b_configs/)
@@ -310,7 +310,8 @@ def _fold_ok(split: int, n: int, out: torch.Tensor, compute_bf16: bool) -> bool:
 
 
 def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_accumulate=True,
-                 compute_bf16=True, cols=None, defer: list | None = None, policy=None) -> torch.Tensor:
+                 compute_bf16=True, cols=None, defer: list | None = None, policy=None,
+                 wgrad_target: int | None = None) -> torch.Tensor:
     """G[N,K] = dy2d[M,N]^T @ x2d[M,K] in f32 (split-K over M into slabs, then one reduce pass that
     writes -- or, with ``accumulate``, adds -- into ``out``).  With ``bias_out`` the column sums of
     dy2d (the bias gradient) come out of the same GEMM (SV_EPI_SLAB colsum).  ``cols``: use only the
@@ -319,7 +320,7 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     M, N = dy2d.shape
     ldx = x2d.shape[1]
     K = ldx if cols is None else cols
-    split = _wgrad_split_for(N, K, M)
+    split = _wgrad_split_for(N, K, M, wgrad_target)
     cs = torch.empty(split * N, device=dy2d.device, dtype=torch.float32) if bias_out is not None else None
     if (out is not None and _bf16_slabs(N, K, M, split, compute_bf16, policy) and out.is_contiguous()
             and out.numel() == N * K):
@@ -370,7 +371,8 @@ def linear_wgrad(dy2d, x2d, *, out=None, accumulate=False, bias_out=None, bias_a
     return out
 
 
-def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf16=True, policy=None):
+def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf16=True, policy=None,
+                     wgrad_target: int | None = None):
     """fc2 weight / bias / layer-scale gradients of out = x + gamma * (a W2^T + b2) from d_out:
     dW2 += gamma (.) d^T a, dgamma += rowdot(W2, d^T a) + b2 (.) colsum(d), db2 += gamma (.) colsum(d).
     The wgrad GEMM writes split-K slabs (+ colsum partials); ONE fused pass (a workgroup per row)
@@ -378,7 +380,7 @@ def layerscale_wgrad(dsrc2d, a2d, w2, gamma, b2, *, dw2, dgamma, db2, compute_bf
     never materialised."""
     M, C = dsrc2d.shape
     K4 = a2d.shape[1]
-    split = _wgrad_split_for(C, K4, M)
+    split = _wgrad_split_for(C, K4, M, wgrad_target)
     cs = torch.empty(split * C, device=dsrc2d.device, dtype=torch.float32)
     if _bf16_slabs(C, K4, M, split, compute_bf16, policy):
         slab16 = torch.empty(split * C * K4, device=dsrc2d.device, dtype=torch.bfloat16)

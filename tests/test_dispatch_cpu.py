@@ -67,3 +67,13 @@ def test_wgrad_split_fills_half_the_chip(N, Kd, M):
     assert M % (s * 64) == 0
     assert tiles9 * s <= 256
     assert abs(tiles9 * s - K._WGRAD9_TARGET) <= max(tiles9, K._WGRAD9_TARGET // 2)
+
+
+@pytest.mark.parametrize("N,Kd,M", CONVNEXT_WGRADS)
+def test_wgrad_split_whole_chip_target(N, Kd, M):
+    """the ConvNeXt backward's target (256: the whole chip, with bf16 slabs): whole 64-row K-tiles per slice, at most
+    one workgroup per CU, never fewer workgroups than the 128 target gives"""
+    s = K._wgrad_split_for(N, Kd, M, 256)
+    tiles9 = -(-N // 256) * -(-Kd // 256)
+    assert M % (s * 64) == 0 and tiles9 * s <= 256
+    assert tiles9 * s >= tiles9 * K._wgrad_split_for(N, Kd, M)
