@@ -159,6 +159,8 @@ class ConvNeXtHip(nn.Module):
         # whole chip (256) beats half of it (128) here, +0.8 % (1108-1112 vs 1097-1105 img/s interleaved; ResNet's
         # stay at 128, where 256 measured -2 %: profiles/round4/r9zn_wgrad_target_bf16_slabs.txt); SV_CNX_WGRAD_WGS
         self.wgrad_target = int(os.environ.get("SV_CNX_WGRAD_WGS", "256"))
+        # the side stream's GEMMs at raised wave priority (SV_SIDE_PRIO=0: normal, A/B runs)
+        self.side_prio = int(os.environ.get("SV_SIDE_PRIO", "1"))
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -519,7 +521,7 @@ class ConvNeXtHip(nn.Module):
         side_cap = pol.grid_cap
         if self.side_grid_cap is not None:
             side_cap = min(self.side_grid_cap, side_cap) if side_cap > 0 else self.side_grid_cap
-        spol = nv.policy(impl=self.side_impl, grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=1)
+        spol = nv.policy(impl=self.side_impl, grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=self.side_prio)
         with torch.cuda.stream(side):
             K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
                                dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
