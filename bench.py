@@ -67,6 +67,18 @@ PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsam
 # over five boxes: worst 0.2-2.9 ms during the backward; at its end, with nothing else queued, the 14-19 us of an
 # idle wake-up, tools/event_wake_probe.py -- charged as 0.05 ms): folded into dp_rehearsal's predicted scaling
 RESERVE_COST = float(os.environ.get("SV_RESERVE_COST", "0.0"))
+HBM_SUSTAINED_GBS = 6300.0  # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy)
+
+
+def comm_latency_samples():
+    """Measured comm-kernel start latencies (ms) of the default schedule, committed from tests/test_comm_reserve_gpu.py
+    (profiles/comm_latency.json), and their source; None when absent."""
+    p = os.path.join(ROOT, "profiles", "comm_latency.json")
+    try:
+        d = json.load(open(p))
+        return [v * 1e-3 for v in d["latency_us"]], d.get("source", p)
+    except Exception:
+        return None
 COMM_DELAY_MS = (float(os.environ.get("SV_COMM_DELAY_MS", "2.9")), float(os.environ.get("SV_COMM_DELAY_END_MS", "0.05")))
 # HBM-bound kernel classes timed by kernels.OpProbe (SURVEY section 8d: reported separately against 8 TB/s)
 OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "fold")
@@ -107,6 +119,8 @@ def parse():
     ap.add_argument("--native", type=int, default=640, help="--trainer: side of the PNGs on disk (resized to 512)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU sample budget")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--rocprof-file", default=os.path.join(ROOT, "profiles", "rocprof_avg.json"),
+                    help="per-class rocprofv3 average launch durations (tools/rocprof_avg.py) for frac_rocprof")
     args = ap.parse_args()
     cls = args.workload == "classification"
     if args.image_size is None:
@@ -467,6 +481,21 @@ def kernel_roofline(name: str, probe, steps_probed: int, peak: float, traffic: d
     return out
 
 
+def rocprof_frac(path: str, key: str, cls: str, kr: dict, peak: float) -> dict:
+    """The dominant class's roofline fraction from the profiler's average launch duration of the same kernels
+    (profiles/rocprof_avg.json, tools/rocprof_avg.py) beside the HIP-event probe's: roof time per launch (this line's
+    algorithmic bytes / FLOPs) / rocprof's average.  {} when no profile of this configuration is committed."""
+    try:
+        ent = json.load(open(path))["configs"][key][cls]
+    except Exception:
+        return {}
+    t_roof = max(kr["algorithmic_bytes_per_launch"] / (PEAK_HBM_GBS * 1e9),
+                 kr["algorithmic_gflop_per_launch"] * 1e9 / (peak * 1e12))
+    avg = ent["avg_launch_us"] * 1e-6
+    return {"frac_rocprof": round(t_roof / avg, 4), "rocprof_avg_launch_us": ent["avg_launch_us"],
+            "rocprof_source": ent["source"], "frac_probe": kr["frac"]}
+
+
 def step_floor(kern: dict, ms: float, peak: float) -> dict:
     """The step against its own floor: for every probed class of algorithmic work, launches x max(algorithmic
     bytes / 8 TB/s, FLOPs / bf16 peak) per launch, summed (the split-K folds are overhead, not algorithmic,
@@ -665,6 +694,9 @@ def main():
         roof["step_mfma_frac"] = step_frac
         roof["traffic_config"] = traffic_key if traffic else None
         roof["step_floor"] = step_floor(kern, ms, peak)
+        rp = rocprof_frac(args.rocprof_file, traffic_key, dominant, kern[dominant], peak)
+        if rp:
+            roof.update(rp)
         roof["kernels"] = kern
     else:
         # no per-kernel probe: report the whole-step model FLOP rate against the peak
@@ -722,6 +754,7 @@ def main():
         step_last = tl_ev["start"].elapsed_time(tl_ev["end"])
         # xGMI bus bandwidth of RCCL's ring all-reduce on 8 MI355X: not measurable on a 1-GPU box; the
         # prediction is given at 200 / 300 / 400 GB/s (DESIGN.md "Multi-GPU": 7 links x ~153 GB/s per GPU)
+        samples = comm_latency_samples()
         result["dp_rehearsal"] = {
             "buckets_mb_ready_ms": ready,
             "backward_end_ms": round(bwd_end, 3), "step_ms_last": round(step_last, 3),
@@ -729,9 +762,18 @@ def main():
             # world 1 as an interleaved A/B (SV_BENCH_RESERVE, DESIGN.md "Multi-GPU"), stretches every time
             "reserve_cost_frac": RESERVE_COST,
             "comm_launch_delay_ms": list(COMM_DELAY_MS),
+            # every bucket charged the worst start latency ever measured, plus RCCL's own HBM traffic beside the
+            # backward at the HBM rate the chip sustains (comm.BucketTimeline.predict)
             "predictions": [timeline.predict(ready, bwd_end, ms, 8, bw, reserve_cost=RESERVE_COST,
-                                             launch_delay_ms=COMM_DELAY_MS) for bw in (200.0, 300.0, 400.0)],
+                                             launch_delay_ms=COMM_DELAY_MS, hbm_gbs=HBM_SUSTAINED_GBS)
+                            for bw in (200.0, 300.0, 400.0)],
         }
+        if samples:
+            # each bucket waits for the slowest of 8 ranks: the expected max of 8 draws from the measured latencies
+            result["dp_rehearsal"]["comm_latency_source"] = samples[1]
+            result["dp_rehearsal"]["predictions_max_over_ranks"] = [
+                timeline.predict(ready, bwd_end, ms, 8, bw, reserve_cost=RESERVE_COST, launch_delay_ms=COMM_DELAY_MS,
+                                 latency_samples_ms=samples[0], hbm_gbs=HBM_SUSTAINED_GBS) for bw in (200.0, 300.0, 400.0)]
     if world > 1:
         result["config"]["comm_reserve_cus"] = engine.comm_reserve_cus
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -77,18 +77,33 @@ int device_cus(hipStream_t s) {
   return ctx_locked(dev).cus;
 }
 
-void ensure_lds_attr(const void* kernel, int bytes, hipStream_t s) {
-  if (bytes <= 65536) return;
+int stream_cus(hipStream_t s) {
+  const int all = device_cus(s);
+  uint32_t mask[32] = {};
+  const int words = (all + 31) / 32;
+  if (words > 32 || hipExtStreamGetCUMask(s, (uint32_t)words, mask) != hipSuccess) return all;
+  int n = 0;
+  for (int w = 0; w < words; ++w) n += __builtin_popcount(mask[w]);
+  return n > 0 && n < all ? n : all;
+}
+
+int ensure_lds_attr(const void* kernel, int bytes, hipStream_t s) {
+  if (bytes <= 65536) return SV_OK;
   const int dev = stream_device(s);
-  if (dev < 0 || dev >= kMaxDevices) return;
+  if (dev < 0 || dev >= kMaxDevices) return SV_OK;
   std::lock_guard<std::mutex> lk(g_dev_mu);
-  if (ctx_locked(dev).lds_raised.insert(kernel).second) {
-    int cur = -1;
-    hipGetDevice(&cur);
-    if (cur != dev) hipSetDevice(dev);
-    hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (cur != dev) hipSetDevice(cur);
-  }
+  sv_ctx& c = ctx_locked(dev);
+  if (c.lds_raised.count(kernel)) return SV_OK;
+  int cur = -1;
+  hipGetDevice(&cur);
+  if (cur != dev) hipSetDevice(dev);
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (cur != dev) hipSetDevice(cur);
+  if (e != hipSuccess)
+    return set_error(SV_ERR_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize = %d) failed on device %d: %s", bytes,
+                     dev, hipGetErrorString(e));
+  c.lds_raised.insert(kernel);  // remembered only once raised: a failed attempt is retried at the next launch
+  return SV_OK;
 }
 
 int policy_grid(const sv_gemm_policy* pol, int total, int per_cu_default, hipStream_t s) {

@@ -22,8 +22,10 @@ int check_launch(const char* what);
 // mutex -- no launch inherits another device's CU count, and the library is reentrant across devices ----
 int stream_device(hipStream_t s);   // the device a stream belongs to (the null stream: the current device)
 int device_cus(hipStream_t s);      // compute units of that device
-// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device) before its first launch there
-void ensure_lds_attr(const void* kernel, int bytes, hipStream_t s);
+int stream_cus(hipStream_t s);      // compute units a launch on that stream may use (its CU mask, if any)
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device) before its first launch there;
+// SV_OK, or the failure reported through set_error (retried on the next launch: only a success is remembered)
+int ensure_lds_attr(const void* kernel, int bytes, hipStream_t s);
 // the grid of a persistent launch of `total` tiles under `pol` (nullable): one workgroup per tile, or
 // wg_per_cu x CUs, then at most pol->grid_cap
 int policy_grid(const sv_gemm_policy* pol, int total, int per_cu_default, hipStream_t s);

@@ -382,7 +382,7 @@ static int launch(const Args& a, int split, hipStream_t s) {
   constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
   static_assert(lds <= 160 * 1024, "conv kernel LDS");
-  ensure_lds_attr(reinterpret_cast<const void*>(&conv_kernel<BF16, MODE>), (int)lds, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&conv_kernel<BF16, MODE>), (int)lds, s)) return rc_;
   dim3 grid(tilesM * tilesN, 1, split);
   conv_kernel<BF16, MODE><<<grid, kGemmThreads, lds, s>>>(a, tilesM, tilesN);
   return check_launch(MODE == FPROP ? "sv_conv_fwd" : MODE == DGRAD ? "sv_conv_bwd_data" : "sv_conv_bwd_weight");

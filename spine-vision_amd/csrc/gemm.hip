@@ -264,7 +264,7 @@ static int launch(const sv_gemm_desc* d, hipStream_t s) {
   constexpr size_t epi_lds = 4 * 16 * EPI_LD * sizeof(float);
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
   dim3 grid(tilesM * tilesN, 1, split);
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm_kernel<BF16, TA, TB, AK, BKM>), (int)lds, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm_kernel<BF16, TA, TB, AK, BKM>), (int)lds, s)) return rc_;
   gemm_kernel<BF16, TA, TB, AK, BKM><<<grid, kGemmThreads, lds, s>>>(
       reinterpret_cast<const TA*>(d->A), d->lda, reinterpret_cast<const TB*>(d->B), d->ldb, d->a_scale_k, d->K,
       kper, tilesM, tilesN, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr);

@@ -242,7 +242,7 @@ static int launch(const sv_gemm_desc* d, int split, int kper, hipStream_t s) {
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
   constexpr size_t lds = Cfg<BN>::LDS;
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm2_kernel<AK, BKM, BN>), (int)lds, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm2_kernel<AK, BKM, BN>), (int)lds, s)) return rc_;
   dim3 grid(tilesM * tilesN, 1, split);
   gemm2_kernel<AK, BKM, BN><<<grid, THREADS, lds, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,

@@ -454,7 +454,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
     e.rm_ghw_shift = cg->ghw_shift;
     e.rm_prow = ceil_div(d->M, 64);
   }
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>), (int)C::LDS, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>), (int)C::LDS, s)) return rc_;
   // one workgroup per tile, which lets kernels of the side stream take CUs as tiles retire
   const int total = tilesM * tilesN * split;
   // (policy.wg_per_cu: co-residency with a concurrent GEMM; policy.grid_cap: persistent over the rest)

@@ -243,7 +243,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm8_kernel<AK, BKM, EPI, BKT, S, OCC>), (int)C::LDS, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm8_kernel<AK, BKM, EPI, BKT, S, OCC>), (int)C::LDS, s)) return rc_;
   const int total = tilesM * tilesN * split;
   gemm8_kernel<AK, BKM, EPI, BKT, S, OCC><<<total, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,

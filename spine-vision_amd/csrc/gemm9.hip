@@ -466,6 +466,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
 template <int FB>
 __device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const Fold& f, int m0, int n0, int nsplit,
                                           int r_lo = 0, int r_hi = BM) {
+  // a spread slice's range may run past the tile when nsplit does not divide BM: never fold the next tile's rows
+  if (r_hi > BM) r_hi = BM;
   if (e.M - m0 < r_hi) r_hi = e.M - m0;
   m0 += r_lo;
   const int rows = r_hi - r_lo;
@@ -840,7 +842,7 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   x.a = (uint32_t)((AK ? (size_t)(d->M - 1) * d->lda + d->K : (size_t)(d->K - 1) * d->lda + d->M) * 2);
   x.b = (uint32_t)((BKM ? (size_t)(d->N - 1) * d->ldb + d->K : (size_t)(d->K - 1) * d->ldb + d->N) * 2);
   constexpr int LDS = lds_total<AK, EPI, FOLD>();
-  ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, FOLD>), LDS, s);
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, FOLD>), LDS, s)) return rc_;
   const int total = tilesM * tilesN * split;
   const int grid = policy_grid(&d->policy, total, 1, s);  // persistent: one workgroup per CU (or the cap)
   const Fold fold{d->fold_out, d->fold_ld, d->fold_accumulate, d->fold_counters};
@@ -848,10 +850,14 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
     // the spread fold waits for a tile's other slices: only when every (tile, slice) unit has a workgroup of its
     // own and the grid is at most half the chip (one workgroup per CU): then two such launches on two streams
     // can never hold every CU with partly-resident grids, so a waiting workgroup's peers always find a CU.
+    // "The chip" is the CUs this stream may use: a CU-masked stream (training/cumask.py) or a grid cap
+    // (sv_gemm_policy.grid_cap, which also marks a launch that shares the chip by design) shrinks it.
     // Otherwise the wait-free last-arriver form.
-    if (grid == total && 2 * total <= device_cus(s)) {
+    int usable = stream_cus(s);
+    if (d->policy.grid_cap > 0 && d->policy.grid_cap < usable) usable = d->policy.grid_cap;
+    if (grid == total && 2 * total <= usable) {
       constexpr int LDS2 = lds_total<AK, EPI, kFoldSpread>();
-      ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, kFoldSpread>), LDS2, s);
+      if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm9_kernel<AK, BKM, EPI, P8, kFoldSpread>), LDS2, s)) return rc_;
       gemm9_kernel<AK, BKM, EPI, P8, kFoldSpread><<<grid, THREADS, LDS2, s>>>(
           reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, nk, tilesM,
           tilesN, split, e, x, fold);

@@ -246,8 +246,24 @@ class BucketTimeline:
         return out
 
     @staticmethod
+    def expected_max(samples, n: int) -> float:
+        """E[max of ``n`` independent draws] from the empirical distribution ``samples`` (order statistics:
+        sum_i x_(i) [(i/N)^n - ((i-1)/N)^n]).  A collective starts when its slowest rank's comm kernel has started, so
+        at ``n`` ranks each bucket waits for the max of ``n`` start latencies, not one rank's."""
+        xs = sorted(float(x) for x in samples)
+        N = len(xs)
+        if N == 0:
+            return 0.0
+        return sum(x * ((i / N) ** n - ((i - 1) / N) ** n) for i, x in enumerate(xs, start=1))
+
+    # HBM bytes a ring all-reduce moves per rank per byte reduced: reduce-scatter (n-1)/n x {local chunk read, the
+    # peer's chunk landing in the staging buffer (written) and read back, the sum written} + all-gather (n-1)/n x
+    # {the peer's chunk written, read to forward} = 6 (n-1)/n
+    RCCL_HBM_PER_BYTE = 6.0
+
+    @staticmethod
     def predict(ready: list, bwd_end_ms: float, step_ms: float, world: int, busbw_gbs: float,
-                reserve_cost: float = 0.0, launch_delay_ms=0.0) -> dict:
+                reserve_cost: float = 0.0, launch_delay_ms=0.0, latency_samples_ms=None, hbm_gbs: float = 0.0) -> dict:
         """Exposed exchange and scaling at ``world`` ranks if every bucket's ring all-reduce takes
         2 (n-1)/n x bytes / busbw on one comm stream, launched at its ready time (a bucket never ready in the
         backward launches at its end); the step grows by what finishes after the backward's end.
@@ -256,21 +272,41 @@ class BucketTimeline:
         ``launch_delay_ms``: (mid, end) -- how long a comm kernel may wait behind the backward's kernels after its
         ready event while the backward runs (mid), and its start latency once the compute queues are idle (end).  A
         bucket that becomes ready shortly before the backward's end waits at most for the rest of the backward:
-        delay = min(mid, time left in the backward + end).  A scalar applies to both."""
+        delay = min(mid, time left in the backward + end).  A scalar applies to both.
+        ``latency_samples_ms``: measured per-launch start latencies during the backward (tests/test_comm_reserve_gpu.py);
+        when given, the mid delay of every bucket is the expected MAX over ``world`` ranks' draws from them (the
+        collective waits for its slowest rank) -- never below it: max(that, the scalar mid) is NOT taken, the scalar is
+        then ignored, so the caller picks the model.
+        ``hbm_gbs`` > 0: RCCL's own HBM traffic (RCCL_HBM_PER_BYTE (n-1)/n x the bytes reduced) competes with the
+        backward; charged as a stretch of the backward by traffic / hbm_gbs (an upper bound: it assumes the backward is
+        HBM-bound for the whole overlap)."""
         f = 1.0 + reserve_cost
         bwd_end_ms, step_dp = bwd_end_ms * f, step_ms * f
         d_mid, d_end = launch_delay_ms if isinstance(launch_delay_ms, (tuple, list)) else (launch_delay_ms,) * 2
+        if latency_samples_ms:
+            d_mid = BucketTimeline.expected_max(latency_samples_ms, world)
+        total_mb = sum(mb for mb, _ in ready)
+        hbm_ms = 0.0
+        if hbm_gbs > 0 and world > 1:
+            hbm_ms = BucketTimeline.RCCL_HBM_PER_BYTE * (world - 1) / world * total_mb * 2**20 / (hbm_gbs * 1e9) * 1e3
+        # the stretch is spread over the backward: a bucket ready at r has paid (r / bwd_end) of it
+        g = 1.0 + hbm_ms / bwd_end_ms if bwd_end_ms > 0 else 1.0
         t = 0.0
         for mb, r in sorted(ready, key=lambda x: (x[1] is None, x[1] if x[1] is not None else 0.0)):
-            rr = r * f if r is not None else bwd_end_ms
-            start = max(t, rr + min(d_mid, max(0.0, bwd_end_ms - rr) + d_end))
+            rr = r * f * g if r is not None else bwd_end_ms * g
+            start = max(t, rr + min(d_mid, max(0.0, bwd_end_ms * g - rr) + d_end))
             t = start + 2.0 * (world - 1) / world * mb * 2**20 / (busbw_gbs * 1e9) * 1e3
-        exposed = max(0.0, t - bwd_end_ms)
+        bwd_end_g = bwd_end_ms * g
+        exposed = max(0.0, t - bwd_end_g)
+        step_pred = step_dp + hbm_ms + exposed
         return {"world": world, "busbw_gbs": busbw_gbs, "reserve_cost_frac": reserve_cost,
-                "launch_delay_ms": [d_mid, d_end],
+                "launch_delay_ms": [round(d_mid, 6), d_end],
+                "launch_delay_model": (f"expected max over {world} ranks of {len(latency_samples_ms)} measured latencies"
+                                       if latency_samples_ms else "fixed"),
+                "rccl_hbm_stretch_ms": round(hbm_ms, 3),
                 "comm_end_ms": round(t, 3), "exposed_ms": round(exposed, 3),
-                "predicted_step_ms": round(step_dp + exposed, 3),
-                "predicted_scaling": round(world * step_ms / (step_dp + exposed), 3)}
+                "predicted_step_ms": round(step_pred, 3),
+                "predicted_scaling": round(world * step_ms / step_pred, 3)}
 
 
 class BufferSync:

@@ -6,7 +6,7 @@ The test stands in for RCCL with a proxy kernel (a torch reduction, which needs 
 high-priority comm stream, launched the moment each block's gradients are reported ready in the ConvNeXt-base
 bs32 512x512 backward.  It records, per launch, the time from the ready event to the proxy's completion minus
 the proxy's standalone duration (its start latency), for the default data-parallel setup (no CU reserve) and
-for a 32-CU reserve by grid caps (round 3's mechanism), and bounds the default's median AND maximum.
+for a 32-CU reserve by grid caps (round 3's mechanism, printed only), and bounds the default's median AND maximum.
 
 Measured (profiles/round4/r7b_* .. r7h_*; rocprofv3 trace of this test, tools/comm_trace.py): the worst waits
 follow readiness reports recorded on the MAIN stream -- the stage-transition downsample gradients -- and the
@@ -80,7 +80,14 @@ def _latencies(dev, reserve):
     return alone_us, lat
 
 
-def test_comm_stream_kernel_starts_with_reserved_cus(dev):
+def test_comm_stream_start_latency_default_no_reserve(dev):
+    """Bounds the comm-stream kernel's start latency of the DEFAULT data-parallel schedule (no CU reserve: median and
+    max); the 32-CU grid-cap reserve is measured and printed beside it for DESIGN.md, not asserted.  The default run's
+    per-launch latencies are written to gpurun_out/comm_latency.json, which bench.py's dp_rehearsal reads (from
+    profiles/, once committed) to charge every bucket the expected MAX over the ranks' draws."""
+    import json
+    import os
+
     res = {}
     for reserve in (0, 32):
         alone, lat = _latencies(dev, reserve)
@@ -88,5 +95,9 @@ def test_comm_stream_kernel_starts_with_reserved_cus(dev):
         print(f"[comm] reserve {reserve:2d} CUs: proxy alone {alone:.1f} us; start latency over {len(lat)} "
               f"launches: median {np.median(lat):.1f} us, p90 {np.percentile(lat, 90):.1f} us, max {lat.max():.1f} us")
     lat0 = res[0][1]
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "comm_latency.json"), "w") as f:
+        json.dump({"source": "tests/test_comm_reserve_gpu.py, ConvNeXt-base bs32 512x512 backward, reserve 0",
+                   "proxy_alone_us": round(res[0][0], 2), "latency_us": [round(float(v), 2) for v in lat0]}, f)
     assert len(lat0) > 30
     assert np.median(lat0) < DEFAULT_MEDIAN_US and lat0.max() < DEFAULT_MAX_US, (np.median(lat0), lat0.max())

@@ -240,8 +240,9 @@ def test_gemm_policy_is_per_call(dev):
         K.linear_wgrad(dh, y, policy=nv.policy(impl=5))
 
 
-@pytest.mark.parametrize("M,C", [(4096, 128), (131072, 256), (32768, 512), (8192, 1024), (2048 + 512, 512)],
-                         ids=["half-tiles", "S2", "S3", "S4", "ragged-split"])
+@pytest.mark.parametrize("M,C", [(4096, 128), (131072, 256), (32768, 512), (8192, 1024), (2048 + 512, 512),
+                                 (6272, 512)],
+                         ids=["half-tiles", "S2", "S3", "S4", "ragged-split", "split7"])
 def test_wgrad_inkernel_fold_bitwise(dev, M, C):
     """The split-K fold inside the persistent v9 weight-gradient GEMM (sv_gemm_desc.fold_out) equals the slabs +
     separate fold bit for bit -- written or accumulated, under the default grid (every slice its own workgroup: the
@@ -278,6 +279,10 @@ def test_wgrad_inkernel_fold_bitwise(dev, M, C):
             K._INKERNEL_FOLD, K._FOLD_MAX_SPLIT = saved
 
     split = K._wgrad_split_for(4 * C, C, M)
+    if M == 6272:
+        # a split that does not divide the 256-row tile (per-slice rows 37: the last slice's range runs past its
+        # tile) over 8 M tiles, so an unclamped spread fold would add the next tile's rows twice
+        assert split == 7 and 256 % split != 0
     ref = run(False, None)
     for pol in (None, nv.policy(grid_cap=37), nv.policy(wg_per_cu=1, priority=1, grid_cap=224), nv.policy(impl=3)):
         # (v3 sums the fused bias column in its own order: its reference is its own slabs + fold)

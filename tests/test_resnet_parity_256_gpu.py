@@ -42,7 +42,12 @@ LABELS = ["pfirrmann", "modic", "herniation"]
 # clamp, and the cosine guard.  Measured on MI355X (profiles/round4/r7c_tests.log): ratio median 0.97-1.02,
 # worst 1.24-1.53, min cosine 0.934-0.999 (B=2 eval / train, B=32 train) -- the HIP path is as far from the
 # float64 emulation as the float32 emulation is
-FLOOR = {"ratio_median": 1.5, "ratio_max": 2.5, "min_floor": 1e-2, "min_cos": 0.5}
+FLOOR = {"ratio_median": 1.5, "ratio_max": 2.5, "min_floor": 1e-2, "min_cos": 0.9}
+# the reference-anchored bound beside the floor check (an emulation that rounds where the HIP path rounds
+# cannot see a rounding scheme drifting away from the reference's autocast): the bf16 path against the fp32 oracle
+# (logits rel, worst gradient, median gradient), ~2x the round-3 measurements (DESIGN.md "Classification at the
+# BASELINE geometry": eval 1.6e-2 / 8.7e-2 / 2.1e-2, train 1.1e-2 / 0.52 / 0.37)
+BF16_VS_FP32 = {"eval": (3.2e-2, 0.18, 4.5e-2), "train": (2.2e-2, 1.05, 0.75)}
 
 
 def rel(a, b):
@@ -184,9 +189,12 @@ def test_resnet50_256_bf16_vs_emulation(dev, mode):
 
 
 @pytest.mark.parametrize("mode", ["eval", "train"])
-def test_resnet50_256_bf16_vs_fp32_reported(dev, mode):
-    """The bf16 path against the fp32 oracle: reported for DESIGN.md, not bounded -- that distance is the bf16
-    noise itself (test_resnet50_256_bf16_vs_emulation carries the bound)."""
+def test_resnet50_256_bf16_vs_fp32(dev, mode):
+    """The bf16 path against the fp32 oracle -- the reference's own arithmetic -- under absolute bounds (BF16_VS_FP32,
+    ~2x measured).  Most of that distance is the bf16 noise itself (test_resnet50_256_bf16_vs_emulation pins the
+    kernels against it); this bound is what catches a rounding design that drifts from the reference."""
     logit, grads, buf = _case(dev, "bf16", mode)
-    _report(f"resnet50@256 B2 bf16 {mode} (vs fp32 oracle)", logit, grads)
+    lw, worst, med = _report(f"resnet50@256 B2 bf16 {mode} (vs fp32 oracle)", logit, grads)
+    bl, bw, bm = BF16_VS_FP32[mode]
+    assert lw < bl and worst < bw and med < bm, (lw, worst, med)
     assert all(v < 1e-2 for v in buf.values()), buf
