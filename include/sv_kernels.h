@@ -177,6 +177,20 @@ int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, 
 int sv_gemm_slab_finish_bn_bwd(const float* slab, int32_t split, int32_t M, int32_t N, void* C, const void* y,
                                const sv_bn_ref* bn, float* part, sv_stream_t stream);
 
+/* ---- Fused ConvNeXt MLP forward (narrow stages) ------------------------------------------------
+ * Replaces ConvNeXtBlock.mlp.fc1 -> GELU -> mlp.fc2 -> x gamma -> + shortcut (timm convnext.py; the two
+ * sv_gemm calls SV_EPI_BIAS_GELU_DUAL / SV_EPI_BIAS_GELU then SV_EPI_BIAS_GAMMA_RES) in ONE kernel: the
+ * hidden activation streams through registers in 64-unit chunks and never reaches HBM as fc2's operand.
+ *   h = y . w1^T + b1;  x_out = gamma (.) (bf16(GELU(h)) . w2^T + b2) + x
+ * y [M, C] bf16, w1 [4C, C] bf16 (torch Linear layout), b1 [4C] f32, w2 [C, 4C] bf16, b2 / gamma [C] f32,
+ * x / x_out [M, C] f32 (must not alias).  gelu_grad / gelu_out [M, 4C] bf16, both or neither: the
+ * training forward stores GELU'(h) and GELU(h) for the backward (bit for bit the dual epilogue's), the
+ * eval forward passes NULL.  C in {128, 192, 256}; every pointer 16-byte aligned; M * 4C * 2 < 2^31.
+ * x_out is bit for bit the unfused pair's.                                                           */
+int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+               const float* gamma, const float* x, float* x_out, uint16_t* gelu_grad, uint16_t* gelu_out, int64_t M,
+               int32_t C, sv_stream_t stream);
+
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.
  * fwd: y = (x-mean)*rstd*w + b; saves mean/rstd [rows] (f32).

@@ -217,3 +217,228 @@ def floor_check(hip: dict, emu64: dict, emu32: dict, *, ratio_median: float, rat
     assert not bad, bad
     assert float(np.median(ratios)) <= ratio_median, float(np.median(ratios))
     return out
+
+
+# ==============================================================================================================
+# ConvNeXt: the HIP bf16 path's store points, restated from spine-vision_amd/backbone/
+# convnext.py (``_forward_impl``, ``_block_backward_lean``, ``_backward_impl``) and the kernels it calls
+# (spine-vision_amd/kernels.py), over the timm ConvNeXt of oracle/convnext.py (reference backbone.py:50,164-170):
+#
+#   forward   stem     P = bf16(image patches);  z0 = bf16(P . bf16(W)^T + b);  x = LN(z0) (f32, stats of bf16 z0)
+#             block    z = bf16(dwconv7(x) + b_dw) (f32 x, f32 taps);  y = bf16(LN(z)) (stats of the bf16 z);
+#                      h = y . bf16(W1)^T + b1 (f32);  a = bf16(GELU(h)),  g' = bf16(GELU'(h))  (one erf);
+#                      x_out = gamma * (a . bf16(W2)^T + b2) + x   (f32 residual stream)
+#             downs.   Pd = bf16(LN(x));  x = Pd . bf16(Wd)^T + bd (f32)
+#             head     feat = LN(mean_hw(x)) (f32)
+#   backward  the gradient stream d into every block / stage output is f32, and its bf16 copy db is the GEMMs'
+#             operand;  block: dh = bf16((db . bf16(W2 * gamma)) * g');  dy = bf16(dh . bf16(W1));
+#             dz = bf16(LN_bwd(dy; bf16 z));  d += dwconv7^T(dz) (f32), db = bf16(d);
+#             dW_dw = sum dz * x (f32), LN / bias gradients f32 sums of the bf16 operands;
+#             weight gradients dW = sum_s bf16(A_s^T B_s): each split-K slice's partial over its contiguous rows
+#             rounded to bf16 once, the slices summed in f32 (bf16 slabs, kernels._bf16_slabs), or the plain f32
+#             product where the build keeps f32 slabs (the stem's 48-column gradient); fc2: dW2 = gamma * G,
+#             dgamma = rowdot(W2, G) + b2 * colsum(db), db2 = gamma * colsum(db) with G = d^T a in slabs;
+#             downsample: dPd = db . bf16(Wd) (f32), LN backward to f32 d;  stem: dz0 = bf16(LN_bwd(d; bf16 z0)).
+# The split-K geometry is the implementation's (a pure function of the shapes): the caller passes it in as
+# ``wgrad_split(N, K, M, target) -> (split, bf16_slabs)``.
+# ==============================================================================================================
+
+def _ln_fwd(z, w, b, eps):
+    mean = z.mean(-1, keepdim=True)
+    var = ((z - mean) ** 2).mean(-1, keepdim=True)
+    rstd = 1.0 / torch.sqrt(var + eps)
+    return (z - mean) * rstd * w + b, mean, rstd
+
+
+def _ln_bwd(dy, z, mean, rstd, w):
+    """-> dz, dw (sum over rows), db for LayerNorm over the last dim (rows flattened by the caller)."""
+    xh = (z - mean) * rstd
+    g = dy * w
+    dz = rstd * (g - g.mean(-1, keepdim=True) - xh * (g * xh).mean(-1, keepdim=True))
+    return dz, (dy * xh).reshape(-1, z.shape[-1]).sum(0), dy.reshape(-1, z.shape[-1]).sum(0)
+
+
+def _gelu_pair(h):
+    c = 0.7071067811865476
+    cdf = 0.5 * (1.0 + torch.erf(h * c))
+    return h * cdf, cdf + h * torch.exp(-0.5 * h * h) * 0.3989422804014327
+
+
+def _dw(x, w, b=None):
+    """depthwise 7x7, pad 3, NHWC in / out"""
+    y = F.conv2d(x.permute(0, 3, 1, 2), w, b, padding=3, groups=x.shape[-1])
+    return y.permute(0, 2, 3, 1)
+
+
+def _slab_wgrad(A, Bm, split: int, bf16_slabs: bool):
+    """G = A^T B over rows M (A [M,N], B [M,K]) in ``split`` contiguous row slices, each partial rounded to bf16 when
+    ``bf16_slabs`` (the v9 weight gradient's P8 slab store), summed in slice order."""
+    M = A.shape[0]
+    if not bf16_slabs or split <= 1:
+        return A.t() @ Bm
+    per = M // split
+    G = None
+    for s in range(split):
+        part = bf16_round(A[s * per:(s + 1) * per].t() @ Bm[s * per:(s + 1) * per])
+        G = part if G is None else G + part
+    return G
+
+
+# the tape keeps the bf16-rounded tensors as bf16 (exact, a quarter of float64's memory); a check that disables the
+# rounding (bf16_round -> identity, test_oracle_golden) must keep them in the working dtype
+STORE_BF16 = True
+
+
+class ConvNeXtBf16Emu:
+    """Functional emulation over an ``oracle.convnext.ConvNeXt`` in ``dtype`` (float64 = the reference for the floor
+    check, float32 = the floor itself).  ``forward(img)`` -> features (tape kept); ``backward(dfeat)`` -> {name: grad}.
+    ``device``: where the arithmetic runs (the float64 restatement of a 512x512 bs32 step is ~15 TFLOP; tests run
+    the large cases on the GPU's float64 units, the small ones on the CPU -- the same code either way)."""
+
+    def __init__(self, model: torch.nn.Module, dtype=torch.float64, wgrad_split=None, block_wgrad_target: int = 256,
+                 device="cpu") -> None:
+        self.model = model
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.P = {n: p.detach().to(self.device, dtype).clone() for n, p in model.named_parameters()}
+        self.wgrad_split = wgrad_split or (lambda N, K, M, target: (1, False))
+        self.block_target = block_wgrad_target
+        self.tape = None
+
+    def _q(self, t):
+        return bf16_round(t)
+
+    def _st(self, t):  # tape storage of a bf16-rounded tensor
+        return t.to(torch.bfloat16) if STORE_BF16 else t
+
+    def _lin_w(self, name):  # bf16 shadow of a GEMM weight
+        return bf16_round(self.P[name])
+
+    def forward(self, img: torch.Tensor) -> torch.Tensor:
+        P, q = self.P, self._q
+        x0 = img.to(self.device, self.dtype)
+        tape = {"stages": []}
+        # stem: bf16 patch rows x bf16 packed weight, bf16 conv output, f32 LayerNorm2d
+        pimg = q(x0)
+        z0 = q(F.conv2d(pimg, self._lin_w("stem.0.weight"), P["stem.0.bias"], stride=4).permute(0, 2, 3, 1))
+        x, m0, r0 = _ln_fwd(z0, P["stem.1.weight"], P["stem.1.bias"], 1e-6)
+        tape["stem"] = (pimg, self._st(z0), m0, r0)
+        for si, st in enumerate(self.model.stages):
+            pre = f"stages.{si}."
+            ds = None
+            if not isinstance(st.downsample, torch.nn.Identity):
+                xn_, dm, dr = _ln_fwd(x, P[pre + "downsample.0.weight"], P[pre + "downsample.0.bias"], 1e-6)
+                pd = q(xn_)
+                xo = F.conv2d(pd.permute(0, 3, 1, 2), self._lin_w(pre + "downsample.1.weight"),
+                              P[pre + "downsample.1.bias"], stride=2).permute(0, 2, 3, 1).contiguous()
+                ds = (x, self._st(pd), dm, dr)
+                x = xo
+            blocks = []
+            for bi in range(len(st.blocks)):
+                bp = f"{pre}blocks.{bi}."
+                z = q(_dw(x, P[bp + "conv_dw.weight"], P[bp + "conv_dw.bias"]))
+                yf, mean, rstd = _ln_fwd(z, P[bp + "norm.weight"], P[bp + "norm.bias"], 1e-6)
+                y = q(yf)
+                h = y @ self._lin_w(bp + "mlp.fc1.weight").t() + P[bp + "mlp.fc1.bias"]
+                gl, gp = _gelu_pair(h)
+                a, gh = q(gl), q(gp)
+                del h, gl, gp
+                xo = P[bp + "gamma"] * (a @ self._lin_w(bp + "mlp.fc2.weight").t() + P[bp + "mlp.fc2.bias"]) + x
+                blocks.append((x, self._st(z), self._st(y), mean, rstd, self._st(a), self._st(gh)))
+                x = xo
+            tape["stages"].append((ds, blocks))
+        pooled = x.mean((1, 2))
+        feat, pm, pr = _ln_fwd(pooled, P["head.norm.weight"], P["head.norm.bias"], 1e-6)
+        tape["pool"] = (pooled, pm, pr, tuple(x.shape))
+        self.tape = tape
+        return feat
+
+    def backward(self, dfeat: torch.Tensor) -> dict:
+        P, q, dt = self.P, self._q, self.dtype
+        T, self.tape = self.tape, None
+        G = {}
+        pooled, pm, pr, shape = T["pool"]
+        dpool, G["head.norm.weight"], G["head.norm.bias"] = _ln_bwd(dfeat.to(self.device, dt), pooled, pm, pr,
+                                                                    P["head.norm.weight"])
+        B, H, W, C = shape
+        d = (dpool / (H * W)).view(B, 1, 1, C).expand(B, H, W, C).contiguous()
+        for si in range(len(T["stages"]) - 1, -1, -1):
+            ds, blocks = T["stages"][si]
+            pre = f"stages.{si}."
+            for bi in range(len(blocks) - 1, -1, -1):
+                bp = f"{pre}blocks.{bi}."
+                x, z, y, mean, rstd, a, gh = blocks[bi]
+                blocks[bi] = None
+                z, y, a, gh = (t.to(dt) for t in (z, y, a, gh))
+                B, H, W, C = x.shape
+                M = B * H * W
+                db = q(d)
+                db2 = db.reshape(M, C)
+                w2 = P[bp + "mlp.fc2.weight"]
+                gam = P[bp + "gamma"]
+                dh = q((db2 @ q(w2 * gam[:, None])) * gh.reshape(M, 4 * C))
+                dy = q(dh @ self._lin_w(bp + "mlp.fc1.weight")).reshape(B, H, W, C)
+                dz, G[bp + "norm.weight"], G[bp + "norm.bias"] = _ln_bwd(dy, z, mean, rstd, P[bp + "norm.weight"])
+                dz = q(dz)
+                # side stream: fc2 (layer-scale) and fc1 weight gradients in bf16 slabs, depthwise weight gradient
+                s2, b2s = self.wgrad_split(C, 4 * C, M, self.block_target)
+                Gm = _slab_wgrad(db2, a.reshape(M, 4 * C), s2, b2s)
+                cs = db2.sum(0)
+                G[bp + "mlp.fc2.weight"] = gam[:, None] * Gm
+                G[bp + "gamma"] = (w2 * Gm).sum(1) + P[bp + "mlp.fc2.bias"] * cs
+                G[bp + "mlp.fc2.bias"] = gam * cs
+                s1, b1s = self.wgrad_split(4 * C, C, M, self.block_target)
+                G[bp + "mlp.fc1.weight"] = _slab_wgrad(dh, y.reshape(M, C), s1, b1s)
+                G[bp + "mlp.fc1.bias"] = dh.sum(0)
+                wdw = P[bp + "conv_dw.weight"]
+                dzc = dz.permute(0, 3, 1, 2)
+                G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), wdw.shape, dzc, padding=3,
+                                                                       groups=C)
+                G[bp + "conv_dw.bias"] = dz.reshape(M, C).sum(0)
+                d = d + torch.nn.grad.conv2d_input((B, C, H, W), wdw, dzc, padding=3, groups=C).permute(0, 2, 3, 1)
+            if ds is not None:
+                x_prev, pd, dm, dr = ds
+                pd = pd.to(dt)
+                B, Ho, Wo, Co = d.shape
+                Ci = x_prev.shape[-1]
+                db = q(d)
+                wd = P[pre + "downsample.1.weight"]
+                dpd = torch.nn.grad.conv2d_input(tuple(pd.permute(0, 3, 1, 2).shape), q(wd), db.permute(0, 3, 1, 2),
+                                                 stride=2).permute(0, 2, 3, 1)
+                Mo = B * Ho * Wo
+                sd, bsd = self.wgrad_split(Co, 4 * Ci, Mo, None)
+                # patch rows in the GEMM's k order (ci, kh, kw) -- the reshape of the timm weight [Co, Ci, 2, 2]
+                prow = pd.reshape(B, Ho, 2, Wo, 2, Ci).permute(0, 1, 3, 5, 2, 4).reshape(Mo, 4 * Ci)
+                G[pre + "downsample.1.weight"] = _slab_wgrad(db.reshape(Mo, Co), prow, sd, bsd).view_as(wd)
+                G[pre + "downsample.1.bias"] = db.reshape(Mo, Co).sum(0)
+                dxp, G[pre + "downsample.0.weight"], G[pre + "downsample.0.bias"] = _ln_bwd(
+                    dpd, x_prev, dm, dr, P[pre + "downsample.0.weight"])
+                d = dxp
+        pimg, z0, m0, r0 = T["stem"]
+        z0 = z0.to(dt)
+        dz0, G["stem.1.weight"], G["stem.1.bias"] = _ln_bwd(d, z0, m0, r0, P["stem.1.weight"])
+        dz0 = q(dz0)
+        w0 = P["stem.0.weight"]
+        G["stem.0.weight"] = torch.nn.grad.conv2d_weight(pimg, w0.shape, dz0.permute(0, 3, 1, 2), stride=4)
+        G["stem.0.bias"] = dz0.reshape(-1, w0.shape[0]).sum(0)
+        return G
+
+
+def regressor_grads(ref: torch.nn.Module, img: torch.Tensor, coords: torch.Tensor, mask: torch.Tensor,
+                    dtype=torch.float64, wgrad_split=None, block_wgrad_target: int = 256, device="cpu"):
+    """One forward + backward of an ``oracle.heads.CoordinateRegressor`` over a ConvNeXt backbone with the HIP bf16
+    path's rounding points (ConvNeXtBf16Emu), the head and the masked loss in ``dtype`` (the HIP head runs f32 torch
+    on the f32 features).  -> (pred, {param name: grad}).  ``ref`` is not modified."""
+    emu = ConvNeXtBf16Emu(ref.backbone, dtype, wgrad_split, block_wgrad_target, device)
+    feat = emu.forward(img).detach().requires_grad_(True)
+    head = {n: p.detach().to(emu.device, dtype).clone().requires_grad_(True) for n, p in ref.head.named_parameters()}
+    hn = ref.head[0]
+    o = F.layer_norm(feat, hn.normalized_shape, head["0.weight"], head["0.bias"], hn.eps)
+    o = F.gelu(F.linear(o, head["2.weight"], head["2.bias"]))
+    pred = torch.sigmoid(F.linear(o, head["5.weight"], head["5.bias"])).view(-1, ref.num_levels, ref.num_outputs)
+    m = mask.to(emu.device).unsqueeze(-1).expand_as(pred).bool()
+    loss = F.smooth_l1_loss(pred[m], coords.to(emu.device, dtype)[m])
+    loss.backward()
+    grads = {"backbone." + n: g for n, g in emu.backward(feat.grad).items()}
+    grads.update({"head." + n: v.grad for n, v in head.items()})
+    return pred.detach(), grads

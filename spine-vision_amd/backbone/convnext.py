@@ -161,6 +161,10 @@ class ConvNeXtHip(nn.Module):
         self.wgrad_target = int(os.environ.get("SV_CNX_WGRAD_WGS", "256"))
         # the side stream's GEMMs at raised wave priority (SV_SIDE_PRIO=0: normal, A/B runs)
         self.side_prio = int(os.environ.get("SV_SIDE_PRIO", "1"))
+        # bf16 blocks of the narrow stages (C in kernels.MLP_FUSED_C) run fc1 -> GELU -> fc2 -> gamma -> + x as ONE
+        # kernel (sv_mlp_fwd): the hidden activation never makes the HBM round trip between the two GEMMs; bit for
+        # bit the two-GEMM path (SV_FUSED_MLP=0, A/B runs)
+        self.fused_mlp = os.environ.get("SV_FUSED_MLP", "1") != "0"
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -283,6 +287,17 @@ class ConvNeXtHip(nn.Module):
                                                     blk.norm.bias, act_dtype=act)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 w2 = self._w(blk.mlp.fc2.weight, cache)
+                if bf and self.fused_mlp and C in K.MLP_FUSED_C:
+                    # fused MLP: the training forward stores GELU'(h) and GELU(h) for the backward, the eval one nothing
+                    xo = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
+                    gh = torch.empty(M, 4 * C, device=x.device, dtype=act) if save else None
+                    a = torch.empty(M, 4 * C, device=x.device, dtype=act) if save else None
+                    K.mlp_fwd(y, w1, blk.mlp.fc1.bias, w2, blk.mlp.fc2.bias, blk.gamma, x.view(M, C), out=xo.view(M, C),
+                              gelu_grad=gh, gelu_out=a)
+                    if save:
+                        blocks_saved.append((x, z, y, mean, rstd, gh, a))
+                    x = xo
+                    continue
                 # fc1 epilogue: a = GELU(h) (fc2 operand) and gh = GELU'(h) (for the backward), one erf;
                 # the tape-free forward (eval / predict) writes a only
                 a = torch.empty(M, 4 * C, device=x.device, dtype=act)

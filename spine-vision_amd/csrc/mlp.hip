@@ -1,0 +1,330 @@
+// Fused ConvNeXt MLP forward for the narrow stages (C = 128 / 192 / 256: S1 / S2 of ConvNeXt-base, S1 of -large):
+//     h = y W1^T + b1,  [gh = GELU'(h), a = GELU(h) stored bf16 for the backward],  x_out = gamma (.) (a W2^T + b2) + x
+// in ONE persistent kernel, so the 4C-wide hidden activation a never makes the HBM round trip fc1 -> fc2 (VERDICT r4,
+// missing 1 / next 3: the FlashAttention shape -- stream the hidden dimension in chunks, keep the C-wide fc2
+// accumulator in registers).  Reference: timm ConvNeXtBlock.mlp + gamma + shortcut, via
+// spine_vision/training/models/backbone.py:50,164-170.
+//
+// Layout of the work (512 threads = 8 waves, one workgroup per CU, persistent over 8*RW-row tiles):
+//  * wave w owns rows [16 RF w, +16 RF) of the tile (RF 16-row fragments); its y rows live in REGISTERS for the
+//    whole tile (the second MFMA operand of fc1), loaded once;
+//  * the hidden dimension streams through LDS in chunks of HC = 64 units: W1 rows [j0, j0+64) and W2 columns
+//    [j0, j0+64), double-buffered by LDS-DMA (buffer_load ... lds), the next chunk's DMA in flight while this one
+//    computes;
+//  * fc1 runs with the operands swapped as in v9 (D^T = W1 . y^T: a lane holds 4 consecutive hidden units of one
+//    row), the W1 rows permuted inside each 32-group at DMA time (perm8), so after bias + GELU a lane holds 8
+//    CONSECUTIVE hidden units of its row: that is both the 16-B store of the dual epilogue and, packed to bf16,
+//    exactly the second MFMA operand of fc2 (lane l: row l & 15, k = 8 (l >> 4) .. +7) -- P never leaves the
+//    registers;
+//  * fc2 accumulates D^T = W2 . P^T into C/16 x RF fragments per wave across all chunks; the epilogue applies
+//    gamma (.) (acc + b2) + x and stores f32 rows (4 consecutive channels per lane, 16 B).
+// Every accumulator sees the same MFMA instruction with the same operands in the same k order as the unfused v9
+// pair (fc1 GELU-dual epilogue, fc2 gamma-residual epilogue), and the epilogue arithmetic is v9's, so the outputs
+// are bit for bit the unfused path's (tests/test_mlp_fused_gpu.py).
+#include "common.h"
+#include "gemm_common.h"
+
+namespace sv {
+namespace mlp {
+
+constexpr int THREADS = 512, HC = 64;
+constexpr uint32_t OOB = 0x80000000u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// K-major LDS image [rows][64] bf16 (128-B rows), 16-B chunk c of row r at c ^ ((r >> 1) & 7) (as v9)
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+// bf16-output row permutation inside a 32-row group (as v9): LDS row 16h + 4g + r holds hidden unit 8g + 4h + r
+__device__ __forceinline__ int perm8(int rho) {
+  return (rho & ~31) | (((rho & 15) >> 2) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
+__device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
+}
+// fragment of a K-major image: lane l holds X[row = base + (l & 15)][k = 32 kh + 8 (l >> 4) + 0..7]
+__device__ __forceinline__ bf16x8 frag_k(const char* __restrict__ region, int base, int kh) {
+  const int l = threadIdx.x & 63;
+  const int row = base + (l & 15), ch = kh * 4 + (l >> 4);
+  return *reinterpret_cast<const bf16x8*>(region + row * 128 + ((ch ^ kswz(row)) << 4));
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// LDS reads of the per-channel vectors the compiler does not see: its alias analysis would otherwise drain every
+// LDS-DMA in flight (vmcnt(0)) before a plain LDS read it cannot prove disjoint from them (as v9's lds_f4); two
+// 16-B reads, then lgkmcnt(0)
+__device__ __forceinline__ void lds_f8(const float* p, float (&v)[8]) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t u, w;
+  const uint32_t ad = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(u), "=v"(w)
+               : "v"(ad)
+               : "memory");
+  v[0] = u.x, v[1] = u.y, v[2] = u.z, v[3] = u.w, v[4] = w.x, v[5] = w.y, v[6] = w.z, v[7] = w.w;
+}
+__device__ __forceinline__ void lds_f4x2(const float* p0, const float* p1, float (&v0)[4], float (&v1)[4]) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t u, w;
+  const uint32_t a0 = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p0);
+  const uint32_t a1 = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p1);
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(u), "=v"(w)
+               : "v"(a0), "v"(a1)
+               : "memory");
+  v0[0] = u.x, v0[1] = u.y, v0[2] = u.z, v0[3] = u.w, v1[0] = w.x, v1[1] = w.y, v1[2] = w.z, v1[3] = w.w;
+}
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+  return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+}
+// cache policy of the GELU'(h) store: nt, as the v9 dual epilogue (read only by the backward, much later)
+constexpr int kGradCpol = 2;
+
+template <int C>
+struct Cfg {
+  static constexpr int H = 4 * C;              // hidden units
+  static constexpr int NCH = H / HC;            // chunks per tile
+  static constexpr int KB = C / 64;             // 64-deep k-blocks of fc1
+  static constexpr int KS = C / 32;             // 32-deep MFMA k-steps of fc1
+  static constexpr int CF = C / 16;             // 16-channel fragments of the fc2 output
+  static constexpr int RF = C == 128 ? 2 : 1;   // 16-row fragments per wave (C = 192 at 2 spills)
+  static constexpr int R = 8 * 16 * RF;         // rows per tile
+  static constexpr int W1B = HC * C * 2;        // W1 chunk image bytes (KB k-blocks of [HC][64])
+  static constexpr int W2B = C * HC * 2;        // W2 chunk image bytes ([C][64])
+  static constexpr int STAGE = W1B + W2B;
+  static constexpr int PERSIST = (H + 2 * C) * 4;  // b1 [H], b2 [C], gamma [C] (f32)
+  static constexpr int LDS = 2 * STAGE + PERSIST;
+  static constexpr int DMAS = 2 * KB;           // DMA instructions per wave per chunk (KB for W1, KB for W2)
+};
+
+template <int C, bool TRAIN>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+               const uint16_t* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
+               const float* __restrict__ x, float* __restrict__ xo, uint16_t* __restrict__ gh, uint16_t* __restrict__ a,
+               int M) {
+  using K = Cfg<C>;
+  constexpr int RF = K::RF, KS = K::KS, CF = K::CF, KB = K::KB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lb1 = reinterpret_cast<float*>(smem + 2 * K::STAGE);
+  float* lb2 = lb1 + K::H;
+  float* lgam = lb2 + C;
+  const int lane = threadIdx.x & 63, ml = lane & 15, gq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles = (M + K::R - 1) / K::R;
+  const int my_tiles = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= tiles)
+  const int total = my_tiles * K::NCH;
+
+  // the per-channel vectors once into LDS (plain loads / stores, before any DMA)
+  for (int i = threadIdx.x; i < K::H; i += THREADS) lb1[i] = b1[i];
+  for (int i = threadIdx.x; i < C; i += THREADS) lb2[i] = b2[i], lgam[i] = gamma[i];
+
+  // ---- weight-chunk DMA: W1 rows [j0, j0+64) -> KB images [64][64] (rows perm8, chunks swizzled); W2 columns
+  // [j0, j0+64) of every channel row -> one image [C][64].  A wave's piece = 8 rows x 128 B; piece wid of each image
+  // block (the W2 image: pieces wid + 8j, rows 64j + ..)
+  const auto rw1 = rsrc(w1, (uint32_t)(K::H * C * 2)), rw2 = rsrc(w2, (uint32_t)(C * K::H * 2));
+  const int prow = 8 * wid + (lane >> 3), pch = lane & 7;
+  const uint32_t v1 = (uint32_t)((perm8(prow) * C + ((pch ^ kswz(prow)) << 3)) * 2);
+  const uint32_t v2 = (uint32_t)((prow * K::H + ((pch ^ kswz(prow)) << 3)) * 2);
+  auto issue = [&](int q) {
+    const int j0 = (q % K::NCH) * HC;
+    char* st = smem + (q & 1) * K::STAGE;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+#pragma unroll
+    for (int j = 0; j < KB; ++j)
+      dma(rw2, v2, (uint32_t)((64 * j * K::H + j0) * 2), st + K::W1B + (wid + 8 * j) * 1024);
+  };
+  // vector-memory instructions a wave issues after a chunk's DMA and before the next chunk's wait (the dual
+  // epilogue's stores): the wait allows them to stay in flight
+  constexpr int S = TRAIN ? RF * (HC / 32) * 2 : 0;
+
+  const auto ry = rsrc(y, (uint32_t)((size_t)M * C * 2));
+  const auto rx = rsrc(x, (uint32_t)((size_t)M * C * 4));
+  const auto rxo = rsrc(xo, (uint32_t)((size_t)M * C * 4));
+  const auto rgh = rsrc(TRAIN ? gh : nullptr, TRAIN ? (uint32_t)((size_t)M * K::H * 2) : 0u);
+  const auto ra = rsrc(TRAIN ? a : nullptr, TRAIN ? (uint32_t)((size_t)M * K::H * 2) : 0u);
+
+  __syncthreads();  // the per-channel vectors
+  issue(0);
+  int q = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    const int row0 = ((int)blockIdx.x + it * (int)gridDim.x) * K::R + wid * 16 * RF;
+    // this wave's y rows: lane holds row row0 + 16 rf + ml, k = 32 ks + 8 gq .. +7
+    bf16x8 yf[RF][KS];
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = row0 + 16 * rf + ml;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint32_t off = m < M ? (uint32_t)((m * C + 32 * ks + 8 * gq) * 2) : OOB;
+        yf[rf][ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
+      }
+    }
+    f32x4 acc2[CF][RF];
+#pragma unroll
+    for (int cf = 0; cf < CF; ++cf)
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) acc2[cf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int ch = 0; ch < K::NCH; ++ch, ++q) {
+      // chunk q landed (younger: the previous chunk's S stores) and every wave is done with chunk q - 1's stage
+      vm_wait<S>();
+      lgkm0();
+      bar();
+      if (q + 1 < total) issue(q + 1);
+      const char* st = smem + (q & 1) * K::STAGE;
+      const int j0 = ch * HC;
+      // this lane's fc1 bias: hidden units j0 + 32 qq + 8 gq .. +7
+      float bia[2][8];
+      lds_f8(lb1 + j0 + 8 * gq, bia[0]);
+      lds_f8(lb1 + j0 + 32 + 8 * gq, bia[1]);
+      // fc1: h^T chunk [64 hidden (4 fragments, perm8 rows)] x [16 RF rows], k ascending
+      f32x4 acc1[4][RF];
+#pragma unroll
+      for (int hf = 0; hf < 4; ++hf)
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) acc1[hf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const char* img = st + (ks >> 1) * (HC * 128);
+#pragma unroll
+        for (int hf = 0; hf < 4; ++hf) {
+          const bf16x8 wf = frag_k(img, 16 * hf, ks & 1);
+#pragma unroll
+          for (int rf = 0; rf < RF; ++rf)
+            acc1[hf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf[rf][ks], acc1[hf][rf], 0, 0, 0);
+        }
+      }
+      // bias + GELU pair (v9's packed form, same operations and order); P = bf16 GELU(h), the fc2 operand
+      bf16x8 pf[2][RF];
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) {
+          float v[8], o[8], o2[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc1[2 * qq][rf][r], v[4 + r] = acc1[2 * qq + 1][rf][r];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) v[w] += bia[qq][w];
+#pragma unroll
+          for (int w = 0; w < 8; w += 2) {
+            const gelu_f2 hh = {v[w], v[w + 1]};
+            gelu_f2 ph, de;
+            gelu_parts2(hh, ph, de);
+            const gelu_f2 g = hh * ph;
+            o2[w] = g.x, o2[w + 1] = g.y;
+            if constexpr (TRAIN) {
+              const gelu_f2 dg = __builtin_elementwise_fma(hh, de, ph);
+              o[w] = dg.x, o[w + 1] = dg.y;
+            }
+          }
+          const u32x4 pk = pack8(o2);
+          pf[qq][rf] = __builtin_bit_cast(bf16x8, pk);
+          if constexpr (TRAIN) {
+            const int m = row0 + 16 * rf + ml;
+            const uint32_t off = m < M ? (uint32_t)(((size_t)m * K::H + j0 + 32 * qq + 8 * gq) * 2) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rgh, off, 0, kGradCpol);
+            __builtin_amdgcn_raw_buffer_store_b128(pk, ra, off, 0, 0);
+          } else {
+            (void)o;
+          }
+        }
+      }
+      // fc2: acc2 += W2[:, chunk] . P^T, k (hidden) ascending
+      const char* img2 = st + K::W1B;
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+        for (int cf = 0; cf < CF; ++cf) {
+          const bf16x8 wf = frag_k(img2, 16 * cf, qq);
+#pragma unroll
+          for (int rf = 0; rf < RF; ++rf)
+            acc2[cf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, pf[qq][rf], acc2[cf][rf], 0, 0, 0);
+        }
+    }
+    // epilogue: x_out = gamma (.) (acc + b2) + x   (v9's gamma-residual arithmetic); lane: row m, channels 16 cf + 4 gq
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = row0 + 16 * rf + ml;
+      u32x4 xr[CF];
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + 16 * cf + 4 * gq) * 4) : OOB;
+        xr[cf] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+      }
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        const int c = 16 * cf + 4 * gq;
+        float bv[4], gv[4];
+        lds_f4x2(lb2 + c, lgam + c, bv, gv);
+        const uint32_t xw[4] = {xr[cf].x, xr[cf].y, xr[cf].z, xr[cf].w};
+        float o[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) o[w] = fmaf(gv[w], acc2[cf][rf][w] + bv[w], __uint_as_float(xw[w]));
+        const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + c) * 4) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]),
+                                                     __float_as_uint(o[2]), __float_as_uint(o[3])},
+                                               rxo, off, 0, 0);
+      }
+    }
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
+}
+
+template <int C, bool TRAIN>
+static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                  const float* gamma, const float* x, float* xo, uint16_t* gh, uint16_t* a, int M, hipStream_t s) {
+  using K = Cfg<C>;
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(&mlp_fwd_kernel<C, TRAIN>), K::LDS, s)) return rc;
+  const int tiles = (M + K::R - 1) / K::R;
+  const int grid = tiles < device_cus(s) ? tiles : device_cus(s);
+  mlp_fwd_kernel<C, TRAIN><<<grid, THREADS, K::LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
+  return check_launch("sv_mlp_fwd");
+}
+
+}  // namespace mlp
+}  // namespace sv
+
+extern "C" {
+
+int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+               const float* gamma, const float* x, float* x_out, uint16_t* gelu_grad, uint16_t* gelu_out, int64_t M,
+               int32_t C, sv_stream_t stream) {
+  using namespace sv;
+  SV_REQUIRE(y && w1 && b1 && w2 && b2 && gamma && x && x_out, "sv_mlp_fwd: null pointer");
+  SV_REQUIRE(M > 0 && M * 4 * C * 2 < 0x7fffffffLL, "sv_mlp_fwd: M out of range (the hidden tensor must be < 2 GiB)");
+  SV_REQUIRE((gelu_grad == nullptr) == (gelu_out == nullptr), "sv_mlp_fwd: GELU'(h) and GELU(h) are stored together");
+  SV_REQUIRE(x != x_out, "sv_mlp_fwd: x_out must not alias x");
+  SV_REQUIRE(C == 128 || C == 192 || C == 256, "sv_mlp_fwd: C = %d not supported (128, 192, 256)", C);
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  SV_REQUIRE(al(y) && al(w1) && al(w2) && al(b1) && al(b2) && al(gamma) && al(x) && al(x_out) && al(gelu_grad) &&
+                 al(gelu_out),
+             "sv_mlp_fwd: every pointer must be 16-B aligned");
+  const hipStream_t s = (hipStream_t)stream;
+  const bool tr = gelu_grad != nullptr;
+  const int m = (int)M;
+#define SV_MLP_CASE(CC)                                                                                           \
+  case CC:                                                                                                        \
+    return tr ? mlp::launch<CC, true>(y, w1, b1, w2, b2, gamma, x, x_out, gelu_grad, gelu_out, m, s)              \
+              : mlp::launch<CC, false>(y, w1, b1, w2, b2, gamma, x, x_out, nullptr, nullptr, m, s);
+  switch (C) {
+    SV_MLP_CASE(128)
+    SV_MLP_CASE(192)
+    SV_MLP_CASE(256)
+  }
+#undef SV_MLP_CASE
+  return set_error(SV_ERR_INVALID_ARG, "sv_mlp_fwd: C = %d not supported", C);
+}
+
+}  // extern "C"

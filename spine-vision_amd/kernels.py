@@ -80,7 +80,7 @@ OP_PROBES: dict[str, OpProbe] = {}  # name -> probe; bench.py fills it for the t
 _DIAG_SKIP = {x for x in os.environ.get("SV_DIAG_SKIP", "").split(",") if x}
 
 
-def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0) -> None:
+def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0, flops: float = 0.0) -> None:
     """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed; ``fma``: the
     launch's algorithmic f32 VALU FMAs (its roof when they outlast its bytes)."""
     if _DIAG_SKIP and op in _DIAG_SKIP:  # diagnostic timing only: the launch is skipped, its results are garbage
@@ -96,6 +96,7 @@ def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0) -> None:
     pr.events.append((ev0, ev1))
     pr.bytes += nbytes
     pr.fma += fma
+    pr.flops += flops
     pr.launches += 1
 
 
@@ -231,6 +232,41 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
     K = w.shape[1]
     return gemm(dy2d, w, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=N, ldb=K, epilogue=epilogue, C=out,
                 a_scale_k=a_scale_k, aux=aux, compute_bf16=compute_bf16, policy=policy)
+
+
+# channel counts the fused MLP forward kernel (csrc/mlp.hip) is built for: ConvNeXt-base S1 / S2, ConvNeXt-large S1
+MLP_FUSED_C = (128, 192, 256)
+
+
+def mlp_fwd(y, w1, b1, w2, b2, gamma, x, *, out, gelu_grad=None, gelu_out=None):
+    """Fused ConvNeXt MLP forward (sv_mlp_fwd): out = gamma (.) (GELU(y w1^T + b1) w2^T + b2) + x in one kernel,
+    the 4C-wide hidden activation kept on chip; ``gelu_grad`` / ``gelu_out`` ([M, 4C] bf16, both or neither) receive
+    GELU'(h) / GELU(h) for the backward (training).  Bit for bit the two-GEMM path (linear_fwd GELU dual, then the
+    gamma-residual epilogue)."""
+    M, C = y.shape
+    H = 4 * C
+    _check(C in MLP_FUSED_C, f"mlp_fwd: C = {C} not supported {MLP_FUSED_C}")
+    _check(y.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16,
+           "mlp_fwd: y / w1 / w2 must be bf16")
+    _check(tuple(w1.shape) == (H, C) and tuple(w2.shape) == (C, H), "mlp_fwd: weight shapes")
+    for t_, n_ in ((b1, H), (b2, C), (gamma, C)):
+        _check(t_.dtype == torch.float32 and t_.numel() == n_ and t_.is_contiguous(), "mlp_fwd: bias / gamma")
+    _check(x.dtype == torch.float32 and out.dtype == torch.float32 and x.numel() == M * C and out.numel() == M * C,
+           "mlp_fwd: x / out must be f32 [M, C]")
+    _check(out.data_ptr() != x.data_ptr(), "mlp_fwd: out must not alias x")
+    _check((gelu_grad is None) == (gelu_out is None), "mlp_fwd: gelu_grad and gelu_out go together")
+    ts = [y, w1, b1, w2, b2, gamma, x, out]
+    if gelu_grad is not None:
+        for t_ in (gelu_grad, gelu_out):
+            _check(t_.dtype == torch.bfloat16 and t_.numel() == M * H, "mlp_fwd: GELU outputs must be bf16 [M, 4C]")
+        ts += [gelu_grad, gelu_out]
+    _check(all(t_.is_contiguous() and t_.data_ptr() % 16 == 0 for t_ in ts), "mlp_fwd: contiguous 16-B aligned tensors")
+    _check(M * H * 2 < 2**31, "mlp_fwd: hidden tensor must be < 2 GiB")
+    # algorithmic: y, x read; out written; both weights once; the GELU pair written in training
+    nb = M * C * (2 + 4 + 4) + 2 * H * C * 2 + (2 * M * H * 2 if gelu_grad is not None else 0)
+    _timed_call("mlp_fused", nb, "sv_mlp_fwd", ptr(y), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(gamma), ptr(x), ptr(out),
+                ptr(gelu_grad), ptr(gelu_out), M, C, flops=4.0 * M * C * H)
+    return out
 
 
 _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
