@@ -27,7 +27,12 @@
 namespace sv {
 namespace mlp {
 
-constexpr int THREADS = 512, HC = 64;
+constexpr int HC = 64;
+// diagnostic builds only (tools/sessions): 1 = no GELU arithmetic, 2 = no weight DMA after chunk 0, 4 = no chunk
+// barriers, 8 = weight fragments from registers instead of LDS (results wrong)
+#ifndef SV_MLP_DIAG
+#define SV_MLP_DIAG 0
+#endif
 constexpr uint32_t OOB = 0x80000000u;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
@@ -98,17 +103,21 @@ struct Cfg {
   static constexpr int KS = C / 32;             // 32-deep MFMA k-steps of fc1
   static constexpr int CF = C / 16;             // 16-channel fragments of the fc2 output
   static constexpr int RF = C == 128 ? 2 : 1;   // 16-row fragments per wave (C = 192 at 2 spills)
-  static constexpr int R = 8 * 16 * RF;         // rows per tile
+  // waves per workgroup: C = 128 runs two 4-wave workgroups per CU (67 KiB of LDS each), which desynchronise -- one
+  // computes while the other streams its tile's y / x / x_out; the wider C need one 8-wave workgroup per CU (the
+  // second group staggered half a chunk behind)
+  static constexpr int NW = C == 128 ? 4 : 8;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int WG_PER_CU = NW == 4 ? 2 : 1;
+  static constexpr int R = NW * 16 * RF;        // rows per tile
   static constexpr int W1B = HC * C * 2;        // W1 chunk image bytes (KB k-blocks of [HC][64])
   static constexpr int W2B = C * HC * 2;        // W2 chunk image bytes ([C][64])
-  static constexpr int STAGE = W1B + W2B;
   static constexpr int PERSIST = (H + 2 * C) * 4;  // b1 [H], b2 [C], gamma [C] (f32)
-  static constexpr int LDS = 2 * STAGE + PERSIST;
-  static constexpr int DMAS = 2 * KB;           // DMA instructions per wave per chunk (KB for W1, KB for W2)
+  static constexpr int LDS = 2 * (W1B + W2B) + PERSIST;
 };
 
 template <int C, bool TRAIN>
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ void __launch_bounds__(Cfg<C>::THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
                const uint16_t* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
                const float* __restrict__ x, float* __restrict__ xo, uint16_t* __restrict__ gh, uint16_t* __restrict__ a,
@@ -116,7 +125,7 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
   using K = Cfg<C>;
   constexpr int RF = K::RF, KS = K::KS, CF = K::CF, KB = K::KB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* lb1 = reinterpret_cast<float*>(smem + 2 * K::STAGE);
+  float* lb1 = reinterpret_cast<float*>(smem + 2 * (K::W1B + K::W2B));
   float* lb2 = lb1 + K::H;
   float* lgam = lb2 + C;
   const int lane = threadIdx.x & 63, ml = lane & 15, gq = lane >> 4;
@@ -126,28 +135,46 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
   const int total = my_tiles * K::NCH;
 
   // the per-channel vectors once into LDS (plain loads / stores, before any DMA)
-  for (int i = threadIdx.x; i < K::H; i += THREADS) lb1[i] = b1[i];
-  for (int i = threadIdx.x; i < C; i += THREADS) lb2[i] = b2[i], lgam[i] = gamma[i];
+  for (int i = threadIdx.x; i < K::H; i += K::THREADS) lb1[i] = b1[i];
+  for (int i = threadIdx.x; i < C; i += K::THREADS) lb2[i] = b2[i], lgam[i] = gamma[i];
 
-  // ---- weight-chunk DMA: W1 rows [j0, j0+64) -> KB images [64][64] (rows perm8, chunks swizzled); W2 columns
-  // [j0, j0+64) of every channel row -> one image [C][64].  A wave's piece = 8 rows x 128 B; piece wid of each image
-  // block (the W2 image: pieces wid + 8j, rows 64j + ..)
+  // ---- two wave groups, B (waves 4-7) one barrier = half a chunk behind A (waves 0-3): on every SIMD one wave's
+  // GELU (VALU) runs beside its partner's MFMAs (MI355X_MICROARCH.md "Two waves per SIMD", item 9: stagger waves
+  // 4-7).  Chunk q is two halves: X_q [fc1, bias + GELU, the dual epilogue's stores] Y_q [fc2].  W1 and W2 chunks live
+  // in separate 2-slot rings; only group A issues their DMA: W1(q+1) right after its X_q barrier (B is then at Y_{q-1},
+  // done with W1(q-1), whose slot it takes), W2(q+1) right after its Y_q barrier (B at X_q: done with W2(q-1)); each
+  // lands within a chunk -- A waits for it before its next barrier of the same kind, which B passes only later.
+  const int grp = wid >> 2, wa = wid & 3;
   const auto rw1 = rsrc(w1, (uint32_t)(K::H * C * 2)), rw2 = rsrc(w2, (uint32_t)(C * K::H * 2));
-  const int prow = 8 * wid + (lane >> 3), pch = lane & 7;
+  // a DMA piece = 8 rows x 128 B; A-wave wa issues pieces wa and wa + 4 of every 64-row block (+32 rows via soffset:
+  // perm8 and the swizzle commute with it)
+  const int prow = 8 * wa + (lane >> 3), pch = lane & 7;
   const uint32_t v1 = (uint32_t)((perm8(prow) * C + ((pch ^ kswz(prow)) << 3)) * 2);
   const uint32_t v2 = (uint32_t)((prow * K::H + ((pch ^ kswz(prow)) << 3)) * 2);
-  auto issue = [&](int q) {
+  char* w1r = smem;                 // W1 ring: 2 x [KB][HC][64]
+  char* w2r = smem + 2 * K::W1B;    // W2 ring: 2 x [C][64]
+  auto issue_w1 = [&](int q) {
     const int j0 = (q % K::NCH) * HC;
-    char* st = smem + (q & 1) * K::STAGE;
+    char* st = w1r + (q & 1) * K::W1B;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dma(rw1, v1, (uint32_t)(((j0 + 32 * h) * C + 64 * kb) * 2), st + kb * (HC * 128) + (wa + 4 * h) * 1024);
+  };
+  auto issue_w2 = [&](int q) {
+    const int j0 = (q % K::NCH) * HC;
+    char* st = w2r + (q & 1) * K::W2B;
 #pragma unroll
     for (int j = 0; j < KB; ++j)
-      dma(rw2, v2, (uint32_t)((64 * j * K::H + j0) * 2), st + K::W1B + (wid + 8 * j) * 1024);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dma(rw2, v2, (uint32_t)(((64 * j + 32 * h) * K::H + j0) * 2), st + (8 * j + wa + 4 * h) * 1024);
   };
-  // vector-memory instructions a wave issues after a chunk's DMA and before the next chunk's wait (the dual
-  // epilogue's stores): the wait allows them to stay in flight
+  // vector-memory instructions of group A younger than the DMA each wait retires: the dual epilogue's S stores per
+  // chunk, the other ring's N1 pieces (the counts allow them to stay in flight)
   constexpr int S = TRAIN ? RF * (HC / 32) * 2 : 0;
+  constexpr int N1 = 2 * KB;
 
   const auto ry = rsrc(y, (uint32_t)((size_t)M * C * 2));
   const auto rx = rsrc(x, (uint32_t)((size_t)M * C * 4));
@@ -155,8 +182,13 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
   const auto rgh = rsrc(TRAIN ? gh : nullptr, TRAIN ? (uint32_t)((size_t)M * K::H * 2) : 0u);
   const auto ra = rsrc(TRAIN ? a : nullptr, TRAIN ? (uint32_t)((size_t)M * K::H * 2) : 0u);
 
-  __syncthreads();  // the per-channel vectors
-  issue(0);
+  if (grp == 0) {
+    issue_w1(0);
+    issue_w2(0);
+    vm_wait<0>();
+  }
+  __syncthreads();  // the per-channel vectors and chunk 0
+  if (K::NW == 8 && grp == 1) bar();  // group B one barrier behind
   int q = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int row0 = ((int)blockIdx.x + it * (int)gridDim.x) * K::R + wid * 16 * RF;
@@ -178,12 +210,12 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
       for (int rf = 0; rf < RF; ++rf) acc2[cf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int ch = 0; ch < K::NCH; ++ch, ++q) {
-      // chunk q landed (younger: the previous chunk's S stores) and every wave is done with chunk q - 1's stage
-      vm_wait<S>();
+      // X_q: W1(q) landed (A: issued after X_{q-1}; younger: chunk q-1's stores, W2(q)'s pieces)
+      if (grp == 0) vm_wait<S + N1>();
       lgkm0();
-      bar();
-      if (q + 1 < total) issue(q + 1);
-      const char* st = smem + (q & 1) * K::STAGE;
+      if (!(SV_MLP_DIAG & 4)) bar();
+      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
+      const char* st = w1r + (q & 1) * K::W1B;
       const int j0 = ch * HC;
       // this lane's fc1 bias: hidden units j0 + 32 qq + 8 gq .. +7
       float bia[2][8];
@@ -200,7 +232,7 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
         const char* img = st + (ks >> 1) * (HC * 128);
 #pragma unroll
         for (int hf = 0; hf < 4; ++hf) {
-          const bf16x8 wf = frag_k(img, 16 * hf, ks & 1);
+          const bf16x8 wf = (SV_MLP_DIAG & 8) ? yf[0][(ks + hf) % KS] : frag_k(img, 16 * hf, ks & 1);
 #pragma unroll
           for (int rf = 0; rf < RF; ++rf)
             acc1[hf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf[rf][ks], acc1[hf][rf], 0, 0, 0);
@@ -221,7 +253,11 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
           for (int w = 0; w < 8; w += 2) {
             const gelu_f2 hh = {v[w], v[w + 1]};
             gelu_f2 ph, de;
+#if SV_MLP_DIAG & 1
+            ph = (gelu_f2){1.0f, 1.0f}, de = hh;  // diagnostic: no GELU arithmetic (results wrong)
+#else
             gelu_parts2(hh, ph, de);
+#endif
             const gelu_f2 g = hh * ph;
             o2[w] = g.x, o2[w + 1] = g.y;
             if constexpr (TRAIN) {
@@ -241,13 +277,18 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
           }
         }
       }
+      // Y_q: W2(q) landed (A: issued after Y_{q-1}; younger: W1(q+1)'s pieces, this chunk's stores)
+      if (grp == 0) vm_wait<N1 + S>();
+      lgkm0();
+      if (!(SV_MLP_DIAG & 4)) bar();
+      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
       // fc2: acc2 += W2[:, chunk] . P^T, k (hidden) ascending
-      const char* img2 = st + K::W1B;
+      const char* img2 = w2r + (q & 1) * K::W2B;
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
         for (int cf = 0; cf < CF; ++cf) {
-          const bf16x8 wf = frag_k(img2, 16 * cf, qq);
+          const bf16x8 wf = (SV_MLP_DIAG & 8) ? yf[0][(cf + qq) % KS] : frag_k(img2, 16 * cf, qq);
 #pragma unroll
           for (int rf = 0; rf < RF; ++rf)
             acc2[cf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, pf[qq][rf], acc2[cf][rf], 0, 0, 0);
@@ -279,6 +320,7 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
       }
     }
   }
+  if (K::NW == 8 && grp == 0) bar();  // the barrier group B is behind
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
@@ -288,8 +330,9 @@ static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const 
   using K = Cfg<C>;
   if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(&mlp_fwd_kernel<C, TRAIN>), K::LDS, s)) return rc;
   const int tiles = (M + K::R - 1) / K::R;
-  const int grid = tiles < device_cus(s) ? tiles : device_cus(s);
-  mlp_fwd_kernel<C, TRAIN><<<grid, THREADS, K::LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
+  const int slots = K::WG_PER_CU * device_cus(s);
+  const int grid = tiles < slots ? tiles : slots;
+  mlp_fwd_kernel<C, TRAIN><<<grid, K::THREADS, K::LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
   return check_launch("sv_mlp_fwd");
 }
 
