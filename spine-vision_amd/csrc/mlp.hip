@@ -24,6 +24,8 @@
 #include "common.h"
 #include "gemm_common.h"
 
+#include <stdlib.h>
+
 namespace sv {
 namespace mlp {
 
@@ -324,6 +326,242 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
   vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
+// ---- C = 128 (ConvNeXt-base S1, the largest fused shape: 3 blocks of 524288 rows at bs32): two 4-wave workgroups
+// per CU, hidden chunks of 32 units, and nothing waits on HBM at a tile boundary -- each wave DMAs its NEXT tile's y
+// fragments into its own LDS region at the start of the current tile (64 lanes x 16 B per fragment: the LDS image IS
+// the register image), and loads the tile's residual x at the start of its last chunk, a chunk ahead of the epilogue.
+// The W2 chunk image has 64-B rows ([128][32]); 16-B chunk c of row r sits at c ^ {0,2,3,1}[(r >> 2) & 3], which
+// keeps the fragment reads (16 rows x one 16-B chunk per lane group of ds_read_b128) conflict-free.
+namespace c128 {
+constexpr int C = 128, H = 512, HC = 32, NCH = H / HC, KB = 2, KS = 4, CF = 8, RF = 2, NW = 4, THREADS = 256;
+constexpr int R = NW * 16 * RF;                 // 128 rows per tile
+constexpr int W1B = KB * HC * 128;              // [KB][32][64] bf16 = 8 KiB
+constexpr int W2B = C * HC * 2;                 // [128][32] bf16 = 8 KiB
+constexpr int YB = RF * KS * 1024;              // one wave's y fragments, 8 KiB
+constexpr int OFF_W1 = 0, OFF_W2 = 2 * W1B, OFF_Y = OFF_W2 + 2 * W2B, OFF_P = OFF_Y + NW * YB;
+constexpr int LDS = OFF_P + (H + 2 * C) * 4;    // 67 KiB: two workgroups per CU
+// vector-memory instructions per wave: W1 / W2 pieces per chunk, y fragments per tile, x loads and x_out stores per tile
+constexpr int N1 = KB, N2 = 2, YP = RF * KS, XL = RF * CF, XO = RF * CF;
+
+__device__ __forceinline__ int w2swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }  // {0,2,3,1}
+__device__ __forceinline__ bf16x8 frag64(const char* __restrict__ region, int base) {
+  const int l = threadIdx.x & 63;
+  const int row = base + (l & 15);
+  return *reinterpret_cast<const bf16x8*>(region + row * 64 + (((l >> 4) ^ w2swz(row)) << 4));
+}
+__device__ __forceinline__ bf16x8 lds_frag(const char* p) {  // ds_read_b128 the compiler does not see (see lds_f8)
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t u;
+  const uint32_t ad = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b128 %0, %1" : "=v"(u) : "v"(ad) : "memory");
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+              const uint16_t* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
+              const float* __restrict__ x, float* __restrict__ xo, uint16_t* __restrict__ gh, uint16_t* __restrict__ a,
+              int M) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lb1 = reinterpret_cast<float*>(smem + OFF_P);
+  float* lb2 = lb1 + H;
+  float* lgam = lb2 + C;
+  const int lane = threadIdx.x & 63, ml = lane & 15, gq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles = (M + R - 1) / R;
+  const int my_tiles = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= tiles)
+  for (int i = threadIdx.x; i < H; i += THREADS) lb1[i] = b1[i];
+  for (int i = threadIdx.x; i < C; i += THREADS) lb2[i] = b2[i], lgam[i] = gamma[i];
+
+  const auto rw1 = rsrc(w1, (uint32_t)(H * C * 2)), rw2 = rsrc(w2, (uint32_t)(C * H * 2));
+  const auto ry = rsrc(y, (uint32_t)((size_t)M * C * 2));
+  const auto rx = rsrc(x, (uint32_t)((size_t)M * C * 4));
+  const auto rxo = rsrc(xo, (uint32_t)((size_t)M * C * 4));
+  const auto rgh = rsrc(TRAIN ? gh : nullptr, TRAIN ? (uint32_t)((size_t)M * H * 2) : 0u);
+  const auto ra = rsrc(TRAIN ? a : nullptr, TRAIN ? (uint32_t)((size_t)M * H * 2) : 0u);
+  // W1 chunk: rows [j0, j0 + 32) permuted (perm8), two k-blocks [32][64]; wave wid's piece = rows 8 wid .. + 7
+  const int p1 = 8 * wid + (lane >> 3);
+  const uint32_t v1 = (uint32_t)((perm8(p1) * C + (((lane & 7) ^ kswz(p1)) << 3)) * 2);
+  // W2 chunk: columns [j0, j0 + 32) of the 128 channel rows; wave wid's pieces = rows 16 wid + 64 h .. + 15
+  const int p2 = 16 * wid + (lane >> 2);
+  const uint32_t v2 = (uint32_t)((p2 * H + (((lane & 3) ^ w2swz(p2)) << 3)) * 2);
+  auto issue_w1 = [&](int q) {
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W1 + (q & 1) * W1B;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+  };
+  auto issue_w2 = [&](int q) {
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W2 + (q & 1) * W2B;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wid + 4 * h) * 1024);
+  };
+  // this wave's y fragments of tile t into its own region (rows past M, and tiles past the end, read as zeros)
+  char* ybuf = smem + OFF_Y + wid * YB;
+  auto issue_y = [&](int it) {
+    const int wrow = ((int)blockIdx.x + it * (int)gridDim.x) * R + wid * 16 * RF;
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = wrow + 16 * rf + ml;
+      const uint32_t vy = (it < my_tiles && m < M) ? (uint32_t)((m * C + 8 * gq) * 2) : OOB;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dma(ry, vy, (uint32_t)(64 * ks), ybuf + (rf * KS + ks) * 1024);
+    }
+  };
+  constexpr int S = TRAIN ? RF * 2 : 0;  // the dual epilogue's stores per chunk
+
+  issue_w1(0);
+  issue_w2(0);
+  issue_y(0);
+  vm_wait<0>();
+  __syncthreads();  // the per-channel vectors, chunk 0 and every wave's y of its first tile
+  int q = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    const int row0 = ((int)blockIdx.x + it * (int)gridDim.x) * R + wid * 16 * RF;
+    // y of this tile landed (issued at the previous tile's start: a whole tile of vector-memory instructions -- at
+    // least 16 chunks x (N1 + N2) -- is younger)
+    vm_wait<32>();
+    bf16x8 yf[RF][KS];
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) yf[rf][ks] = lds_frag(ybuf + (rf * KS + ks) * 1024 + lane * 16);
+    lgkm0();
+    issue_y(it + 1);
+    f32x4 acc2[CF][RF];
+#pragma unroll
+    for (int cf = 0; cf < CF; ++cf)
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) acc2[cf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 xr[RF][CF];
+
+    for (int ch = 0; ch < NCH; ++ch, ++q) {
+      // X_q: W1(q) landed.  Younger than it (issued after the previous X barrier): that chunk's stores and W2(q);
+      // across a tile boundary also the x loads, the x_out stores and this tile's y prefetch
+      if (ch == 0) vm_wait<XL + S + N2 + XO + YP>();
+      else vm_wait<S + N2>();
+      lgkm0();
+      bar();
+      issue_w1(q + 1);  // past the end: a harmless re-load of chunk 0 into the free slot (uniform counts)
+      if (ch == NCH - 1) {  // the epilogue's residual, a chunk ahead
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) {
+          const int m = row0 + 16 * rf + ml;
+#pragma unroll
+          for (int cf = 0; cf < CF; ++cf) {
+            const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + 16 * cf + 4 * gq) * 4) : OOB;
+            xr[rf][cf] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+          }
+        }
+      }
+      const char* st1 = smem + OFF_W1 + (q & 1) * W1B;
+      const int j0 = ch * HC;
+      float bia[8];
+      lds_f8(lb1 + j0 + 8 * gq, bia);
+      // fc1: h^T chunk [32 hidden (2 fragments, perm8 rows)] x [32 rows], k ascending
+      f32x4 acc1[2][RF];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) acc1[hf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const char* img = st1 + (ks >> 1) * (HC * 128);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const bf16x8 wf = frag_k(img, 16 * hf, ks & 1);
+#pragma unroll
+          for (int rf = 0; rf < RF; ++rf)
+            acc1[hf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf[rf][ks], acc1[hf][rf], 0, 0, 0);
+        }
+      }
+      // bias + GELU pair (v9's packed form); P = bf16 GELU(h), fc2's operand; both stored nt (read only by the backward)
+      bf16x8 pf[RF];
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) {
+        float v[8], o[8], o2[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc1[0][rf][r], v[4 + r] = acc1[1][rf][r];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v[w] += bia[w];
+#pragma unroll
+        for (int w = 0; w < 8; w += 2) {
+          const gelu_f2 hh = {v[w], v[w + 1]};
+          gelu_f2 ph, de;
+          gelu_parts2(hh, ph, de);
+          const gelu_f2 g = hh * ph;
+          o2[w] = g.x, o2[w + 1] = g.y;
+          if constexpr (TRAIN) {
+            const gelu_f2 dg = __builtin_elementwise_fma(hh, de, ph);
+            o[w] = dg.x, o[w + 1] = dg.y;
+          }
+        }
+        const u32x4 pk = pack8(o2);
+        pf[rf] = __builtin_bit_cast(bf16x8, pk);
+        if constexpr (TRAIN) {
+          const int m = row0 + 16 * rf + ml;
+          const uint32_t off = m < M ? (uint32_t)(((size_t)m * H + j0 + 8 * gq) * 2) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rgh, off, 0, kGradCpol);
+          __builtin_amdgcn_raw_buffer_store_b128(pk, ra, off, 0, kGradCpol);
+        } else {
+          (void)o;
+        }
+      }
+      // Y_q: W2(q) landed.  Younger (issued after the previous Y barrier): W1(q+1) and this chunk's stores; in a
+      // tile's first chunk also the x_out stores and the y prefetch, in its last the x loads
+      if (ch == 0) vm_wait<XO + YP + N1 + S>();
+      else if (ch == NCH - 1) vm_wait<N1 + XL + S>();
+      else vm_wait<N1 + S>();
+      lgkm0();
+      bar();
+      issue_w2(q + 1);
+      // fc2: acc2 += W2[:, chunk] . P^T, k (hidden) ascending
+      const char* st2 = smem + OFF_W2 + (q & 1) * W2B;
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        const bf16x8 wf = frag64(st2, 16 * cf);
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf)
+          acc2[cf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, pf[rf], acc2[cf][rf], 0, 0, 0);
+      }
+    }
+    // epilogue: x_out = gamma (.) (acc + b2) + x   (v9's gamma-residual arithmetic)
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = row0 + 16 * rf + ml;
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        const int c = 16 * cf + 4 * gq;
+        float bv[4], gv[4];
+        lds_f4x2(lb2 + c, lgam + c, bv, gv);
+        const uint32_t xw[4] = {xr[rf][cf].x, xr[rf][cf].y, xr[rf][cf].z, xr[rf][cf].w};
+        float o[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) o[w] = fmaf(gv[w], acc2[cf][rf][w] + bv[w], __uint_as_float(xw[w]));
+        const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + c) * 4) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]),
+                                                     __float_as_uint(o[2]), __float_as_uint(o[3])},
+                                               rxo, off, 0, 0);
+      }
+    }
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
+}
+
+template <bool TRAIN>
+static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                  const float* gamma, const float* x, float* xo, uint16_t* gh, uint16_t* a, int M, hipStream_t s) {
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(&mlp128_kernel<TRAIN>), LDS, s)) return rc;
+  const int tiles = (M + R - 1) / R;
+  const int slots = 2 * device_cus(s);
+  const int grid = tiles < slots ? tiles : slots;
+  mlp128_kernel<TRAIN><<<grid, THREADS, LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
+  return check_launch("sv_mlp_fwd");
+}
+}  // namespace c128
+
 template <int C, bool TRAIN>
 static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                   const float* gamma, const float* x, float* xo, uint16_t* gh, uint16_t* a, int M, hipStream_t s) {
@@ -338,6 +576,17 @@ static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const 
 
 }  // namespace mlp
 }  // namespace sv
+
+namespace {
+// SV_MLP128_V1=1: C = 128 on the general kernel (A/B runs)
+bool getenv_flag_mlp_v1() {
+  static const bool v = [] {
+    const char* e = getenv("SV_MLP128_V1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+}  // namespace
 
 extern "C" {
 
@@ -361,6 +610,9 @@ int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uin
   case CC:                                                                                                        \
     return tr ? mlp::launch<CC, true>(y, w1, b1, w2, b2, gamma, x, x_out, gelu_grad, gelu_out, m, s)              \
               : mlp::launch<CC, false>(y, w1, b1, w2, b2, gamma, x, x_out, nullptr, nullptr, m, s);
+  if (C == 128 && !getenv_flag_mlp_v1())
+    return tr ? mlp::c128::launch<true>(y, w1, b1, w2, b2, gamma, x, x_out, gelu_grad, gelu_out, m, s)
+              : mlp::c128::launch<false>(y, w1, b1, w2, b2, gamma, x, x_out, nullptr, nullptr, m, s);
   switch (C) {
     SV_MLP_CASE(128)
     SV_MLP_CASE(192)
