@@ -32,6 +32,7 @@ CLASSES = {
     "dw_wgrad": [("dwconv7_wgrad_ring_kernel<",)],
     "ln_bwd": [("ln_bwd_vec_kernel<",), ("ln_bwd_kernel<",)],
     "adamw": [("adamw_kernel",)],
+    "mlp_fused": [("mlp_fwd_kernel<",), ("mlp128_kernel<",)],
     "fold": [("reduce_pair_kernel",), ("reduce_partials_kernel",), ("reduce_multi_kernel",),
              ("layerscale_reduce_kernel",)],
 }
