@@ -60,6 +60,8 @@ PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsam
                "ln_bwd": "block LayerNorm backward (sv_layernorm_bwd)",
                "adamw": "fused AdamW over the flat buffers (+ bf16 shadow refresh)",
                "mlp_fused": "fused narrow-stage MLP forward (sv_mlp_fwd: fc1 -> GELU -> fc2 -> gamma -> + x, S1 / S2)",
+               "mlp_bwd_fused": "fused S1 MLP backward (sv_mlp_bwd: fc2 dgrad x GELU' -> fc1 dgrad -> LayerNorm "
+                                "backward + its weight / bias partials, C = 128)",
                "fold": "split-K / partial-sum folds (reduce_multi, reduce_pair, layer-scale fold): bytes = the slab "
                        "bytes they move, overhead of split-K rather than algorithmic work"}
 # step-time cost of the data-parallel CU reserve (SV_COMM_RESERVE_CUS, default 0 = none) measured at world 1
@@ -82,7 +84,7 @@ def comm_latency_samples():
         return None
 COMM_DELAY_MS = (float(os.environ.get("SV_COMM_DELAY_MS", "2.9")), float(os.environ.get("SV_COMM_DELAY_END_MS", "0.05")))
 # HBM-bound kernel classes timed by kernels.OpProbe (reported separately against 8 TB/s)
-OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "mlp_fused", "fold")
+OP_PROBE_KEYS = ("dw_fwd", "dw_bwd_data", "dw_wgrad", "ln_bwd", "adamw", "mlp_fused", "mlp_bwd_fused", "fold")
 
 
 def parse():

@@ -191,6 +191,21 @@ int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uin
                const float* gamma, const float* x, float* x_out, uint16_t* gelu_grad, uint16_t* gelu_out, int64_t M,
                int32_t C, sv_stream_t stream);
 
+/* Fused backward of the same block part at C = 128 (ConvNeXt-base S1): from d [M, C] bf16 (the bf16 copy of the
+ * gradient at the block output),
+ *   dh = bf16((d . w2t^T) (.) gelu_grad)        [M, 4C] bf16 (the fc1 weight gradient's operand)
+ *   dy = bf16(dh . w1t^T)                        kept on chip
+ *   dz = LayerNorm backward of dy over (z bf16 [M, C], mean, rstd [M], lnw [C])   [M, C] bf16
+ * and the LayerNorm weight / bias partial sums ln_part [2][P][C] (sum dy x^, sum dy; P = sv_mlp_bwd_nparts(M, C),
+ * fold with sv_reduce_partials_multi).  w2t = bf16(W2 gamma)^T [4C, C] and w1t = bf16(W1)^T [C, 4C]
+ * (sv_transpose_scale_bf16).  Replaces the fc2 data gradient (SV_EPI_MUL_AUX), the fc1 data gradient and
+ * sv_layernorm_bwd of the block: dh is bit for bit theirs, dz and the sums within f32 summation order.
+ * Every pointer 16-byte aligned; M * 4C * 2 < 2^31.                                                   */
+int sv_mlp_bwd_nparts(int64_t M, int32_t C);
+int sv_mlp_bwd(const uint16_t* d, const uint16_t* w2t, const uint16_t* gelu_grad, const uint16_t* w1t, const uint16_t* z,
+               const float* mean, const float* rstd, const float* lnw, uint16_t* dh, uint16_t* dz, float* ln_part,
+               int64_t M, int32_t C, sv_stream_t stream);
+
 /* ---- LayerNorm over the channel (last) dim -------------------------------------------------
  * Replaces timm LayerNorm / LayerNorm2d (eps 1e-6) on channels-last rows.
  * fwd: y = (x-mean)*rstd*w + b; saves mean/rstd [rows] (f32).
@@ -388,6 +403,10 @@ int sv_adamw_flat_dev(float* p, const float* g, float* m, float* v, uint16_t* p_
                       sv_stream_t stream);
 /* out[r][k] = bf16(W[r][k] * scale[r]): fc2 weight with the layer-scale gamma folded in, so the fc2
  * dgrad GEMM reads bf16 operands only.                                                              */
+/* out[c][r] = bf16(W[r][c] * (scale ? scale[r] : 1)) for W [rows, cols] f32: the transposed bf16 operand images of
+ * sv_mlp_bwd (scale = gamma for the fc2 weight, NULL for the fc1 weight).                             */
+int sv_transpose_scale_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,
+                            sv_stream_t stream);
 int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,
                        sv_stream_t stream);
 /* y = bf16(x) over n elements (weight shadows after load_state_dict / init).                       */

@@ -90,6 +90,7 @@ class _Tape:
     out_shape: tuple = ()
     wcache: dict = field(default_factory=dict)  # bf16 weight casts shared by forward and backward
     w2g: dict = field(default_factory=dict)  # bf16 (fc2 weight x gamma) per block, for the fc2 dgrad
+    wt: dict = field(default_factory=dict)  # (bf16 (W2 gamma)^T, bf16 W1^T) per block of the fused MLP backward
     w2g_ready: object = None  # event on the side stream after the last w2g
 
 
@@ -165,6 +166,10 @@ class ConvNeXtHip(nn.Module):
         # kernel (sv_mlp_fwd): the hidden activation never makes the HBM round trip between the two GEMMs; bit for
         # bit the two-GEMM path (SV_FUSED_MLP=0, A/B runs)
         self.fused_mlp = os.environ.get("SV_FUSED_MLP", "1") != "0"
+        # ... and its backward (C in kernels.MLP_BWD_FUSED_C, the bf16 lean side-stream backward): the fc2 data gradient
+        # (x GELU'), the fc1 data gradient and the LayerNorm backward as ONE kernel (sv_mlp_bwd): dh is not read back and
+        # dy never reaches HBM (SV_FUSED_MLP_BWD=0: the three kernels, A/B runs)
+        self.fused_mlp_bwd = os.environ.get("SV_FUSED_MLP_BWD", "1") != "0"
         self._init_weights()
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
@@ -243,12 +248,23 @@ class ConvNeXtHip(nn.Module):
             main = torch.cuda.current_stream()
             side = self._side_stream(main.device)
             blocks = [blk for st in self.stages for blk in st.blocks]
+            fused_b = {id(blk) for blk in blocks if self._fused_bwd(blk)}
             for blk in blocks:
-                tape.w2g[id(blk)] = torch.empty(blk.mlp.fc2.weight.shape, device=img.device, dtype=torch.bfloat16)
+                if id(blk) in fused_b:
+                    w1, w2 = blk.mlp.fc1.weight, blk.mlp.fc2.weight
+                    tape.wt[id(blk)] = (torch.empty(w2.shape[1], w2.shape[0], device=img.device, dtype=torch.bfloat16),
+                                        torch.empty(w1.shape[1], w1.shape[0], device=img.device, dtype=torch.bfloat16))
+                else:
+                    tape.w2g[id(blk)] = torch.empty(blk.mlp.fc2.weight.shape, device=img.device, dtype=torch.bfloat16)
             side.wait_event(main.record_event())
             with torch.cuda.stream(side):
                 for blk in blocks:
-                    K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach(), out=tape.w2g[id(blk)])
+                    if id(blk) in fused_b:
+                        w2t, w1t = tape.wt[id(blk)]
+                        K.transpose_scale_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach(), out=w2t)
+                        K.transpose_scale_bf16(blk.mlp.fc1.weight.detach(), None, out=w1t)
+                    else:
+                        K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach(), out=tape.w2g[id(blk)])
             tape.w2g_ready = side.record_event()
         if bf:
             # stem conv on MFMA: 4x4 patch rows (bf16, K padded to 64) x packed weight, then LayerNorm2d
@@ -329,6 +345,12 @@ class ConvNeXtHip(nn.Module):
         return feat, tape
 
     # -- backward ----------------------------------------------------------------------------------
+    def _fused_bwd(self, blk) -> bool:
+        """Whether this block's backward runs the fused fc2 -> fc1 -> LayerNorm data-gradient kernel (bf16 lean
+        side-stream schedule only: its operand images are made beside the forward)."""
+        return (self.fused_mlp_bwd and self.compute_bf16 and self.overlap_wgrad and self.lean_sync
+                and blk.conv_dw.weight.shape[0] in K.MLP_BWD_FUSED_C)
+
     def _side_stream(self, device) -> torch.cuda.Stream:
         """The weight-gradient side stream; CU-masked (never on the CUs reserved for RCCL, training/cumask.py) when
         StepEngine asks for it (comm_reserve_cus > 0 and SV_COMM_CU_MASK=1)."""
@@ -521,16 +543,29 @@ class ConvNeXtHip(nn.Module):
         x, z, y, mean, rstd, gh, a = saved
         B, H, W, C = x.shape
         M = B * H * W
-        w1 = self._w(blk.mlp.fc1.weight, cache)
-        w2g = tape.w2g.pop(id(blk), None)
-        if w2g is None:
-            w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+        wt = tape.wt.pop(id(blk), None)
         dh = torch.empty(M, 4 * C, device=d.device, dtype=torch.bfloat16)
-        K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True, policy=pol)
-        dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
-        K.linear_dgrad(dh, w1, out=dy, compute_bf16=True, policy=pol)
-        dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
-                                        db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
+        if wt is not None:
+            # fused: fc2 data gradient (x GELU') -> fc1 data gradient -> LayerNorm backward in one kernel
+            dz = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
+            part, P = K.mlp_bwd(dsrc, wt[0], gh, wt[1], z.view(M, C), mean, rstd, blk.norm.weight, dh=dh, dz=dz)
+            dw_ln, db_ln = g(blk.norm.weight), g(blk.norm.bias)
+
+            def ln_finish(record: bool = True, defer: list | None = None, _p=part, _n=P):
+                if defer is not None:
+                    defer += [(_p[0], dw_ln, _n, True), (_p[1], db_ln, _n, True)]
+                else:
+                    K.reduce_pair(_p[0], dw_ln, _p[1], db_ln, _n)
+        else:
+            w1 = self._w(blk.mlp.fc1.weight, cache)
+            w2g = tape.w2g.pop(id(blk), None)
+            if w2g is None:
+                w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
+            K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True, policy=pol)
+            dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
+            K.linear_dgrad(dh, w1, out=dy, compute_bf16=True, policy=pol)
+            dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                            db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
         side_cap = pol.grid_cap

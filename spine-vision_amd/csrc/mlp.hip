@@ -37,6 +37,7 @@ constexpr int HC = 64;
 #endif
 constexpr uint32_t OOB = 0x80000000u;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
@@ -90,6 +91,13 @@ __device__ __forceinline__ void lds_f4x2(const float* p0, const float* p1, float
                : "v"(a0), "v"(a1)
                : "memory");
   v0[0] = u.x, v0[1] = u.y, v0[2] = u.z, v0[3] = u.w, v1[0] = w.x, v1[1] = w.y, v1[2] = w.z, v1[3] = w.w;
+}
+__device__ __forceinline__ void lds_f4(const float* p, float (&v)[4]) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t u;
+  const uint32_t ad = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(u) : "v"(ad) : "memory");
+  v[0] = u.x, v[1] = u.y, v[2] = u.z, v[3] = u.w;
 }
 __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
@@ -340,6 +348,7 @@ constexpr int W2B = C * HC * 2;                 // [128][32] bf16 = 8 KiB
 constexpr int YB = RF * KS * 1024;              // one wave's y fragments, 8 KiB
 constexpr int OFF_W1 = 0, OFF_W2 = 2 * W1B, OFF_Y = OFF_W2 + 2 * W2B, OFF_P = OFF_Y + NW * YB;
 constexpr int LDS = OFF_P + (H + 2 * C) * 4;    // 67 KiB: two workgroups per CU
+constexpr int LDS_BWD = OFF_P + (C + NW * 2 * C) * 4;  // the backward: LayerNorm weight + per-wave partials
 // vector-memory instructions per wave: W1 / W2 pieces per chunk, y fragments per tile, x loads and x_out stores per tile
 constexpr int N1 = KB, N2 = 2, YP = RF * KS, XL = RF * CF, XO = RF * CF;
 
@@ -560,6 +569,280 @@ static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const 
   mlp128_kernel<TRAIN><<<grid, THREADS, LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
   return check_launch("sv_mlp_fwd");
 }
+// ---- fused backward of the same block part, C = 128: from the gradient at the block output d
+// (the bf16 copy of the gradient stream), in one kernel
+//     dh = (d . (W2 gamma)) (.) GELU'(h)          -> stored bf16 (the fc1 weight gradient's operand)
+//     dy = bf16(dh . W1)                           -> kept on chip (the C-wide accumulator)
+//     dz = LayerNorm backward of dy (bf16 z, mean, rstd, weight)  -> stored bf16;  per-wave partial sums of
+//          dy x^ and dy for the LayerNorm weight / bias gradients
+// -- the unfused path's fc2 data gradient (x GELU' epilogue), fc1 data gradient and LayerNorm backward: dh is not read
+// back, dy never reaches HBM.  Same skeleton as the forward kernel: the weight images are the transposed operands
+// (w2t = (W2 gamma)^T [512][128] in W1's layout, w1t = W1^T [128][512] in W2's), GELU'(h) is loaded a chunk ahead,
+// z / mean / rstd a chunk ahead of the epilogue.  dh and bf16(dy) are bit for bit the unfused GEMMs' (same MFMA,
+// operands and k order); dz and the partial sums differ from sv_layernorm_bwd only by f32 summation order.
+constexpr int MAX_BWD_WG = 512;  // the grid: min(tiles, 512) workgroups (two per CU), 4 partial rows each
+
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t, const uint16_t* __restrict__ gh,
+               const uint16_t* __restrict__ w1t, const uint16_t* __restrict__ z, const float* __restrict__ mean,
+               const float* __restrict__ rstd, const float* __restrict__ lnw, uint16_t* __restrict__ dh,
+               uint16_t* __restrict__ dz, float* __restrict__ lnpart, int M) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* llw = reinterpret_cast<float*>(smem + OFF_P);   // LayerNorm weight [C]
+  float* lacc = llw + C;                                  // per-wave partials [NW][2][C]
+  const int lane = threadIdx.x & 63, ml = lane & 15, gq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles = (M + R - 1) / R;
+  const int my_tiles = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= tiles)
+  for (int i = threadIdx.x; i < C; i += THREADS) llw[i] = lnw[i];
+  for (int i = threadIdx.x; i < NW * 2 * C; i += THREADS) lacc[i] = 0.f;
+
+  const auto rw1 = rsrc(w2t, (uint32_t)(H * C * 2)), rw2 = rsrc(w1t, (uint32_t)(C * H * 2));
+  const auto ry = rsrc(d, (uint32_t)((size_t)M * C * 2));
+  const auto rg = rsrc(gh, (uint32_t)((size_t)M * H * 2));
+  const auto rdh = rsrc(dh, (uint32_t)((size_t)M * H * 2));
+  const auto rz = rsrc(z, (uint32_t)((size_t)M * C * 2));
+  const auto rdz = rsrc(dz, (uint32_t)((size_t)M * C * 2));
+  const auto rmu = rsrc(mean, (uint32_t)((size_t)M * 4));
+  const auto rrs = rsrc(rstd, (uint32_t)((size_t)M * 4));
+  const int p1 = 8 * wid + (lane >> 3);
+  const uint32_t v1 = (uint32_t)((perm8(p1) * C + (((lane & 7) ^ kswz(p1)) << 3)) * 2);
+  const int p2 = 16 * wid + (lane >> 2);
+  const uint32_t v2 = (uint32_t)((p2 * H + (((lane & 3) ^ w2swz(p2)) << 3)) * 2);
+  auto issue_w1 = [&](int q) {
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W1 + (q & 1) * W1B;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+  };
+  auto issue_w2 = [&](int q) {
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W2 + (q & 1) * W2B;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wid + 4 * h) * 1024);
+  };
+  char* ybuf = smem + OFF_Y + wid * YB;
+  auto tile_row = [&](int it) { return ((int)blockIdx.x + it * (int)gridDim.x) * R + wid * 16 * RF; };
+  auto issue_y = [&](int it) {
+    const int wrow = tile_row(it);
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = wrow + 16 * rf + ml;
+      const uint32_t vy = (it < my_tiles && m < M) ? (uint32_t)((m * C + 8 * gq) * 2) : OOB;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dma(ry, vy, (uint32_t)(64 * ks), ybuf + (rf * KS + ks) * 1024);
+    }
+  };
+  // GELU'(h) of chunk q (tile it = q / NCH): lane -> row, 8 consecutive hidden units, loaded a chunk ahead (two
+  // chunks ahead in two alternating register sets measured slower: 444 vs 426 us at base S1)
+  u32x4 ghn[RF];
+  auto load_gh = [&](int q) {
+    const int it = q / NCH, j0 = (q % NCH) * HC, wrow = tile_row(it);
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = wrow + 16 * rf + ml;
+      const uint32_t off = (it < my_tiles && m < M) ? (uint32_t)(((size_t)m * H + j0 + 8 * gq) * 2) : OOB;
+      ghn[rf] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+    }
+  };
+  // vector-memory instructions per wave younger than each DMA a barrier waits for (cf. mlp128_kernel): GL GELU'
+  // loads and SD dh stores per chunk; per tile ZL z / mean / rstd loads, ZO dz stores
+  constexpr int GL = RF, SD = RF, ZL = RF * CF + 2 * RF, ZO = RF * CF;
+
+  issue_w1(0);
+  issue_w2(0);
+  issue_y(0);
+  vm_wait<0>();
+  load_gh(0);
+  __syncthreads();
+  int q = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    const int row0 = tile_row(it);
+    vm_wait<32>();  // this tile's d fragments (issued a tile ago)
+    bf16x8 yf[RF][KS];
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) yf[rf][ks] = lds_frag(ybuf + (rf * KS + ks) * 1024 + lane * 16);
+    lgkm0();
+    issue_y(it + 1);
+    f32x4 acc2[CF][RF];
+#pragma unroll
+    for (int cf = 0; cf < CF; ++cf)
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) acc2[cf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x2 zr[RF][CF];
+    float mu[RF], rs[RF];
+
+    for (int ch = 0; ch < NCH; ++ch, ++q) {
+#if defined(SV_MLPB_DIAG) && (SV_MLPB_DIAG & 2)
+      vm_wait<0>();
+#endif
+      // X_q: W1(q) (here (W2 gamma)^T) landed; younger: the previous chunk's GELU' loads and dh stores, W2(q); across
+      // a tile boundary also the z / mean / rstd loads, the dz stores and the d prefetch
+      if (ch == 0) vm_wait<GL + SD + N2 + ZL + ZO + YP>();
+      else vm_wait<GL + SD + N2>();
+      lgkm0();
+      bar();
+      issue_w1(q + 1);
+      u32x4 ghc[RF];
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) ghc[rf] = ghn[rf];
+      load_gh(q + 1);
+      if (ch == NCH - 1) {  // the LayerNorm backward's operands, a chunk ahead
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) {
+          const int m = row0 + 16 * rf + ml;
+#pragma unroll
+          for (int cf = 0; cf < CF; ++cf) {
+            const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + 16 * cf + 4 * gq) * 2) : OOB;
+            zr[rf][cf] = __builtin_amdgcn_raw_buffer_load_b64(rz, off, 0, 0);
+          }
+          const uint32_t mo = m < M ? (uint32_t)(m * 4) : OOB;
+          mu[rf] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmu, mo, 0, 0));
+          rs[rf] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, mo, 0, 0));
+        }
+      }
+      const char* st1 = smem + OFF_W1 + (q & 1) * W1B;
+      const int j0 = ch * HC;
+      // stage 1: dA^T chunk [32 hidden (perm8)] x [32 rows] = (W2 gamma)^T . d^T, k (channels) ascending
+      f32x4 acc1[2][RF];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) acc1[hf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const char* img = st1 + (ks >> 1) * (HC * 128);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const bf16x8 wf = frag_k(img, 16 * hf, ks & 1);
+#pragma unroll
+          for (int rf = 0; rf < RF; ++rf)
+            acc1[hf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf[rf][ks], acc1[hf][rf], 0, 0, 0);
+        }
+      }
+      // dh = dA (.) GELU'(h) (the x GELU' epilogue's arithmetic), stored bf16; the packed value is stage 2's operand
+      bf16x8 pf[RF];
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf) {
+        const uint32_t wd[4] = {ghc[rf].x, ghc[rf].y, ghc[rf].z, ghc[rf].w};
+        float o[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = acc1[0][rf][r] * __uint_as_float((r & 1) ? (wd[r >> 1] & 0xffff0000u) : (wd[r >> 1] << 16));
+          o[4 + r] = acc1[1][rf][r] * __uint_as_float(((4 + r) & 1) ? (wd[(4 + r) >> 1] & 0xffff0000u)
+                                                                      : (wd[(4 + r) >> 1] << 16));
+        }
+        const u32x4 pk = pack8(o);
+        pf[rf] = __builtin_bit_cast(bf16x8, pk);
+        const int m = row0 + 16 * rf + ml;
+        const uint32_t off = m < M ? (uint32_t)(((size_t)m * H + j0 + 8 * gq) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(pk, rdh, off, 0, 0);
+      }
+      // Y_q: W2(q) (here W1^T) landed; younger: W1(q+1), the GELU' loads, this chunk's dh stores; in a tile's first
+      // chunk also the dz stores and the d prefetch, in its last the LayerNorm operand loads
+      if (ch == 0) vm_wait<ZO + YP + N1 + GL + SD>();
+      else if (ch == NCH - 1) vm_wait<N1 + GL + ZL + SD>();
+      else vm_wait<N1 + GL + SD>();
+      lgkm0();
+      bar();
+      issue_w2(q + 1);
+      // stage 2: dy^T += W1^T[:, chunk] . dh^T, k (hidden) ascending
+      const char* st2 = smem + OFF_W2 + (q & 1) * W2B;
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        const bf16x8 wf = frag64(st2, 16 * cf);
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf)
+          acc2[cf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, pf[rf], acc2[cf][rf], 0, 0, 0);
+      }
+    }
+#if defined(SV_MLPB_DIAG) && (SV_MLPB_DIAG & 1)
+    vm_wait<0>();
+#endif
+    // the z / mean / rstd loads (last chunk): younger only that chunk's dh stores and the W2 DMA.  Explicit: the
+    // compiler's own wait here was short (tools/mlp_bwd_diag.py: dz / dw differed run to run at M = 524288 without it)
+    vm_wait<SD + N2>();
+    float* la = lacc + wid * 2 * C;
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+      const int m = row0 + 16 * rf + ml;
+      auto dyv = [&](int cf, int w) { return __uint_as_float((uint32_t)f2bf(acc2[cf][rf][w]) << 16); };
+      auto xhat = [&](int cf, int w) {
+        const uint32_t zw = w < 2 ? zr[rf][cf].x : zr[rf][cf].y;
+        const float zz = __uint_as_float((w & 1) ? (zw & 0xffff0000u) : (zw << 16));
+        return (zz - mu[rf]) * rs[rf];
+      };
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        float lw[4];
+        lds_f4(llw + 16 * cf + 4 * gq, lw);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float g = dyv(cf, w) * lw[w];
+          s1 += g;
+          s2 += g * xhat(cf, w);
+        }
+      }
+      s1 += __shfl_xor(s1, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 16);
+      s2 += __shfl_xor(s2, 32);
+      s1 *= 1.0f / (float)C;
+      s2 *= 1.0f / (float)C;
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) {
+        float lw[4], o[4], pw[4], pb[4];
+        lds_f4(llw + 16 * cf + 4 * gq, lw);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float dv = dyv(cf, w), xh = xhat(cf, w);
+          o[w] = rs[rf] * (dv * lw[w] - s1 - xh * s2);
+          pw[w] = dv * xh;
+          pb[w] = dv;
+        }
+        const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + 16 * cf + 4 * gq) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])}, rdz, off, 0, 0);
+        // the LayerNorm weight / bias partials of these 4 channels over the 16 rows of the fragment (fixed xor order);
+        // lane ml == 0 adds them into the wave's own LDS row (one writer per word: deterministic)
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+          for (int sh = 1; sh < 16; sh <<= 1) {
+            pw[w] += __shfl_xor(pw[w], sh);
+            pb[w] += __shfl_xor(pb[w], sh);
+          }
+        if (ml == 0) {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            la[16 * cf + 4 * gq + w] += pw[w];
+            la[C + 16 * cf + 4 * gq + w] += pb[w];
+          }
+        }
+      }
+    }
+  }
+  vm_wait<0>();
+  __syncthreads();
+  // the workgroup's 4 wave partials -> lnpart [2][gridDim.x * NW][C]
+  const int np = (int)gridDim.x * NW;
+  for (int i = threadIdx.x; i < NW * 2 * C; i += THREADS) {
+    const int wv = i / (2 * C), k = (i / C) & 1, c = i % C;
+    lnpart[((size_t)k * np + (size_t)blockIdx.x * NW + wv) * C + c] = lacc[i];
+  }
+}
+
+static int launch_bwd(const uint16_t* d, const uint16_t* w2t, const uint16_t* gh, const uint16_t* w1t, const uint16_t* z,
+                      const float* mean, const float* rstd, const float* lnw, uint16_t* dh, uint16_t* dz, float* lnpart,
+                      int M, hipStream_t s) {
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(&mlpb128_kernel), LDS_BWD, s)) return rc;
+  const int tiles = (M + R - 1) / R;
+  const int grid = tiles < MAX_BWD_WG ? tiles : MAX_BWD_WG;
+  mlpb128_kernel<<<grid, THREADS, LDS_BWD, s>>>(d, w2t, gh, w1t, z, mean, rstd, lnw, dh, dz, lnpart, M);
+  return check_launch("sv_mlp_bwd");
+}
 }  // namespace c128
 
 template <int C, bool TRAIN>
@@ -620,6 +903,26 @@ int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uin
   }
 #undef SV_MLP_CASE
   return set_error(SV_ERR_INVALID_ARG, "sv_mlp_fwd: C = %d not supported", C);
+}
+
+int sv_mlp_bwd_nparts(int64_t M, int32_t C) {
+  if (C != 128 || M <= 0) return 0;
+  const int64_t tiles = (M + sv::mlp::c128::R - 1) / sv::mlp::c128::R;
+  return (int)((tiles < sv::mlp::c128::MAX_BWD_WG ? tiles : sv::mlp::c128::MAX_BWD_WG) * sv::mlp::c128::NW);
+}
+
+int sv_mlp_bwd(const uint16_t* d, const uint16_t* w2t, const uint16_t* gelu_grad, const uint16_t* w1t, const uint16_t* z,
+               const float* mean, const float* rstd, const float* lnw, uint16_t* dh, uint16_t* dz, float* ln_part,
+               int64_t M, int32_t C, sv_stream_t stream) {
+  using namespace sv;
+  SV_REQUIRE(d && w2t && gelu_grad && w1t && z && mean && rstd && lnw && dh && dz && ln_part, "sv_mlp_bwd: null pointer");
+  SV_REQUIRE(C == 128, "sv_mlp_bwd: C = %d not supported (128)", C);
+  SV_REQUIRE(M > 0 && M * 4 * C * 2 < 0x7fffffffLL, "sv_mlp_bwd: M out of range (the hidden tensor must be < 2 GiB)");
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  SV_REQUIRE(al(d) && al(w2t) && al(gelu_grad) && al(w1t) && al(z) && al(mean) && al(rstd) && al(lnw) && al(dh) &&
+                 al(dz) && al(ln_part),
+             "sv_mlp_bwd: every pointer must be 16-B aligned");
+  return mlp::c128::launch_bwd(d, w2t, gelu_grad, w1t, z, mean, rstd, lnw, dh, dz, ln_part, (int)M, (hipStream_t)stream);
 }
 
 }  // extern "C"

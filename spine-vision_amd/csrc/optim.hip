@@ -460,6 +460,25 @@ __global__ void __launch_bounds__(kThreads) scale_rows_bf16_kernel(const float* 
     out[i] = f2bf(W[i] * scale[i / cols]);
 }
 
+// out[c][r] = bf16(W[r][c] * (scale ? scale[r] : 1)): the transposed bf16 operand images of the fused MLP backward
+// (W2 gamma and W1); 32 x 32 tiles through LDS so both the reads and the writes are row-contiguous
+__global__ void __launch_bounds__(256) transpose_scale_bf16_kernel(const float* __restrict__ W,
+                                                                   const float* __restrict__ scale,
+                                                                   uint16_t* __restrict__ out, int rows, int cols) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    t[k][tx] = (r < rows && c < cols) ? W[(size_t)r * cols + c] * (scale ? scale[r] : 1.0f) : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (c < cols && r < rows) out[(size_t)c * rows + r] = f2bf(t[tx][k]);
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) cast_bf16_kernel(const float* __restrict__ x,
                                                              uint16_t* __restrict__ y, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -700,6 +719,14 @@ int sv_scale_rows_bf16(const float* W, const float* scale, uint16_t* out, int32_
   scale_rows_bf16_kernel<<<stream_grid((int64_t)rows * cols, 1), kThreads, 0, (hipStream_t)stream>>>(W, scale, out,
                                                                                                       rows, cols);
   return check_launch("sv_scale_rows_bf16");
+}
+
+int sv_transpose_scale_bf16(const float* W, const float* scale, uint16_t* out, int32_t rows, int32_t cols,
+                            sv_stream_t stream) {
+  SV_REQUIRE(W && out && rows > 0 && cols > 0, "sv_transpose_scale_bf16: bad args");
+  const dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+  transpose_scale_bf16_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(W, scale, out, rows, cols);
+  return check_launch("sv_transpose_scale_bf16");
 }
 
 int sv_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, sv_stream_t stream) {

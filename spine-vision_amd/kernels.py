@@ -269,6 +269,47 @@ def mlp_fwd(y, w1, b1, w2, b2, gamma, x, *, out, gelu_grad=None, gelu_out=None):
     return out
 
 
+def transpose_scale_bf16(W: torch.Tensor, scale: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """bf16(W * scale[:, None])^T for a 2-D f32 weight [R, C] -> [C, R] bf16 (the operand images of mlp_bwd)."""
+    R_, C_ = W.shape
+    _check(W.dtype == torch.float32 and W.is_contiguous(), "transpose_scale_bf16: need contiguous f32")
+    _check(scale is None or (scale.numel() == R_ and scale.dtype == torch.float32), "transpose_scale_bf16: bad scale")
+    if out is None:
+        out = torch.empty(C_, R_, device=W.device, dtype=torch.bfloat16)
+    _check(tuple(out.shape) == (C_, R_) and out.dtype == torch.bfloat16 and out.is_contiguous(),
+           "transpose_scale_bf16: bad out")
+    call("sv_transpose_scale_bf16", ptr(W), ptr(scale), ptr(out), R_, C_)
+    return out
+
+
+MLP_BWD_FUSED_C = (128,)
+
+
+def mlp_bwd(d, w2t, gelu_grad, w1t, z, mean, rstd, lnw, *, dh, dz):
+    """Fused backward of fc2 (x GELU') -> fc1 -> LayerNorm of a ConvNeXt block at C = 128 (sv_mlp_bwd): dh (bf16
+    [M, 4C], bit for bit linear_dgrad(d, W2 gamma, x GELU')), dz (bf16 [M, C], the LayerNorm backward of bf16(dh W1)).
+    Returns the LayerNorm weight / bias partial sums (ln_part [2][P][C] f32) and P, to fold into dw / db."""
+    M, C = d.shape
+    H = 4 * C
+    _check(C in MLP_BWD_FUSED_C, f"mlp_bwd: C = {C} not supported {MLP_BWD_FUSED_C}")
+    for t_, shp in ((d, (M, C)), (w2t, (H, C)), (gelu_grad, (M, H)), (w1t, (C, H)), (z, (M, C)), (dh, (M, H)),
+                    (dz, (M, C))):
+        _check(t_.dtype == torch.bfloat16 and t_.numel() == shp[0] * shp[1] and t_.is_contiguous(),
+               f"mlp_bwd: bf16 [{shp[0]}, {shp[1]}] operand expected")
+    for t_, n_ in ((mean, M), (rstd, M), (lnw, C)):
+        _check(t_.dtype == torch.float32 and t_.numel() == n_ and t_.is_contiguous(), "mlp_bwd: f32 vector")
+    P = value("sv_mlp_bwd_nparts", M, C)
+    part = torch.empty(2, P, C, device=d.device, dtype=torch.float32)
+    ts = [d, w2t, gelu_grad, w1t, z, mean, rstd, lnw, dh, dz, part]
+    _check(all(t_.data_ptr() % 16 == 0 for t_ in ts), "mlp_bwd: 16-B aligned tensors")
+    _check(M * H * 2 < 2**31, "mlp_bwd: hidden tensor must be < 2 GiB")
+    # algorithmic: d, GELU'(h), z read; dh, dz written; both weights, mean / rstd once
+    nb = M * (C * 2 + H * 2 + C * 2 + H * 2 + C * 2 + 8) + 2 * H * C * 2
+    _timed_call("mlp_bwd_fused", nb, "sv_mlp_bwd", ptr(d), ptr(w2t), ptr(gelu_grad), ptr(w1t), ptr(z), ptr(mean),
+                ptr(rstd), ptr(lnw), ptr(dh), ptr(dz), ptr(part), M, C, flops=4.0 * M * C * H)
+    return part, P
+
+
 _WGRAD_TARGET = 512  # workgroups per split-K wgrad launch (2 per CU)
 # persistent 256x256 wgrads: tiles x split ~ this many workgroups (SV_WGRAD9_WGS for A/B runs).  Half the chip
 # (128): the side-stream weight gradients share it with the main stream's data gradients anyway, and half the

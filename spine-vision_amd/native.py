@@ -112,6 +112,9 @@ _SIGS = {
     "sv_gemm_slab_finish": [_p, _i32, _i32, _i32, _p, _i32, _i64, _i32, _p, _p],
     "sv_gemm_slab_finish_bn_bwd": [_p, _i32, _i32, _i32, _p, _p, ctypes.POINTER(BnRef), _p, _p],
     "sv_mlp_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _p],
+    "sv_mlp_bwd_nparts": [_i64, _i32],
+    "sv_mlp_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _p],
+    "sv_transpose_scale_bf16": [_p, _p, _p, _i32, _i32, _p],
     "sv_layernorm_fwd": [_p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _f32, _p],
     "sv_layernorm_bwd_nparts": [_i64, _i32],
     "sv_layernorm_bwd": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _i64, _i32, _p],

@@ -39,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", default="base-S1,base-S2,large-S1")
+    ap.add_argument("--bwd", action="store_true", help="also the fused backward (C = 128) against its three kernels")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
@@ -55,6 +56,8 @@ def main():
         xo = torch.empty(M, C, device=dev)
         gh = torch.empty(M, H, device=dev, dtype=bf)
         a = torch.empty(M, H, device=dev, dtype=bf)
+        if args.bwd and C in K.MLP_BWD_FUSED_C:
+            bwd_case(name, M, C, args.iters, dev)
         for train in (True, False):
             nb = M * C * 10 + (2 * M * H * 2 if train else 0)
             floor = nb / HBM * 1e6
@@ -72,6 +75,33 @@ def main():
             print(f"{name:9s} {'train' if train else 'eval ':5s} fused {tf:7.1f} us ({nb / tf / 1e3:6.0f} GB/s, "
                   f"{fl / tf / 1e6:6.0f} TF/s) | fc1 {t1:6.1f} + fc2 {t2:6.1f} = {t1 + t2:6.1f} us | HBM floor "
                   f"{floor:6.1f} us", flush=True)
+
+
+def bwd_case(name, M, C, iters, dev):
+    bf = torch.bfloat16
+    H = 4 * C
+    d = (torch.randn(M, C, device=dev) * 0.1).to(bf)
+    w1 = torch.randn(H, C, device=dev) * 0.08
+    w2 = torch.randn(C, H, device=dev) * 0.05
+    gam = torch.rand(C, device=dev) * 0.25 + 0.05
+    gh = (torch.rand(M, H, device=dev) * 1.2 - 0.1).to(bf)
+    z = torch.randn(M, C, device=dev).to(bf)
+    mean = z.float().mean(1)
+    rstd = 1.0 / torch.sqrt(z.float().var(1, unbiased=False) + 1e-6)
+    lnw = torch.rand(C, device=dev) + 0.5
+    w2t, w1t = K.transpose_scale_bf16(w2, gam), K.transpose_scale_bf16(w1)
+    w2g, w1b = K.scale_rows_bf16(w2, gam), K.cast_bf16(w1)
+    dh = torch.empty(M, H, device=dev, dtype=bf)
+    dz = torch.empty(M, C, device=dev, dtype=bf)
+    dy = torch.empty(M, C, device=dev, dtype=bf)
+    dw, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    tf = timed(lambda: K.mlp_bwd(d, w2t, gh, w1t, z, mean, rstd, lnw, dh=dh, dz=dz), iters)
+    t1 = timed(lambda: K.linear_dgrad(d, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh), iters)
+    t2 = timed(lambda: K.linear_dgrad(dh, w1b, out=dy), iters)
+    t3 = timed(lambda: K.layernorm_bwd(dy, z, mean, rstd, lnw, dw=dw, db=db, out_dtype=bf), iters)
+    nb = M * (C * 2 + H * 2 + C * 2 + H * 2 + C * 2 + 8)
+    print(f"{name:9s} bwd   fused {tf:7.1f} us ({nb / tf / 1e3:6.0f} GB/s) | fc2 dgrad {t1:6.1f} + fc1 dgrad {t2:6.1f} + "
+          f"ln bwd {t3:6.1f} = {t1 + t2 + t3:6.1f} us | HBM floor {nb / HBM * 1e6:6.1f} us", flush=True)
 
 
 if __name__ == "__main__":

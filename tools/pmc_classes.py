@@ -33,6 +33,7 @@ CLASSES = {
     "ln_bwd": [("ln_bwd_vec_kernel<",), ("ln_bwd_kernel<",)],
     "adamw": [("adamw_kernel",)],
     "mlp_fused": [("mlp_fwd_kernel<",), ("mlp128_kernel<",)],
+    "mlp_bwd_fused": [("mlpb128_kernel",)],
     "fold": [("reduce_pair_kernel",), ("reduce_partials_kernel",), ("reduce_multi_kernel",),
              ("layerscale_reduce_kernel",)],
 }
