@@ -166,6 +166,9 @@ class ConvNeXtHip(nn.Module):
         # kernel (sv_mlp_fwd): the hidden activation never makes the HBM round trip between the two GEMMs; bit for
         # bit the two-GEMM path (SV_FUSED_MLP=0, A/B runs)
         self.fused_mlp = os.environ.get("SV_FUSED_MLP", "1") != "0"
+        # the fused-MLP channel widths in use: S1 / S2 (and -large S1); the C = 512 kernel (S3) measured slower than the
+        # two GEMMs and stays opt-in (SV_FUSED_MLP_C=128,192,256,512; csrc/mlp.hip c512)
+        self.fused_mlp_c = tuple(int(c) for c in os.environ.get("SV_FUSED_MLP_C", "128,192,256").split(",") if c)
         # ... and its backward (C in kernels.MLP_BWD_FUSED_C, the bf16 lean side-stream backward): the fc2 data gradient
         # (x GELU'), the fc1 data gradient and the LayerNorm backward as ONE kernel (sv_mlp_bwd): dh is not read back and
         # dy never reaches HBM (SV_FUSED_MLP_BWD=0: the three kernels, A/B runs)
@@ -303,7 +306,7 @@ class ConvNeXtHip(nn.Module):
                                                     blk.norm.bias, act_dtype=act)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 w2 = self._w(blk.mlp.fc2.weight, cache)
-                if bf and self.fused_mlp and C in K.MLP_FUSED_C:
+                if bf and self.fused_mlp and C in K.MLP_FUSED_C and C in self.fused_mlp_c:
                     # fused MLP: the training forward stores GELU'(h) and GELU(h) for the backward, the eval one nothing
                     xo = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
                     gh = torch.empty(M, 4 * C, device=x.device, dtype=act) if save else None

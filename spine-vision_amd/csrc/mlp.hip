@@ -845,6 +845,308 @@ static int launch_bwd(const uint16_t* d, const uint16_t* w2t, const uint16_t* gh
 }
 }  // namespace c128
 
+// ---- C = 512 (ConvNeXt-base S3: 27 blocks of 32768 rows at bs32).  A wave's C-wide fc2 accumulator and its y
+// fragments grow with rows x C: at C = 512 a 16-row wave needs 128 + 64 registers, so at two waves per SIMD a wave
+// holds 16 rows and every W fragment it reads from LDS feeds ONE MFMA (the LDS array at its 256 B/clk at full MFMA
+// rate).  Here fc1 and fc2 split the tile differently: in fc1 each of the 8 waves computes its own 16 rows (y in
+// registers, one MFMA per W1 fragment); its GELU(h) chunk (16 rows x 32 hidden, already in the MFMA operand layout)
+// goes through an LDS slot of its own; in fc2 the wave pair (2 rg, 2 rg + 1) shares rows 32 rg .. + 31 and each
+// takes half the 512 channels, so every W2 fragment feeds two MFMAs (32 rows) against a 16 x 2 fragment
+// accumulator: 50 instead of 64 KiB of LDS reads per wave and chunk.  Chunks of 32 hidden units (W1 image [8][32][64],
+// W2 image [512][32] with 64-B rows), double-buffered by group A's LDS-DMA; waves 4-7 one barrier behind (their GELU
+// beside the others' MFMAs, as the general kernel).  Operands, k order and epilogue arithmetic are v9's: bit for bit
+// the two-GEMM path.  MEASURED SLOWER than the two GEMMs (r10o / r10p, tools/mlp_bench.py base-S3: train 231 vs 191 us,
+// eval 188 vs 160; with the GELU, the weight DMA and the barriers all compiled out still 164 us in eval against a
+// 55 us MFMA floor: one W1 fragment per MFMA in fc1 and a 3-deep read pipeline at 256 VGPRs leave the LDS latency
+// exposed), so the host leaves it off (convnext.py fused_mlp_c; SV_FUSED_MLP_C=128,192,256,512 turns it on).
+namespace c512 {
+constexpr int C = 512, H = 2048, HC = 32, NCH = H / HC, KB = C / 64, KS = C / 32, NW = 8, THREADS = 512;
+constexpr int CF2 = C / 2 / 16;                 // fc2 output fragments per wave (its half of the channels)
+constexpr int R = NW * 16;                      // 128 rows per tile
+constexpr int W1B = KB * HC * 128;              // [8][32][64] bf16 = 32 KiB
+constexpr int W2B = C * HC * 2;                 // [512][32] bf16 = 32 KiB
+constexpr int OFF_W1 = 0, OFF_W2 = 2 * W1B, OFF_PB = OFF_W2 + 2 * W2B, OFF_P = OFF_PB + NW * 1024;
+constexpr int LDS = OFF_P + (H + 2 * C) * 4;    // 148 KiB: one workgroup per CU
+constexpr int N1 = KB, N2 = C / 64;             // DMA pieces per group-A wave per chunk: W1, W2
+using c128::frag64;
+using c128::w2swz;
+using c128::lds_frag;
+// the lane id from an asm statement the compiler cannot hoist: the per-lane offsets derived from it inside the chunk
+// loop are recomputed each chunk (a few VALU) instead of held across it -- at 256 VGPRs the held ones were spilled
+// and their reloads waited vmcnt(0), draining the weight DMA every chunk
+__device__ __forceinline__ int lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+__device__ __forceinline__ bf16x8 frag_k_l(const char* __restrict__ region, int base, int kh, int l) {
+  const int row = base + (l & 15), ch = kh * 4 + (l >> 4);
+  return *reinterpret_cast<const bf16x8*>(region + row * 128 + ((ch ^ kswz(row)) << 4));
+}
+__device__ __forceinline__ bf16x8 frag64_l(const char* __restrict__ region, int base, int l) {
+  const int row = base + (l & 15);
+  return *reinterpret_cast<const bf16x8*>(region + row * 64 + (((l >> 4) ^ w2swz(row)) << 4));
+}
+// LDS fragment reads software-pipelined by hand: at 256 VGPRs the compiler issues each read right before its MFMA
+// (ds_read; s_waitcnt lgkmcnt(0); MFMA).  Inline-asm ds_read_b128 (the compiler inserts no wait for them) PD reads
+// ahead; before a fragment's MFMAs a counted lgkmcnt wait that takes the fragment as an in/out operand, so the MFMA
+// cannot be scheduled above it.  LDS reads return in order: lgkmcnt(n) = at most the n younger reads outstanding.
+constexpr int PD = 4;
+__device__ __forceinline__ bf16x8 ds_frag(uint32_t ad) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t u;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(u) : "v"(ad) : "memory");
+  return __builtin_bit_cast(bf16x8, u);
+}
+template <int N>
+__device__ __forceinline__ void lgkm_dep(bf16x8& f) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f) : "n"(N));
+}
+// fragment i of an L-read sequence issued PD ahead: younger reads outstanding min(PD - 1, L - 1 - i)
+__device__ __forceinline__ void wait_frag(bf16x8& f, int i, int L) {
+  const int n = L - 1 - i < PD - 1 ? L - 1 - i : PD - 1;
+  if (n >= 3) lgkm_dep<3>(f);
+  else if (n == 2) lgkm_dep<2>(f);
+  else if (n == 1) lgkm_dep<1>(f);
+  else lgkm_dep<0>(f);
+}
+static_assert(PD == 4, "wait_frag's ladder");
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+}
+__device__ __forceinline__ void lds_st16(char* p, u32x4 v) {  // LDS store the compiler does not see (see lds_f8)
+  const uint32_t ad = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_write_b128 %0, %1" : : "v"(ad), "v"(v) : "memory");
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mlp512_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+              const uint16_t* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
+              const float* __restrict__ x, float* __restrict__ xo, uint16_t* __restrict__ gh, uint16_t* __restrict__ a,
+              int M) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lb1 = reinterpret_cast<float*>(smem + OFF_P);
+  float* lb2 = lb1 + H;
+  float* lgam = lb2 + C;
+  const int lane = threadIdx.x & 63, ml = lane & 15, gq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wid >> 2, wa = wid & 3, rg = wid >> 1, chh = wid & 1;
+  const int tiles = (M + R - 1) / R;
+  const int my_tiles = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= tiles)
+  const int total = my_tiles * NCH;
+  for (int i = threadIdx.x; i < H; i += THREADS) lb1[i] = b1[i];
+  for (int i = threadIdx.x; i < C; i += THREADS) lb2[i] = b2[i], lgam[i] = gamma[i];
+
+  const auto rw1 = rsrc(w1, (uint32_t)(H * C * 2)), rw2 = rsrc(w2, (uint32_t)(C * H * 2));
+  const auto ry = rsrc(y, (uint32_t)((size_t)M * C * 2));
+  const auto rx = rsrc(x, (uint32_t)((size_t)M * C * 4));
+  const auto rxo = rsrc(xo, (uint32_t)((size_t)M * C * 4));
+  const auto rgh = rsrc(TRAIN ? gh : nullptr, TRAIN ? (uint32_t)((size_t)M * H * 2) : 0u);
+  const auto ra = rsrc(TRAIN ? a : nullptr, TRAIN ? (uint32_t)((size_t)M * H * 2) : 0u);
+  // W1 chunk: rows [j0, j0 + 32) permuted (perm8), 8 k-blocks [32][64]; A-wave wa's piece of each = rows 8 wa .. + 7
+  // W2 chunk: columns [j0, j0 + 32) of the 512 channel rows; A-wave wa's pieces = rows 16 wa + 64 h .. + 15
+  auto issue_w1 = [&](int q) {
+    const int ln = lane_id();
+    const int p1 = 8 * wa + (ln >> 3);
+    const uint32_t v1 = (uint32_t)((perm8(p1) * C + (((ln & 7) ^ kswz(p1)) << 3)) * 2);
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W1 + (q & 1) * W1B;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wa * 1024);
+  };
+  auto issue_w2 = [&](int q) {
+    const int ln = lane_id();
+    const int p2 = 16 * wa + (ln >> 2);
+    const uint32_t v2 = (uint32_t)((p2 * H + (((ln & 3) ^ w2swz(p2)) << 3)) * 2);
+    const int j0 = (q % NCH) * HC;
+    char* st = smem + OFF_W2 + (q & 1) * W2B;
+#pragma unroll
+    for (int h = 0; h < N2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wa + 4 * h) * 1024);
+  };
+  // P slots: this wave's GELU(h) chunk (register image) at OFF_PB + 1 KiB wid; the pair's two at 1 KiB (2 rg + rf)
+  constexpr int S = TRAIN ? 2 : 0;  // the dual epilogue's stores per chunk
+
+  if (grp == 0) {
+    issue_w1(0);
+    issue_w2(0);
+  }
+  int q = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    const int t0 = ((int)blockIdx.x + it * (int)gridDim.x) * R;
+    const int row1 = t0 + 16 * wid;  // fc1 rows of this wave
+    bf16x8 yf[KS];
+    {
+      const int m = row1 + ml;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint32_t off = m < M ? (uint32_t)((m * C + 32 * ks + 8 * gq) * 2) : OOB;
+        yf[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
+      }
+    }
+    // everything in flight lands here, once per tile: y, chunk 0's weights (group A), the previous tile's x_out
+    vm_wait<0>();
+    if (it == 0) {
+      __syncthreads();  // the per-channel vectors and chunk 0 (group A's DMA) for every wave
+      if (grp == 1) bar();  // group B one barrier behind
+    }
+    f32x4 acc2[CF2][2];
+#pragma unroll
+    for (int cf = 0; cf < CF2; ++cf)
+#pragma unroll
+      for (int rf = 0; rf < 2; ++rf) acc2[cf][rf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int ch = 0; ch < NCH; ++ch, ++q) {
+      // X_q: W1(q) landed (A: issued after X_{q-1}; younger: chunk q-1's stores, W2(q)'s pieces)
+      if (grp == 0 && ch > 0) vm_wait<S + N2>();
+      lgkm0();
+      if (!(SV_MLP_DIAG & 4)) bar();
+      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
+      const int ln = lane_id();
+      const char* st1 = smem + OFF_W1 + (q & 1) * W1B;
+      const int j0 = ch * HC;
+      // fc1: h^T chunk [32 hidden (2 fragments, perm8 rows)] x [16 rows], k ascending
+      f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      {
+        // fragment i = (ks, hf) = (i >> 1, i & 1): frag_k(st1 + (ks >> 1) * 4 KiB, 16 hf, ks & 1); row 16 hf + (l & 15)
+        // has the swizzle of row l & 15 (kswz ignores bit 4)
+        const int r = ln & 15, sw = kswz(r);
+        const uint32_t b1a = lds_addr(st1) + (uint32_t)(r * 128);
+        const uint32_t c0 = (uint32_t)((((ln >> 4)) ^ sw) << 4), c1 = (uint32_t)(((4 + (ln >> 4)) ^ sw) << 4);
+        auto rd = [&](int i) {
+          return ds_frag(b1a + (uint32_t)((i >> 2) * (HC * 128) + (i & 1) * (16 * 128)) + (((i >> 1) & 1) ? c1 : c0));
+        };
+        bf16x8 fr[2 * KS];
+#pragma unroll
+        for (int i = 0; i < PD; ++i) fr[i] = rd(i);
+#pragma unroll
+        for (int i = 0; i < 2 * KS; ++i) {
+          wait_frag(fr[i], i, 2 * KS);
+          acc1[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i], yf[i >> 1], acc1[i & 1], 0, 0, 0);
+          if (i + PD < 2 * KS) fr[i + PD] = rd(i + PD);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // bias + GELU pair (v9's packed form); P = bf16 GELU(h) into this wave's LDS slot (fc2's operand image).  The
+      // bias is read only now: during fc1 its 8 registers deepen the fragment prefetch instead
+      {
+        float bia[8];
+        lds_f8(lb1 + j0 + 8 * (ln >> 4), bia);
+        float v[8], o[8], o2[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc1[0][r], v[4 + r] = acc1[1][r];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v[w] += bia[w];
+#pragma unroll
+        for (int w = 0; w < 8; w += 2) {
+          const gelu_f2 hh = {v[w], v[w + 1]};
+          gelu_f2 ph, de;
+#if SV_MLP_DIAG & 1
+          ph = (gelu_f2){1.0f, 1.0f}, de = hh;  // diagnostic: no GELU arithmetic (results wrong)
+#else
+          gelu_parts2(hh, ph, de);
+#endif
+          const gelu_f2 g = hh * ph;
+          o2[w] = g.x, o2[w + 1] = g.y;
+          if constexpr (TRAIN) {
+            const gelu_f2 dg = __builtin_elementwise_fma(hh, de, ph);
+            o[w] = dg.x, o[w + 1] = dg.y;
+          }
+        }
+        const u32x4 pk = pack8(o2);
+        lds_st16(smem + OFF_PB + wid * 1024 + ln * 16, pk);
+        if constexpr (TRAIN) {
+          const int m = row1 + (ln & 15);
+          const uint32_t off = m < M ? (uint32_t)(((size_t)m * H + j0 + 8 * (ln >> 4)) * 2) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rgh, off, 0, kGradCpol);
+          __builtin_amdgcn_raw_buffer_store_b128(pk, ra, off, 0, kGradCpol);
+        } else {
+          (void)o;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // Y_q: W2(q) landed (A: issued after Y_{q-1}; younger: W1(q+1)'s pieces, this chunk's stores); every wave of the
+      // group wrote its P slot
+      if (grp == 0) vm_wait<N1 + S>();
+      lgkm0();
+      if (!(SV_MLP_DIAG & 4)) bar();
+      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
+      // fc2: acc2 += W2[half, chunk] . P^T over the pair's 32 rows, k (hidden) ascending
+      {
+        const int ln2 = lane_id();
+        bf16x8 pf[2];
+        pf[0] = lds_frag(smem + OFF_PB + (2 * rg) * 1024 + ln2 * 16);
+        pf[1] = lds_frag(smem + OFF_PB + (2 * rg + 1) * 1024 + ln2 * 16);
+        // fragment cf: frag64(st2, 16 cf) = st2 + 1 KiB cf + the lane's offset (row l & 15: the swizzle of every
+        // 16-row block is the same)
+        const int r = ln2 & 15;
+        const uint32_t b2a = lds_addr(smem + OFF_W2 + (q & 1) * W2B + chh * (256 * 64)) +
+                             (uint32_t)(r * 64 + (((ln2 >> 4) ^ w2swz(r)) << 4));
+        auto rd = [&](int cf) { return ds_frag(b2a + (uint32_t)(cf * 1024)); };
+        bf16x8 fr[CF2];
+#pragma unroll
+        for (int i = 0; i < PD; ++i) fr[i] = rd(i);
+        lgkm_dep<PD>(pf[0]);  // the two P reads were issued before the PD fragment reads
+        lgkm_dep<PD>(pf[1]);
+#pragma unroll
+        for (int cf = 0; cf < CF2; ++cf) {
+          wait_frag(fr[cf], cf, CF2);
+#pragma unroll
+          for (int rf = 0; rf < 2; ++rf)
+            acc2[cf][rf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[cf], pf[rf], acc2[cf][rf], 0, 0, 0);
+          if (cf + PD < CF2) fr[cf + PD] = rd(cf + PD);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue: x_out = gamma (.) (acc + b2) + x   (v9's gamma-residual arithmetic); rows 32 rg + 16 rf + (l & 15),
+    // channels 256 chh + 16 cf + 4 gq .. +3; x loaded 8 fragments at a time
+#pragma unroll
+    for (int rf = 0; rf < 2; ++rf) {
+      const int m = t0 + 32 * rg + 16 * rf + ml;
+#pragma unroll
+      for (int c8 = 0; c8 < CF2; c8 += 8) {
+        u32x4 xr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = 256 * chh + 16 * (c8 + j) + 4 * gq;
+          const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + c) * 4) : OOB;
+          xr[j] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        }
+        vm_wait<0>();  // explicit (a compiler wait once fell short at a fused kernel's epilogue: sv_mlp_bwd)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = 256 * chh + 16 * (c8 + j) + 4 * gq;
+          float bv[4], gv[4];
+          lds_f4x2(lb2 + c, lgam + c, bv, gv);
+          const uint32_t xw[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+          float o[4];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) o[w] = fmaf(gv[w], acc2[c8 + j][rf][w] + bv[w], __uint_as_float(xw[w]));
+          const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + c) * 4) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]),
+                                                       __float_as_uint(o[2]), __float_as_uint(o[3])},
+                                                 rxo, off, 0, 0);
+        }
+      }
+    }
+  }
+  if (grp == 0) bar();  // the barrier group B is behind
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup's LDS is released
+}
+
+template <bool TRAIN>
+static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                  const float* gamma, const float* x, float* xo, uint16_t* gh, uint16_t* a, int M, hipStream_t s) {
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(&mlp512_kernel<TRAIN>), LDS, s)) return rc;
+  const int tiles = (M + R - 1) / R;
+  const int slots = device_cus(s);
+  const int grid = tiles < slots ? tiles : slots;
+  mlp512_kernel<TRAIN><<<grid, THREADS, LDS, s>>>(y, w1, b1, w2, b2, gamma, x, xo, gh, a, M);
+  return check_launch("sv_mlp_fwd");
+}
+}  // namespace c512
+
 template <int C, bool TRAIN>
 static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                   const float* gamma, const float* x, float* xo, uint16_t* gh, uint16_t* a, int M, hipStream_t s) {
@@ -881,7 +1183,7 @@ int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uin
   SV_REQUIRE(M > 0 && M * 4 * C * 2 < 0x7fffffffLL, "sv_mlp_fwd: M out of range (the hidden tensor must be < 2 GiB)");
   SV_REQUIRE((gelu_grad == nullptr) == (gelu_out == nullptr), "sv_mlp_fwd: GELU'(h) and GELU(h) are stored together");
   SV_REQUIRE(x != x_out, "sv_mlp_fwd: x_out must not alias x");
-  SV_REQUIRE(C == 128 || C == 192 || C == 256, "sv_mlp_fwd: C = %d not supported (128, 192, 256)", C);
+  SV_REQUIRE(C == 128 || C == 192 || C == 256 || C == 512, "sv_mlp_fwd: C = %d not supported (128, 192, 256, 512)", C);
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   SV_REQUIRE(al(y) && al(w1) && al(w2) && al(b1) && al(b2) && al(gamma) && al(x) && al(x_out) && al(gelu_grad) &&
                  al(gelu_out),
@@ -896,6 +1198,9 @@ int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uin
   if (C == 128 && !getenv_flag_mlp_v1())
     return tr ? mlp::c128::launch<true>(y, w1, b1, w2, b2, gamma, x, x_out, gelu_grad, gelu_out, m, s)
               : mlp::c128::launch<false>(y, w1, b1, w2, b2, gamma, x, x_out, nullptr, nullptr, m, s);
+  if (C == 512)
+    return tr ? mlp::c512::launch<true>(y, w1, b1, w2, b2, gamma, x, x_out, gelu_grad, gelu_out, m, s)
+              : mlp::c512::launch<false>(y, w1, b1, w2, b2, gamma, x, x_out, nullptr, nullptr, m, s);
   switch (C) {
     SV_MLP_CASE(128)
     SV_MLP_CASE(192)

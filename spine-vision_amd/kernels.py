@@ -235,7 +235,7 @@ def linear_dgrad(dy2d, w, *, out, epilogue=nv.SV_EPI_STORE, a_scale_k=None, aux=
 
 
 # channel counts the fused MLP forward kernel (csrc/mlp.hip) is built for: ConvNeXt-base S1 / S2, ConvNeXt-large S1
-MLP_FUSED_C = (128, 192, 256)
+MLP_FUSED_C = (128, 192, 256, 512)
 
 
 def mlp_fwd(y, w1, b1, w2, b2, gamma, x, *, out, gelu_grad=None, gelu_out=None):

@@ -75,7 +75,7 @@ def _check(o, train):
     assert err < 2e-3, err
 
 
-@pytest.mark.parametrize("C", [128, 192, 256])
+@pytest.mark.parametrize("C", [128, 192, 256, 512])
 @pytest.mark.parametrize("train", [True, False], ids=["train", "eval"])
 @pytest.mark.parametrize("M", [4096, 1000, 8 * 256 * 3 + 17])
 def test_mlp_fused_matches_two_gemm_path(dev, C, train, M):
@@ -83,7 +83,8 @@ def test_mlp_fused_matches_two_gemm_path(dev, C, train, M):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("M,C", [(524288, 128), (131072, 256), (1048576, 192)], ids=["base-S1", "base-S2", "large-S1"])
+@pytest.mark.parametrize("M,C", [(524288, 128), (131072, 256), (1048576, 192), (32768, 512)],
+                         ids=["base-S1", "base-S2", "large-S1", "base-S3"])
 def test_mlp_fused_production_shapes(dev, M, C):
     o = _ops(dev, M, C, seed=7)
     _check(o, True)
@@ -96,12 +97,12 @@ def test_mlp_fused_rejects_bad_arguments(dev):
     o = _ops(dev, 256, 128, seed=1)
     with pytest.raises(ValueError):
         K.mlp_fwd(o["y"], o["w1"], o["b1"], o["w2"], o["b2"], o["gam"], o["x"], out=o["x"])  # aliasing
-    y = torch.zeros(256, 512, device=dev, dtype=torch.bfloat16)
-    w1 = torch.zeros(2048, 512, device=dev, dtype=torch.bfloat16)
-    w2 = torch.zeros(512, 2048, device=dev, dtype=torch.bfloat16)
-    with pytest.raises(ValueError):  # C = 512: not a fused-MLP shape
-        K.mlp_fwd(y, w1, torch.zeros(2048, device=dev), w2, torch.zeros(512, device=dev), torch.zeros(512, device=dev),
-                  torch.zeros(256, 512, device=dev), out=torch.empty(256, 512, device=dev))
+    y = torch.zeros(256, 384, device=dev, dtype=torch.bfloat16)
+    w1 = torch.zeros(1536, 384, device=dev, dtype=torch.bfloat16)
+    w2 = torch.zeros(384, 1536, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):  # C = 384 (large S2): not a fused-MLP shape
+        K.mlp_fwd(y, w1, torch.zeros(1536, device=dev), w2, torch.zeros(384, device=dev), torch.zeros(384, device=dev),
+                  torch.zeros(256, 384, device=dev), out=torch.empty(256, 384, device=dev))
 
 
 @pytest.mark.parametrize("name", ["convnext_base", "convnext_large"])

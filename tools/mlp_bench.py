@@ -38,7 +38,7 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--shapes", default="base-S1,base-S2,large-S1")
+    ap.add_argument("--shapes", default="base-S1,base-S2,large-S1,base-S3")
     ap.add_argument("--bwd", action="store_true", help="also the fused backward (C = 128) against its three kernels")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
