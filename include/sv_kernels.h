@@ -164,7 +164,8 @@ typedef struct {
 
 int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream);
 /* Finish of a split-K GEMM (SV_EPI_SLAB): C[m, n] = (accumulate ? C[m, n] : 0) + sum_s slab[s][m][n],
- * slices summed in order (deterministic); c_dtype f32 or bf16 (accumulate: f32 only).  stats != NULL
+ * slices summed in order (deterministic); c_dtype f32 or bf16 (accumulate into bf16: the sum in f32, stored
+ * bf16 -- the ResNet bf16 gradient stream).  stats != NULL
  * (bf16 C): also the SV_EPI_STORE_STATS partials [ceil(M/64)][2][N] of the values as stored.
  * N, ldc multiples of 4; slab, C, stats 16-byte aligned.                                          */
 int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, int32_t N, void* C, int32_t c_dtype, int64_t ldc,
@@ -448,8 +449,9 @@ int sv_conv_fwd(const void* x, const void* wp, void* y, int32_t y_dtype, int32_t
                 const sv_gemm_policy* policy, sv_stream_t stream);
 /* dx (+)= conv_transpose(dy, w): dy [B][OH][OW][Cout] (dtype), dx [B][H][W][Cs] (dx_dtype). Stride-2
  * convolutions run as four stride-1 sub-convolutions, one per output parity class; bf16 with even H, W,
- * more than one tap, Cout >= 32 and Cs % 8 == 0 (accumulate: f32 dx) as ONE gathered GEMM launch whose
- * epilogue stores each class's rows at their dx pixels (no workspace, no scatter pass).              */
+ * Cout >= 32 and Cs % 8 == 0 as ONE gathered GEMM launch whose epilogue stores each class's rows at their dx
+ * pixels (no workspace, no scatter pass).  accumulate with a bf16 dx (the ResNet gradient stream, ABI v6): the
+ * f32 sum of dx and the product, stored bf16.                                                        */
 int sv_conv_bwd_data(const void* dy, const void* wp, void* dx, int32_t dx_dtype, int32_t accumulate,
                      int32_t dtype, const sv_conv_shape* s, const sv_gemm_policy* policy, sv_stream_t stream);
 /* dw (+)= dy^T * im2col(x) into torch layout [Cout][Cin][KH][KW] f32, through split-K f32 slabs in
@@ -474,7 +476,7 @@ int sv_conv_fwd_stats(const void* x, const void* wp, void* y, int32_t y_dtype, i
 /* Split-K forms for grids smaller than the chip (the deep ResNet stages: few 256x128 output tiles,
  * long K = taps x channels): the gathered GEMM writes `split` f32 slabs [split][M][N] into `work`
  * (split * M * N floats), then sv_gemm_slab_finish sums them into y (+ the STORE_STATS partials when
- * stats != NULL) / into dx (+= when accumulate, f32 dx).  bf16 gathered-operand shapes only (as
+ * stats != NULL) / into dx (+= when accumulate, f32 or bf16 dx).  bf16 gathered-operand shapes only (as
  * sv_conv_fwd_stats; dgrad: stride 1, Cout >= 32); others are an error.
  * Stride-2 dgrad (bf16, Cout >= 32, Cs % 8 == 0): one gathered GEMM per output parity class writes
  * compact slabs into `work` (split * B*H*W*Cs floats in all), one pass scatters them into dx (+= when
@@ -525,11 +527,12 @@ int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, const float
 int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                     int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
                     sv_stream_t stream);
-/* sv_bn_bwd_stats for an f32 dout with the act mask, also overwriting dout with g = dout * (act > 0)
- * in place (the residual block's output gradient: the apply pass then runs with act == NULL and the
- * shortcut reads dout itself — no separate masked copy).                                            */
-int sv_bn_bwd_stats_mask(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
-                         const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
+/* sv_bn_bwd_stats with the act mask, also overwriting dout with g = dout * (act > 0) in place, in dout's
+ * dtype (the residual block's output gradient -- the gradient stream, bf16 in the bf16 model as under the
+ * reference's fp16 autocast: the apply pass then runs with act == NULL and the shortcut reads dout itself,
+ * no separate masked copy).  ABI v6: dout_dtype added (was f32 only).                                 */
+int sv_bn_bwd_stats_mask(void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                         int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
                          sv_stream_t stream);
 int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
                      sv_stream_t stream);
@@ -538,15 +541,16 @@ int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, 
  * one ReLU mask.  One statistics pass writes g = dout * (act > 0) over dout and both BatchNorms' partials
  * (part: sums of g and g*xhat; part2: sums of g and g*xhat2) -- bit for bit sv_bn_bwd_stats_mask then
  * sv_bn_bwd_stats(g) of the shortcut -- reading dout once; one apply pass writes both data gradients from g
- * (bit for bit two sv_bn_bwd_apply calls).  Both BatchNorms have rows x C; dx, dx2 share dx_dtype.     */
-int sv_bn_bwd_stats_mask_dual(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
-                              const float* mean, const float* rstd, const void* y2, int32_t y2_dtype,
+ * (bit for bit two sv_bn_bwd_apply calls).  Both BatchNorms have rows x C; dx, dx2 share dx_dtype.  ABI v6:
+ * dout_dtype / g_dtype added (the gradient stream's dtype; was f32 only).                             */
+int sv_bn_bwd_stats_mask_dual(void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                              int32_t y_dtype, const float* mean, const float* rstd, const void* y2, int32_t y2_dtype,
                               const float* mean2, const float* rstd2, int64_t rows, int32_t C, float* part,
                               float* part2, sv_stream_t stream);
-int sv_bn_bwd_apply_dual(const float* g, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
-                         const float* gamma, const float* sums, const void* y2, int32_t y2_dtype, const float* mean2,
-                         const float* rstd2, const float* gamma2, const float* sums2, void* dx, void* dx2,
-                         int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
+int sv_bn_bwd_apply_dual(const void* g, int32_t g_dtype, const void* y, int32_t y_dtype, const float* mean,
+                         const float* rstd, const float* gamma, const float* sums, const void* y2, int32_t y2_dtype,
+                         const float* mean2, const float* rstd2, const float* gamma2, const float* sums2, void* dx,
+                         void* dx2, int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
 int sv_bn_bwd_apply(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                     int32_t y_dtype, const float* mean, const float* rstd, const float* gamma, const float* sums,
                     void* dx, int32_t dx_dtype, float* gmask, int64_t rows, int32_t C, sv_stream_t stream);
@@ -560,17 +564,18 @@ int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const void* y, in
                          const float* rstd, const float* gamma, const float* beta, const float* sums, void* dx,
                          int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream);
 /* The stem's BN + ReLU backward fed by the max-pool 3x3/2 (pad 1) backward: the incoming gradient of
- * input pixel p is the sum of dpool [B][OH][OW][C] (f32) over the windows whose argmax tap (idx, as
+ * input pixel p is the sum of dpool [B][OH][OW][C] (f32 or bf16, dpool_dtype: ABI v6) over the windows whose
+ * argmax tap (idx, as
  * sv_maxpool3s2_fwd writes it) is p, gathered inside both passes in sv_maxpool3s2_bwd's order (bit for
  * bit sv_maxpool3s2_bwd then sv_bn_relu_bwd_*, without writing the [B][H][W][C] f32 gradient).
  * y [B*H*W][C]; dpool 16-B and idx 4-B aligned.                                                     */
-int sv_bn_relu_bwd_stats_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W, const void* y,
-                              int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
-                              const float* beta, int32_t C, float* part, sv_stream_t stream);
-int sv_bn_relu_bwd_apply_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W, const void* y,
-                              int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
-                              const float* beta, const float* sums, void* dx, int32_t dx_dtype, int32_t C,
-                              sv_stream_t stream);
+int sv_bn_relu_bwd_stats_pool(const void* dpool, int32_t dpool_dtype, const uint8_t* idx, int32_t B, int32_t H,
+                              int32_t W, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                              const float* gamma, const float* beta, int32_t C, float* part, sv_stream_t stream);
+int sv_bn_relu_bwd_apply_pool(const void* dpool, int32_t dpool_dtype, const uint8_t* idx, int32_t B, int32_t H,
+                              int32_t W, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                              const float* gamma, const float* beta, const float* sums, void* dx, int32_t dx_dtype,
+                              int32_t C, sv_stream_t stream);
 /* One launch per BatchNorm for small row counts (rows <= SV_BN_SMALL_MAX_ROWS and the geometry
  * sv_bn_small_ok accepts: ResNet layers 3-4 at 256 px).  One workgroup owns 8 channels over all rows, so
  * the statistics and the pass that uses them share the launch; the sums are taken in the multi-launch
@@ -611,10 +616,12 @@ int sv_maxpool3s2_fwd(const void* x, int32_t x_dtype, void* y, uint8_t* idx, int
                       int32_t C, sv_stream_t stream);
 int sv_maxpool3s2_bwd(const void* dout, int32_t dout_dtype, const uint8_t* idx, void* dx, int32_t dx_dtype,
                       int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
-/* global average pool: feat[b][c] = mean_hw x; bwd: dx[b][hw][c] = dfeat[b][c] / HW (f32).        */
+/* global average pool: feat[b][c] = mean_hw x; bwd: dx[b][hw][c] = dfeat[b][c] / HW, dx in dx_dtype (the
+ * ResNet gradient stream's: bf16 in the bf16 model; ABI v6).                                        */
 int sv_avgpool_fwd(const void* x, int32_t x_dtype, float* feat, int32_t B, int32_t HW, int32_t C,
                    sv_stream_t stream);
-int sv_avgpool_bwd(const float* dfeat, float* dx, int32_t B, int32_t HW, int32_t C, sv_stream_t stream);
+int sv_avgpool_bwd(const float* dfeat, void* dx, int32_t dx_dtype, int32_t B, int32_t HW, int32_t C,
+                   sv_stream_t stream);
 
 #ifdef __cplusplus
 }

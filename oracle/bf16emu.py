@@ -16,9 +16,12 @@ Rounding points restated from spine-vision_amd/backbone/resnet.py (``_forward_im
             BN statistics of the bf16 y;  inner BN + ReLU -> bf16 a;  block output
             out = bf16(ReLU(BN(y_last) + shortcut)), shortcut = x_in or BN(bf16(conv_ds(x_in)));
             stem a0 = bf16(ReLU(BN(y0))) -> max-pool;  features = avgpool(out) in f32.
-  backward  the gradient stream into a block output (avg-pool / next block's dx) stays f32; the gradient at
-            every conv OUTPUT y (BN backward result) is stored bf16; the gradient at every inner
-            activation a (conv data gradient) is stored bf16; a block's input gradient dx stays f32; weight
+  backward  the gradient stream -- into every block output (avg-pool backward / the next block's dx) and
+            into the max-pool output -- is stored bf16 (``grad_bf16``, the default, as resnet.py's grad_dtype;
+            False: f32, the round-4 layout); a projection block's conv1 data gradient is stored bf16 into dx
+            before the shortcut's is added (two roundings), an identity block's dx is the f32 sum of the
+            masked stream and conv1's data gradient, rounded once; the gradient at every conv OUTPUT y (BN
+            backward result) and at every inner activation a (conv data gradient) is stored bf16; weight
             gradients are f32 products of the bf16 operands.
 """
 
@@ -73,10 +76,11 @@ class ResNetBf16Emu:
     """Functional emulation over an ``oracle.resnet.ResNet`` (its parameters, promoted to ``dtype``, are leaf
     tensors with ``.grad``).  ``forward(img)`` -> features; call ``.backward`` on a loss of them."""
 
-    def __init__(self, model: torch.nn.Module, dtype=torch.float64, train: bool = True) -> None:
+    def __init__(self, model: torch.nn.Module, dtype=torch.float64, train: bool = True, grad_bf16: bool = True) -> None:
         self.model = model
         self.dtype = dtype
         self.train = train
+        self.grad_bf16 = grad_bf16
         self.params = {id(p): p.detach().to(dtype).clone().requires_grad_(True) for p in model.parameters()}
         # BN buffers promoted too (updated in place in train mode)
         self.state = {}
@@ -107,15 +111,17 @@ class ResNetBf16Emu:
 
     def _block(self, blk, x_in):
         P = self.params
+        # a projection block stores conv1's data gradient into the bf16 dx before adding the shortcut's
+        xc = qg(x_in) if (self.grad_bf16 and blk.downsample is not None) else x_in
         if hasattr(blk, "conv3"):  # Bottleneck: stride on the 3x3
-            y1 = qg(_conv(x_in, blk.conv1, P, 1, 0))
+            y1 = qg(_conv(xc, blk.conv1, P, 1, 0))
             a1 = qg(qf(F.relu(self._bnf(y1, blk.bn1))))
             y2 = qg(_conv(a1, blk.conv2, P, blk.conv2.stride, 1))
             a2 = qg(qf(F.relu(self._bnf(y2, blk.bn2))))
             y_last = qg(_conv(a2, blk.conv3, P, 1, 0))
             bn_last = blk.bn3
         else:  # BasicBlock
-            y1 = qg(_conv(x_in, blk.conv1, P, blk.conv1.stride, 1))
+            y1 = qg(_conv(xc, blk.conv1, P, blk.conv1.stride, 1))
             a1 = qg(qf(F.relu(self._bnf(y1, blk.bn1))))
             y_last = qg(_conv(a1, blk.conv2, P, 1, 1))
             bn_last = blk.bn2
@@ -125,7 +131,8 @@ class ResNetBf16Emu:
             sc = self._bnf(yd, dbn)
         else:
             sc = x_in
-        return qf(F.relu(self._bnf(y_last, bn_last) + sc))
+        out = qf(F.relu(self._bnf(y_last, bn_last) + sc))
+        return qg(out) if self.grad_bf16 else out
 
     def forward(self, img: torch.Tensor) -> torch.Tensor:
         m = self.model
@@ -133,6 +140,8 @@ class ResNetBf16Emu:
         y0 = qg(_conv(x0, m.conv1, self.params, 2, 3))
         a0 = qf(F.relu(self._bnf(y0, m.bn1)))
         x = F.max_pool2d(a0, 3, 2, 1)
+        if self.grad_bf16:
+            x = qg(x)  # the stem's max-pool backward reads the bf16 stream
         for i in range(1, 5):
             for blk in getattr(m, f"layer{i}"):
                 x = self._block(blk, x)
@@ -167,11 +176,11 @@ def classifier_loss(out: dict, targets: dict, task_names, label_smoothing: float
 
 
 def classifier_grads(ref: torch.nn.Module, img: torch.Tensor, targets: dict, dtype=torch.float64,
-                     train: bool = True) -> tuple[dict, dict, dict]:
+                     train: bool = True, grad_bf16: bool = True) -> tuple[dict, dict, dict]:
     """One forward + backward of an ``oracle.heads.Classifier`` over a ResNet backbone with the HIP bf16 path's
     rounding points, the arithmetic in ``dtype``.  -> (logits {task}, grads {param name}, BN buffers {name}).
     ``ref`` is not modified."""
-    emu = ResNetBf16Emu(ref.backbone, dtype=dtype, train=train)
+    emu = ResNetBf16Emu(ref.backbone, dtype=dtype, train=train, grad_bf16=grad_bf16)
     out, hp = classifier_forward(emu, ref.heads, img)
     classifier_loss(out, targets, ref.task_names).backward()
     grads = {"backbone." + n: g for n, g in emu.named_grads().items()}

@@ -336,9 +336,10 @@ __host__ __device__ __forceinline__ int pool_out(int n) { return (n + 2 - 3) / 2
 // output gradients d [B][OH][OW][C] (f32) whose argmax tap (idx) is this pixel, windows taken in the
 // order of maxpool_bwd_kernel (oy, then ox, ascending) so the values are bit for bit its output.
 struct PoolSrc {
-  const float* d;
+  const void* d;
   const uint8_t* idx;
   int H, W;
+  int ddt;  // d's dtype (SV_F32 = 0 when omitted)
 };
 
 template <int V>
@@ -369,11 +370,7 @@ __device__ __forceinline__ void pool_grad(const PoolSrc& p, int C, size_t e, flo
 #pragma unroll
       for (int k = 0; k < V / 4; ++k) ib[k] = *reinterpret_cast<const uint32_t*>(p.idx + o + 4 * k);
       float dv[V];
-#pragma unroll
-      for (int k = 0; k < V; k += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(p.d + o + k);
-        dv[k] = x.x; dv[k + 1] = x.y; dv[k + 2] = x.z; dv[k + 3] = x.w;
-      }
+      ldv<V>(p.d, p.ddt, o, dv);
 #pragma unroll
       for (int q = 0; q < V; ++q)
         if ((int)((ib[q >> 2] >> (8 * (q & 3))) & 0xffu) == tap) g[q] += dv[q];
@@ -418,9 +415,10 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int64_t rows, int C,
                                                              int tpr, int rp, int64_t rpp, float* __restrict__ part,
-                                                             float* gout, const PoolSrc pool) {
-  // gout (act-mask form, f32 dout): g = dout * (act > 0) written back over dout by the thread that read
-  // it, so the apply pass and the block's shortcut read the masked gradient without a separate copy
+                                                             void* gout, const PoolSrc pool) {
+  // gout (act-mask form): g = dout * (act > 0) written back over dout (its dtype: the ResNet gradient stream is
+  // bf16 in the bf16 model) by the thread that read it, so the apply pass and the block's shortcut read the masked
+  // gradient without a separate copy
   const int t = threadIdx.x;
   const int c = (blockIdx.x * tpr + t % tpr) * V;
   const int rsub = t / tpr;
@@ -443,8 +441,8 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
     grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0, &pool, C);
     grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1, &pool, C);
     if (gout) {
-      stv<V>(gout, SV_F32, e0, g0);
-      stv<V>(gout, SV_F32, e1, g1);
+      stv<V>(gout, ddt, e0, g0);
+      stv<V>(gout, ddt, e1, g1);
     }
 #pragma unroll
     for (int q = 0; q < V; ++q) {
@@ -459,7 +457,7 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
     float v[V], g[V];
     ldv<V>(y, ydt, e, v);
     grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g, &pool, C);
-    if (gout) stv<V>(gout, SV_F32, e, g);
+    if (gout) stv<V>(gout, ddt, e, g);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
       s1[q] += g[q];
@@ -487,7 +485,7 @@ __global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float*
 // the main BN's sums (g, g * xhat) and the shortcut BN's g * xhat2 (its sum of g is the same), in the order of
 // bwd_stats_kernel (bit for bit its partials for either BatchNorm), reading d once instead of twice.
 template <int V>
-__global__ void __launch_bounds__(kThreads) bwd_stats_dual_kernel(float* __restrict__ dout, const void* __restrict__ act,
+__global__ void __launch_bounds__(kThreads) bwd_stats_dual_kernel(void* __restrict__ dout, int ddt, const void* __restrict__ act,
                                                                   int adt, const void* __restrict__ y, int ydt,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ rstd,
@@ -517,10 +515,10 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_dual_kernel(float* __restr
     ldv<V>(y, ydt, e1, v1);
     ldv<V>(y2, y2dt, e0, w0);
     ldv<V>(y2, y2dt, e1, w1);
-    grad_masked<V, false>(dout, SV_F32, act, adt, e0, v0, mu, rs, nullptr, nullptr, c, g0);
-    grad_masked<V, false>(dout, SV_F32, act, adt, e1, v1, mu, rs, nullptr, nullptr, c, g1);
-    stv<V>(dout, SV_F32, e0, g0);
-    stv<V>(dout, SV_F32, e1, g1);
+    grad_masked<V, false>(dout, ddt, act, adt, e0, v0, mu, rs, nullptr, nullptr, c, g0);
+    grad_masked<V, false>(dout, ddt, act, adt, e1, v1, mu, rs, nullptr, nullptr, c, g1);
+    stv<V>(dout, ddt, e0, g0);
+    stv<V>(dout, ddt, e1, g1);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
       s1[q] += g0[q];
@@ -536,8 +534,8 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_dual_kernel(float* __restr
     float v[V], g[V], w[V];
     ldv<V>(y, ydt, e, v);
     ldv<V>(y2, y2dt, e, w);
-    grad_masked<V, false>(dout, SV_F32, act, adt, e, v, mu, rs, nullptr, nullptr, c, g);
-    stv<V>(dout, SV_F32, e, g);
+    grad_masked<V, false>(dout, ddt, act, adt, e, v, mu, rs, nullptr, nullptr, c, g);
+    stv<V>(dout, ddt, e, g);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
       s1[q] += g[q];
@@ -590,7 +588,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
 
 // both BatchNorms' data gradients from the shared masked gradient g (bwd_apply_kernel's formula for each)
 struct BwdDualArgs {
-  const float* g;
+  const void* g; int gdt;
   const void* y; int ydt;
   const float *mean, *rstd, *gamma, *sums;
   const void* y2; int y2dt;
@@ -608,7 +606,7 @@ __global__ void __launch_bounds__(kThreads) bwd_apply_dual_kernel(const BwdDualA
     const size_t e = (size_t)i * V;
     const int c = chan_of(e, a.C, a.rows * a.C);
     float g[V], v[V], w[V], o[V], o2[V], mu[V], rs[V], ga[V], sg[V], sgx[V];
-    ldv<V>(a.g, SV_F32, e, g);
+    ldv<V>(a.g, a.gdt, e, g);
     ldv<V>(a.y, a.ydt, e, v);
     ldv<V>(a.y2, a.y2dt, e, w);
     ldp<V>(a.mean, c, mu);
@@ -737,8 +735,8 @@ __global__ void __launch_bounds__(kThreads) avgpool_fwd_kernel(const void* __res
   *reinterpret_cast<float4*>(feat + b * C + c) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
 }
 
-__global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const float* __restrict__ dfeat, float* __restrict__ dx,
-                                                               int B, int HW, int C) {
+__global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const float* __restrict__ dfeat, void* __restrict__ dx,
+                                                               int xdt, int B, int HW, int C) {
   const int64_t n4 = (int64_t)B * HW * C / 4;
   const float inv = 1.0f / (float)HW;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
@@ -746,7 +744,7 @@ __global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const float* __re
     const int c = (int)(e % C);
     const int64_t b = e / ((int64_t)HW * C);
     const float4 g = *reinterpret_cast<const float4*>(dfeat + b * C + c);
-    *reinterpret_cast<float4*>(dx + e) = make_float4(g.x * inv, g.y * inv, g.z * inv, g.w * inv);
+    st4d(dx, xdt, (size_t)e, make_float4(g.x * inv, g.y * inv, g.z * inv, g.w * inv));
   }
 }
 
@@ -789,7 +787,7 @@ __device__ __forceinline__ float stream_fold(F&& part_at, int j, int P) {
 }
 
 struct SmallBwdArgs {
-  void* dout; int ddt;             // MODE 0 / 2: f32, overwritten with g = dout * (act > 0)
+  void* dout; int ddt;             // MODE 0 / 2: overwritten with g = dout * (act > 0) (in its dtype)
   const void* act; int adt;
   const void* y; int ydt;
   const float *mean, *rstd, *gamma, *beta;  // beta: MODE 1 (the BN's own ReLU, recomputed from y)
@@ -845,7 +843,7 @@ __global__ void __launch_bounds__(kSmallThreads) bwd_small_kernel(const SmallBwd
           ldv<8>(a.act, a.adt, e, m);
 #pragma unroll
           for (int q = 0; q < 8; ++q) g[q] = m[q] > 0.f ? g[q] : 0.f;
-          stv<8>(a.dout, SV_F32, e, g);
+          stv<8>(a.dout, a.ddt, e, g);
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -926,7 +924,7 @@ __global__ void __launch_bounds__(kSmallThreads) bwd_small_kernel(const SmallBwd
 #pragma unroll
         for (int q = 0; q < 8; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
       } else {
-        ldv<8>(a.dout, SV_F32, e, g);
+        ldv<8>(a.dout, a.ddt, e, g);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
@@ -1105,13 +1103,13 @@ extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, 
 static int bwd_stats_launch(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
                             int32_t y_dtype, const float* mean, const float* rstd, const float* gamma,
                             const float* beta, int64_t rows, int32_t C, float* part, sv_stream_t stream,
-                            float* gout = nullptr, const PoolSrc* pool = nullptr) {
+                            void* gout = nullptr, const PoolSrc* pool = nullptr) {
   const RedGeo g = red_geo(C);
   const int P = nparts_for(rows, C);
   const int64_t rpp = (rows + P - 1) / P;
   const dim3 grid(g.cslices, P);
   hipStream_t st = (hipStream_t)stream;
-  const PoolSrc ps = pool ? *pool : PoolSrc{nullptr, nullptr, 0, 0};
+  const PoolSrc ps = pool ? *pool : PoolSrc{nullptr, nullptr, 0, 0, SV_F32};
 #define BWDS(VV, RY)                                                                                              \
   bwd_stats_kernel<VV, RY><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, gamma, \
                                                       beta, rows, C, g.tpr, g.rp, rpp, part, gout, ps)
@@ -1142,13 +1140,14 @@ extern "C" int sv_bn_bwd_stats(const void* dout, int32_t dout_dtype, const void*
                           stream);
 }
 
-extern "C" int sv_bn_bwd_stats_mask(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
-                                    const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
-                                    sv_stream_t stream) {
+extern "C" int sv_bn_bwd_stats_mask(void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, const void* y,
+                                    int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C,
+                                    float* part, sv_stream_t stream) {
   BN_REQUIRE_C(C, "sv_bn_bwd_stats_mask");
-  SV_REQUIRE(dout && act && y && mean && rstd && part && rows > 0 && dt_ok(act_dtype) && dt_ok(y_dtype),
+  SV_REQUIRE(dout && act && y && mean && rstd && part && rows > 0 && dt_ok(dout_dtype) && dt_ok(act_dtype) &&
+                 dt_ok(y_dtype),
              "sv_bn_bwd_stats_mask: bad arguments");
-  return bwd_stats_launch(dout, SV_F32, act, act_dtype, y, y_dtype, mean, rstd, nullptr, nullptr, rows, C, part,
+  return bwd_stats_launch(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, nullptr, nullptr, rows, C, part,
                           stream, dout);
 }
 
@@ -1213,33 +1212,35 @@ extern "C" int sv_bn_relu_bwd_apply(const void* dout, int32_t dout_dtype, const 
 }
 
 // The stem: BatchNorm (+ its own ReLU) backward whose incoming gradient is the max-pool 3x3/2 backward of
-// dpool [B][OH][OW][C] (f32) through idx, gathered inside both passes instead of materialised
-static bool pool_args_ok(const float* dpool, const uint8_t* idx, int B, int H, int W, int C) {
-  return dpool && idx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && ((uintptr_t)dpool & 15) == 0 &&
+// dpool [B][OH][OW][C] (f32 or bf16: the gradient stream's dtype) through idx, gathered inside both passes instead of
+// materialised
+static bool pool_args_ok(const void* dpool, int dpool_dtype, const uint8_t* idx, int B, int H, int W, int C) {
+  return dpool && dt_ok(dpool_dtype) && idx && B > 0 && H > 0 && W > 0 && C % 4 == 0 && C > 0 && ((uintptr_t)dpool & 15) == 0 &&
          ((uintptr_t)idx & 3) == 0 && (int64_t)B * H * W * C < (1ll << 31);  // pool_grad's 32-bit indexing
 }
 
-extern "C" int sv_bn_relu_bwd_stats_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W,
-                                         const void* y, int32_t y_dtype, const float* mean, const float* rstd,
-                                         const float* gamma, const float* beta, int32_t C, float* part,
-                                         sv_stream_t stream) {
+extern "C" int sv_bn_relu_bwd_stats_pool(const void* dpool, int32_t dpool_dtype, const uint8_t* idx, int32_t B,
+                                         int32_t H, int32_t W, const void* y, int32_t y_dtype, const float* mean,
+                                         const float* rstd, const float* gamma, const float* beta, int32_t C,
+                                         float* part, sv_stream_t stream) {
   BN_REQUIRE_C(C, "sv_bn_relu_bwd_stats_pool");
-  SV_REQUIRE(pool_args_ok(dpool, idx, B, H, W, C) && y && mean && rstd && gamma && beta && part && dt_ok(y_dtype),
+  SV_REQUIRE(pool_args_ok(dpool, dpool_dtype, idx, B, H, W, C) && y && mean && rstd && gamma && beta && part &&
+                 dt_ok(y_dtype),
              "sv_bn_relu_bwd_stats_pool: bad arguments");
-  const PoolSrc ps{dpool, idx, H, W};
+  const PoolSrc ps{dpool, idx, H, W, dpool_dtype};
   return bwd_stats_launch(nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, (int64_t)B * H * W, C,
                           part, stream, nullptr, &ps);
 }
 
-extern "C" int sv_bn_relu_bwd_apply_pool(const float* dpool, const uint8_t* idx, int32_t B, int32_t H, int32_t W,
-                                         const void* y, int32_t y_dtype, const float* mean, const float* rstd,
-                                         const float* gamma, const float* beta, const float* sums, void* dx,
-                                         int32_t dx_dtype, int32_t C, sv_stream_t stream) {
-  SV_REQUIRE(pool_args_ok(dpool, idx, B, H, W, C) && y && mean && rstd && gamma && beta && sums && dx &&
+extern "C" int sv_bn_relu_bwd_apply_pool(const void* dpool, int32_t dpool_dtype, const uint8_t* idx, int32_t B,
+                                         int32_t H, int32_t W, const void* y, int32_t y_dtype, const float* mean,
+                                         const float* rstd, const float* gamma, const float* beta, const float* sums,
+                                         void* dx, int32_t dx_dtype, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(pool_args_ok(dpool, dpool_dtype, idx, B, H, W, C) && y && mean && rstd && gamma && beta && sums && dx &&
                  dt_ok(y_dtype) && dt_ok(dx_dtype),
              "sv_bn_relu_bwd_apply_pool: bad arguments");
   BwdArgs a{nullptr, SV_F32, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, sums, dx, dx_dtype, nullptr,
-            (int64_t)B * H * W, C, PoolSrc{dpool, idx, H, W}};
+            (int64_t)B * H * W, C, PoolSrc{dpool, idx, H, W, dpool_dtype}};
   return bwd_apply_launch(a, stream);
 }
 
@@ -1280,19 +1281,21 @@ extern "C" int sv_avgpool_fwd(const void* x, int32_t x_dtype, float* feat, int32
   return check_launch("sv_avgpool_fwd");
 }
 
-extern "C" int sv_avgpool_bwd(const float* dfeat, float* dx, int32_t B, int32_t HW, int32_t C, sv_stream_t stream) {
-  SV_REQUIRE(dfeat && dx && B > 0 && HW > 0 && C % 4 == 0 && C > 0, "sv_avgpool_bwd: bad arguments");
-  avgpool_bwd_kernel<<<grid_for((int64_t)B * HW * C / 4), kThreads, 0, (hipStream_t)stream>>>(dfeat, dx, B, HW, C);
+extern "C" int sv_avgpool_bwd(const float* dfeat, void* dx, int32_t dx_dtype, int32_t B, int32_t HW, int32_t C,
+                              sv_stream_t stream) {
+  SV_REQUIRE(dfeat && dx && B > 0 && HW > 0 && C % 4 == 0 && C > 0 && dt_ok(dx_dtype), "sv_avgpool_bwd: bad arguments");
+  avgpool_bwd_kernel<<<grid_for((int64_t)B * HW * C / 4), kThreads, 0, (hipStream_t)stream>>>(dfeat, dx, dx_dtype, B, HW,
+                                                                                             C);
   return check_launch("sv_avgpool_bwd");
 }
 
-extern "C" int sv_bn_bwd_stats_mask_dual(float* dout, const void* act, int32_t act_dtype, const void* y, int32_t y_dtype,
-                                         const float* mean, const float* rstd, const void* y2, int32_t y2_dtype,
-                                         const float* mean2, const float* rstd2, int64_t rows, int32_t C, float* part,
-                                         float* part2, sv_stream_t stream) {
+extern "C" int sv_bn_bwd_stats_mask_dual(void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype,
+                                         const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                                         const void* y2, int32_t y2_dtype, const float* mean2, const float* rstd2,
+                                         int64_t rows, int32_t C, float* part, float* part2, sv_stream_t stream) {
   BN_REQUIRE_C(C, "sv_bn_bwd_stats_mask_dual");
-  SV_REQUIRE(dout && act && y && mean && rstd && y2 && mean2 && rstd2 && part && part2 && rows > 0 && dt_ok(act_dtype) &&
-                 dt_ok(y_dtype) && dt_ok(y2_dtype),
+  SV_REQUIRE(dout && act && y && mean && rstd && y2 && mean2 && rstd2 && part && part2 && rows > 0 && dt_ok(dout_dtype) &&
+                 dt_ok(act_dtype) && dt_ok(y_dtype) && dt_ok(y2_dtype),
              "sv_bn_bwd_stats_mask_dual: bad arguments");
   const RedGeo g = red_geo(C);
   const int P = nparts_for(rows, C);
@@ -1300,23 +1303,24 @@ extern "C" int sv_bn_bwd_stats_mask_dual(float* dout, const void* act, int32_t a
   const dim3 grid(g.cslices, P);
   hipStream_t st = (hipStream_t)stream;
   if (g.vec == 8)
-    bwd_stats_dual_kernel<8><<<grid, kThreads, 0, st>>>(dout, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
+    bwd_stats_dual_kernel<8><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
                                                         rstd2, rows, C, g.tpr, g.rp, rpp, part, part2);
   else
-    bwd_stats_dual_kernel<4><<<grid, kThreads, 0, st>>>(dout, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
+    bwd_stats_dual_kernel<4><<<grid, kThreads, 0, st>>>(dout, dout_dtype, act, act_dtype, y, y_dtype, mean, rstd, y2, y2_dtype, mean2,
                                                         rstd2, rows, C, g.tpr, g.rp, rpp, part, part2);
   return check_launch("sv_bn_bwd_stats_mask_dual");
 }
 
-extern "C" int sv_bn_bwd_apply_dual(const float* g, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
-                                    const float* gamma, const float* sums, const void* y2, int32_t y2_dtype,
-                                    const float* mean2, const float* rstd2, const float* gamma2, const float* sums2,
-                                    void* dx, void* dx2, int32_t dx_dtype, int64_t rows, int32_t C, sv_stream_t stream) {
+extern "C" int sv_bn_bwd_apply_dual(const void* g, int32_t g_dtype, const void* y, int32_t y_dtype, const float* mean,
+                                    const float* rstd, const float* gamma, const float* sums, const void* y2,
+                                    int32_t y2_dtype, const float* mean2, const float* rstd2, const float* gamma2,
+                                    const float* sums2, void* dx, void* dx2, int32_t dx_dtype, int64_t rows, int32_t C,
+                                    sv_stream_t stream) {
   SV_REQUIRE(C % 4 == 0 && C > 0 && rows > 0, "sv_bn_bwd_apply_dual: C must be a multiple of 4");
   SV_REQUIRE(g && y && mean && rstd && gamma && sums && y2 && mean2 && rstd2 && gamma2 && sums2 && dx && dx2 &&
-                 dt_ok(y_dtype) && dt_ok(y2_dtype) && dt_ok(dx_dtype),
+                 dt_ok(g_dtype) && dt_ok(y_dtype) && dt_ok(y2_dtype) && dt_ok(dx_dtype),
              "sv_bn_bwd_apply_dual: bad arguments");
-  BwdDualArgs a{g, y, y_dtype, mean, rstd, gamma, sums, y2, y2_dtype, mean2, rstd2, gamma2, sums2, dx, dx2, dx_dtype,
+  BwdDualArgs a{g, g_dtype, y, y_dtype, mean, rstd, gamma, sums, y2, y2_dtype, mean2, rstd2, gamma2, sums2, dx, dx2, dx_dtype,
                 rows, C};
   hipStream_t st = (hipStream_t)stream;
   if (vec_for(C) == 8)
@@ -1357,8 +1361,8 @@ extern "C" int sv_bn_bwd_small(int32_t mode, void* dout, int32_t dout_dtype, con
   SV_REQUIRE(dout && y && mean && rstd && gamma && dx && dt_ok(dout_dtype) && dt_ok(y_dtype) && dt_ok(dx_dtype) &&
                  al16(dout) && al16(y) && al16(dx) && al16(mean) && al16(rstd) && al16(gamma),
              "sv_bn_bwd_small: bad arguments");
-  SV_REQUIRE(mode == SV_BN_SMALL_RELU || (dout_dtype == SV_F32 && act && dt_ok(act_dtype) && al16(act) && !part),
-             "sv_bn_bwd_small: the mask modes need an f32 dout, act and no given partials");
+  SV_REQUIRE(mode == SV_BN_SMALL_RELU || (act && dt_ok(act_dtype) && al16(act) && !part),
+             "sv_bn_bwd_small: the mask modes need act and no given partials");
   SV_REQUIRE(mode != SV_BN_SMALL_RELU || (beta && al16(beta)), "sv_bn_bwd_small: the ReLU mode needs beta");
   SV_REQUIRE(mode != SV_BN_SMALL_DUAL || (y2 && mean2 && rstd2 && gamma2 && dx2 && dt_ok(y2_dtype) && al16(y2) &&
                                           al16(dx2) && al16(mean2) && al16(rstd2) && al16(gamma2)),

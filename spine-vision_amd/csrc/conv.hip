@@ -841,7 +841,7 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
   const int st = s->stride;
   const int T_ = s->KH * s->KW;
   if (dtype == SV_BF16 && st == 1 && s->Cout >= 32 && (s->Cs % 8) == 0 &&
-      (!accumulate || dx_dtype == SV_F32) && ((int64_t)T_ * s->Cout) % 32 == 0) {
+      ((int64_t)T_ * s->Cout) % 32 == 0) {
     // stride 1: one gather conv over dy (taps pad - kh, pad - kw) against the weight's rows
     ConvG g = make_convg(OH, OW, s->Cout, s->H, s->W, 1);
     g.lcout = ilog2(s->Cout);
@@ -875,10 +875,10 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
       d.c2_dtype = SV_F32;
       return launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
     }
-    if (accumulate) {  // dx += conv^T(dy): residual epilogue with gamma = 1 reading dx in place
-      d.epilogue = SV_EPI_BIAS_GAMMA_RES;
+    if (accumulate) {  // dx += conv^T(dy): residual epilogue with gamma = 1 reading dx in place (f32, or the
+      d.epilogue = SV_EPI_BIAS_GAMMA_RES;  // bf16 gradient stream: the sum in f32, stored bf16)
       d.aux = dx;
-      d.aux_dtype = SV_F32;
+      d.aux_dtype = dx_dtype;
       d.ld_aux = s->Cs;
     }
     const int rc = launch_gemm3_conv(&d, g, 2, (hipStream_t)stream);
@@ -889,7 +889,7 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
   const bool s2_even = s2_grid && s->KH * s->KW > 1;
   // ... and without a workspace their rows go straight into dx (plain store, in-place f32 accumulate, or
   // bf16 with the BatchNorm statistics); any kernel size (1x1: only class (0, 0) has a tap)
-  const bool s2_direct = s2_grid && !slab && (!accumulate || dx_dtype == SV_F32) && (!bn || dx_dtype == SV_BF16);
+  const bool s2_direct = s2_grid && !slab && (!bn || dx_dtype == SV_BF16);
   if (dtype == SV_BF16 && st == 2 && (slab || s2_direct) && s->Cout >= 32 && (s->Cs % 8) == 0 && s->Cs >= 8) {
     // stride 2: one gather GEMM per parity class into compact slabs, then one scatter pass.  Even H, W
     // and no split: all four classes run as ONE launch (mode 5) -- the per-class launches are each below
@@ -934,10 +934,10 @@ static int conv_bwd_data_impl(const void* dy, const void* wp, void* dx, int32_t 
           d.bn = bn;
           d.C2 = bnpart;
           d.c2_dtype = SV_F32;
-        } else if (accumulate) {  // dx += conv^T(dy) in place (gamma = 1)
+        } else if (accumulate) {  // dx += conv^T(dy) in place (gamma = 1; f32 or bf16 dx)
           d.epilogue = SV_EPI_BIAS_GAMMA_RES;
           d.aux = dx;
-          d.aux_dtype = SV_F32;
+          d.aux_dtype = dx_dtype;
           d.ld_aux = s->Cs;
         }
         // accumulating: trailing classes without taps would only re-add zero (1x1: one class of four)

@@ -446,8 +446,14 @@ __global__ void __launch_bounds__(SF_THREADS) slab_finish_kernel(const float* __
         }
         *cp = v;
       } else {
+        uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci);
+        if (accumulate) {  // the bf16 gradient stream: the sum in f32, stored bf16
+          const uint2 o = *cp;
+          v.x += __uint_as_float(o.x << 16); v.y += __uint_as_float(o.x & 0xffff0000u);
+          v.z += __uint_as_float(o.y << 16); v.w += __uint_as_float(o.y & 0xffff0000u);
+        }
         const uint2 u = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + ci) = u;
+        *cp = u;
         // statistics of the values as stored
         v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                         __uint_as_float(u.y & 0xffff0000u));
@@ -557,7 +563,6 @@ extern "C" int sv_gemm_slab_finish(const float* slab, int32_t split, int32_t M, 
   SV_REQUIRE(split >= 1 && M >= 0 && N >= 0 && N % 4 == 0 && ldc % 4 == 0 && ldc >= N,
              "sv_gemm_slab_finish: bad sizes (N, ldc multiples of 4)");
   SV_REQUIRE(c_dtype == SV_F32 || c_dtype == SV_BF16, "sv_gemm_slab_finish: bad C dtype");
-  SV_REQUIRE(!accumulate || c_dtype == SV_F32, "sv_gemm_slab_finish: accumulate needs f32 C");
   SV_REQUIRE(!stats || c_dtype == SV_BF16, "sv_gemm_slab_finish: statistics are of bf16 outputs");
   SV_REQUIRE(al16(slab) && al16(C) && (!stats || al16(stats)), "sv_gemm_slab_finish: operands must be 16-byte aligned");
   if (M == 0 || N == 0) return SV_OK;

@@ -257,7 +257,9 @@ __device__ __forceinline__ void ring_wait(int younger) {
   }
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC, int CONV = 0>
+// AUXO >= 0: the epilogue operand's dtype, overriding the one the epilogue kind implies (the bf16 gradient stream's
+// in-place accumulate: SV_EPI_BIAS_GAMMA_RES over a bf16 dx)
+template <bool AK, bool BKM, int EPI, int BKT, int S, int OCC, int CONV = 0, int AUXO = -1>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int K, int kper,
              int tilesM, int tilesN, int nsplit, EpiArgs e, float* __restrict__ colsum, ConvG cg) {
@@ -417,7 +419,8 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     }
     if (do_cs && threadIdx.x < BM && m0 + (int)threadIdx.x < e.M) colsum[(size_t)split * e.M + m0 + threadIdx.x] = csum;
     // the epilogue operand is bf16 (GELU'(h), pre-activation) or the f32 residual stream
-    constexpr int AUXT = (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD || EPI == SV_EPI_STORE_BN_BWD) ? SV_BF16
+    constexpr int AUXT = AUXO >= 0 ? AUXO
+                         : (EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD || EPI == SV_EPI_STORE_BN_BWD) ? SV_BF16
                          : EPI == SV_EPI_BIAS_GAMMA_RES ? SV_F32 : -1;
     // mode 5 with a non-slab epilogue: each class's rows go straight to their dx pixels
     constexpr bool REMAP = CONV == 5 && EPI != SV_EPI_SLAB;
@@ -426,12 +429,12 @@ gemm3_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
 }
 
-template <bool AK, bool BKM, int EPI, int BKT, int S, int CONV = 0>
+template <bool AK, bool BKM, int EPI, int BKT, int S, int CONV = 0, int AUXO = -1>
 static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* cg = nullptr) {
   using C = Cfg<BKT, S>;
   // the kernels are specialised for the operand dtype each epilogue carries in the bf16 model
   if ((EPI == SV_EPI_MUL_AUX || EPI == SV_EPI_GELU_GRAD) && d->aux_dtype != SV_BF16) return SV_ERR_UNSUPPORTED;
-  if (EPI == SV_EPI_BIAS_GAMMA_RES && d->aux_dtype != SV_F32) return SV_ERR_UNSUPPORTED;
+  if (EPI == SV_EPI_BIAS_GAMMA_RES && d->aux_dtype != (AUXO >= 0 ? AUXO : SV_F32)) return SV_ERR_UNSUPPORTED;
   if (EPI == SV_EPI_STORE_BN_BWD && (d->aux_dtype != SV_BF16 || !d->bn || d->c_dtype != SV_BF16)) return SV_ERR_UNSUPPORTED;
   constexpr int OCC = C::TWO_PER_CU ? 4 : 2;
   const int kper = ceil_div(ceil_div(d->K, split), BKT) * BKT;
@@ -454,12 +457,12 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s, const ConvG* 
     e.rm_ghw_shift = cg->ghw_shift;
     e.rm_prow = ceil_div(d->M, 64);
   }
-  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV>), (int)C::LDS, s)) return rc_;
+  if (const int rc_ = ensure_lds_attr(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV, AUXO>), (int)C::LDS, s)) return rc_;
   // one workgroup per tile, which lets kernels of the side stream take CUs as tiles retire
   const int total = tilesM * tilesN * split;
   // (policy.wg_per_cu: co-residency with a concurrent GEMM; policy.grid_cap: persistent over the rest)
   const int grid = policy_grid(&d->policy, total, 0, s);
-  gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV><<<grid, THREADS, C::LDS, s>>>(
+  gemm3_kernel<AK, BKM, EPI, BKT, S, OCC, CONV, AUXO><<<grid, THREADS, C::LDS, s>>>(
       reinterpret_cast<const uint16_t*>(d->A), d->lda, reinterpret_cast<const uint16_t*>(d->B), d->ldb, d->K, kper,
       tilesM, tilesN, split, e, d->epilogue == SV_EPI_SLAB ? reinterpret_cast<float*>(d->C2) : nullptr,
       cg ? *cg : ConvG{});
@@ -505,8 +508,9 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   if (mode == 1 && d->epilogue == SV_EPI_STORE_STATS)
     return launch<true, true, SV_EPI_STORE_STATS, 32, S, 1>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 2>(d, 1, s, &g);
-  if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
-    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 2>(d, 1, s, &g);
+  if (mode == 2 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)  // in-place accumulate into an f32 or a bf16 dx
+    return d->aux_dtype == SV_BF16 ? launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 2, SV_BF16>(d, 1, s, &g)
+                                   : launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 2>(d, 1, s, &g);
   if (mode == 2 && d->epilogue == SV_EPI_STORE_BN_BWD)
     return launch<true, false, SV_EPI_STORE_BN_BWD, 32, S, 2>(d, 1, s, &g);
   // split-K fprop / dgrad for grids below one workgroup per CU: f32 slabs, summed by sv_gemm_slab_finish
@@ -521,7 +525,8 @@ static int conv_fd(const sv_gemm_desc* d, const ConvG& g, int mode, hipStream_t 
   const int ncls = d->split_k >= 1 && d->split_k <= 4 ? d->split_k : 4;
   if (mode == 5 && d->epilogue == SV_EPI_STORE) return launch<true, false, SV_EPI_STORE, 32, S, 5>(d, ncls, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_BIAS_GAMMA_RES)
-    return launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5>(d, ncls, s, &g);
+    return d->aux_dtype == SV_BF16 ? launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5, SV_BF16>(d, ncls, s, &g)
+                                   : launch<true, false, SV_EPI_BIAS_GAMMA_RES, 32, S, 5>(d, ncls, s, &g);
   if (mode == 5 && d->epilogue == SV_EPI_STORE_BN_BWD)
     return launch<true, false, SV_EPI_STORE_BN_BWD, 32, S, 5>(d, 4, s, &g);
   // 8-channel pixels (the ResNet stem), plain store or with the BatchNorm statistics

@@ -1090,8 +1090,9 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
                  lda=s.Cout, ldb=s.Cs, C=dx.view(M, s.Cs), compute_bf16=True, policy=policy)
         return dx
     T = s.KH * s.KW
-    if (wp.dtype == torch.bfloat16 and s.stride == 1 and s.Cout >= 32 and s.Cs % 8 == 0
-            and (not accumulate or dx.dtype == torch.float32) and (T * s.Cout) % 32 == 0):
+    # (a bf16 dx accumulates here too -- the ResNet gradient stream: the sum in f32, stored bf16 -- rather than in
+    # the pointwise path above, whose residual epilogue reads an f32 operand)
+    if (wp.dtype == torch.bfloat16 and s.stride == 1 and s.Cout >= 32 and s.Cs % 8 == 0 and (T * s.Cout) % 32 == 0):
         M = s.B * s.H * s.W
         split = _conv_split(M, s.Cs, T * s.Cout)
         if split > 1:
@@ -1105,7 +1106,7 @@ def conv_bwd_data(dy: torch.Tensor, wp: torch.Tensor, s: nv.ConvShape, *, dx: to
         # without a split: the one-launch form stores each class's rows straight into dx (no workspace)
         M = s.B * s.H * s.W
         split = _s2_split(s, M, T)
-        if split == 1 and _s2_direct(s) and (not accumulate or dx.dtype == torch.float32):
+        if split == 1 and _s2_direct(s):
             call("sv_conv_bwd_data", ptr(dy), ptr(wp), ptr(dx), dt(dx), int(accumulate), dt(wp), ctypes.byref(s),
                  nv.pol_ref(policy))
             return dx
@@ -1337,7 +1338,7 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     """BatchNorm backward with an optional ReLU mask on dout; dgamma/dbeta accumulate.  The mask is
     act > 0, or -- ``relu_beta`` = the BN's beta, for a BN followed by its own ReLU -- recomputed from y
     like the forward's pre-activation (sv_bn_relu_bwd_*: the activation is not read again).
-    ``mask_inplace`` (act form, f32 dout): the statistics pass overwrites dout with the masked gradient
+    ``mask_inplace`` (act form, f32 or bf16 dout): the statistics pass overwrites dout with the masked gradient
     (sv_bn_bwd_stats_mask), which the apply pass then reads without the mask and the caller keeps as the
     shortcut's gradient; ``gmask`` instead writes it to a separate f32 buffer from the apply pass.
     ``batch_stats``: train mode (mean / rstd are the batch's own, so dx carries the two mean corrections);
@@ -1354,8 +1355,8 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
         _check(gmask.dtype == torch.float32 and gmask.numel() == rows * C and relu_beta is None,
                "bn_bwd: gmask must be f32 [rows,C] (act-mask form only)")
     if mask_inplace:
-        _check(act is not None and gmask is None and dout2d.dtype == torch.float32,
-               "bn_bwd: mask_inplace needs act, an f32 dout and no gmask")
+        _check(act is not None and gmask is None and dout2d.dtype in (torch.float32, torch.bfloat16),
+               "bn_bwd: mask_inplace needs act, an f32 / bf16 dout and no gmask")
     given = part is not None
     if given:
         _check(relu_beta is not None and part.dtype == torch.float32 and part.is_contiguous() and part.dim() == 3
@@ -1380,8 +1381,8 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
         call("sv_bn_relu_bwd_stats", ptr(dout2d), dt(dout2d), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma),
              ptr(relu_beta), rows, C, ptr(part))
     elif mask_inplace:
-        call("sv_bn_bwd_stats_mask", ptr(dout2d), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
-             rows, C, ptr(part))
+        call("sv_bn_bwd_stats_mask", ptr(dout2d), dt(dout2d), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), rows, C, ptr(part))
         act = None  # dout now holds the masked gradient
     else:
         call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
@@ -1404,10 +1405,10 @@ def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dg
                 dgamma2=None, dbeta2=None, dx_dtype=torch.float32, batch_stats: bool = True):
     """A projection-shortcut block's two output BatchNorms from one masked gradient: equals
     ``bn_bwd(gm, y2d, ..., act=act, mask_inplace=True)`` followed by ``bn_bwd(gm, y2, mean2, rstd2, gamma2)``
-    bit for bit (gm, f32, is overwritten with the masked gradient the same way), with gm read once per pass
+    bit for bit (gm, f32 or bf16, is overwritten with the masked gradient the same way), with gm read once per pass
     instead of twice (sv_bn_bwd_stats_mask_dual / sv_bn_bwd_apply_dual). -> (dx, dx2)."""
     rows, C = y2d.shape
-    _check(_bn_c_ok(C) and gm.dtype == torch.float32 and gm.numel() == rows * C and gm.is_contiguous()
+    _check(_bn_c_ok(C) and gm.dtype in (torch.float32, torch.bfloat16) and gm.numel() == rows * C and gm.is_contiguous()
            and act.numel() == rows * C and act.is_contiguous() and y2.numel() == rows * C and y2.is_contiguous(),
            "bn_bwd_dual: bad shapes")
     if bn_small_ok(rows, C) and _bn_small_args_ok(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, dgamma,
@@ -1420,8 +1421,8 @@ def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dg
         return dx, dx2
     P = value("sv_bn_nparts", rows, C)
     part = torch.empty(2, P, 2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_bwd_stats_mask_dual", ptr(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(y2),
-         dt(y2), ptr(mean2), ptr(rstd2), rows, C, ptr(part[0]), ptr(part[1]))
+    call("sv_bn_bwd_stats_mask_dual", ptr(gm), dt(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
+         ptr(y2), dt(y2), ptr(mean2), ptr(rstd2), rows, C, ptr(part[0]), ptr(part[1]))
     sums = torch.empty(2, 2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_finish", ptr(part[0]), P, C, ptr(sums[0]), ptr(dgamma), ptr(dbeta))
     call("sv_bn_bwd_finish", ptr(part[1]), P, C, ptr(sums[1]), ptr(dgamma2), ptr(dbeta2))
@@ -1429,8 +1430,8 @@ def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dg
         sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
     dx2 = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
-    call("sv_bn_bwd_apply_dual", ptr(gm), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums[0]), ptr(y2),
-         dt(y2), ptr(mean2), ptr(rstd2), ptr(gamma2), ptr(sums[1]), ptr(dx), ptr(dx2), dt(dx), rows, C)
+    call("sv_bn_bwd_apply_dual", ptr(gm), dt(gm), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums[0]),
+         ptr(y2), dt(y2), ptr(mean2), ptr(rstd2), ptr(gamma2), ptr(sums[1]), ptr(dx), ptr(dx2), dt(dx), rows, C)
     return dx, dx2
 
 
@@ -1440,20 +1441,20 @@ def bn_relu_bwd_pooled(dpool4d: torch.Tensor, idx: torch.Tensor, H: int, W: int,
     backward: both BatchNorm passes gather it from dpool / idx (sv_bn_relu_bwd_*_pool), bit for bit."""
     B, OH, OW, C = dpool4d.shape
     rows = y2d.shape[0]
-    _check(dpool4d.dtype == torch.float32 and dpool4d.is_contiguous() and idx.shape == dpool4d.shape
+    _check(dpool4d.dtype in (torch.float32, torch.bfloat16) and dpool4d.is_contiguous() and idx.shape == dpool4d.shape
            and idx.is_contiguous() and (OH, OW) == conv_out_hw(H, W, 3, 2, 1) and rows == B * H * W
            and y2d.shape[1] == C and _bn_c_ok(C), "bn_relu_bwd_pooled: shape mismatch")
     P = value("sv_bn_nparts", rows, C)
     part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_relu_bwd_stats_pool", ptr(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
-         ptr(gamma), ptr(beta), C, ptr(part))
+    call("sv_bn_relu_bwd_stats_pool", ptr(dpool4d), dt(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean),
+         ptr(rstd), ptr(gamma), ptr(beta), C, ptr(part))
     sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
     if not batch_stats:
         sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
-    call("sv_bn_relu_bwd_apply_pool", ptr(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
-         ptr(gamma), ptr(beta), ptr(sums), ptr(dx), dt(dx), C)
+    call("sv_bn_relu_bwd_apply_pool", ptr(dpool4d), dt(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean),
+         ptr(rstd), ptr(gamma), ptr(beta), ptr(sums), ptr(dx), dt(dx), C)
     return dx
 
 
@@ -1484,10 +1485,10 @@ def avgpool_fwd(x4d: torch.Tensor) -> torch.Tensor:
     return feat
 
 
-def avgpool_bwd(dfeat: torch.Tensor, shape: tuple) -> torch.Tensor:
+def avgpool_bwd(dfeat: torch.Tensor, shape: tuple, dx_dtype=torch.float32) -> torch.Tensor:
     B, H, W, C = shape
     dfeat = dfeat.float().contiguous()
     _check(tuple(dfeat.shape) == (B, C), "avgpool_bwd: dfeat shape")
-    dx = torch.empty(B, H, W, C, device=dfeat.device, dtype=torch.float32)
-    call("sv_avgpool_bwd", ptr(dfeat), ptr(dx), B, H * W, C)
+    dx = torch.empty(B, H, W, C, device=dfeat.device, dtype=dx_dtype)
+    call("sv_avgpool_bwd", ptr(dfeat), ptr(dx), dt(dx), B, H * W, C)
     return dx

@@ -172,14 +172,15 @@ _SIGS = {
     "sv_bn_eval_params": [_p, _p, _f32, _p, _p, _i32, _p],
     "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
-    "sv_bn_bwd_stats_mask": [_p, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
+    "sv_bn_bwd_stats_mask": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
-    "sv_bn_bwd_stats_mask_dual": [_p, _p, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p, _p, _p],
-    "sv_bn_bwd_apply_dual": [_p, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
+    "sv_bn_bwd_stats_mask_dual": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p, _p, _p],
+    "sv_bn_bwd_apply_dual": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32,
+                             _p],
     "sv_bn_relu_bwd_stats": [_p, _i32, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_relu_bwd_apply": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32, _p],
-    "sv_bn_relu_bwd_stats_pool": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _i32, _p, _p],
-    "sv_bn_relu_bwd_apply_pool": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
+    "sv_bn_relu_bwd_stats_pool": [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _i32, _p, _p],
+    "sv_bn_relu_bwd_apply_pool": [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i32, _p],
     "sv_bn_bwd_apply": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _i64, _i32, _p],
     "sv_bn_small_ok": [_i64, _i32],
     "sv_bn_bwd_small": [_i32, _p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _p,
@@ -190,7 +191,7 @@ _SIGS = {
     "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_maxpool3s2_bwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_avgpool_fwd": [_p, _i32, _p, _i32, _i32, _i32, _p],
-    "sv_avgpool_bwd": [_p, _p, _i32, _i32, _i32, _p],
+    "sv_avgpool_bwd": [_p, _p, _i32, _i32, _i32, _i32, _p],
 }
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}

@@ -281,6 +281,57 @@ def test_conv_s2_direct_matches_scatter(dev, case):
     assert rel((out[True][2] - base).permute(0, 3, 1, 2), ref) < 1e-5
 
 
+DGRAD_ACC_CASES = [
+    # B, H, W, Cs, Cout, k, stride, pad, split?  -- the ResNet bf16 gradient stream's dx += conv^T(dy) shapes
+    (2, 16, 16, 64, 256, 1, 1, 0, False),    # bottleneck conv1 dgrad onto the shortcut gradient: gathered, mode 2
+    (4, 64, 64, 256, 1024, 1, 1, 0, True),   # the same, split-K: slabs + slab_finish reading dx bf16
+    (2, 16, 16, 64, 64, 3, 1, 1, False),     # 3x3 stride 1
+    (2, 14, 10, 64, 256, 3, 1, 1, True),     # 3x3 stride 1, split-K
+    (2, 16, 16, 256, 512, 1, 2, 0, False),   # projection shortcut 1x1 stride 2: one-launch parity classes
+    (2, 16, 16, 64, 128, 3, 2, 1, False),    # 3x3 stride 2, direct into dx
+    (2, 15, 13, 64, 64, 3, 2, 1, False),     # odd grid: compact slabs + the scatter pass adding onto dx bf16
+]
+
+
+def _bf16_ulp(v: torch.Tensor) -> torch.Tensor:
+    _, e = torch.frexp(v.double())
+    return torch.ldexp(torch.ones_like(v, dtype=torch.float64), (e - 8).clamp(min=-133))
+
+
+@pytest.mark.parametrize("case", DGRAD_ACC_CASES, ids=lambda c: "x".join(map(str, c[:8])) + ("_split" if c[8] else ""))
+def test_conv_dgrad_accumulate_bf16(dev, case):
+    """conv_bwd_data(accumulate=True) onto a bf16 dx (the ResNet bf16 gradient stream): the sum
+    dx + conv^T(dy) formed in f32 from the stored bf16 dx and rounded to bf16 once -- so within one bf16 ulp
+    of the float64 sum of the same bf16 operands, and equal to the f32 accumulate path rounded to bf16 except
+    where an f32 ordering difference crosses a rounding boundary (the two paths may take different GEMMs)."""
+    B, H, W, Cs, Cout, k, st, pad, want_split = case
+    g = torch.Generator().manual_seed(B * H * W + Cs + Cout + k)
+    s = K.conv_shape(B, H, W, Cs, Cout, k, st, pad)
+    OH, OW = K.conv_out_hw(H, W, k, st, pad)
+    M, T = B * H * W, k * k
+    if st == 1:
+        assert (K._conv_split(M, Cs, T * Cout) > 1) == want_split, "case must take the intended path"
+    w = (torch.randn(Cout, Cs, k, k, generator=g) * (1.0 / (Cs * k * k)) ** 0.5).to(torch.bfloat16).float()
+    wp = K.conv_weight_pack(w.to(dev), Cs, torch.bfloat16)
+    dy = torch.randn(B, OH, OW, Cout, generator=g).to(torch.bfloat16).to(dev)
+    base = torch.randn(B, H, W, Cs, generator=g).to(torch.bfloat16).to(dev)
+    acc16 = base.clone()
+    K.conv_bwd_data(dy, wp, s, dx=acc16, accumulate=True)
+    acc32 = base.float()
+    K.conv_bwd_data(dy, wp, s, dx=acc32, accumulate=True)
+    torch.cuda.synchronize()
+    assert acc16.dtype == torch.bfloat16
+    oh_ = H - ((OH - 1) * st - 2 * pad + k)
+    ow_ = W - ((OW - 1) * st - 2 * pad + k)
+    ref = F.conv_transpose2d(dy.double().cpu().permute(0, 3, 1, 2), w.double(), stride=st, padding=pad,
+                             output_padding=(oh_, ow_)).permute(0, 2, 3, 1) + base.double().cpu()
+    out = acc16.double().cpu()
+    err = (out - ref).abs()
+    assert bool((err <= _bf16_ulp(ref) + 1e-6 * ref.abs().max()).all()), float(err.max())
+    same = (acc16 == acc32.to(torch.bfloat16)).double().mean().item()
+    assert same > 0.99, same
+
+
 @pytest.mark.parametrize("C", [64, 256, 2048])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_batchnorm_train_fwd_bwd(dev, C, precision):
@@ -352,7 +403,8 @@ def test_bn_relu_bwd_recomputed_mask_matches_act_mask(dev, C, precision):
 
 @pytest.mark.parametrize("B,H,W,C,dt_", [(32, 128, 128, 64, torch.bfloat16), (2, 33, 30, 64, torch.bfloat16),
                                           (3, 17, 21, 12, torch.float32), (2, 64, 64, 64, torch.float32)])
-def test_bn_relu_bwd_pooled_matches_maxpool_then_bn(dev, B, H, W, C, dt_):
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16], ids=["f32grad", "bf16grad"])
+def test_bn_relu_bwd_pooled_matches_maxpool_then_bn(dev, B, H, W, C, dt_, gdt):
     """The stem's BatchNorm backward with the max-pool backward gathered inside its two passes
     (sv_bn_relu_bwd_*_pool) is bit for bit sv_maxpool3s2_bwd followed by the relu_beta BatchNorm
     backward: dx, dgamma, dbeta.  32 x 128^2 x 64 is ResNet-50's stem at 256^2, bs32; the odd sizes take
@@ -365,10 +417,10 @@ def test_bn_relu_bwd_pooled_matches_maxpool_then_bn(dev, B, H, W, C, dt_):
     a = K.bn_act(y, mean, rstd, gam, bet, relu=True, out_dtype=dt_).view(B, H, W, C)
     _, idx = K.maxpool_fwd(a)
     OH, OW = idx.shape[1], idx.shape[2]
-    d = torch.randn(B, OH, OW, C, generator=g).to(dev)
+    d = torch.randn(B, OH, OW, C, generator=g).to(dev, gdt)  # bf16grad: the pooled gradient as the bf16 stream
     dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-    da = K.maxpool_bwd(d, idx, H, W, dx_dtype=torch.float32)
+    da = K.maxpool_bwd(d.float(), idx, H, W, dx_dtype=torch.float32)
     dx1 = K.bn_bwd(da.view(-1, C), y, mean, rstd, gam, relu_beta=bet, dgamma=dg1, dbeta=db1, dx_dtype=dt_)
     dx2 = K.bn_relu_bwd_pooled(d, idx, H, W, y, mean, rstd, gam, bet, dgamma=dg2, dbeta=db2, dx_dtype=dt_)
     torch.cuda.synchronize()
@@ -390,36 +442,40 @@ def test_conv_weight_pack_multi_matches_single(dev, dtype):
         assert torch.equal(wp, K.conv_weight_pack(w, cs, dtype))
 
 
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16], ids=["f32grad", "bf16grad"])
 @pytest.mark.parametrize("rows,C", [(131072, 256), (4099, 12), (2048, 2048), (3000, 64)])
-def test_bn_bwd_mask_inplace_matches_gmask(dev, rows, C):
+def test_bn_bwd_mask_inplace_matches_gmask(dev, rows, C, gdt):
     """sv_bn_bwd_stats_mask (the block output's masked gradient written over dout by the statistics
     pass, the apply pass then reading it unmasked) is bit for bit the gmask form: dx, dgamma, dbeta and
-    the masked gradient.  rows = 131072 x C = 256 is ResNet-50 layer1 at 256^2, bs32 (1024 partials)."""
+    the masked gradient.  rows = 131072 x C = 256 is ResNet-50 layer1 at 256^2, bs32 (1024 partials).
+    bf16grad: the ResNet bf16 gradient stream -- dout bf16, the masked gradient written back bf16 (exact:
+    a mask of bf16 values), every sum in f32 on the same values as the f32 form of that dout."""
     g = torch.Generator().manual_seed(rows + C)
     y = torch.randn(rows, C, generator=g).to(dev, torch.bfloat16)
     gam = (torch.rand(C, generator=g) + 0.5).to(dev)
     bet = (torch.randn(C, generator=g) * 0.3).to(dev)
     mean, rstd = K.bn_stats(y)
     a = K.bn_act(y, mean, rstd, gam, bet, relu=True, out_dtype=torch.bfloat16)
-    dout = torch.randn(rows, C, generator=g).to(dev)
+    dout = torch.randn(rows, C, generator=g).to(dev, gdt).float()
     dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     gm = torch.empty(rows, C, device=dev)
     dx1 = K.bn_bwd(dout, y, mean, rstd, gam, act=a, dgamma=dg1, dbeta=db1, dx_dtype=torch.bfloat16, gmask=gm)
-    d2 = dout.clone()
+    d2 = dout.to(gdt)
     dx2 = K.bn_bwd(d2, y, mean, rstd, gam, act=a, dgamma=dg2, dbeta=db2, dx_dtype=torch.bfloat16,
                    mask_inplace=True)
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
-    assert torch.equal(d2, gm) and torch.equal(gm, dout * (a > 0).float())
+    assert torch.equal(d2.float(), gm) and torch.equal(gm, dout * (a > 0).float())
     # the finish over many partials against a float64 sum of the masked gradient
     g64 = (dout * (a > 0).float()).double()
     assert rel(db1, g64.sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16], ids=["f32grad", "bf16grad"])
 @pytest.mark.parametrize("rows,C,dt_", [(4099, 256, torch.bfloat16), (2 * 64 * 64, 256, torch.bfloat16),
                                         (1000, 2048, torch.bfloat16), (515, 12, torch.float32)])
-def test_bn_bwd_dual_matches_two_passes(dev, rows, C, dt_):
+def test_bn_bwd_dual_matches_two_passes(dev, rows, C, dt_, gdt):
     """bn_bwd_dual (a projection-shortcut block's main and shortcut output BatchNorms from one masked gradient,
     one statistics and one apply pass) is bit for bit bn_bwd(mask_inplace) then bn_bwd of the shortcut: the
     masked gradient written over gm, both data gradients, dgamma / dbeta of both.  C = 12 takes the 4-channel
@@ -432,16 +488,16 @@ def test_bn_bwd_dual_matches_two_passes(dev, rows, C, dt_):
     m1, r1 = K.bn_stats(y)
     m2, r2 = K.bn_stats(yd)
     out = K.bn_act(y, m1, r1, gam, bet, res=yd, res_bn=(m2, r2, gd, bd), relu=True, out_dtype=dt_)
-    d0 = torch.randn(rows, C, generator=g).to(dev)
+    d0 = torch.randn(rows, C, generator=g).to(dev, gdt)  # bf16grad: the masked gradient written back bf16
     grads = [torch.zeros(C, device=dev) for _ in range(8)]
-    ga = d0.clone()
+    ga = d0.float()
     dx1 = K.bn_bwd(ga, y, m1, r1, gam, act=out, dgamma=grads[0], dbeta=grads[1], dx_dtype=dt_, mask_inplace=True)
     dx2 = K.bn_bwd(ga, yd, m2, r2, gd, dgamma=grads[2], dbeta=grads[3], dx_dtype=dt_)
     gb = d0.clone()
     ex1, ex2 = K.bn_bwd_dual(gb, y, m1, r1, gam, out, yd, m2, r2, gd, dgamma=grads[4], dbeta=grads[5],
                              dgamma2=grads[6], dbeta2=grads[7], dx_dtype=dt_)
     torch.cuda.synchronize()
-    assert torch.equal(ga, gb) and torch.equal(dx1, ex1) and torch.equal(dx2, ex2)
+    assert torch.equal(ga, gb.float()) and torch.equal(dx1, ex1) and torch.equal(dx2, ex2)
     for a, b in zip(grads[:4], grads[4:]):
         assert torch.equal(a, b)
 
@@ -476,6 +532,9 @@ def test_maxpool_avgpool(dev, shape):
     df = _rand((B, C), 19).float()
     dxa = K.avgpool_bwd(df.to(dev), (B, H, W, C))
     assert rel(dxa.permute(0, 3, 1, 2), (df / (H * W))[:, :, None, None].expand(B, C, H, W)) < 1e-6
+    # the bf16 gradient stream's head: the same f32 quotient rounded once
+    dxb = K.avgpool_bwd(df.to(dev), (B, H, W, C), dx_dtype=torch.bfloat16)
+    assert dxb.dtype == torch.bfloat16 and torch.equal(dxb, dxa.to(torch.bfloat16))
 
 
 def _pair(name, precision, dev):
@@ -592,6 +651,7 @@ def test_resnet_block_backward_teacher_forced(dev, name, precision, B, R):
         rbc = copy.deepcopy(rb)
         o = rbc(xr)
         d = torch.randn(o.shape, generator=torch.Generator().manual_seed(i))
+        d = d.to(hip.grad_dtype).float()  # the bf16 gradient stream hands blocks a bf16 output gradient
         o.backward(d)
         # train-mode BN backward subtracts batch means: the fp32 oracle block itself is measurably off
         # float64 at large B*H*W, so fp32 is held to max(1e-3, 3x the fp32 oracle's own error)
@@ -601,7 +661,7 @@ def test_resnet_block_backward_teacher_forced(dev, name, precision, B, R):
         rb64(x64).backward(d.double())
         for p in hb.parameters():
             p.grad = torch.zeros_like(p)
-        dx = hip._block_backward(hb, sb, d.permute(0, 2, 3, 1).contiguous().to(dev))
+        dx = hip._block_backward(hb, sb, d.permute(0, 2, 3, 1).contiguous().to(dev, hip.grad_dtype))
         # fp32: the HIP error against float64; bf16: against the fp32 oracle
         hp = dict(hb.named_parameters())
         p64 = dict(rb64.named_parameters())

@@ -39,7 +39,7 @@ for name, B, R in [("resnet18", 4, 64), ("resnet18", 16, 128), ("resnet50", 8, 1
             o.backward(d)
             for p in hb.parameters():
                 p.grad = torch.zeros_like(p)
-            dx = hip._block_backward(hb, sb, d.permute(0, 2, 3, 1).contiguous().cuda())
+            dx = hip._block_backward(hb, sb, d.permute(0, 2, 3, 1).contiguous().cuda().to(hip.grad_dtype))
             e_dx = rel(dx.permute(0, 3, 1, 2), xr.grad)
             hp = dict(hb.named_parameters())
             e_p = {n: rel(hp[n].grad, p.grad) for n, p in rbc.named_parameters()}
