@@ -506,10 +506,15 @@ int sv_image_to_nhwc(const float* img, void* out, int32_t dtype, int32_t B, int3
 int sv_bn_nparts(int64_t rows, int32_t C);
 int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t C, float* part, sv_stream_t stream);
 /* num_batches_tracked (int64, nullable): incremented by one on the device (BatchNorm2d.num_batches_tracked).
- * y == NULL: `part` holds UNSHIFTED sums (the SV_EPI_STORE_STATS / sv_conv_fwd_stats partials).   */
+ * y == NULL: `part` holds UNSHIFTED sums (the SV_EPI_STORE_STATS / sv_conv_fwd_stats partials).
+ * The fold of nparts partials runs in chunks of 1024 (each: 128 streams, then the streams in order; chunk sums in
+ * chunk order).  ctl / ws (ABI v7, nullable; SV_BN_FOLD_CTL_INTS zeroed int32 / SV_BN_FOLD_WS_FLOATS f32, one pair
+ * per stream, as the fold kernels below): one workgroup per chunk and channel group instead of one per channel
+ * group (the stem's 8192 partials: 43 us as one), the last to finish adding the chunk sums -- the same bits.  Same
+ * for sv_bn_bwd_finish.                                                                            */
 int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows, int32_t C,
                        float eps, float momentum, float* mean, float* rstd, float* running_mean,
-                       float* running_var, int64_t* num_batches_tracked, sv_stream_t stream);
+                       float* running_var, int64_t* num_batches_tracked, int32_t* ctl, float* ws, sv_stream_t stream);
 /* eval mode: mean = running_mean, rstd = 1/sqrt(running_var + eps).                               */
 int sv_bn_eval_params(const float* running_mean, const float* running_var, float eps, float* mean, float* rstd,
                       int32_t C, sv_stream_t stream);
@@ -535,7 +540,7 @@ int sv_bn_bwd_stats_mask(void* dout, int32_t dout_dtype, const void* act, int32_
                          int32_t y_dtype, const float* mean, const float* rstd, int64_t rows, int32_t C, float* part,
                          sv_stream_t stream);
 int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
-                     sv_stream_t stream);
+                     int32_t* ctl, float* ws, sv_stream_t stream);
 /* A residual block with a projection shortcut (timm Bottleneck's downsample): the block output's gradient
  * dout feeds the main path's last BatchNorm (y, mean, rstd) and the shortcut's (y2, mean2, rstd2) through
  * one ReLU mask.  One statistics pass writes g = dout * (act > 0) over dout and both BatchNorms' partials
@@ -607,6 +612,38 @@ int sv_bn_act_small(const void* y, int32_t y_dtype, const float* part, int32_t n
                     const float* res_gamma, const float* res_beta, float* res_mean, float* res_rstd,
                     float* res_running_mean, float* res_running_var, int64_t* res_num_batches_tracked, int32_t relu,
                     void* out, int32_t out_dtype, int64_t rows, int32_t C, sv_stream_t stream);
+/* The statistics fold inside the consuming pass (ABI v7): one launch fewer per BatchNorm at any row count.
+ *   sv_bn_act_fold       = sv_bn_stats_finish(y = NULL, part) [+ the shortcut's] + sv_bn_act_fwd; arguments as
+ *                          sv_bn_act_small (nparts = ceil(rows / 64), the conv epilogue's; res_nparts equal).
+ *   sv_bn_bwd_apply_fold = sv_bn_bwd_finish [x2] + the apply pass, after the statistics pass (or the dgrad
+ *                          epilogue) wrote `part` [nparts][2][C] (and `part2`):
+ *                          mode SV_BN_SMALL_MASK: sv_bn_bwd_apply(dout = the masked gradient, act = NULL)
+ *                          mode SV_BN_SMALL_RELU: sv_bn_relu_bwd_apply; pool_idx != NULL: sv_bn_relu_bwd_apply_pool
+ *                                                 (dout = the pooled gradient, the BN input pool_H x pool_W)
+ *                          mode SV_BN_SMALL_DUAL: sv_bn_bwd_apply_dual (dout = g; part2 the shortcut's partials)
+ *                          batch_stats == 0: eval-mode apply (dgamma / dbeta still accumulate)
+ * Bit for bit the multi-launch results.  ctl: SV_BN_FOLD_CTL_INTS int32, zero before the first launch and left
+ * zero by every launch (ctl[3] != 0 flags a poll that timed out); ws: SV_BN_FOLD_WS_FLOATS f32 scratch.  One
+ * (ctl, ws) per stream: two fold launches must not run at once on one pair.  sv_bn_fold_ok: 1 when (rows, C,
+ * nparts) has the fold kernels' geometry (C a power of two in 32..2048, nparts <= 16384).
+ * Replaces: timm Bottleneck BatchNorm2d forward + autograd backward (backbone.py:166 -> timm resnet.py).      */
+#define SV_BN_FOLD_CTL_INTS 256
+#define SV_BN_FOLD_WS_FLOATS (2 * 2 * 2048 + 2 * 64 * 16 * 64)
+int sv_bn_fold_ok(int64_t rows, int32_t C, int32_t nparts);
+int sv_bn_act_fold(const void* y, int32_t y_dtype, const float* part, int32_t nparts, float eps, float momentum,
+                   const float* gamma, const float* beta, float* mean, float* rstd, float* running_mean,
+                   float* running_var, int64_t* num_batches_tracked, const void* res, int32_t res_dtype,
+                   const float* res_part, int32_t res_nparts, float res_eps, float res_momentum,
+                   const float* res_gamma, const float* res_beta, float* res_mean, float* res_rstd,
+                   float* res_running_mean, float* res_running_var, int64_t* res_num_batches_tracked, int32_t relu,
+                   void* out, int32_t out_dtype, int64_t rows, int32_t C, int32_t* ctl, float* ws, sv_stream_t stream);
+int sv_bn_bwd_apply_fold(int32_t mode, const void* dout, int32_t dout_dtype, const uint8_t* pool_idx, int32_t pool_H,
+                         int32_t pool_W, const void* y, int32_t y_dtype, const float* mean, const float* rstd,
+                         const float* gamma, const float* beta, const void* y2, int32_t y2_dtype, const float* mean2,
+                         const float* rstd2, const float* gamma2, const float* part, const float* part2,
+                         int32_t nparts, void* dx, void* dx2, int32_t dx_dtype, float* dgamma, float* dbeta,
+                         float* dgamma2, float* dbeta2, int32_t batch_stats, int64_t rows, int32_t C, int32_t* ctl,
+                         float* ws, sv_stream_t stream);
 /* g = dout * (act > 0), f32 out (block-output ReLU of the residual join).                         */
 int sv_relu_mask(const void* dout, int32_t dout_dtype, const void* act, int32_t act_dtype, float* g, int64_t n,
                  sv_stream_t stream);

@@ -254,10 +254,13 @@ class ResNetHip(nn.Module):
         return K.bn_eval_params(bn.running_mean, bn.running_var, bn.eps)
 
     def _small_bn(self, y4d: torch.Tensor, part: torch.Tensor | None) -> bool:
-        """Train-mode BatchNorm whose statistics partials the conv produced and whose rows are few enough for the
-        one-launch form (K.bn_act_small)."""
-        return (self.training and part is not None and K.bn_small_ok(y4d.numel() // y4d.shape[-1], y4d.shape[-1])
-                and part.data_ptr() % 16 == 0)
+        """Train-mode BatchNorm whose statistics partials the conv produced, in a shape that K.bn_act_partials
+        serves in one launch: the one-workgroup-per-8-channels form (rows <= 8192, SV_BN_SMALL) or the fold kernels
+        (the fold inside the activation pass, SV_BN_FOLD)."""
+        if not (self.training and part is not None and part.data_ptr() % 16 == 0):
+            return False
+        rows, C = y4d.numel() // y4d.shape[-1], y4d.shape[-1]
+        return K.bn_small_ok(rows, C) or K.bn_fold_ok(rows, C, part.shape[0])
 
     @staticmethod
     def _bn_params(bn: nn.BatchNorm2d) -> tuple:
@@ -353,8 +356,12 @@ class ResNetHip(nn.Module):
                 [(w.detach(), c) for w, c in ws], act))}
         y0, wp0, s0, p0 = self._conv(x0, self.conv1, 7, 2, 3, Cin=3, packed=packed)
         B, H, W, C = y0.shape
-        m0, r0 = self._bn(self.bn1, y0.view(-1, C), p0)
-        a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act).view(B, H, W, C)
+        if self._small_bn(y0, p0):
+            a0, m0, r0 = K.bn_act_partials(y0.view(-1, C), p0, self._bn_params(self.bn1), relu=True, out_dtype=act)
+        else:
+            m0, r0 = self._bn(self.bn1, y0.view(-1, C), p0)
+            a0 = K.bn_act(y0.view(-1, C), m0, r0, self.bn1.weight, self.bn1.bias, relu=True, out_dtype=act)
+        a0 = a0.view(B, H, W, C)
         x, idx = K.maxpool_fwd(a0)
         tape = _Tape(batch_stats=self.training) if save else None
         if save:
@@ -372,7 +379,7 @@ class ResNetHip(nn.Module):
                 small = self._small_bn(y, part)
                 if not last:
                     if small:  # statistics fold + BatchNorm + ReLU in one launch (bit for bit the two below)
-                        a, mean, rstd = K.bn_act_small(y.view(-1, Cq), part, self._bn_params(bn), relu=True,
+                        a, mean, rstd = K.bn_act_partials(y.view(-1, Cq), part, self._bn_params(bn), relu=True,
                                                        out_dtype=act)
                     else:
                         mean, rstd = self._bn(bn, y.view(-1, Cq), part)
@@ -395,7 +402,7 @@ class ResNetHip(nn.Module):
                 dconv, dbn = blk.downsample[0], blk.downsample[1]
                 yd, wpd, sd, pd = self._conv(x_in, dconv, 1, blk.stride, 0)
                 if last_part is not None and self._small_bn(yd, pd):
-                    out, m_last, r_last, md, rd = K.bn_act_small(
+                    out, m_last, r_last, md, rd = K.bn_act_partials(
                         y_last.view(-1, Cq), last_part, self._bn_params(bn_last), res=yd.view(-1, Cq), res_part=pd,
                         res_params=self._bn_params(dbn), relu=True, out_dtype=act)
                 else:
@@ -406,7 +413,7 @@ class ResNetHip(nn.Module):
                                    res=yd.view(-1, Cq), res_bn=(md, rd, dbn.weight, dbn.bias), relu=True, out_dtype=act)
                 ds_saved = (yd, md, rd, wpd, sd)
             elif last_part is not None:
-                out, m_last, r_last = K.bn_act_small(y_last.view(-1, Cq), last_part, self._bn_params(bn_last),
+                out, m_last, r_last = K.bn_act_partials(y_last.view(-1, Cq), last_part, self._bn_params(bn_last),
                                                      res=x_in.view(-1, Cq), relu=True, out_dtype=act)
             else:
                 out = K.bn_act(y_last.view(-1, Cq), m_last, r_last, bn_last.weight, bn_last.bias,

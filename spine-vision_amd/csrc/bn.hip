@@ -9,6 +9,7 @@
 // Batch statistics use shifted sums (shift = the channel's value in row 0) so mean^2 >> var does
 // not cancel catastrophically in f32.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -174,6 +175,13 @@ __global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict_
   reduce_write<V>(s1, s2, tpr, rp, c, C, part);
 }
 
+// 4-B stores / loads that bypass L1 and write through L2 (sc1): the hand-off of values between workgroups of one
+// launch (the fold kernels below), MI355X_MICROARCH.md's inter-workgroup table row 1
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Sum of the per-block partials [P][2][C] for kFinCh = 32 channels per workgroup.  Lane l of wave w
 // reads channels 4 (l & 7) .. +3 of its slice (one 16-B load per sum; 8 lanes cover a 128-B row
 // segment) from partials j, j + 128, j + 256, .. with j = 8 w + (l >> 3): 128 partial streams per
@@ -182,18 +190,47 @@ __global__ void __launch_bounds__(kThreads) stats_kernel(const void* __restrict_
 // version (64 channels per workgroup, lane = channel, one 4-B load per lane and sum) kept a quarter of
 // the bytes in flight on half the workgroups: 7-8 us per finish at P = 512-2048.
 constexpr int kFinWaves = 16, kFinCh = 32, kFinStreams = kFinWaves * 64 / (kFinCh / 4);
-__device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int P, int C, float& s1, float& s2,
-                                              int& c_out) {
+// Partials are folded in chunks of kFoldQ parts: each chunk as above (128 streams, then the streams in order), the
+// chunk sums then added in chunk order.  One chunk up to 1024 parts (every backward statistics pass, and the
+// one-launch small kernels, whose order is the single-chunk one); the forward's GEMM-epilogue partials of the
+// stem and layer 1 (one per 64 rows: 2048-8192) take 2-8 chunks, which the fold kernels below hand to as many
+// workgroups.
+constexpr int kFoldQ = 1024, kFoldMaxS = 16;
+__host__ __device__ __forceinline__ int fold_chunks(int P) { return (P + kFoldQ - 1) / kFoldQ; }
+
+// The 128 stream sums of parts [p0, p1) for channels 32 cg .. +31, folded in stream order by wave 0: lane l of
+// wave 0 returns sum (l >> 5) (0: of g or y, 1: of the second quantity) of channel 32 cg + (l & 31); other waves 0.
+// Every thread of the 1024-thread workgroup calls it (two barriers; the LDS is free again on return).
+__device__ __forceinline__ float fold_chunk(const float* __restrict__ part, int p0, int p1, int C, int cg) {
   __shared__ float red[2][kFinStreams][kFinCh];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane & 7, j = w * 8 + (lane >> 3);
-  const int c = blockIdx.x * kFinCh + 4 * q;
+  const int c = cg * kFinCh + 4 * q;
   float4 a1[4], a2[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) a1[u] = a2[u] = f4(0.f);
   if (c < C) {  // C % 4 == 0: a 4-channel group is wholly in or out
-    int p = j;
-    for (; p + 3 * kFinStreams < P; p += 4 * kFinStreams) {
+    int p = p0 + j;
+    // 8 partials (16 loads) in flight per lane, then 4, then 1: accumulator u still takes parts p + u S, p + (u + 4) S,
+    // .. in ascending order, so the sums are those of the 4-part loop (one HBM round trip per 8 parts, not per 4:
+    // the finishes of 2048 partials measured 14 us, four round trips)
+    for (; p + 7 * kFinStreams < p1; p += 8 * kFinStreams) {
+      float4 x1[8], x2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float* r = part + (size_t)(p + u * kFinStreams) * 2 * C + c;
+        x1[u] = ld4f(r, 0);
+        x2[u] = ld4f(r + C, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float4& b1 = a1[u & 3];
+        float4& b2 = a2[u & 3];
+        b1.x += x1[u].x; b1.y += x1[u].y; b1.z += x1[u].z; b1.w += x1[u].w;
+        b2.x += x2[u].x; b2.y += x2[u].y; b2.z += x2[u].z; b2.w += x2[u].w;
+      }
+    }
+    for (; p + 3 * kFinStreams < p1; p += 4 * kFinStreams) {
       float4 x1[4], x2[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -207,7 +244,7 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, in
         a2[u].x += x2[u].x; a2[u].y += x2[u].y; a2[u].z += x2[u].z; a2[u].w += x2[u].w;
       }
     }
-    for (; p < P; p += kFinStreams) {
+    for (; p < p1; p += kFinStreams) {
       const float* r = part + (size_t)p * 2 * C + c;
       const float4 x1 = ld4f(r, 0), x2 = ld4f(r + C, 0);
       a1[0].x += x1.x; a1[0].y += x1.y; a1[0].z += x1.z; a1[0].w += x1.w;
@@ -221,20 +258,65 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, in
   *reinterpret_cast<float4*>(&red[0][j][4 * q]) = t1;
   *reinterpret_cast<float4*>(&red[1][j][4 * q]) = t2;
   __syncthreads();
-  if (w != 0) return false;
-  const int which = lane >> 5, ch = lane & 31;
   float s = 0.f;
+  if (w == 0) {
+    const int which = lane >> 5, ch = lane & 31;
 #pragma unroll 16
-  for (int i = 0; i < kFinStreams; ++i) s += red[which][i][ch];
-  const float other = __shfl_xor(s, 32);
+    for (int i = 0; i < kFinStreams; ++i) s += red[which][i][ch];
+  }
+  __syncthreads();
+  return s;
+}
+
+// Sum of the per-block partials [P][2][C] for kFinCh = 32 channels per workgroup.  Lane l of wave w
+// reads channels 4 (l & 7) .. +3 of its slice (one 16-B load per sum; 8 lanes cover a 128-B row
+// segment) from partials j, j + 128, j + 256, .. with j = 8 w + (l >> 3): 128 partial streams per
+// workgroup, each lane with 4 partials (8 loads) in flight.  Wave 0 then folds the 128 stream sums in a
+// fixed order through LDS (lanes 0-31: S1, lanes 32-63: S2), so the result is bit-stable; chunks of kFoldQ parts
+// in chunk order.  Round 2's version (64 channels per workgroup, lane = channel, one 4-B load per lane and sum)
+// kept a quarter of the bytes in flight on half the workgroups: 7-8 us per finish at P = 512-2048.
+// Split form (gridDim.y = the chunk count, cnt / ws given): workgroup (x, y) folds chunk y of channel group x, stores
+// its 64 sums write-through (sc1) and adds one to cnt[x] once that wave's stores are complete; the workgroup whose
+// add returns S - 1 reads the S chunk sums (sc1 loads), adds them in chunk order -- the sequential form's bits -- and
+// re-arms cnt[x] (MICROARCH inter-workgroup table row 1: the last adder told by its add's return value).
+__device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int P, int C, float& s1, float& s2,
+                                              int& c_out, int* cnt = nullptr, float* ws = nullptr) {
+  const int S = fold_chunks(P);
+  float tot = 0.f;
+  if (gridDim.y == 1) {
+    for (int k = 0; k < S; ++k) {
+      const int p0 = k * kFoldQ, p1 = p0 + kFoldQ < P ? p0 + kFoldQ : P;
+      const float v = fold_chunk(part, p0, p1, C, blockIdx.x);
+      tot = k == 0 ? v : tot + v;
+    }
+    if (threadIdx.x >= 64) return false;
+  } else {
+    const int k = blockIdx.y, p0 = k * kFoldQ, p1 = p0 + kFoldQ < P ? p0 + kFoldQ : P;
+    const float v = fold_chunk(part, p0, p1, C, blockIdx.x);
+    if (threadIdx.x >= 64) return false;
+    const int lane = threadIdx.x;
+    float* slot = ws + (size_t)blockIdx.x * S * 64;
+    st_sc1(slot + k * 64 + lane, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__shfl(old, 0) != S - 1) return false;
+    tot = ld_sc1(slot + lane);
+    for (int q = 1; q < S; ++q) tot += ld_sc1(slot + q * 64 + lane);
+    if (lane == 0) __hip_atomic_store(cnt + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int lane = threadIdx.x, which = lane >> 5, ch = lane & 31;
+  const float other = __shfl_xor(tot, 32);
   c_out = blockIdx.x * kFinCh + ch;
   if (which != 0 || c_out >= C) return false;
-  s1 = s;
+  s1 = tot;
   s2 = other;
   return true;
 }
 
-// batch statistics of channel c from its (shifted by k) sums; running statistics updated torch's way
+// batch statistics of channel c from its (shifted by k) sums; running statistics updated torch's way.  SC1: mean /
+// rstd stored write-through for other workgroups of the same launch
+template <bool SC1 = false>
 __device__ __forceinline__ float bn_finish_channel(float s1, float s2, float k, int64_t rows, float eps, float momentum,
                                                    int c, float* mean, float* rstd, float* rmean, float* rvar) {
   const float n = (float)rows;
@@ -242,8 +324,13 @@ __device__ __forceinline__ float bn_finish_channel(float s1, float s2, float k, 
   const float var = fmaxf(fmaf(-m1, m1, s2 / n), 0.f);
   const float mu = k + m1;
   const float r = 1.0f / sqrtf(var + eps);
-  mean[c] = mu;
-  rstd[c] = r;
+  if constexpr (SC1) {
+    st_sc1(mean + c, mu);
+    st_sc1(rstd + c, r);
+  } else {
+    mean[c] = mu;
+    rstd[c] = r;
+  }
   if (rmean) rmean[c] = fmaf(momentum, mu, (1.f - momentum) * rmean[c]);
   if (rvar) rvar[c] = fmaf(momentum, rows > 1 ? (var * n) / (n - 1.f) : var, (1.f - momentum) * rvar[c]);
   return r;
@@ -252,11 +339,11 @@ __device__ __forceinline__ float bn_finish_channel(float s1, float s2, float k, 
 __global__ void __launch_bounds__(64 * kFinWaves) stats_finish_kernel(
     const void* __restrict__ y, int ydt, const float* __restrict__ part, int P, int64_t rows, int C, float eps,
     float momentum, float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rmean,
-    float* __restrict__ rvar, int64_t* __restrict__ nbt) {
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+    float* __restrict__ rvar, int64_t* __restrict__ nbt, int* cnt, float* ws) {
+  if (nbt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) nbt[0] += 1;
   float s1, s2;
   int c;
-  if (!fold_partials(part, P, C, s1, s2, c)) return;
+  if (!fold_partials(part, P, C, s1, s2, c, cnt, ws)) return;
   // shift k: row 0 of y (sv_bn_stats partials); y == NULL: unshifted partials (SV_EPI_STORE_STATS)
   const float k = y == nullptr ? 0.f
                   : ydt == SV_F32 ? reinterpret_cast<const float*>(y)[c] : bf2f(reinterpret_cast<const uint16_t*>(y)[c]);
@@ -470,10 +557,11 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
 __global__ void __launch_bounds__(64 * kFinWaves) bwd_finish_kernel(const float* __restrict__ part, int P, int C,
                                                                      float* __restrict__ sums,
                                                                      float* __restrict__ dgamma,
-                                                                     float* __restrict__ dbeta) {
+                                                                     float* __restrict__ dbeta, int* cnt,
+                                                                     float* ws) {
   float s1, s2;
   int c;
-  if (!fold_partials(part, P, C, s1, s2, c)) return;
+  if (!fold_partials(part, P, C, s1, s2, c, cnt, ws)) return;
   sums[c] = s1;
   sums[C + c] = s2;
   if (dgamma) dgamma[c] += s2;
@@ -1030,6 +1118,258 @@ __global__ void __launch_bounds__(kSmallThreads) act_small_kernel(const SmallAct
   }
 }
 
+// ---- the statistics fold inside the pass that consumes it ---------------------------------------------------
+// Every BatchNorm above is a statistics producer (the conv GEMM epilogue, or bwd_stats), a fold launch
+// (stats_finish / bwd_finish) and the apply pass.  At bs32 the 106 folds of a ResNet-50 step are 4.5-43 us each,
+// mostly launch and one-CU latency: skipping them (SV_DIAG_SKIP=bn_fin) measured 7.88 -> 7.05 ms/step (r11c).  Here
+// the apply pass folds the partials itself.  Its first workgroups to start (tickets from an agent-scope counter, so
+// the folding workgroups are always resident ones -- no wait on an unscheduled workgroup, whatever the dispatch
+// order) each fold one chunk of one 32-channel group exactly as fold_partials does (same code, same order: the
+// results are bit for bit the separate fold's); with several chunks the last to arrive adds the chunk sums in chunk
+// order.  The finished mean / rstd (forward) or correction sums (backward) are stored write-through (sc1), one
+// counter add per channel group after that wave's stores complete; every workgroup polls the counter (one lane,
+// sc1), then reads them with sc1 loads -- MI355X_MICROARCH.md's inter-workgroup table, row 1.  The last workgroup
+// past the poll re-arms the counters for the next launch on the stream (ctl is per stream).
+constexpr int kFoldThreads = 1024, kFoldMaxC = 2048, kFoldMaxGrid = 2048;
+constexpr int kFoldSlot = 16;                   // ctl: [0] tickets, [1] channel groups finished, [2] exits,
+                                                // [3] poll timeout flag, [16 + job * ncg + cg] chunk arrivals
+constexpr int kFoldWsSums = 2 * 2 * kFoldMaxC;  // ws: backward correction sums [job][2][C], then the chunk sums
+                                                // [job][cg][chunk][64] (lane l: sum l >> 5 of channel l & 31)
+struct FoldJob {
+  const float* part;
+  float *mean, *rstd, *rmean, *rvar;  // forward: batch statistics (mean / rstd handed off), running statistics
+  int64_t* nbt;
+  float eps, momentum;
+  float *dgamma, *dbeta;              // backward (the sums go to ws)
+};
+struct FoldCtl {
+  int* ctl;
+  float* ws;
+  FoldJob job[2];
+  int njobs, P, S, ncg, C, stats;     // stats = 0: eval-mode backward (zero correction sums)
+  int64_t rows;
+  int diag;                           // SV_FOLD_DIAG (timing only, results wrong): 1 = no tickets, poll or re-arm
+};
+
+template <bool BWD>
+__device__ __forceinline__ void fold_phase(const FoldCtl& f) {
+  __shared__ int s_ticket;
+  int* const ctl = f.ctl;
+  if (threadIdx.x == 0)
+    s_ticket = f.diag & 1 ? (int)blockIdx.x : __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int t = s_ticket, per_job = f.ncg * f.S;
+  if (t < f.njobs * per_job) {  // workgroup-uniform: this workgroup folds chunk s of channel group cg of job
+    const int job = t >= per_job ? 1 : 0, r = t - job * per_job, cg = r / f.S, s = r - cg * f.S;
+    const FoldJob J = job ? f.job[1] : f.job[0];
+    const int p0 = s * kFoldQ, p1 = p0 + kFoldQ < f.P ? p0 + kFoldQ : f.P;
+    float v = fold_chunk(J.part, p0, p1, f.C, cg);
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      bool fin = true;
+      if (f.S > 1) {
+        float* slot = f.ws + kFoldWsSums + (size_t)(job * f.ncg + cg) * f.S * 64;
+        st_sc1(slot + s * 64 + lane, v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int old = 0;
+        if (lane == 0)
+          old = __hip_atomic_fetch_add(ctl + kFoldSlot + job * f.ncg + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin = __shfl(old, 0) == f.S - 1;
+        if (fin) {  // every chunk of this channel group has landed: their sums in chunk order
+          float tot = ld_sc1(slot + lane);
+          for (int k = 1; k < f.S; ++k) tot += ld_sc1(slot + k * 64 + lane);
+          v = tot;
+          if (lane == 0) __hip_atomic_store(ctl + kFoldSlot + job * f.ncg + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (fin) {
+        const float other = __shfl_xor(v, 32);
+        const int c = cg * kFinCh + lane;
+        if (lane < 32 && c < f.C) {
+          if constexpr (BWD) {
+            float* sums = f.ws + (size_t)job * 2 * f.C;
+            st_sc1(sums + c, v);
+            st_sc1(sums + f.C + c, other);
+            if (J.dgamma) J.dgamma[c] += other;
+            if (J.dbeta) J.dbeta[c] += v;
+          } else {
+            bn_finish_channel<true>(v, other, 0.f, f.rows, J.eps, J.momentum, c, J.mean, J.rstd, J.rmean, J.rvar);
+            if (c == 0 && J.nbt) J.nbt[0] += 1;
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if (threadIdx.x == 0 && !(f.diag & 1)) {
+    const int target = f.njobs * f.ncg;
+    int n = 0;
+    while (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++n > (1 << 24)) {  // never expected: flag it (tests read ctl[3]) rather than hang the queue
+        __hip_atomic_store(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    // past the poll: the last workgroup here re-arms the launch's counters (every ticket is taken by then)
+    if (__hip_atomic_fetch_add(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+}
+
+// 8 per-channel values handed off by the fold (sc1 loads)
+__device__ __forceinline__ void ldp_sc1(const float* p, int c, float (&o)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = ld_sc1(p + c + k);
+}
+
+// act_kernel with the forward fold (mean / rstd of a.y, and with RBN of the projection shortcut, from their GEMM
+// epilogue partials).  Each thread's 8 channels are the same every grid-stride step (host: grid * 8192 % C == 0),
+// so the statistics are read once.
+template <bool RES, bool RBN>
+__global__ void __launch_bounds__(kFoldThreads) act_fold_kernel(const ActArgs a, const FoldCtl f) {
+  fold_phase<false>(f);
+  const int64_t nv = a.rows * a.C / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const int c = chan_of((size_t)i * 8, a.C, a.rows * a.C);
+  float mu[8], rs[8], g[8], b[8], rm[8], rr[8], rg[8], rb[8];
+  ldp_sc1(a.mean, c, mu);
+  ldp_sc1(a.rstd, c, rs);
+  ldp<8>(a.gamma, c, g);
+  ldp<8>(a.beta, c, b);
+  if constexpr (RBN) {
+    ldp_sc1(a.rmean, c, rm);
+    ldp_sc1(a.rrstd, c, rr);
+    ldp<8>(a.rgamma, c, rg);
+    ldp<8>(a.rbeta, c, rb);
+  }
+  for (; i < nv; i += stride) {
+    const size_t e = (size_t)i * 8;
+    float v[8], o[8];
+    ldv<8>(a.y, a.ydt, e, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = bn_pre(g[q], rs[q], v[q], mu[q], b[q]);
+    if constexpr (RES) {
+      float r[8];
+      ldv<8>(a.res, a.rdt, e, r);
+      if constexpr (RBN) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = bn_pre(rg[q], rr[q], r[q], rm[q], rb[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] += r[q];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = fmaxf(o[q], 0.f);
+    }
+    stv<8>(a.out, a.odt, e, o);
+  }
+}
+
+// bwd_apply_kernel with the backward fold (the correction sums from bwd_stats' or the dgrad epilogue's partials)
+template <bool RELU_Y, bool POOL>
+__global__ void __launch_bounds__(kFoldThreads) bwd_apply_fold_kernel(const BwdArgs a, const FoldCtl f) {
+  fold_phase<true>(f);
+  const int64_t nv = a.rows * a.C / 8;
+  const float inv_n = 1.0f / (float)a.rows;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const int c = chan_of((size_t)i * 8, a.C, a.rows * a.C);
+  float mu[8], rs[8], ga[8], sg[8], sgx[8];
+  ldp<8>(a.mean, c, mu);
+  ldp<8>(a.rstd, c, rs);
+  ldp<8>(a.gamma, c, ga);
+  if (f.stats) {
+    ldp_sc1(f.ws, c, sg);
+    ldp_sc1(f.ws + a.C, c, sgx);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sg[q] = sgx[q] = 0.f;
+  }
+  for (; i < nv; i += stride) {
+    const size_t e = (size_t)i * 8;
+    float v[8], g[8], o[8];
+    ldv<8>(a.y, a.ydt, e, v);
+    grad_masked<8, RELU_Y, POOL>(a.dout, a.ddt, a.act, a.adt, e, v, mu, rs, a.gamma, a.beta, c, g, &a.pool, a.C);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
+    stv<8>(a.dx, a.xdt, e, o);
+  }
+}
+
+// bwd_apply_dual_kernel with both BatchNorms' folds (jobs 0 and 1)
+__global__ void __launch_bounds__(kFoldThreads) bwd_apply_dual_fold_kernel(const BwdDualArgs a, const FoldCtl f) {
+  fold_phase<true>(f);
+  const int64_t nv = a.rows * a.C / 8;
+  const float inv_n = 1.0f / (float)a.rows;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const int c = chan_of((size_t)i * 8, a.C, a.rows * a.C);
+  float mu[8], rs[8], ga[8], sg[8], sgx[8], mu2[8], rs2[8], ga2[8], sg2[8], sgx2[8];
+  ldp<8>(a.mean, c, mu);
+  ldp<8>(a.rstd, c, rs);
+  ldp<8>(a.gamma, c, ga);
+  ldp<8>(a.mean2, c, mu2);
+  ldp<8>(a.rstd2, c, rs2);
+  ldp<8>(a.gamma2, c, ga2);
+  if (f.stats) {
+    ldp_sc1(f.ws, c, sg);
+    ldp_sc1(f.ws + a.C, c, sgx);
+    ldp_sc1(f.ws + 2 * a.C, c, sg2);
+    ldp_sc1(f.ws + 3 * a.C, c, sgx2);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sg[q] = sgx[q] = sg2[q] = sgx2[q] = 0.f;
+  }
+  for (; i < nv; i += stride) {
+    const size_t e = (size_t)i * 8;
+    float g[8], v[8], w[8], o[8], o2[8];
+    ldv<8>(a.g, a.gdt, e, g);
+    ldv<8>(a.y, a.ydt, e, v);
+    ldv<8>(a.y2, a.y2dt, e, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
+      o2[q] = bn_dx(ga2[q], rs2[q], g[q], sg2[q], w[q], mu2[q], sgx2[q], inv_n);
+    }
+    stv<8>(a.dx, a.xdt, e, o);
+    stv<8>(a.dx2, a.xdt, e, o2);
+  }
+}
+
+// launch geometry of the fold kernels: -> grid, 0 when (rows, C, P) is not theirs
+// chunk workgroups per channel group of a separate fold launch: one per kFoldQ partials given a workspace (ctl, ws
+// of SV_BN_FOLD_*), else 1 (the workgroup folds the chunks in turn: same bits)
+static int fin_split(int P, int C, const int* ctl, const float* ws) {
+  static const bool on = !getenv("SV_FIN_SPLIT") || atoi(getenv("SV_FIN_SPLIT")) != 0;
+  const int S = fold_chunks(P);
+  return (on && ctl && ws && S > 1 && S <= kFoldMaxS && C <= kFoldMaxC) ? S : 1;
+}
+static int fold_diag() {
+  static const int d = getenv("SV_FOLD_DIAG") ? atoi(getenv("SV_FOLD_DIAG")) : 0;
+  return d;
+}
+static int fold_grid(int64_t rows, int C, int P) {
+  static const int cap = getenv("SV_FOLD_MAX_GRID") ? atoi(getenv("SV_FOLD_MAX_GRID")) : kFoldMaxGrid;
+  if (C < 32 || C > kFoldMaxC || (C & (C - 1)) || rows <= 0 || P <= 0 || fold_chunks(P) > kFoldMaxS) return 0;
+  const int64_t nv = rows * C / 8;
+  int64_t g = (nv + kFoldThreads - 1) / kFoldThreads;
+  if (g > cap) g = cap;
+  const int64_t units = 2 * (C / kFinCh) * fold_chunks(P);
+  if (g < units) g = units;
+  return (g * kFoldThreads * 8) % C == 0 ? (int)g : 0;
+}
+
 static int grid_for(int64_t n4) {
   int64_t b = (n4 + kThreads - 1) / kThreads;
   if (b > 8192) b = 8192;
@@ -1066,12 +1406,14 @@ extern "C" int sv_bn_stats(const void* y, int32_t y_dtype, int64_t rows, int32_t
 
 extern "C" int sv_bn_stats_finish(const void* y, int32_t y_dtype, const float* part, int32_t nparts, int64_t rows,
                                   int32_t C, float eps, float momentum, float* mean, float* rstd, float* running_mean,
-                                  float* running_var, int64_t* num_batches_tracked, sv_stream_t stream) {
+                                  float* running_var, int64_t* num_batches_tracked, int32_t* ctl, float* ws,
+                                  sv_stream_t stream) {
   SV_REQUIRE(part && mean && rstd && nparts > 0 && rows > 0 && C > 0 && C % 4 == 0 && dt_ok(y_dtype),
              "sv_bn_stats_finish: bad arguments");
-  stats_finish_kernel<<<(C + kFinCh - 1) / kFinCh, 64 * kFinWaves, 0, (hipStream_t)stream>>>(y, y_dtype, part, nparts, rows, C, eps,
-                                                                        momentum, mean, rstd, running_mean, running_var,
-                                                                        num_batches_tracked);
+  const int S = fin_split(nparts, C, ctl, ws);
+  stats_finish_kernel<<<dim3((C + kFinCh - 1) / kFinCh, S), 64 * kFinWaves, 0, (hipStream_t)stream>>>(
+      y, y_dtype, part, nparts, rows, C, eps, momentum, mean, rstd, running_mean, running_var, num_batches_tracked,
+      ctl ? ctl + kFoldSlot : nullptr, ws);
   return check_launch("sv_bn_stats_finish");
 }
 
@@ -1162,9 +1504,11 @@ extern "C" int sv_bn_relu_bwd_stats(const void* dout, int32_t dout_dtype, const 
 }
 
 extern "C" int sv_bn_bwd_finish(const float* part, int32_t nparts, int32_t C, float* sums, float* dgamma, float* dbeta,
-                                sv_stream_t stream) {
+                                int32_t* ctl, float* ws, sv_stream_t stream) {
   SV_REQUIRE(part && sums && nparts > 0 && C > 0 && C % 4 == 0, "sv_bn_bwd_finish: bad arguments");
-  bwd_finish_kernel<<<(C + kFinCh - 1) / kFinCh, 64 * kFinWaves, 0, (hipStream_t)stream>>>(part, nparts, C, sums, dgamma, dbeta);
+  const int S = fin_split(nparts, C, ctl, ws);
+  bwd_finish_kernel<<<dim3((C + kFinCh - 1) / kFinCh, S), 64 * kFinWaves, 0, (hipStream_t)stream>>>(
+      part, nparts, C, sums, dgamma, dbeta, ctl ? ctl + kFoldSlot : nullptr, ws);
   return check_launch("sv_bn_bwd_finish");
 }
 
@@ -1409,4 +1753,102 @@ extern "C" int sv_bn_act_small(const void* y, int32_t y_dtype, const float* part
   else if (res) act_small_kernel<true, false><<<grid, kSmallThreads, 0, st>>>(a);
   else act_small_kernel<false, false><<<grid, kSmallThreads, 0, st>>>(a);
   return check_launch("sv_bn_act_small");
+}
+
+// ---- fold kernels (the statistics fold inside the consuming pass) -------------------------------------------
+extern "C" int sv_bn_fold_ok(int64_t rows, int32_t C, int32_t nparts) { return fold_grid(rows, C, nparts) > 0 ? 1 : 0; }
+
+extern "C" int sv_bn_act_fold(const void* y, int32_t y_dtype, const float* part, int32_t nparts, float eps,
+                              float momentum, const float* gamma, const float* beta, float* mean, float* rstd,
+                              float* running_mean, float* running_var, int64_t* num_batches_tracked, const void* res,
+                              int32_t res_dtype, const float* res_part, int32_t res_nparts, float res_eps,
+                              float res_momentum, const float* res_gamma, const float* res_beta, float* res_mean,
+                              float* res_rstd, float* res_running_mean, float* res_running_var,
+                              int64_t* res_num_batches_tracked, int32_t relu, void* out, int32_t out_dtype,
+                              int64_t rows, int32_t C, int32_t* ctl, float* ws, sv_stream_t stream) {
+  const int grid = fold_grid(rows, C, nparts);
+  SV_REQUIRE(grid > 0, "sv_bn_act_fold: rows=%lld C=%d nparts=%d outside the fold kernels' geometry (sv_bn_fold_ok)",
+             (long long)rows, (int)C, (int)nparts);
+  SV_REQUIRE(y && part && gamma && beta && mean && rstd && out && ctl && ws && dt_ok(y_dtype) && dt_ok(out_dtype) &&
+                 al16(y) && al16(part) && al16(gamma) && al16(beta) && al16(out),
+             "sv_bn_act_fold: bad arguments");
+  SV_REQUIRE(nparts == (rows + 63) / 64, "sv_bn_act_fold: nparts=%d is not the conv epilogue's ceil(rows / 64)",
+             (int)nparts);
+  SV_REQUIRE(!res || (dt_ok(res_dtype) && al16(res)), "sv_bn_act_fold: bad residual");
+  SV_REQUIRE(!res_part || (res && res_nparts == nparts && al16(res_part) && res_gamma && res_beta && res_mean &&
+                           res_rstd && al16(res_gamma) && al16(res_beta)),
+             "sv_bn_act_fold: incomplete residual BatchNorm (its partials must match the main ones)");
+  ActArgs a{y, y_dtype, mean, rstd, gamma, beta, res, res_dtype, res_mean, res_rstd, res_gamma, res_beta,
+            relu ? 1 : 0, out, out_dtype, rows, C};
+  FoldCtl f{};
+  f.ctl = ctl;
+  f.ws = ws;
+  f.job[0] = FoldJob{part, mean, rstd, running_mean, running_var, num_batches_tracked, eps, momentum, nullptr, nullptr};
+  f.job[1] = FoldJob{res_part, res_mean, res_rstd, res_running_mean, res_running_var, res_num_batches_tracked, res_eps,
+                     res_momentum, nullptr, nullptr};
+  f.njobs = res_part ? 2 : 1;
+  f.P = nparts;
+  f.S = fold_chunks(nparts);
+  f.ncg = C / kFinCh;
+  f.C = C;
+  f.stats = 1;
+  f.rows = rows;
+  f.diag = fold_diag();
+  hipStream_t st = (hipStream_t)stream;
+  if (res_part) act_fold_kernel<true, true><<<grid, kFoldThreads, 0, st>>>(a, f);
+  else if (res) act_fold_kernel<true, false><<<grid, kFoldThreads, 0, st>>>(a, f);
+  else act_fold_kernel<false, false><<<grid, kFoldThreads, 0, st>>>(a, f);
+  return check_launch("sv_bn_act_fold");
+}
+
+extern "C" int sv_bn_bwd_apply_fold(int32_t mode, const void* dout, int32_t dout_dtype, const uint8_t* pool_idx,
+                                    int32_t pool_H, int32_t pool_W, const void* y, int32_t y_dtype, const float* mean,
+                                    const float* rstd, const float* gamma, const float* beta, const void* y2,
+                                    int32_t y2_dtype, const float* mean2, const float* rstd2, const float* gamma2,
+                                    const float* part, const float* part2, int32_t nparts, void* dx, void* dx2,
+                                    int32_t dx_dtype, float* dgamma, float* dbeta, float* dgamma2, float* dbeta2,
+                                    int32_t batch_stats, int64_t rows, int32_t C, int32_t* ctl, float* ws,
+                                    sv_stream_t stream) {
+  const int grid = fold_grid(rows, C, nparts);
+  SV_REQUIRE(grid > 0, "sv_bn_bwd_apply_fold: rows=%lld C=%d nparts=%d outside the fold kernels' geometry",
+             (long long)rows, (int)C, (int)nparts);
+  SV_REQUIRE(mode >= SV_BN_SMALL_MASK && mode <= SV_BN_SMALL_DUAL, "sv_bn_bwd_apply_fold: bad mode %d", (int)mode);
+  SV_REQUIRE(dout && y && mean && rstd && gamma && part && dx && ctl && ws && dt_ok(dout_dtype) && dt_ok(y_dtype) &&
+                 dt_ok(dx_dtype) && al16(dout) && al16(y) && al16(mean) && al16(rstd) && al16(gamma) && al16(part) &&
+                 al16(dx),
+             "sv_bn_bwd_apply_fold: bad arguments");
+  SV_REQUIRE(mode != SV_BN_SMALL_RELU || (beta && al16(beta)), "sv_bn_bwd_apply_fold: the ReLU mode needs beta");
+  SV_REQUIRE(!pool_idx || (mode == SV_BN_SMALL_RELU && pool_H > 0 && pool_W > 0 && rows % ((int64_t)pool_H * pool_W) == 0 &&
+                           rows * C < (1ll << 31)),
+             "sv_bn_bwd_apply_fold: the pooled form is the ReLU mode over rows = B * H * W (< 2^31 elements)");
+  SV_REQUIRE(mode != SV_BN_SMALL_DUAL || (y2 && dt_ok(y2_dtype) && al16(y2) && mean2 && rstd2 && gamma2 && part2 &&
+                                          dx2 && al16(mean2) && al16(rstd2) && al16(gamma2) && al16(part2) && al16(dx2)),
+             "sv_bn_bwd_apply_fold: the dual mode needs y2, mean2, rstd2, gamma2, part2 and dx2");
+  FoldCtl f{};
+  f.ctl = ctl;
+  f.ws = ws;
+  f.job[0] = FoldJob{part, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, dgamma, dbeta};
+  f.job[1] = FoldJob{part2, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, dgamma2, dbeta2};
+  f.njobs = mode == SV_BN_SMALL_DUAL ? 2 : 1;
+  f.P = nparts;
+  f.S = fold_chunks(nparts);
+  f.ncg = C / kFinCh;
+  f.C = C;
+  f.stats = batch_stats ? 1 : 0;
+  f.rows = rows;
+  f.diag = fold_diag();
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == SV_BN_SMALL_DUAL) {
+    BwdDualArgs a{dout, dout_dtype, y, y_dtype, mean, rstd, gamma, nullptr, y2, y2_dtype, mean2, rstd2, gamma2,
+                  nullptr, dx, dx2, dx_dtype, rows, C};
+    bwd_apply_dual_fold_kernel<<<grid, kFoldThreads, 0, st>>>(a, f);
+    return check_launch("sv_bn_bwd_apply_fold");
+  }
+  const PoolSrc ps = pool_idx ? PoolSrc{dout, pool_idx, pool_H, pool_W, dout_dtype} : PoolSrc{nullptr, nullptr, 0, 0, SV_F32};
+  BwdArgs a{dout, dout_dtype, nullptr, SV_F32, y, y_dtype, mean, rstd, gamma, beta, nullptr, dx, dx_dtype, nullptr,
+            rows, C, ps};
+  if (mode == SV_BN_SMALL_MASK) bwd_apply_fold_kernel<false, false><<<grid, kFoldThreads, 0, st>>>(a, f);
+  else if (pool_idx) bwd_apply_fold_kernel<true, true><<<grid, kFoldThreads, 0, st>>>(a, f);
+  else bwd_apply_fold_kernel<true, false><<<grid, kFoldThreads, 0, st>>>(a, f);
+  return check_launch("sv_bn_bwd_apply_fold");
 }

@@ -80,6 +80,13 @@ OP_PROBES: dict[str, OpProbe] = {}  # name -> probe; bench.py fills it for the t
 _DIAG_SKIP = {x for x in os.environ.get("SV_DIAG_SKIP", "").split(",") if x}
 
 
+def _fin(name: str, *args) -> None:
+    """call() of a BatchNorm fold / activation launch; SV_DIAG_SKIP=bn_fin / bn_act skips those (diagnostic only)"""
+    if _DIAG_SKIP and not name.endswith("_fold") and ("bn_act" if name == "sv_bn_act_fwd" else "bn_fin") in _DIAG_SKIP:
+        return
+    call(name, *args)
+
+
 def _timed_call(op: str, nbytes: float, *args, fma: float = 0.0, flops: float = 0.0) -> None:
     """call(*args), bracketed by HIP events on the current stream when ``op`` is being probed; ``fma``: the
     launch's algorithmic f32 VALU FMAs (its roof when they outlast its bytes)."""
@@ -1056,8 +1063,8 @@ def bn_stats_from_partials(part: torch.Tensor, rows: int, *, eps: float = EPS_BN
     _check(two == 2 and part.dtype == torch.float32 and part.is_contiguous(), "bn_stats_from_partials: bad partials")
     mean = torch.empty(C, device=part.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
-    call("sv_bn_stats_finish", None, SV_F32, ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
-         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked))
+    _fin("sv_bn_stats_finish", None, SV_F32, ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked), *_fin_ws(part.device))
     return mean, rstd
 
 
@@ -1255,8 +1262,8 @@ def bn_stats(y2d: torch.Tensor, *, eps: float = EPS_BN, momentum: float = 0.1, r
     call("sv_bn_stats", ptr(y2d), dt(y2d), rows, C, ptr(part))
     mean = torch.empty(C, device=y2d.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
-    call("sv_bn_stats_finish", ptr(y2d), dt(y2d), ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
-         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked))
+    _fin("sv_bn_stats_finish", ptr(y2d), dt(y2d), ptr(part), P, rows, C, float(eps), float(momentum), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches_tracked), *_fin_ws(part.device))
     return mean, rstd
 
 
@@ -1278,7 +1285,7 @@ def bn_act(y2d, mean, rstd, gamma, beta, *, res=None, res_bn=None, relu=True, ou
     rm, rr, rg, rb = res_bn if res_bn is not None else (None, None, None, None)
     if out is None:
         out = torch.empty(rows, C, device=y2d.device, dtype=out_dtype)
-    call("sv_bn_act_fwd", ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), ptr(res),
+    _fin("sv_bn_act_fwd", ptr(y2d), dt(y2d), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), ptr(res),
          nv.dt_none(res), ptr(rm), ptr(rr), ptr(rg), ptr(rb), int(relu), ptr(out), dt(out), rows, C)
     return out
 
@@ -1303,6 +1310,105 @@ def bn_small_ok(rows: int, C: int) -> bool:
 
 def _bn_small_args_ok(*ts) -> bool:
     return all(t is None or (t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0) for t in ts)
+
+
+# The statistics fold inside the consuming pass (sv_bn_act_fold / sv_bn_bwd_apply_fold): one launch fewer per
+# BatchNorm, bit for bit the separate fold.  Opt-in (SV_BN_FOLD=1): measured slower -- classification 2713-2718 vs
+# 4076-4093 img/s with up to 2048 workgroups (their ticket / exit atomics on one counter serialise), and a graph-timed
+# launch at 256 workgroups still 1.1-2.2x the separate finish + activation (profiles/round5/r11e_fold_bench.txt):
+# the fold's round trips sit in front of every workgroup's first load.  The separate fold's chunks run in parallel
+# workgroups instead (_fin_ws).
+_BN_FOLD = os.environ.get("SV_BN_FOLD", "0") != "0"
+_FOLD_OK: dict = {}
+_FOLD_WS: dict = {}
+
+
+def _fin_ws(device) -> tuple:
+    """(ctl, ws) pointers for a separate fold launch on the current stream: its chunks of 1024 partials then fold in
+    parallel workgroups (sv_bn_stats_finish / sv_bn_bwd_finish; same bits)."""
+    ctl, ws = _fold_ws(device)
+    return ptr(ctl), ptr(ws)
+
+
+def bn_fold_ok(rows: int, C: int, nparts: int) -> bool:
+    """Whether (rows, C, nparts) has the fold kernels' geometry (sv_bn_fold_ok), and SV_BN_FOLD is on."""
+    key = (rows, C, nparts)
+    ok = _FOLD_OK.get(key)
+    if ok is None:
+        ok = _FOLD_OK[key] = bool(value("sv_bn_fold_ok", rows, C, nparts))
+    return _BN_FOLD and ok
+
+
+def _fold_ws(device):
+    """(ctl, ws) of the fold kernels on the current stream: the counters start zero and every launch leaves them
+    zero; never reallocated (a captured graph keeps the pointers)."""
+    key = (device, nv._stream())
+    t = _FOLD_WS.get(key)
+    if t is None:
+        t = _FOLD_WS[key] = (torch.zeros(nv.SV_BN_FOLD_CTL_INTS, device=device, dtype=torch.int32),
+                             torch.empty(nv.SV_BN_FOLD_WS_FLOATS, device=device, dtype=torch.float32))
+    return t
+
+
+def bn_fold_timeouts(device) -> int:
+    """Fold-kernel polls that timed out on any stream of ``device`` since the workspaces were made (0 expected)."""
+    return sum(int(ctl[3].item()) for (d, _), (ctl, _) in _FOLD_WS.items() if d == device)
+
+
+def bn_act_fold(y2d, part, bn_params: tuple, *, res=None, res_part=None, res_params: tuple | None = None,
+                relu=True, out_dtype=torch.float32):
+    """bn_act_small's contract at any row count the fold kernels take (bn_fold_ok): the statistics fold of the conv
+    epilogue's partials inside the activation pass (sv_bn_act_fold) -- bit for bit ``bn_stats_from_partials`` +
+    ``bn_act``.  -> (out, mean, rstd[, mean2, rstd2])."""
+    rows, C = y2d.shape
+    g, b, eps, mom, rm, rv, nbt = bn_params
+    dev = y2d.device
+    mean = torch.empty(C, device=dev, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    out = torch.empty(rows, C, device=dev, dtype=out_dtype)
+    if res_part is not None:
+        g2, b2, eps2, mom2, rm2, rv2, nbt2 = res_params
+        mean2, rstd2 = torch.empty_like(mean), torch.empty_like(mean)
+    else:
+        g2 = b2 = rm2 = rv2 = nbt2 = mean2 = rstd2 = None
+        eps2, mom2 = 0.0, 0.0
+    ctl, ws = _fold_ws(dev)
+    _fin("sv_bn_act_fold", ptr(y2d), dt(y2d), ptr(part), part.shape[0], float(eps), float(mom), ptr(g), ptr(b),
+         ptr(mean), ptr(rstd), ptr(rm), ptr(rv), ptr(nbt), ptr(res), nv.dt_none(res), ptr(res_part),
+         res_part.shape[0] if res_part is not None else 0, float(eps2), float(mom2), ptr(g2), ptr(b2), ptr(mean2),
+         ptr(rstd2), ptr(rm2), ptr(rv2), ptr(nbt2), int(relu), ptr(out), dt(out), rows, C, ptr(ctl), ptr(ws))
+    if res_part is not None:
+        return out, mean, rstd, mean2, rstd2
+    return out, mean, rstd
+
+
+def bn_act_partials(y2d, part, bn_params: tuple, *, res=None, res_part=None, res_params: tuple | None = None,
+                    relu=True, out_dtype=torch.float32):
+    """Train-mode BatchNorm (+ residual, + ReLU) from the conv epilogue's partials with the fewest launches the shape
+    allows: bn_act_small (rows <= 8192, opt-in SV_BN_SMALL), bn_act_fold, else bn_stats_from_partials + bn_act.  All
+    three give the same bits.  -> (out, mean, rstd[, mean2, rstd2])."""
+    rows, C = y2d.shape
+    args = (y2d, part, res, res_part) + bn_params[:2] + (res_params[:2] if res_params else ())
+    if bn_small_ok(rows, C) and _bn_small_args_ok(*args):
+        return bn_act_small(y2d, part, bn_params, res=res, res_part=res_part, res_params=res_params, relu=relu,
+                            out_dtype=out_dtype)
+    if (bn_fold_ok(rows, C, part.shape[0]) and _bn_small_args_ok(*args)
+            and (res_part is None or res_part.shape[0] == part.shape[0])):
+        return bn_act_fold(y2d, part, bn_params, res=res, res_part=res_part, res_params=res_params, relu=relu,
+                           out_dtype=out_dtype)
+    g, b, eps, mom, rm, rv, nbt = bn_params
+    mean, rstd = bn_stats_from_partials(part, rows, eps=eps, momentum=mom, running_mean=rm, running_var=rv,
+                                        num_batches_tracked=nbt)
+    res_bn = None
+    if res_part is not None:
+        g2, b2, eps2, mom2, rm2, rv2, nbt2 = res_params
+        mean2, rstd2 = bn_stats_from_partials(res_part, rows, eps=eps2, momentum=mom2, running_mean=rm2,
+                                              running_var=rv2, num_batches_tracked=nbt2)
+        res_bn = (mean2, rstd2, g2, b2)
+    out = bn_act(y2d, mean, rstd, g, b, res=res, res_bn=res_bn, relu=relu, out_dtype=out_dtype)
+    if res_part is not None:
+        return out, mean, rstd, mean2, rstd2
+    return out, mean, rstd
 
 
 def bn_act_small(y2d, part, bn_params: tuple, *, res=None, res_part=None, res_params: tuple | None = None,
@@ -1387,8 +1493,18 @@ def bn_bwd(dout2d, y2d, mean, rstd, gamma, *, act=None, relu_beta=None, dgamma=N
     else:
         call("sv_bn_bwd_stats", ptr(dout2d), dt(dout2d), ptr(act), nv.dt_none(act), ptr(y2d), dt(y2d), ptr(mean),
              ptr(rstd), rows, C, ptr(part))
+    if ((relu_beta is not None or act is None) and gmask is None and bn_fold_ok(rows, C, P)
+            and _bn_small_args_ok(dout2d, y2d, mean, rstd, gamma, relu_beta, part)):
+        # the finish inside the apply pass (sv_bn_bwd_apply_fold): MASK = dout already masked (mask_inplace)
+        dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        ctl, ws = _fold_ws(y2d.device)
+        mode = nv.SV_BN_SMALL_RELU if relu_beta is not None else nv.SV_BN_SMALL_MASK
+        _fin("sv_bn_bwd_apply_fold", mode, ptr(dout2d), dt(dout2d), None, 0, 0, ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), ptr(gamma), ptr(relu_beta), None, 0, None, None, None, ptr(part), None, P, ptr(dx), None,
+             dt(dx), ptr(dgamma), ptr(dbeta), None, None, int(batch_stats), rows, C, ptr(ctl), ptr(ws))
+        return dx
     sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
+    _fin("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta), *_fin_ws(part.device))
     if not batch_stats:
         sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
@@ -1423,9 +1539,18 @@ def bn_bwd_dual(gm, y2d, mean, rstd, gamma, act, y2, mean2, rstd2, gamma2, *, dg
     part = torch.empty(2, P, 2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_bwd_stats_mask_dual", ptr(gm), dt(gm), ptr(act), dt(act), ptr(y2d), dt(y2d), ptr(mean), ptr(rstd),
          ptr(y2), dt(y2), ptr(mean2), ptr(rstd2), rows, C, ptr(part[0]), ptr(part[1]))
+    if bn_fold_ok(rows, C, P) and _bn_small_args_ok(gm, y2d, mean, rstd, gamma, y2, mean2, rstd2, gamma2):
+        dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        dx2 = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        ctl, ws = _fold_ws(y2d.device)
+        _fin("sv_bn_bwd_apply_fold", nv.SV_BN_SMALL_DUAL, ptr(gm), dt(gm), None, 0, 0, ptr(y2d), dt(y2d), ptr(mean),
+             ptr(rstd), ptr(gamma), None, ptr(y2), dt(y2), ptr(mean2), ptr(rstd2), ptr(gamma2), ptr(part[0]),
+             ptr(part[1]), P, ptr(dx), ptr(dx2), dt(dx), ptr(dgamma), ptr(dbeta), ptr(dgamma2), ptr(dbeta2),
+             int(batch_stats), rows, C, ptr(ctl), ptr(ws))
+        return dx, dx2
     sums = torch.empty(2, 2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_bwd_finish", ptr(part[0]), P, C, ptr(sums[0]), ptr(dgamma), ptr(dbeta))
-    call("sv_bn_bwd_finish", ptr(part[1]), P, C, ptr(sums[1]), ptr(dgamma2), ptr(dbeta2))
+    _fin("sv_bn_bwd_finish", ptr(part[0]), P, C, ptr(sums[0]), ptr(dgamma), ptr(dbeta), *_fin_ws(part.device))
+    _fin("sv_bn_bwd_finish", ptr(part[1]), P, C, ptr(sums[1]), ptr(dgamma2), ptr(dbeta2), *_fin_ws(part.device))
     if not batch_stats:
         sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
@@ -1448,8 +1573,16 @@ def bn_relu_bwd_pooled(dpool4d: torch.Tensor, idx: torch.Tensor, H: int, W: int,
     part = torch.empty(P, 2, C, device=y2d.device, dtype=torch.float32)
     call("sv_bn_relu_bwd_stats_pool", ptr(dpool4d), dt(dpool4d), ptr(idx), B, H, W, ptr(y2d), dt(y2d), ptr(mean),
          ptr(rstd), ptr(gamma), ptr(beta), C, ptr(part))
+    if (bn_fold_ok(rows, C, P) and rows * C < 2 ** 31
+            and _bn_small_args_ok(dpool4d, y2d, mean, rstd, gamma, beta)):
+        dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)
+        ctl, ws = _fold_ws(y2d.device)
+        _fin("sv_bn_bwd_apply_fold", nv.SV_BN_SMALL_RELU, ptr(dpool4d), dt(dpool4d), ptr(idx), H, W, ptr(y2d), dt(y2d),
+             ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), None, 0, None, None, None, ptr(part), None, P, ptr(dx),
+             None, dt(dx), ptr(dgamma), ptr(dbeta), None, None, int(batch_stats), rows, C, ptr(ctl), ptr(ws))
+        return dx
     sums = torch.empty(2, C, device=y2d.device, dtype=torch.float32)
-    call("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta))
+    _fin("sv_bn_bwd_finish", ptr(part), P, C, ptr(sums), ptr(dgamma), ptr(dbeta), *_fin_ws(part.device))
     if not batch_stats:
         sums.zero_()
     dx = torch.empty(rows, C, device=y2d.device, dtype=dx_dtype)

@@ -21,6 +21,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 SV_F32, SV_BF16 = 0, 1
 SV_IMG_F32_NCHW, SV_IMG_U8_GRAY = 0, 1
 SV_BN_SMALL_MASK, SV_BN_SMALL_RELU, SV_BN_SMALL_DUAL = 0, 1, 2
+SV_BN_FOLD_CTL_INTS, SV_BN_FOLD_WS_FLOATS = 256, 2 * 2 * 2048 + 2 * 64 * 16 * 64  # include/sv_kernels.h
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
  SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS, SV_EPI_STORE_BN_BWD) = range(10)
 
@@ -168,12 +169,12 @@ _SIGS = {
     "sv_image_u8_hwc_to_nhwc": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_bn_nparts": [_i64, _i32],
     "sv_bn_stats": [_p, _i32, _i64, _i32, _p, _p],
-    "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p],
+    "sv_bn_stats_finish": [_p, _i32, _p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p, _p, _p],
     "sv_bn_eval_params": [_p, _p, _f32, _p, _p, _i32, _p],
     "sv_bn_act_fwd": [_p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
     "sv_bn_bwd_stats": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
     "sv_bn_bwd_stats_mask": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _i64, _i32, _p, _p],
-    "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p],
+    "sv_bn_bwd_finish": [_p, _i32, _i32, _p, _p, _p, _p, _p, _p],
     "sv_bn_bwd_stats_mask_dual": [_p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _i64, _i32, _p, _p, _p],
     "sv_bn_bwd_apply_dual": [_p, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _i64, _i32,
                              _p],
@@ -187,6 +188,11 @@ _SIGS = {
                         _i32, _p, _p, _p, _p, _i32, _i64, _i32, _p],
     "sv_bn_act_small": [_p, _i32, _p, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _f32, _f32,
                         _p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p],
+    "sv_bn_fold_ok": [_i64, _i32, _i32],
+    "sv_bn_act_fold": [_p, _i32, _p, _i32, _f32, _f32, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _f32, _f32,
+                       _p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p, _p, _p],
+    "sv_bn_bwd_apply_fold": [_i32, _p, _i32, _p, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p,
+                             _i32, _p, _p, _i32, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p],
     "sv_relu_mask": [_p, _i32, _p, _i32, _p, _i64, _p],
     "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_maxpool3s2_bwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
@@ -196,7 +202,7 @@ _SIGS = {
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_conv_bwd_weight_work_floats",
+_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_bn_fold_ok", "sv_conv_bwd_weight_work_floats",
                                                                      "sv_stream_create_cu_reserved", "sv_bn_small_ok"}
 
 # entry points that take no stream (call() appends none) but return an sv_status

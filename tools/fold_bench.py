@@ -1,71 +1,59 @@
-"""Standalone timing of the split-K fold passes of the ConvNeXt-base bs32 weight gradients (HIP events):
-the fc2 layer-scale finish (sv_layerscale_wgrad_reduce: slabs -> dW2, dgamma, db2) and the fc1 slab fold
-(sv_reduce_partials_multi wide segment), at each stage's split depth -- their rate alone, to set against their
-in-step rate beside the main stream.
-
-    python tools/fold_bench.py [--iters 20]
-"""
-import argparse
+"""Per-launch time of the BatchNorm fold kernels against the separate fold + apply launches (HIP events, median of
+repeats of a graph of 20 launches), at the ResNet-50 bs32 256^2 shapes.  Knobs read by the library: SV_FOLD_MAX_GRID, SV_FOLD_DIAG.
+    python tools/fold_bench.py"""
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__  # noqa: E402
 
 __graft_entry__.load_package()
 from spine_vision_amd import kernels as K  # noqa: E402
-from spine_vision_amd import native as nv  # noqa: E402
 
-STAGES = {"S1": (524288, 128), "S2": (131072, 256), "S3": (32768, 512), "S4": (8192, 1024)}
+if not torch.cuda.is_available():
+    sys.exit("no GPU")
+dev = torch.device("cuda", 0)
 
 
-def timeit(fn, iters):
-    for _ in range(3):
+def timed(fn, n=20, reps=5):
+    """GPU time per call: n calls captured in one graph, replayed (no host launch cost in the figure)"""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
         fn()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            for _ in range(n):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    graph.replay()
     torch.cuda.synchronize()
-    a.record()
-    for _ in range(iters):
-        fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) * 1e3 / iters
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        graph.replay()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / n)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=20)
-    args = ap.parse_args()
-    dev = torch.device("cuda:0")
-    for st, (M, C) in STAGES.items():
-        K4 = 4 * C
-        split = K._wgrad_split_for(C, K4, M)
-        slab = torch.randn(split * C * K4, device=dev)
-        cs = torch.randn(split * C, device=dev)
-        w2, dw2 = torch.randn(C, K4, device=dev), torch.zeros(C, K4, device=dev)
-        gam, b2 = torch.rand(C, device=dev), torch.randn(C, device=dev)
-        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+g = torch.Generator().manual_seed(0)
+for rows, C in [(524288, 64), (131072, 64), (131072, 256), (32768, 128), (32768, 512), (8192, 1024), (2048, 2048)]:
+    y = torch.randn(rows, C, generator=g).to(dev, torch.bfloat16)
+    P = (rows + 63) // 64
+    part = torch.rand(P, 2, C, generator=g).to(dev)
+    prm = ((torch.rand(C, generator=g) + 0.5).to(dev), torch.zeros(C, device=dev), 1e-5, 0.1, torch.zeros(C, device=dev),
+           torch.ones(C, device=dev), torch.zeros((), dtype=torch.int64, device=dev))
+    tf = timed(lambda: K.bn_act_fold(y, part, prm, relu=True, out_dtype=torch.bfloat16))
 
-        def ls():
-            nv.call("sv_layerscale_wgrad_reduce", nv.ptr(slab), nv.ptr(cs), split, nv.ptr(w2), nv.ptr(gam),
-                    nv.ptr(b2), nv.ptr(dw2), nv.ptr(dg), nv.ptr(db), None, C, K4)
+    def sep():
+        m, r = K.bn_stats_from_partials(part, rows, running_mean=prm[4], running_var=prm[5], num_batches_tracked=prm[6])
+        K.bn_act(y, m, r, prm[0], prm[1], relu=True, out_dtype=torch.bfloat16)
 
-        out = torch.zeros(K4 * C, device=dev)
-        bias_out = torch.zeros(K4, device=dev)
-        cs1 = torch.randn(split * K4, device=dev)
-
-        def multi():
-            K.reduce_multi([(slab, out, split, True), (cs1, bias_out, split, True)])
-
-        nbytes_ls = 4.0 * ((split + 2) * C * K4 + (split + 4) * C)
-        nbytes_m = 4.0 * ((split + 2) * C * K4 + (split + 2) * K4)
-        t_ls, t_m = timeit(ls, args.iters), timeit(multi, args.iters)
-        print(f"{st} C={C:5d} split={split:3d}  layerscale_reduce {t_ls:7.1f} us {nbytes_ls / t_ls / 1e6:6.2f} TB/s"
-              f"  reduce_multi(fc1 slab + bias) {t_m:7.1f} us {nbytes_m / t_m / 1e6:6.2f} TB/s", flush=True)
-
-
-if __name__ == "__main__":
-    main()
+    ts = timed(sep)
+    print(f"rows {rows:7d} C {C:5d} P {P:5d}: fold {tf:7.1f} us   finish+act {ts:7.1f} us", flush=True)
