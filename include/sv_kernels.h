@@ -660,6 +660,30 @@ int sv_avgpool_fwd(const void* x, int32_t x_dtype, float* feat, int32_t B, int32
 int sv_avgpool_bwd(const float* dfeat, void* dx, int32_t dx_dtype, int32_t B, int32_t HW, int32_t C,
                    sv_stream_t stream);
 
+/* ---- classification loss (csrc/loss.hip, ABI v7) ------------------------------------------------
+ * The multi-task loss over the fused head's logits [B][K] (f32, row-major) in one launch: loss[0] =
+ * sum_k weight_k * loss_k, and dlogits [B][K] = d(loss[0]) / d(logits) (every column of a task's range
+ * written; columns no task covers are left alone).  Tasks (host array, 1..8):
+ *   SV_HEAD_CE : torch.nn.CrossEntropyLoss(label_smoothing) over columns [offset, offset + ncls); target
+ *                int64 [B] class indices, -100 ignored; mean over the valid rows (0 if none)
+ *   SV_HEAD_BCE: torch.nn.BCEWithLogitsLoss over [offset, offset + ncls); target [B][ncls] f32 / bf16
+ *                (target_dtype); mean over B * ncls
+ * Replaces: Classifier.get_loss (spine_vision/training/models/generic.py) with core/tasks.py's per-task losses
+ * and their autograd backward.                                                                       */
+#define SV_HEAD_CE 0
+#define SV_HEAD_BCE 1
+typedef struct {
+  int32_t kind;
+  int32_t offset;
+  int32_t ncls;
+  float weight;
+  float label_smoothing;
+  const void* target;
+  int32_t target_dtype;
+} sv_head_task;
+int sv_head_loss(const float* logits, int32_t B, int32_t K, const sv_head_task* tasks, int32_t ntasks, float* loss,
+                 float* dlogits, sv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1591,6 +1591,28 @@ def bn_relu_bwd_pooled(dpool4d: torch.Tensor, idx: torch.Tensor, H: int, W: int,
     return dx
 
 
+def head_loss(logits: torch.Tensor, specs: list) -> tuple:
+    """The multi-task classification loss and its logits gradient in one launch (sv_head_loss).  ``specs``: one
+    (kind, offset, ncls, weight, label_smoothing, target) per task, kind nv.SV_HEAD_CE (target int64 [B]) or
+    nv.SV_HEAD_BCE (target f32 / bf16 [B][ncls]).  -> (loss 0-dim f32, dlogits [B][K] f32)."""
+    _check(logits.dtype == torch.float32 and logits.dim() == 2 and logits.is_contiguous(), "head_loss: logits")
+    B, Kc = logits.shape
+    cover = 0
+    tasks = []
+    for kind, off, n, w, sm, t in specs:
+        if kind == nv.SV_HEAD_CE:
+            _check(t.dtype == torch.int64 and t.is_contiguous() and t.numel() == B, "head_loss: CE target int64 [B]")
+        else:
+            _check(t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous() and t.numel() == B * n,
+                   "head_loss: BCE target f32 / bf16 [B][ncls]")
+        tasks.append(nv.HeadTask(kind, off, n, float(w), float(sm), ptr(t), dt(t) if kind == nv.SV_HEAD_BCE else 0))
+        cover += n
+    loss = torch.empty((), device=logits.device, dtype=torch.float32)
+    dl = (torch.empty_like if cover == Kc else torch.zeros_like)(logits)
+    call("sv_head_loss", ptr(logits), B, Kc, (nv.HeadTask * len(tasks))(*tasks), len(tasks), ptr(loss), ptr(dl))
+    return loss, dl
+
+
 def maxpool_fwd(x4d: torch.Tensor):
     B, H, W, C = x4d.shape
     _check(x4d.is_contiguous() and C % 4 == 0, "maxpool_fwd: need contiguous NHWC, C % 4 == 0")

@@ -21,6 +21,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "sv_kernels.h")
 SV_F32, SV_BF16 = 0, 1
 SV_IMG_F32_NCHW, SV_IMG_U8_GRAY = 0, 1
 SV_BN_SMALL_MASK, SV_BN_SMALL_RELU, SV_BN_SMALL_DUAL = 0, 1, 2
+SV_HEAD_CE, SV_HEAD_BCE = 0, 1
 SV_BN_FOLD_CTL_INTS, SV_BN_FOLD_WS_FLOATS = 256, 2 * 2 * 2048 + 2 * 64 * 16 * 64  # include/sv_kernels.h
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
  SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS, SV_EPI_STORE_BN_BWD) = range(10)
@@ -79,6 +80,12 @@ class GemmDesc(ctypes.Structure):
 class RedSeg(ctypes.Structure):
     """sv_red_seg (include/sv_kernels.h): one partial reduction of sv_reduce_partials_multi."""
     _fields_ = [("part", _p), ("out", _p), ("n", _i64), ("P", _i32), ("accumulate", _i32)]
+
+
+class HeadTask(ctypes.Structure):
+    """sv_head_task (include/sv_kernels.h): one task of sv_head_loss."""
+    _fields_ = [("kind", _i32), ("offset", _i32), ("ncls", _i32), ("weight", _f32), ("label_smoothing", _f32),
+                ("target", _p), ("target_dtype", _i32)]
 
 
 SV_MAX_RED_SEGS = 8
@@ -193,6 +200,7 @@ _SIGS = {
                        _p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i64, _i32, _p, _p, _p],
     "sv_bn_bwd_apply_fold": [_i32, _p, _i32, _p, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p,
                              _i32, _p, _p, _i32, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p],
+    "sv_head_loss": [_p, _i32, _i32, _p, _i32, _p, _p, _p],
     "sv_relu_mask": [_p, _i32, _p, _i32, _p, _i64, _p],
     "sv_maxpool3s2_fwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_maxpool3s2_bwd": [_p, _i32, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],

@@ -26,6 +26,7 @@ from ...core.tasks import (
     get_strategy,
     get_tasks,
 )
+from ...native import SV_HEAD_BCE, SV_HEAD_CE
 from .backbone import BackboneFactory
 
 
@@ -58,6 +59,33 @@ class BaseModel(nn.Module):
 
 # SV_FUSED_HEADS=0: one GEMM per classification head (A/B runs)
 _FUSED_HEADS = os.environ.get("SV_FUSED_HEADS", "1") != "0"
+# the multi-task loss over the fused head's logits in one HIP launch (kernels.head_loss; SV_FUSED_LOSS=0: torch's
+# per-task modules, ~60 launches at bs32)
+_FUSED_LOSS = os.environ.get("SV_FUSED_LOSS", "1") != "0"
+
+
+class _HeadOutputs(dict):
+    """The per-task logits (views of one [B, sum(classes)] tensor, ``.logits``) from the fused head."""
+
+    logits: torch.Tensor
+
+
+class _FusedHeadLoss(torch.autograd.Function):
+    """sum_k w_k loss_k(logits[:, cols_k], target_k) and its logits gradient from one launch (sv_head_loss); the
+    backward scales the saved gradient by the incoming one."""
+
+    @staticmethod
+    def forward(ctx, logits, specs, *targets):
+        from ...kernels import head_loss
+
+        loss, dl = head_loss(logits.detach(), [sp + (t,) for sp, t in zip(specs, targets)])
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return (dl * g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
 class Classifier(BaseModel):
@@ -100,10 +128,45 @@ class Classifier(BaseModel):
             w = torch.cat([h.weight for h in hs])
             b = torch.cat([h.bias for h in hs])
             out = torch.addmm(b, f, w.t())
-            return dict(zip(self.heads.keys(), out.split([h.out_features for h in hs], dim=1)))
+            res = _HeadOutputs(zip(self.heads.keys(), out.split([h.out_features for h in hs], dim=1)))
+            res.logits = out
+            return res
         return {n: h(f) for n, h in self.heads.items()}
 
+    def _fused_loss_specs(self, predictions, targets):
+        """(specs, targets) for _FusedHeadLoss when every task's loss is a default CrossEntropyLoss / BCEWithLogitsLoss
+        over the fused head's logits, else None."""
+        logits = getattr(predictions, "logits", None)
+        if not (_FUSED_LOSS and logits is not None and logits.is_cuda and logits.dtype == torch.float32
+                and logits.dim() == 2 and logits.is_contiguous()):
+            return None
+        specs, tgts, off = [], [], 0
+        for t in self._tasks:
+            if t.name not in predictions or t.name not in targets:
+                return None
+            fn = self._loss_functions[t.name]
+            tgt = get_strategy(t).format_target(targets[t.name])
+            if type(fn) is nn.CrossEntropyLoss and fn.weight is None and fn.ignore_index == -100 \
+                    and fn.reduction == "mean" and tgt.dtype == torch.int64 and tgt.dim() == 1:
+                kind, sm = SV_HEAD_CE, fn.label_smoothing
+            elif type(fn) is nn.BCEWithLogitsLoss and fn.weight is None and fn.pos_weight is None \
+                    and fn.reduction == "mean" and tgt.dtype == torch.float32:
+                kind, sm = SV_HEAD_BCE, 0.0
+            else:
+                return None
+            n = predictions[t.name].shape[1]
+            if tgt.numel() != logits.shape[0] * (1 if kind == SV_HEAD_CE else n) or not tgt.is_cuda:
+                return None
+            specs.append((kind, off, n, float(self._loss_weights[t.name]), float(sm)))
+            tgts.append(tgt.contiguous())
+            off += n
+        return tuple(specs), tgts
+
     def get_loss(self, predictions: dict[str, torch.Tensor], targets: dict[str, torch.Tensor], **kwargs: Any):
+        fused = self._fused_loss_specs(predictions, targets)
+        if fused is not None:
+            specs, tgts = fused
+            return _FusedHeadLoss.apply(predictions.logits, specs, *tgts)
         total = torch.zeros((), device=next(self.parameters()).device)
         for t in self._tasks:
             if t.name not in predictions or t.name not in targets:
