@@ -109,6 +109,13 @@ class _ConvNeXtFn(torch.autograd.Function):
         return None, None, None
 
 
+# the backward's last block: its fc1 and depthwise weight gradients on the main stream after the stem, not behind the
+# side stream's backlog.  Opt-in (SV_TAIL_MAIN=1): the step's end waited ~0.5 ms on the side stream (r11k trace), but
+# moving them measured no different (1088.7-1092.2 vs 1090.7-1091.2 img/s interleaved, r11m); neither did letting the
+# lean release keep 64 blocks of side-stream operands instead of 4 (SV_RELEASE_BATCH: 1092.7-1092.8)
+_TAIL_MAIN = os.environ.get("SV_TAIL_MAIN", "0") != "0"
+
+
 class ConvNeXtHip(nn.Module):
     def __init__(self, depths=(3, 3, 27, 3), dims=(128, 256, 512, 1024), ls_init_value: float = 1e-6,
                  precision: str = "bf16") -> None:
@@ -394,6 +401,7 @@ class ConvNeXtHip(nn.Module):
             comm_cap = min(comm_cap, self.main_bwd_cap) if comm_cap > 0 else self.main_bwd_cap
         pol = nv.policy(grid_cap=comm_cap, wg_per_cu=self.side_wg_per_cu if side is not None else 0)
         lean = side is not None and bf and self.lean_sync
+        tail: list = []  # the last block's weight gradients the main stream runs after the stem (_TAIL_MAIN)
         # lean mode: per block (side-stream event, the operands the side stream reads), oldest first;
         # released in batches once the side stream has passed them (_release_side)
         pending: list = []
@@ -416,7 +424,9 @@ class ConvNeXtHip(nn.Module):
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 dsrc = db.view(M, C) if bf else d2
                 if lean:
-                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol)
+                    last = st is self.stages[0] and bi == 0
+                    d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol,
+                                                      tail=tail if last and _TAIL_MAIN else None)
                     self._release_side(main, pending)
                     continue
                 # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
@@ -513,6 +523,8 @@ class ConvNeXtHip(nn.Module):
             s_mean, s_rstd = tape.stem
             K.stem_bwd(tape.img, conv.weight, conv.bias, ln.weight, s_mean, s_rstd, d, dw=g(conv.weight),
                        db=g(conv.bias), dlnw=g(ln.weight), dlnb=g(ln.bias))
+        for job in tail:
+            job()
         if side is not None:
             main.wait_stream(side)  # clip / AdamW / the next step see every side-stream gradient
             pending.clear()  # safe: later main-stream allocations are ordered after the join
@@ -521,7 +533,7 @@ class ConvNeXtHip(nn.Module):
 
     # lean mode keeps at most 2 x _RELEASE_BATCH blocks of side-stream operands (dh alone is M x 4C
     # bf16) instead of every block's until the backward ends; one main->side wait per batch
-    _RELEASE_BATCH = 4
+    _RELEASE_BATCH = int(os.environ.get("SV_RELEASE_BATCH", "4"))
 
     @classmethod
     def _release_side(cls, main, pending: list) -> None:
@@ -534,14 +546,19 @@ class ConvNeXtHip(nn.Module):
             main.wait_event(pending[cls._RELEASE_BATCH - 1][0])
             del pending[:cls._RELEASE_BATCH]
 
-    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol):
+    def _block_backward_lean(self, blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol, tail=None):
         """bf16 block backward with one main->side hand-off.  Main: fc2 dgrad (x GELU'), fc1 dgrad,
         LayerNorm backward, depthwise backward-data.  Side, after the LayerNorm backward: fc2 wgrad
         (+ gamma, bias), fc1 wgrad (+ bias), the LayerNorm weight/bias fold and the depthwise wgrad of
         the block, beside the main stream's next block.  ``pol``: the main stream's GEMM policy; the side
         stream's GEMMs run at raised wave priority where they share a CU with the main stream's data-gradient
         GEMMs (+1.0% step, interleaved A/B gpurun_out prio2; raising the main stream's instead cost 0.7%,
-        prio1), under side_grid_cap when set.  Returns the new (d, db)."""
+        prio1), under side_grid_cap when set.  Returns the new (d, db).
+
+        ``tail`` (the backward's last block): the side stream, about one block behind the main stream, would run
+        this block's three weight gradients after the main stream has finished (the step's end waited ~0.5 ms on
+        it, r11k trace); only the fc2 one goes there, and the fc1 and depthwise ones (with the block's fold) are
+        appended to ``tail`` for the main stream to run after the stem."""
         g = self._grad
         x, z, y, mean, rstd, gh, a = saved
         B, H, W, C = x.shape
@@ -575,22 +592,36 @@ class ConvNeXtHip(nn.Module):
         if self.side_grid_cap is not None:
             side_cap = min(self.side_grid_cap, side_cap) if side_cap > 0 else self.side_grid_cap
         spol = nv.policy(impl=self.side_impl, grid_cap=side_cap, wg_per_cu=pol.wg_per_cu, priority=self.side_prio)
-        with torch.cuda.stream(side):
-            K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
-                               dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
-                               compute_bf16=True, policy=spol, wgrad_target=self.wgrad_target)
+        def rest(policy):
             # the block's remaining folds (fc1 wgrad slab + bias, LayerNorm and depthwise weight / bias
             # partials) in ONE launch instead of four
             folds: list | None = [] if self.merge_folds else None
             K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True, bias_out=g(blk.mlp.fc1.bias),
-                           compute_bf16=True, defer=folds, policy=spol, wgrad_target=self.wgrad_target)
+                           compute_bf16=True, defer=folds, policy=policy, wgrad_target=self.wgrad_target)
             ln_finish(record=False, defer=folds)
             K.dwconv7_bwd_weight(dz4, x, dw=g(blk.conv_dw.weight), db=g(blk.conv_dw.bias), defer=folds)
             if folds is not None:
                 K.reduce_multi(folds)
-            self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias, blk.mlp.fc1.weight,
-                         blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
+            return folds
+
+        with torch.cuda.stream(side):
+            K.layerscale_wgrad(dsrc, a, blk.mlp.fc2.weight.detach(), blk.gamma.detach(), blk.mlp.fc2.bias.detach(),
+                               dw2=g(blk.mlp.fc2.weight), dgamma=g(blk.gamma), db2=g(blk.mlp.fc2.bias),
+                               compute_bf16=True, policy=spol, wgrad_target=self.wgrad_target)
+            if tail is None:
+                folds = rest(spol)
+                self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
+                             blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
+            else:
+                folds = None
+                self._ready([blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma])
             pending.append((side.record_event(), (dsrc, dh, dz, ln_finish, x, y, a, folds)))
+        if tail is not None:
+            def job(_rest=rest, _pol=pol):
+                _rest(_pol)
+                self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
+                             blk.mlp.fc1.weight, blk.mlp.fc1.bias])
+            tail.append(job)
         # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
         db = torch.empty_like(db)
         K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)

@@ -175,11 +175,13 @@ def test_convnext_bf16_geometry(dev, name, res, B):
     bf16_parity(f"{name}@{res} B{B} bf16", hip, fp32, e64, e32, auto)
 
 
-@pytest.mark.parametrize("knob", ["lean_sync", "overlap_wgrad"])
-def test_convnext_bf16_schedule_knobs_match_default(dev, knob):
-    """SV_LEAN_SYNC=0 / SV_SIDE_STREAM=0 change only WHERE the same kernels run (one main->side hand-off
-    per block vs three; weight gradients on the side stream vs the main stream): every gradient must equal
+@pytest.mark.parametrize("knob", ["lean_sync", "overlap_wgrad", "tail_main"])
+def test_convnext_bf16_schedule_knobs_match_default(dev, knob, monkeypatch):
+    """SV_LEAN_SYNC=0 / SV_SIDE_STREAM=0 / SV_TAIL_MAIN=0 change only WHERE the same kernels run (one main->side
+    hand-off per block vs three; weight gradients on the side stream vs the main stream; the last block's fc1 and
+    depthwise weight gradients after the stem on the main stream vs on the side stream): every gradient must equal
     the default schedule's bit for bit."""
+    from spine_vision_amd.backbone import convnext as cx
     from spine_vision_amd.backbone import create_convnext
 
     ref = ow.fill_module(oc.create("convnext_base"))
@@ -190,7 +192,9 @@ def test_convnext_bf16_schedule_knobs_match_default(dev, knob):
         hip.load_state_dict(ref.state_dict(), strict=True)
         hip = hip.to(dev)
         hip.fused_mlp_bwd = False  # the fused backward runs only in the lean schedule: compare the same kernels
-        if off:
+        if knob == "tail_main":
+            monkeypatch.setattr(cx, "_TAIL_MAIN", not off)
+        elif off:
             setattr(hip, knob, False)
         f = hip(img.to(dev))
         dfeat = torch.from_numpy(ow.uniform("dfeat", f.numel(), -1, 1).reshape(f.shape)).to(dev)
