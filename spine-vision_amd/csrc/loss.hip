@@ -9,7 +9,8 @@
 //   CE (label smoothing e, C classes, targets int64, ignore_index -100): per row with a valid target
 //       loss_i = -sum_c q_c log p_c,  q = (1 - e) onehot(y) + e / C,  dl_c = (p_c - q_c) / N_valid
 //   BCE (targets f32, ncls columns): per element  max(x, 0) - x t + log1p(exp(-|x|)),  dl = (sigmoid(x) - t) / (B ncls)
-// Sums run in a fixed order (each thread its rows in ascending order, then the threads in order): deterministic.
+// Sums run in a fixed order (each thread its rows in ascending order, a butterfly per wave, the 4 waves in order):
+// deterministic.
 #include <math.h>
 
 #include "common.h"
@@ -33,30 +34,36 @@ struct Tasks {
   int n;
 };
 
+// sum over the workgroup of one value per thread: a butterfly within each wave, then the 4 wave sums in order (fixed
+// order: deterministic); every thread gets the total
+__device__ __forceinline__ float block_sum(float v, float* __restrict__ wsum) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // wsum may still be read from the previous call
+  if ((threadIdx.x & 63) == 0) wsum[w] = v;
+  __syncthreads();
+  return (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
 __global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __restrict__ logits, int B, int K, const Tasks ts,
                                                              float* __restrict__ loss, float* __restrict__ dlogits) {
-  __shared__ float red[kMaxTasks][kThreads];
+  static_assert(kThreads == 256, "block_sum: 4 waves");
+  __shared__ float wsum[4];
   __shared__ float scale[kMaxTasks];
   const int tid = threadIdx.x;
   // pass 1: the number of rows each task averages over (CE: valid targets; BCE: every element)
-#pragma unroll
-  for (int k = 0; k < kMaxTasks; ++k) {
-    float cnt = 0.f;
-    if (k < ts.n) {
-      const Task& t = ts.t[k];
-      if (t.kind == SV_HEAD_CE) {
-        for (int i = tid; i < B; i += kThreads) cnt += reinterpret_cast<const int64_t*>(t.target)[i] != -100 ? 1.f : 0.f;
-      } else if (tid == 0) {
-        cnt = (float)B * (float)t.ncls;
-      }
+  for (int k = 0; k < ts.n; ++k) {
+    const Task& t = ts.t[k];
+    float c;
+    if (t.kind == SV_HEAD_CE) {
+      float cnt = 0.f;
+      for (int i = tid; i < B; i += kThreads) cnt += reinterpret_cast<const int64_t*>(t.target)[i] != -100 ? 1.f : 0.f;
+      c = block_sum(cnt, wsum);
+    } else {
+      c = (float)B * (float)t.ncls;
     }
-    red[k][tid] = cnt;
-  }
-  __syncthreads();
-  if (tid < kMaxTasks) {
-    float c = 0.f;
-    for (int j = 0; j < kThreads; ++j) c += red[tid][j];
-    scale[tid] = c > 0.f ? 1.0f / c : 0.f;  // torch: a mean over no elements is NaN; no valid target -> 0 here
+    if (tid == 0) scale[k] = c > 0.f ? 1.0f / c : 0.f;  // torch: a mean over no elements is NaN; here 0
   }
   __syncthreads();
   // pass 2: per-row losses and the gradient, the latter already divided by the count and weighted
@@ -104,18 +111,14 @@ __global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __rest
       }
     }
   }
+  float total = 0.f;
+  for (int k = 0; k < ts.n; ++k) {
+    float pk = 0.f;
 #pragma unroll
-  for (int k = 0; k < kMaxTasks; ++k) red[k][tid] = part[k];
-  __syncthreads();
-  if (tid == 0) {
-    float total = 0.f;
-    for (int k = 0; k < ts.n; ++k) {
-      float s = 0.f;
-      for (int j = 0; j < kThreads; ++j) s += red[k][j];
-      total += ts.t[k].weight * (s * scale[k]);
-    }
-    loss[0] = total;
+    for (int q = 0; q < kMaxTasks; ++q) pk = q == k ? part[q] : pk;  // constant-indexed: part stays in registers
+    total += ts.t[k].weight * (block_sum(pk, wsum) * scale[k]);
   }
+  if (tid == 0) loss[0] = total;
 }
 
 }  // namespace loss
