@@ -113,7 +113,9 @@ class _ConvNeXtFn(torch.autograd.Function):
 # side stream's backlog.  Opt-in (SV_TAIL_MAIN=1): the step's end waited ~0.5 ms on the side stream (r11k trace), but
 # moving them measured no different (1088.7-1092.2 vs 1090.7-1091.2 img/s interleaved, r11m); neither did letting the
 # lean release keep 64 blocks of side-stream operands instead of 4 (SV_RELEASE_BATCH: 1092.7-1092.8)
-_TAIL_MAIN = os.environ.get("SV_TAIL_MAIN", "0") != "0"
+# SV_TAIL_MAIN=2: the same jobs on the main stream BEFORE the stem's backward (the side stream then ends with the block's
+# fc2 weight gradient while the main stream runs them and the stem): 1115.3-1120.6 vs 1116.6-1119.0 img/s (r11s)
+_TAIL_MAIN = int(os.environ.get("SV_TAIL_MAIN", "0"))
 
 
 class ConvNeXtHip(nn.Module):
@@ -428,6 +430,10 @@ class ConvNeXtHip(nn.Module):
                     d, db = self._block_backward_lean(blk, saved, d, db, dsrc, cache, tape, main, side, pending, pol,
                                                       tail=tail if last and _TAIL_MAIN else None)
                     self._release_side(main, pending)
+                    if last and _TAIL_MAIN == 2:
+                        for job in tail:
+                            job()
+                        tail.clear()
                     continue
                 # weight gradients (wgrad GEMMs, split-K reductions, depthwise wgrad) run on the side
                 # stream beside the data-gradient chain of the main stream: the wgrads are MFMA-bound

@@ -175,7 +175,7 @@ def test_convnext_bf16_geometry(dev, name, res, B):
     bf16_parity(f"{name}@{res} B{B} bf16", hip, fp32, e64, e32, auto)
 
 
-@pytest.mark.parametrize("knob", ["lean_sync", "overlap_wgrad", "tail_main"])
+@pytest.mark.parametrize("knob", ["lean_sync", "overlap_wgrad", "tail_main", "tail_main_before_stem"])
 def test_convnext_bf16_schedule_knobs_match_default(dev, knob, monkeypatch):
     """SV_LEAN_SYNC=0 / SV_SIDE_STREAM=0 / SV_TAIL_MAIN=0 change only WHERE the same kernels run (one main->side
     hand-off per block vs three; weight gradients on the side stream vs the main stream; the last block's fc1 and
@@ -192,8 +192,8 @@ def test_convnext_bf16_schedule_knobs_match_default(dev, knob, monkeypatch):
         hip.load_state_dict(ref.state_dict(), strict=True)
         hip = hip.to(dev)
         hip.fused_mlp_bwd = False  # the fused backward runs only in the lean schedule: compare the same kernels
-        if knob == "tail_main":
-            monkeypatch.setattr(cx, "_TAIL_MAIN", not off)
+        if knob.startswith("tail_main"):
+            monkeypatch.setattr(cx, "_TAIL_MAIN", 0 if not off else (2 if knob.endswith("stem") else 1))
         elif off:
             setattr(hip, knob, False)
         f = hip(img.to(dev))
