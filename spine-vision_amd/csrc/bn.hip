@@ -368,29 +368,23 @@ struct ActArgs {
   int64_t rows; int C;
 };
 
-template <int V>
+// FIXC: the grid's stride is a multiple of C (host: grid * kThreads * V % C == 0), so each thread's V channels are the
+// same at every grid-stride step and their parameters are loaded once, not per element group (8 of the 10 loads of
+// an iteration were those L1 / L2 reads); the arithmetic is the same
+template <int V, bool FIXC = false>
 __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
   const int64_t nv = a.rows * a.C / V;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const size_t e = (size_t)i * V;
-    const int c = chan_of(e, a.C, a.rows * a.C);
-    float v[V], mu[V], rs[V], g[V], b[V], o[V];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto body = [&](size_t e, const float (&mu)[V], const float (&rs)[V], const float (&g)[V], const float (&b)[V],
+                  const float (&rm)[V], const float (&rr)[V], const float (&rg)[V], const float (&rb)[V]) {
+    float v[V], o[V];
     ldv<V>(a.y, a.ydt, e, v);
-    ldp<V>(a.mean, c, mu);
-    ldp<V>(a.rstd, c, rs);
-    ldp<V>(a.gamma, c, g);
-    ldp<V>(a.beta, c, b);
 #pragma unroll
     for (int q = 0; q < V; ++q) o[q] = bn_pre(g[q], rs[q], v[q], mu[q], b[q]);
     if (a.res) {
       float r[V];
       ldv<V>(a.res, a.rdt, e, r);
       if (a.rmean) {
-        float rm[V], rr[V], rg[V], rb[V];
-        ldp<V>(a.rmean, c, rm);
-        ldp<V>(a.rrstd, c, rr);
-        ldp<V>(a.rgamma, c, rg);
-        ldp<V>(a.rbeta, c, rb);
 #pragma unroll
         for (int q = 0; q < V; ++q) r[q] = bn_pre(rg[q], rr[q], r[q], rm[q], rb[q]);
       }
@@ -402,6 +396,33 @@ __global__ void __launch_bounds__(kThreads) act_kernel(const ActArgs a) {
       for (int q = 0; q < V; ++q) o[q] = fmaxf(o[q], 0.f);
     }
     stv<V>(a.out, a.odt, e, o);
+  };
+  auto params = [&](int c, float (&mu)[V], float (&rs)[V], float (&g)[V], float (&b)[V], float (&rm)[V],
+                    float (&rr)[V], float (&rg)[V], float (&rb)[V]) {
+    ldp<V>(a.mean, c, mu);
+    ldp<V>(a.rstd, c, rs);
+    ldp<V>(a.gamma, c, g);
+    ldp<V>(a.beta, c, b);
+    if (a.rmean) {
+      ldp<V>(a.rmean, c, rm);
+      ldp<V>(a.rrstd, c, rr);
+      ldp<V>(a.rgamma, c, rg);
+      ldp<V>(a.rbeta, c, rb);
+    }
+  };
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (FIXC) {
+    if (i >= nv) return;
+    float mu[V], rs[V], g[V], b[V], rm[V], rr[V], rg[V], rb[V];
+    params(chan_of((size_t)i * V, a.C, a.rows * a.C), mu, rs, g, b, rm, rr, rg, rb);
+    for (; i < nv; i += stride) body((size_t)i * V, mu, rs, g, b, rm, rr, rg, rb);
+  } else {
+    for (; i < nv; i += stride) {
+      const size_t e = (size_t)i * V;
+      float mu[V], rs[V], g[V], b[V], rm[V], rr[V], rg[V], rb[V];
+      params(chan_of(e, a.C, a.rows * a.C), mu, rs, g, b, rm, rr, rg, rb);
+      body(e, mu, rs, g, b, rm, rr, rg, rb);
+    }
   }
 }
 
@@ -650,12 +671,46 @@ struct BwdArgs {
   PoolSrc pool;  // POOL instantiations: dout is the max-pool backward of pool.d (gathered)
 };
 
-template <int V, bool RELU_Y, bool POOL = false>
+template <int V, bool RELU_Y, bool POOL = false, bool FIXC = false>
 __global__ void __launch_bounds__(kThreads) bwd_apply_kernel(const BwdArgs a) {
   const int64_t nv = a.rows * a.C / V;
   const float inv_n = 1.0f / (float)a.rows;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (FIXC) {  // see act_kernel: the channel's parameters once per thread; the same arithmetic
+    if (i >= nv) return;
+    const int c = chan_of((size_t)i * V, a.C, a.rows * a.C);
+    float mu[V], rs[V], ga[V], be[V], sg[V], sgx[V];
+    ldp<V>(a.mean, c, mu);
+    ldp<V>(a.rstd, c, rs);
+    ldp<V>(a.gamma, c, ga);
+    if constexpr (RELU_Y) ldp<V>(a.beta, c, be);
+    ldp<V>(a.sums, c, sg);
+    ldp<V>(a.sums + a.C, c, sgx);
+    for (; i < nv; i += stride) {
+      const size_t e = (size_t)i * V;
+      float v[V], g[V], o[V];
+      ldv<V>(a.y, a.ydt, e, v);
+      if constexpr (POOL) pool_grad<V>(a.pool, a.C, e, g);
+      else ldv<V>(a.dout, a.ddt, e, g);
+      if constexpr (RELU_Y) {
+#pragma unroll
+        for (int q = 0; q < V; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
+      } else if (a.act) {
+        float m[V];
+        ldv<V>(a.act, a.adt, e, m);
+#pragma unroll
+        for (int q = 0; q < V; ++q) g[q] = m[q] > 0.f ? g[q] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < V; ++q)
+        o[q] = bn_dx(ga[q], rs[q], g[q], sg[q], v[q], mu[q], sgx[q], inv_n);
+      stv<V>(a.dx, a.xdt, e, o);
+      if (a.gmask) stv<V>(a.gmask, SV_F32, e, g);
+    }
+    return;
+  }
+  for (; i < nv; i += stride) {
     const size_t e = (size_t)i * V;
     const int c = chan_of(e, a.C, a.rows * a.C);
     float v[V], mu[V], rs[V], ga[V], sg[V], sgx[V], g[V], o[V];
@@ -1370,6 +1425,11 @@ static int fold_grid(int64_t rows, int C, int P) {
   return (g * kFoldThreads * 8) % C == 0 ? (int)g : 0;
 }
 
+// the hoisted-parameter kernels' condition: a thread's channel is the same at every grid-stride step (SV_BN_FIXC=0: off)
+static bool fixc_ok(int grid, int V, int C) {
+  static const bool on = !getenv("SV_BN_FIXC") || atoi(getenv("SV_BN_FIXC")) != 0;
+  return on && ((int64_t)grid * kThreads * V) % C == 0;
+}
 static int grid_for(int64_t n4) {
   int64_t b = (n4 + kThreads - 1) / kThreads;
   if (b > 8192) b = 8192;
@@ -1435,10 +1495,16 @@ extern "C" int sv_bn_act_fwd(const void* y, int32_t y_dtype, const float* mean, 
   SV_REQUIRE(!res_mean || (res && res_rstd && res_gamma && res_beta), "sv_bn_act_fwd: incomplete residual BN");
   ActArgs a{y, y_dtype, mean, rstd, gamma, beta, res, res_dtype, res_mean, res_rstd, res_gamma, res_beta,
             relu, out, out_dtype, rows, C};
-  if (vec_for(C) == 8)
-    act_kernel<8><<<grid_for(rows * C / 8), kThreads, 0, (hipStream_t)stream>>>(a);
-  else
-    act_kernel<4><<<grid_for(rows * C / 4), kThreads, 0, (hipStream_t)stream>>>(a);
+  hipStream_t st = (hipStream_t)stream;
+  const int V = vec_for(C), grid = grid_for(rows * C / V);
+  const bool fixc = fixc_ok(grid, V, C);
+  if (V == 8) {
+    if (fixc) act_kernel<8, true><<<grid, kThreads, 0, st>>>(a);
+    else act_kernel<8><<<grid, kThreads, 0, st>>>(a);
+  } else {
+    if (fixc) act_kernel<4, true><<<grid, kThreads, 0, st>>>(a);
+    else act_kernel<4><<<grid, kThreads, 0, st>>>(a);
+  }
   return check_launch("sv_bn_act_fwd");
 }
 
@@ -1516,16 +1582,21 @@ static int bwd_apply_launch(const BwdArgs& a, sv_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v8 = vec_for(a.C) == 8;
   const int grid = grid_for(a.rows * a.C / (v8 ? 8 : 4));
+  const bool fixc = fixc_ok(grid, v8 ? 8 : 4, a.C);
+#define BWDA(VV, RY, PL)                                                                              \
+  (fixc ? (bwd_apply_kernel<VV, RY, PL, true><<<grid, kThreads, 0, st>>>(a), 0)                    \
+        : (bwd_apply_kernel<VV, RY, PL><<<grid, kThreads, 0, st>>>(a), 0))
   if (a.pool.d) {
-    if (v8) bwd_apply_kernel<8, true, true><<<grid, kThreads, 0, st>>>(a);
-    else bwd_apply_kernel<4, true, true><<<grid, kThreads, 0, st>>>(a);
+    if (v8) BWDA(8, true, true);
+    else BWDA(4, true, true);
   } else if (a.beta) {
-    if (v8) bwd_apply_kernel<8, true><<<grid, kThreads, 0, st>>>(a);
-    else bwd_apply_kernel<4, true><<<grid, kThreads, 0, st>>>(a);
+    if (v8) BWDA(8, true, false);
+    else BWDA(4, true, false);
   } else {
-    if (v8) bwd_apply_kernel<8, false><<<grid, kThreads, 0, st>>>(a);
-    else bwd_apply_kernel<4, false><<<grid, kThreads, 0, st>>>(a);
+    if (v8) BWDA(8, false, false);
+    else BWDA(4, false, false);
   }
+#undef BWDA
   return check_launch("sv_bn_bwd_apply");
 }
 
