@@ -489,17 +489,24 @@ __device__ __forceinline__ void pool_grad(const PoolSrc& p, int C, size_t e, flo
 // g = dout * mask: mask = (act > 0), or (RELU_Y) recomputed from y as act_kernel computes the
 // pre-activation -- fmaf(gamma rstd, y - mean, beta) > 0 -- so the activation is not read again.
 // POOL: dout is the max-pool backward of `pool` (pool_grad), gathered in place of a load.
+// ga / be: the BatchNorm's gamma / beta at c .. c+V-1 when the caller has them in registers (RELU_Y), else loaded here
 template <int V, bool RELU_Y, bool POOL = false>
 __device__ __forceinline__ void grad_masked(const void* dout, int ddt, const void* act, int adt, size_t e,
                                             const float (&v)[V], const float (&mu)[V], const float (&rs)[V],
                                             const float* gamma, const float* beta, int c, float (&g)[V],
-                                            const PoolSrc* pool = nullptr, int C = 0) {
+                                            const PoolSrc* pool = nullptr, int C = 0, const float* ga_pre = nullptr,
+                                            const float* be_pre = nullptr) {
   if constexpr (POOL) pool_grad<V>(*pool, C, e, g);
   else ldv<V>(dout, ddt, e, g);
   if constexpr (RELU_Y) {
     float ga[V], be[V];
-    ldp<V>(gamma, c, ga);
-    ldp<V>(beta, c, be);
+    if (ga_pre) {
+#pragma unroll
+      for (int q = 0; q < V; ++q) ga[q] = ga_pre[q], be[q] = be_pre[q];
+    } else {
+      ldp<V>(gamma, c, ga);
+      ldp<V>(beta, c, be);
+    }
 #pragma unroll
     for (int q = 0; q < V; ++q) g[q] = bn_pre(ga[q], rs[q], v[q], mu[q], be[q]) > 0.f ? g[q] : 0.f;
   } else {
@@ -530,9 +537,13 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
   const int t = threadIdx.x;
   const int c = (blockIdx.x * tpr + t % tpr) * V;
   const int rsub = t / tpr;
-  float mu[V], rs[V], s1[V], s2[V];
+  float mu[V], rs[V], s1[V], s2[V], ga[V], be[V];
   ldp<V>(mean, c, mu);
   ldp<V>(rstd, c, rs);
+  if constexpr (RELU_Y) {  // once per thread: gout's stores may alias them, so the compiler would reload per row
+    ldp<V>(gamma, c, ga);
+    ldp<V>(beta, c, be);
+  }
 #pragma unroll
   for (int q = 0; q < V; ++q) s1[q] = s2[q] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.y * rpp;
@@ -546,8 +557,10 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
     float v0[V], g0[V], v1[V], g1[V];
     ldv<V>(y, ydt, e0, v0);
     ldv<V>(y, ydt, e1, v1);
-    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0, &pool, C);
-    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1, &pool, C);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e0, v0, mu, rs, gamma, beta, c, g0, &pool, C,
+                                 RELU_Y ? ga : nullptr, RELU_Y ? be : nullptr);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e1, v1, mu, rs, gamma, beta, c, g1, &pool, C,
+                                 RELU_Y ? ga : nullptr, RELU_Y ? be : nullptr);
     if (gout) {
       stv<V>(gout, ddt, e0, g0);
       stv<V>(gout, ddt, e1, g1);
@@ -564,7 +577,8 @@ __global__ void __launch_bounds__(kThreads) bwd_stats_kernel(const void* dout, i
     const size_t e = (size_t)r * C + c;
     float v[V], g[V];
     ldv<V>(y, ydt, e, v);
-    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g, &pool, C);
+    grad_masked<V, RELU_Y, POOL>(dout, ddt, act, adt, e, v, mu, rs, gamma, beta, c, g, &pool, C,
+                                 RELU_Y ? ga : nullptr, RELU_Y ? be : nullptr);
     if (gout) stv<V>(gout, ddt, e, g);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
