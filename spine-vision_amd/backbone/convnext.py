@@ -311,8 +311,9 @@ class ConvNeXtHip(nn.Module):
             for blk in st.blocks:
                 B, H, W, C = x.shape
                 M = B * H * W
+                # the tape-free forward keeps no conv output (the one-pass depthwise + LayerNorm then writes none)
                 z, y, mean, rstd = K.dwconv7_ln_fwd(x, blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight,
-                                                    blk.norm.bias, act_dtype=act)
+                                                    blk.norm.bias, act_dtype=act, save_z=save)
                 w1 = self._w(blk.mlp.fc1.weight, cache)
                 w2 = self._w(blk.mlp.fc2.weight, cache)
                 if bf and self.fused_mlp and C in K.MLP_FUSED_C and C in self.fused_mlp_c:

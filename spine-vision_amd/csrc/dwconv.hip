@@ -341,6 +341,194 @@ static DwGeo dw_geo(int B, int H, int W, int C) {
 
 static int dw_blocks(const DwGeo& g) { return ceil_div((long long)g.ntiles * (g.C / 64), kDwThreads / 64); }
 
+// ---------------------------------------------------------------------------------------------
+// Depthwise conv + LayerNorm in ONE pass (timm ConvNeXtBlock: conv_dw -> norm): one workgroup per strip with one wave
+// per 64-channel group (C / 64 waves), so every output row of the strip holds all C channels of its TW pixels inside
+// the workgroup.  Per output row the waves park the values as stored (z rounded to its dtype) in an LDS tile [TW][C];
+// the first TW * LPR lanes then reduce each pixel exactly as ln_fwd_vec_kernel<LPR, NV> (norm.hip) does -- lane l sums
+// channels 8 (l + LPR j) .. +7 in order, then the LPR-lane butterfly, then the centred second pass -- and every wave
+// normalises its own channel.  y, mean and rstd are bit for bit the two-launch result (dwconv ring kernel, then the
+// vectorised LayerNorm over z), without z's HBM round trip, and without z at all when the caller keeps none (the eval
+// forward).  Two workgroup barriers per output row; the LDS tile is accessed through inline asm so the compiler's
+// LDS-DMA alias tracking does not drain the ring's prefetches (vmcnt(0)) before each access.
+__device__ __forceinline__ void lds_st_f32(float* p, float v) {
+  const uint32_t a = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_ld8_f32(const float* p, float (&v)[8]) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t a, b;
+  const uint32_t o = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(a), "=v"(b)
+               : "v"(o)
+               : "memory");
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ float2 lds_ld2_f32(const float* p) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  f32x2_t a;
+  const uint32_t o = (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(a) : "v"(o) : "memory");
+  return make_float2(a.x, a.y);
+}
+// workgroup barrier that waits for this wave's LDS operations only (not for the ring's DMAs in flight)
+__device__ __forceinline__ void wg_bar_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+template <typename T>
+__device__ __forceinline__ float as_stored(float v) {
+  if constexpr (sizeof(T) == 4) return v;
+  else return bf2f(f2bf(v));
+}
+template <int LPR>
+__device__ __forceinline__ float dw_group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int PF, int TW, typename TIN, typename TOUT, int NWV, int LPR, int NV>
+constexpr size_t dw_ln_lds() {
+  return (size_t)NWV * PF * DwRow<TIN>::template bytes<TW + 6>() + (size_t)TW * 64 * NWV * 4;
+}
+
+template <int PF, int TW, typename TIN, typename TOUT, int NWV, int LPR, int NV>
+__global__ void __launch_bounds__(64 * NWV) dwconv7_ln_ring_kernel(const TIN* __restrict__ x,
+                                                                   const float* __restrict__ wdw,
+                                                                   const float* __restrict__ bdw,
+                                                                   const float* __restrict__ lnw,
+                                                                   const float* __restrict__ lnb, float eps,
+                                                                   TOUT* __restrict__ z, TOUT* __restrict__ y,
+                                                                   float* __restrict__ mean, float* __restrict__ rstd,
+                                                                   DwGeo g) {
+  constexpr int C = 64 * NWV;
+  static_assert(8 * LPR * NV == C, "LayerNorm lane geometry (norm.hip ln_vec_kind)");
+  static_assert((TW * LPR) % 64 == 0 && TW * LPR <= 64 * NWV, "the statistics lanes are whole waves");
+  extern __shared__ __attribute__((aligned(16))) char dw_smem[];
+  constexpr int TC = TW + 6;
+  constexpr int ROWB = DwRow<TIN>::template bytes<TC>();
+  constexpr int NL = DwRow<TIN>::template nd<TC>();  // DMA instructions per row
+  const int lane = threadIdx.x & 63, wv = wave_id_uniform();
+  int b, h0, w0;
+  dw_tile(g, xcd_block(blockIdx.x, gridDim.x, g.xcd), b, h0, w0);
+  const int c0 = wv * 64, c = c0 + lane;
+  char* ring = dw_smem + wv * PF * ROWB;
+  // [TW][C]: the output row as stored; after the statistics pass, pixel p's mean / rstd in its first two slots (read
+  // only by the lane that writes them: lane l = 0 of the pixel's group), so the whole LDS is 80 KiB at C = 512 (two
+  // workgroups per CU)
+  float* zt = reinterpret_cast<float*>(dw_smem + NWV * PF * ROWB);
+  const TIN* xg = x + c0;
+  float wk[49];
+#pragma unroll
+  for (int i = 0; i < 49; ++i) wk[i] = wdw[(size_t)c * 49 + i];
+  const float bias = bdw[c], lw = lnw[c], lb = lnb[c];
+  const float invC = 1.0f / (float)C;
+  float acc[7][TW];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int o = 0; o < TW; ++o) acc[r][o] = bias;
+  float in[TC];
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) dma_row<TC>(xg, g, b, h0 - 3 + p, w0 - 3, lane, ring + p * ROWB);
+#pragma nounroll
+  for (int ib = 0; ib < TR; ib += 7) {
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      const int ir = ib + u;
+      if (ir >= TR) break;
+      if (ir + PF - 1 < TR) dma_row<TC>(xg, g, b, h0 - 3 + ir + PF - 1, w0 - 3, lane, ring + ((ir + PF - 1) % PF) * ROWB);
+      const int rem = TR - 1 - ir;
+      wait_rows<PF, NL>(rem < PF - 1 ? rem : PF - 1);
+      const char* row = ring + (ir % PF) * ROWB;
+#pragma unroll
+      for (int j = 0; j < TC; ++j) in[j] = lds_ld<TIN>(row, j, lane);
+#pragma unroll
+      for (int kh = 0; kh < 7; ++kh) {
+        const int orow = ir - kh;
+        if (orow < 0 || orow >= TH) continue;
+        const int sl = (u - kh + 7) % 7;
+#pragma unroll
+        for (int o = 0; o < TW; ++o)
+#pragma unroll
+          for (int kw = 0; kw < 7; ++kw) acc[sl][o] = fmaf(wk[kh * 7 + kw], in[o + kw], acc[sl][o]);
+      }
+      if (ir >= 6) {  // output row ir - 6 is complete (workgroup-uniform)
+        const int sl = (u + 1) % 7;
+        const int h = h0 + ir - 6;
+        const bool okh = h < g.H;
+        const size_t rbase = ((size_t)b * g.H + (okh ? h : 0)) * g.W;
+        float zq[TW];
+#pragma unroll
+        for (int o = 0; o < TW; ++o) {
+          zq[o] = as_stored<TOUT>(acc[sl][o]);
+          if (z && okh && w0 + o < g.W) st(z + (rbase + w0 + o) * C + c0, lane, acc[sl][o]);
+          lds_st_f32(zt + o * C + c, zq[o]);
+          acc[sl][o] = bias;
+        }
+        wg_bar_lds();
+        if (threadIdx.x < TW * LPR) {  // whole waves: pixel p, LayerNorm lane l (ln_fwd_vec_kernel's reduction)
+          const int p = threadIdx.x / LPR, l = threadIdx.x % LPR;
+          float v[NV][8];
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            lds_ld8_f32(zt + p * C + (l + LPR * j) * 8, v[j]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[j][e];
+          }
+          const float mu = dw_group_sum<LPR>(s) * invC;
+          // the centred second pass as norm.hip's build of ln_fwd_vec_kernel evaluates it (its SLP-packed
+          // v_pk_mul_f32 rounds each square before the add; the variance's scale and eps are one fma)
+          float q = 0.f;
+          {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int j = 0; j < NV; ++j)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float d = v[j][e] - mu;
+                q += d * d;
+              }
+          }
+          const float rs = rsqrtf(fmaf(dw_group_sum<LPR>(q), invC, eps));
+          if (l == 0) {
+            lds_st_f32(zt + p * C, mu);
+            lds_st_f32(zt + p * C + 1, rs);
+            if (okh && w0 + p < g.W) {
+              mean[rbase + w0 + p] = mu;
+              rstd[rbase + w0 + p] = rs;
+            }
+          }
+        }
+        wg_bar_lds();
+#pragma unroll
+        for (int o = 0; o < TW; ++o) {
+          const float2 m = lds_ld2_f32(zt + o * C);
+          if (okh && w0 + o < g.W) st(y + (rbase + w0 + o) * C + c0, lane, (zq[o] - m.x) * m.y * lw + lb);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// the one-pass form: C = 128 / 256 / 512 (the C / 64 waves of a strip fit one workgroup with two or more workgroups per
+// CU), an f32 input (the residual stream) and z / y of one dtype.  Opt-in (SV_DW_LN_FUSED=1): measured no faster than
+// the two launches -- eval forward 3400 / 3393 vs 3386 / 3411 img/s, training step 1089.6 / 1091.4 vs 1094.5 / 1096.7
+// interleaved; in-step kernel time 2.49 vs 2.41 ms (S3 56.8 us per block against ~40 + 14.7): the two barriers per
+// output row tie the strip's 8 waves together, so one wave's DMA wait or statistics pass stalls all of them, which
+// costs what the z round trip saved (profiles/round5/r11z_dw_ln_fused_ab.txt)
+static bool dw_ln_fused(int B, int H, int W, int C, int x_dtype, int z_dtype, int y_dtype) {
+  static const int on = getenv("SV_DW_LN_FUSED") ? atoi(getenv("SV_DW_LN_FUSED")) : 0;
+  (void)B; (void)H; (void)W;
+  return on && (C == 128 || C == 256 || C == 512) && x_dtype == SV_F32 && (z_dtype == y_dtype) &&
+         (y_dtype == SV_F32 || y_dtype == SV_BF16);
+}
+
 }  // namespace sv
 
 using namespace sv;
@@ -351,13 +539,30 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
                       const float* lnw, const float* lnb, float eps, void* z, int32_t z_dtype, void* y,
                       int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
                       int32_t C, sv_stream_t stream) {
-  SV_REQUIRE(x && wdw && bdw && lnw && lnb && z && y && mean && rstd, "sv_dwconv7_ln_fwd: null pointer");
+  SV_REQUIRE(x && wdw && bdw && lnw && lnb && y && mean && rstd, "sv_dwconv7_ln_fwd: null pointer");
   SV_REQUIRE(C % 64 == 0 && C > 0, "sv_dwconv7_ln_fwd: C=%d must be a multiple of 64", C);
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const DwGeo g = dw_geo(B, H, W, C);
+  if (dw_ln_fused(B, H, W, C, x_dtype, z_dtype, y_dtype)) {
+    const int grid = g.ntiles;
+#define FLAUNCH(TI, TO, NWV, LPR, NV)                                                                               \
+  dwconv7_ln_ring_kernel<dw_pf<TI>(), DW_TW, TI, TO, NWV, LPR, NV>                                                  \
+      <<<grid, 64 * NWV, dw_ln_lds<dw_pf<TI>(), DW_TW, TI, TO, NWV, LPR, NV>(), s>>>(                               \
+          (const TI*)x, wdw, bdw, lnw, lnb, eps, (TO*)z, (TO*)y, mean, rstd, g)
+#define FLAUNCH_C(TI, TO)                                                      \
+  if (C == 128) FLAUNCH(TI, TO, 2, 16, 1);                                     \
+  else if (C == 256) FLAUNCH(TI, TO, 4, 32, 1);                                \
+  else FLAUNCH(TI, TO, 8, 64, 1);
+    if (y_dtype == SV_F32) { FLAUNCH_C(float, float) }
+    else { FLAUNCH_C(float, uint16_t) }
+#undef FLAUNCH_C
+#undef FLAUNCH
+    return check_launch("sv_dwconv7_ln_fwd(fused)");
+  }
+  SV_REQUIRE(z, "sv_dwconv7_ln_fwd: z == NULL needs the fused form (sv_dwconv7_ln_fused_ok)");
   const int grid = dw_blocks(g);
-#define RLAUNCH(TI, TO)                                                                                         \
+#define RLAUNCH(TI, TO)                                                                                       \
   dwconv7_ring_kernel<dw_pf<TI>(), DW_TW, TI, TO, false, false><<<grid, kDwThreads, dw_ring_lds<dw_pf<TI>(), DW_TW, TI>(), s>>>( \
       (const TI*)x, wdw, bdw, (TO*)z, nullptr, g)
   if (x_dtype == SV_F32 && z_dtype == SV_F32) RLAUNCH(float, float);
@@ -369,6 +574,11 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   int rc = check_launch("sv_dwconv7_ln_fwd(dwconv)");
   if (rc) return rc;
   return sv_layernorm_fwd(z, z_dtype, lnw, lnb, y, y_dtype, mean, rstd, (int64_t)B * H * W, C, eps, stream);
+}
+
+int sv_dwconv7_ln_fused_ok(int32_t B, int32_t H, int32_t W, int32_t C, int32_t x_dtype, int32_t z_dtype,
+                           int32_t y_dtype) {
+  return dw_ln_fused(B, H, W, C, x_dtype, z_dtype, y_dtype) ? 1 : 0;
 }
 
 int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, float* dx, uint16_t* dx_bf16,

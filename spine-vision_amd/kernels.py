@@ -591,18 +591,25 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
 
 # ----------------------------------------------------------------------------------------------
 # depthwise 7x7 + LN
-def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN):
+def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN, save_z=True):
+    """-> z (the conv output, saved for the LayerNorm backward; None when ``save_z`` is False and the one-pass form
+    runs), y = LN(z), mean, rstd.  C = 128 / 256 / 512 over an f32 input run as ONE kernel (sv_dwconv7_ln_fused_ok),
+    bitwise the two-launch result."""
     B, H, W, C = x4d.shape
     _check(C % 64 == 0, "dwconv7: C must be a multiple of 64")
-    z = torch.empty(B, H, W, C, device=x4d.device, dtype=act_dtype)
+    act_code = SV_BF16 if act_dtype == torch.bfloat16 else SV_F32
+    if not save_z and value("sv_dwconv7_ln_fused_ok", B, H, W, C, dt(x4d), act_code, act_code):
+        z = None
+    else:
+        z = torch.empty(B, H, W, C, device=x4d.device, dtype=act_dtype)
     y = torch.empty(B * H * W, C, device=x4d.device, dtype=act_dtype)
     mean = torch.empty(B * H * W, device=x4d.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
     n = B * H * W * C
     # algorithmic: x read once; z (saved for the LN backward) and y (the fc1 operand) written; mean / rstd
-    nb = n * (x4d.element_size() + z.element_size() + y.element_size()) + B * H * W * 8
+    nb = n * (x4d.element_size() + (z.element_size() if z is not None else 0) + y.element_size()) + B * H * W * 8
     _timed_call("dw_fwd", nb, "sv_dwconv7_ln_fwd", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw), ptr(lnw), ptr(lnb), eps, ptr(z),
-                dt(z), ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C, fma=49.0 * n)
+                dt(y) if z is None else dt(z), ptr(y), dt(y), ptr(mean), ptr(rstd), B, H, W, C, fma=49.0 * n)
     return z, y, mean, rstd
 
 

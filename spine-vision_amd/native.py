@@ -129,6 +129,7 @@ _SIGS = {
     "sv_dwconv7_ln_fwd": [_p, _i32, _p, _p, _p, _p, _f32, _p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_data": [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_weight_nparts": [_i32, _i32, _i32, _i32],
+    "sv_dwconv7_ln_fused_ok": [_i32, _i32, _i32, _i32, _i32, _i32, _i32],
     "sv_dwconv7_bwd_weight": [_p, _i32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_fwd": [_p, _p, _p, _p, _p, _f32, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_stem_patchify_ln_bwd_nparts": [_i32, _i32, _i32, _i32],
@@ -210,7 +211,7 @@ _SIGS = {
 _RESTYPES = {"sv_last_error_string": ctypes.c_char_p, "sv_build_target": ctypes.c_char_p,
              "sv_conv_bwd_weight_work_floats": ctypes.c_int64}
 # entry points that return a value (size / count) rather than an sv_status
-_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_bn_fold_ok", "sv_conv_bwd_weight_work_floats",
+_VALUE_FNS = {n for n in _SIGS if n.endswith(("_nparts", "_ws"))} | {"sv_version", "sv_bn_fold_ok", "sv_dwconv7_ln_fused_ok", "sv_conv_bwd_weight_work_floats",
                                                                      "sv_stream_create_cu_reserved", "sv_bn_small_ok"}
 
 # entry points that take no stream (call() appends none) but return an sv_status

@@ -1,0 +1,84 @@
+"""The one-pass depthwise conv + LayerNorm (sv_dwconv7_ln_fwd at C = 128 / 256 / 512 over an f32 input: one workgroup
+per strip, timm ConvNeXtBlock conv_dw -> norm) against the two-launch form (depthwise ring kernel, then the vectorised
+LayerNorm over the stored z): z, y, mean and rstd bit for bit, with z kept and without it (the eval forward's
+save_z=False).  The one-pass form is opt-in (SV_DW_LN_FUSED=1, read once by the library), so it runs in a child process
+and this process, at the default, runs the two launches."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from spine_vision_amd import kernels as K
+from spine_vision_amd import native as nv
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# ConvNeXt-base S1 / S2 / S3 strips at a small batch, ragged edges (H, W not multiples of the 16 x 4 strip), bf16 / f32
+CASES = [(2, 32, 32, 128, "bf16"), (1, 19, 23, 128, "f32"), (2, 16, 16, 256, "bf16"), (1, 13, 9, 256, "f32"),
+         (3, 32, 32, 512, "bf16"), (1, 7, 6, 512, "f32"), (1, 1, 1, 512, "bf16")]
+
+_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__
+__graft_entry__.load_package()
+from spine_vision_amd import kernels as K
+out = {}
+for i, (B, H, W, C, dts) in enumerate(eval(sys.argv[2])):
+    g = torch.Generator().manual_seed(100 + i)
+    x = (torch.randn(B, H, W, C, generator=g) * 1.5 + 0.2).cuda()
+    w = (torch.randn(C, 49, generator=g) * 0.2).cuda()
+    b = (torch.randn(C, generator=g) * 0.1).cuda()
+    lw = (torch.rand(C, generator=g) + 0.5).cuda()
+    lb = (torch.randn(C, generator=g) * 0.1).cuda()
+    act = torch.bfloat16 if dts == "bf16" else torch.float32
+    z, y, m, r = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act)
+    z2, y2, m2, r2 = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act, save_z=False)
+    assert z2 is None
+    out[i] = [t.cpu() for t in (z, y, m, r, y2, m2, r2)]
+torch.save(out, sys.argv[3])
+"""
+
+
+def _inputs(i, B, H, W, C):
+    g = torch.Generator().manual_seed(100 + i)
+    x = (torch.randn(B, H, W, C, generator=g) * 1.5 + 0.2).cuda()
+    w = (torch.randn(C, 49, generator=g) * 0.2).cuda()
+    b = (torch.randn(C, generator=g) * 0.1).cuda()
+    lw = (torch.rand(C, generator=g) + 0.5).cuda()
+    lb = (torch.randn(C, generator=g) * 0.1).cuda()
+    return x, w, b, lw, lb
+
+
+def test_dw_ln_fused_matches_two_launches(dev, tmp_path):
+    assert os.environ.get("SV_DW_LN_FUSED", "0") == "0"
+    for B, H, W, C, dts in CASES:
+        code = nv.SV_BF16 if dts == "bf16" else nv.SV_F32
+        assert K.value("sv_dwconv7_ln_fused_ok", B, H, W, C, nv.SV_F32, code, code) == 0
+    out_file = tmp_path / "one_pass.pt"
+    env = dict(os.environ, SV_DW_LN_FUSED="1")
+    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, repr(CASES), str(out_file)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(out_file, weights_only=True)
+    for i, (B, H, W, C, dts) in enumerate(CASES):
+        x, w, b, lw, lb = _inputs(i, B, H, W, C)
+        act = torch.bfloat16 if dts == "bf16" else torch.float32
+        z, y, m, rs = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act)
+        torch.cuda.synchronize()
+        ref = [t.cpu() for t in (z, y, m, rs, y, m, rs)]
+        for name, a, e in zip(("z", "y", "mean", "rstd", "y (no z)", "mean (no z)", "rstd (no z)"), got[i], ref):
+            assert torch.equal(a.reshape(e.shape), e), (B, H, W, C, dts, name,
+                                                         float((a.float().reshape(e.shape) - e.float()).abs().max()))
+
+
+def test_dw_ln_unfused_widths_keep_z(dev):
+    """C = 64 / 1024 (not the one-pass form) still write z even when the caller keeps none."""
+    for C in (64, 1024):
+        x, w, b, lw, lb = _inputs(7, 1, 8, 8, C)
+        assert K.value("sv_dwconv7_ln_fused_ok", 1, 8, 8, C, nv.SV_F32, nv.SV_BF16, nv.SV_BF16) == 0
+        z, y, _, _ = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=torch.bfloat16, save_z=False)
+        assert z is not None and z.shape == (1, 8, 8, C) and y.shape == (64, C)
