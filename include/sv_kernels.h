@@ -231,9 +231,10 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
                       const float* lnw, const float* lnb, float eps, void* z, int32_t z_dtype, void* y,
                       int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
                       int32_t C, sv_stream_t stream);
-/* 1 when sv_dwconv7_ln_fwd runs as ONE pass for these arguments (depthwise conv and LayerNorm in one workgroup per
- * strip: C = 128 / 256 / 512, f32 x, z and y of one dtype), 0 when it runs the two launches.  Only the one-pass form
- * accepts z == NULL (no saved conv output: the eval forward).  y / mean / rstd are bitwise the same either way.   */
+/* 1 when sv_dwconv7_ln_fwd may be called with z == NULL for these arguments: it then runs as ONE pass (depthwise conv
+ * and block LayerNorm in one workgroup per strip: C = 128 / 256 / 512, f32 x, z and y of one dtype) and writes no conv
+ * output (the eval forward).  With z given it runs the two launches (SV_DW_LN_FUSED=1: the one pass there too).
+ * y / mean / rstd (and z) are bitwise the same either way.                                                          */
 int sv_dwconv7_ln_fused_ok(int32_t B, int32_t H, int32_t W, int32_t C, int32_t x_dtype, int32_t z_dtype,
                            int32_t y_dtype);
 /* backward-data of the depthwise conv: dx[p] = (accumulate ? dx[p] : 0) + sum_tap w*dz; if dx_bf16

@@ -383,10 +383,27 @@ __device__ __forceinline__ float as_stored(float v) {
   if constexpr (sizeof(T) == 4) return v;
   else return bf2f(f2bf(v));
 }
+// the xor butterfly over LPR lanes in norm.hip group_sum<LPR>'s order (partner distance LPR/2 first, then halving), each
+// partner value from the cross-lane unit instead of a ds_bpermute round trip: permlane32 / permlane16 swaps give the
+// exact xor-32 / xor-16 partners; DPP row rotation by 8 is xor 8 inside a 16-lane row; rotations by 4 and 2 deliver a
+// lane whose value equals the xor partner's (the earlier steps made lanes i, i^8 and then i^4 equal); a quad
+// permutation is xor 1.  Every lane ends with the same sum, bitwise the shuffle form's.
 template <int LPR>
 __device__ __forceinline__ float dw_group_sum(float v) {
-#pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "row-rotation steps need LPR >= 16");
+  const int lane = threadIdx.x & 63;
+  if constexpr (LPR >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float(lane < 32 ? r[1] : r[0]);
+  }
+  if constexpr (LPR >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float((lane & 16) ? r[0] : r[1]);
+  }
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x124, 0xf, 0xf, false));  // row_ror:4
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x122, 0xf, 0xf, false));  // row_ror:2
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
   return v;
 }
 
@@ -517,16 +534,22 @@ __global__ void __launch_bounds__(64 * NWV) dwconv7_ln_ring_kernel(const TIN* __
 }
 
 // the one-pass form: C = 128 / 256 / 512 (the C / 64 waves of a strip fit one workgroup with two or more workgroups per
-// CU), an f32 input (the residual stream) and z / y of one dtype.  Opt-in (SV_DW_LN_FUSED=1): measured no faster than
-// the two launches -- eval forward 3400 / 3393 vs 3386 / 3411 img/s, training step 1089.6 / 1091.4 vs 1094.5 / 1096.7
-// interleaved; in-step kernel time 2.49 vs 2.41 ms (S3 56.8 us per block against ~40 + 14.7): the two barriers per
-// output row tie the strip's 8 waves together, so one wave's DMA wait or statistics pass stalls all of them, which
-// costs what the z round trip saved (profiles/round5/r11z_dw_ln_fused_ab.txt)
-static bool dw_ln_fused(int B, int H, int W, int C, int x_dtype, int z_dtype, int y_dtype) {
-  static const int on = getenv("SV_DW_LN_FUSED") ? atoi(getenv("SV_DW_LN_FUSED")) : 0;
-  (void)B; (void)H; (void)W;
-  return on && (C == 128 || C == 256 || C == 512) && x_dtype == SV_F32 && (z_dtype == y_dtype) &&
+// CU), an f32 input (the residual stream) and z / y of one dtype.  It runs where the caller keeps no z (z == NULL: the
+// eval forward), and there measured +2.4 % (3485 / 3467 vs 3390 / 3400 img/s interleaved); where z is kept (training) it
+// measured no faster than the two launches (1092.9 / 1089.5 vs 1096.4 / 1092.0 img/s): the two barriers per output row
+// tie the strip's waves together, which costs what the z re-read saves (profiles/round5/r11z_dw_ln_fused_ab.txt).
+// SV_DW_LN_FUSED: unset = that split, 1 = the one-pass form whenever it applies, 0 = never (z required; A/B runs)
+static int dw_ln_mode() {
+  static const int m = getenv("SV_DW_LN_FUSED") ? atoi(getenv("SV_DW_LN_FUSED")) : -1;
+  return m;
+}
+static bool dw_ln_fusable(int C, int x_dtype, int z_dtype, int y_dtype) {
+  return (C == 128 || C == 256 || C == 512) && x_dtype == SV_F32 && z_dtype == y_dtype &&
          (y_dtype == SV_F32 || y_dtype == SV_BF16);
+}
+static bool dw_ln_fused(int C, int x_dtype, int z_dtype, int y_dtype, bool keep_z) {
+  const int m = dw_ln_mode();
+  return dw_ln_fusable(C, x_dtype, z_dtype, y_dtype) && (m == 1 || (m < 0 && !keep_z));
 }
 
 }  // namespace sv
@@ -544,7 +567,7 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const DwGeo g = dw_geo(B, H, W, C);
-  if (dw_ln_fused(B, H, W, C, x_dtype, z_dtype, y_dtype)) {
+  if (dw_ln_fused(C, x_dtype, z_dtype, y_dtype, z != nullptr)) {
     const int grid = g.ntiles;
 #define FLAUNCH(TI, TO, NWV, LPR, NV)                                                                               \
   dwconv7_ln_ring_kernel<dw_pf<TI>(), DW_TW, TI, TO, NWV, LPR, NV>                                                  \
@@ -578,7 +601,8 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
 
 int sv_dwconv7_ln_fused_ok(int32_t B, int32_t H, int32_t W, int32_t C, int32_t x_dtype, int32_t z_dtype,
                            int32_t y_dtype) {
-  return dw_ln_fused(B, H, W, C, x_dtype, z_dtype, y_dtype) ? 1 : 0;
+  (void)B; (void)H; (void)W;
+  return dw_ln_fusable(C, x_dtype, z_dtype, y_dtype) && dw_ln_mode() != 0 ? 1 : 0;
 }
 
 int sv_dwconv7_bwd_data(const void* dz, int32_t dz_dtype, const float* wdw, float* dx, uint16_t* dx_bf16,

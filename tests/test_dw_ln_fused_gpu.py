@@ -1,8 +1,7 @@
 """The one-pass depthwise conv + LayerNorm (sv_dwconv7_ln_fwd at C = 128 / 256 / 512 over an f32 input: one workgroup
 per strip, timm ConvNeXtBlock conv_dw -> norm) against the two-launch form (depthwise ring kernel, then the vectorised
-LayerNorm over the stored z): z, y, mean and rstd bit for bit, with z kept and without it (the eval forward's
-save_z=False).  The one-pass form is opt-in (SV_DW_LN_FUSED=1, read once by the library), so it runs in a child process
-and this process, at the default, runs the two launches."""
+LayerNorm over the stored z): y, mean and rstd bit for bit without z (the eval forward's save_z=False, which takes the
+one pass by default), and z too with z kept (SV_DW_LN_FUSED=1, read once by the library: a child process)."""
 import os
 import subprocess
 import sys
@@ -54,10 +53,21 @@ def _inputs(i, B, H, W, C):
 
 
 def test_dw_ln_fused_matches_two_launches(dev, tmp_path):
-    assert os.environ.get("SV_DW_LN_FUSED", "0") == "0"
-    for B, H, W, C, dts in CASES:
+    assert os.environ.get("SV_DW_LN_FUSED") is None
+    refs = []
+    for i, (B, H, W, C, dts) in enumerate(CASES):
         code = nv.SV_BF16 if dts == "bf16" else nv.SV_F32
-        assert K.value("sv_dwconv7_ln_fused_ok", B, H, W, C, nv.SV_F32, code, code) == 0
+        assert K.value("sv_dwconv7_ln_fused_ok", B, H, W, C, nv.SV_F32, code, code) == 1
+        x, w, b, lw, lb = _inputs(i, B, H, W, C)
+        act = torch.bfloat16 if dts == "bf16" else torch.float32
+        z, y, m, rs = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act)  # z kept: the two launches
+        z1, y1, m1, rs1 = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act, save_z=False)  # the one pass
+        torch.cuda.synchronize()
+        assert z1 is None
+        for name, a, e in (("y", y1, y), ("mean", m1, m), ("rstd", rs1, rs)):
+            assert torch.equal(a, e), (B, H, W, C, dts, name, float((a.float() - e.float()).abs().max()))
+        refs.append([t.cpu() for t in (z, y, m, rs, y, m, rs)])
+    # the one pass with z kept (forced), in a child process
     out_file = tmp_path / "one_pass.pt"
     env = dict(os.environ, SV_DW_LN_FUSED="1")
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, repr(CASES), str(out_file)], env=env, capture_output=True,
@@ -65,12 +75,7 @@ def test_dw_ln_fused_matches_two_launches(dev, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     got = torch.load(out_file, weights_only=True)
     for i, (B, H, W, C, dts) in enumerate(CASES):
-        x, w, b, lw, lb = _inputs(i, B, H, W, C)
-        act = torch.bfloat16 if dts == "bf16" else torch.float32
-        z, y, m, rs = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=act)
-        torch.cuda.synchronize()
-        ref = [t.cpu() for t in (z, y, m, rs, y, m, rs)]
-        for name, a, e in zip(("z", "y", "mean", "rstd", "y (no z)", "mean (no z)", "rstd (no z)"), got[i], ref):
+        for name, a, e in zip(("z", "y", "mean", "rstd", "y (no z)", "mean (no z)", "rstd (no z)"), got[i], refs[i]):
             assert torch.equal(a.reshape(e.shape), e), (B, H, W, C, dts, name,
                                                          float((a.float().reshape(e.shape) - e.float()).abs().max()))
 
