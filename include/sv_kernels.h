@@ -231,6 +231,10 @@ int sv_dwconv7_ln_fwd(const void* x, int32_t x_dtype, const float* wdw, const fl
                       const float* lnw, const float* lnb, float eps, void* z, int32_t z_dtype, void* y,
                       int32_t y_dtype, float* mean, float* rstd, int32_t B, int32_t H, int32_t W,
                       int32_t C, sv_stream_t stream);
+/* diagnostic: per lane, the sum over its group of `lanes` (16 / 32 / 64) lanes by the cross-lane butterfly the
+ * LayerNorm kernels use (xlane) and by the ds_bpermute shuffle butterfly (shuffle); the two are bitwise equal.
+ * n: a multiple of 256.                                                                                       */
+int sv_diag_group_sum(const float* in, float* xlane, float* shuffle, int64_t n, int32_t lanes, sv_stream_t stream);
 /* 1 when sv_dwconv7_ln_fwd may be called with z == NULL for these arguments: it then runs as ONE pass (depthwise conv
  * and block LayerNorm in one workgroup per strip: C = 128 / 256 / 512, f32 x, z and y of one dtype) and writes no conv
  * output (the eval forward).  With z given it runs the two launches (SV_DW_LN_FUSED=1: the one pass there too).

@@ -141,6 +141,30 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// xor-butterfly sum over groups of LPR lanes (16, 32 or 64) in __shfl_xor order (partner distance LPR/2 first, then
+// halving), the partners taken from the cross-lane unit instead of ds_bpermute round trips: permlane32 / permlane16
+// swaps for the exact xor-32 / xor-16 partners, DPP row rotation by 8 (xor 8 inside a 16-lane row), rotations by 4 and
+// 2 (they deliver a lane whose value equals the xor partner's: the earlier steps made lanes i, i^8 and then i^4 equal)
+// and a quad permutation (xor 1).  Every lane of a group ends with the same sum, bitwise the shuffle butterfly's.
+template <int LPR>
+__device__ __forceinline__ float xlane_group_sum(float v) {
+  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "row-rotation steps need groups of >= 16 lanes");
+  const int lane = threadIdx.x & 63;
+  if constexpr (LPR >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float(lane < 32 ? r[1] : r[0]);
+  }
+  if constexpr (LPR >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float((lane & 16) ? r[0] : r[1]);
+  }
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x124, 0xf, 0xf, false));  // row_ror:4
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x122, 0xf, 0xf, false));  // row_ror:2
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
+  return v;
+}
+
 // block-wide sum; `red` must hold >= blockDim.x/64 floats; all threads get the result
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

@@ -383,28 +383,10 @@ __device__ __forceinline__ float as_stored(float v) {
   if constexpr (sizeof(T) == 4) return v;
   else return bf2f(f2bf(v));
 }
-// the xor butterfly over LPR lanes in norm.hip group_sum<LPR>'s order (partner distance LPR/2 first, then halving), each
-// partner value from the cross-lane unit instead of a ds_bpermute round trip: permlane32 / permlane16 swaps give the
-// exact xor-32 / xor-16 partners; DPP row rotation by 8 is xor 8 inside a 16-lane row; rotations by 4 and 2 deliver a
-// lane whose value equals the xor partner's (the earlier steps made lanes i, i^8 and then i^4 equal); a quad
-// permutation is xor 1.  Every lane ends with the same sum, bitwise the shuffle form's.
+// norm.hip group_sum<LPR>'s butterfly, bitwise, from the cross-lane unit (common.h)
 template <int LPR>
 __device__ __forceinline__ float dw_group_sum(float v) {
-  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "row-rotation steps need LPR >= 16");
-  const int lane = threadIdx.x & 63;
-  if constexpr (LPR >= 64) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v += __uint_as_float(lane < 32 ? r[1] : r[0]);
-  }
-  if constexpr (LPR >= 32) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v += __uint_as_float((lane & 16) ? r[0] : r[1]);
-  }
-  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x128, 0xf, 0xf, false));  // row_ror:8
-  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x124, 0xf, 0xf, false));  // row_ror:4
-  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x122, 0xf, 0xf, false));  // row_ror:2
-  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
-  return v;
+  return xlane_group_sum<LPR>(v);
 }
 
 template <int PF, int TW, typename TIN, typename TOUT, int NWV, int LPR, int NV>

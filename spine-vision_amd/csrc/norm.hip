@@ -160,11 +160,20 @@ __device__ __forceinline__ void st8v(T* __restrict__ p, const float (&v)[8]) {
         make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
   }
 }
+// the row statistics' butterfly over LPR lanes: from the cross-lane unit for groups of >= 16 lanes (common.h
+// xlane_group_sum, bitwise the shuffle form; -DSV_LN_XLANE=0 keeps ds_bpermute shuffles, A/B builds)
+#ifndef SV_LN_XLANE
+#define SV_LN_XLANE 1
+#endif
 template <int LPR>
 __device__ __forceinline__ float group_sum(float v) {
+  if constexpr (SV_LN_XLANE && LPR >= 16) {
+    return xlane_group_sum<LPR>(v);
+  } else {
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
 }
 
 template <typename TX, typename TY, int LPR, int NV>
@@ -779,11 +788,36 @@ __global__ void __launch_bounds__(kLnThreads) pool_bwd_kernel(
   }
 }
 
+// the two butterfly forms side by side (sv_diag_group_sum: the test of xlane_group_sum's bitwise claim)
+template <int LPR>
+__global__ void __launch_bounds__(256) diag_group_sum_kernel(const float* __restrict__ in, float* __restrict__ xl,
+                                                             float* __restrict__ sh, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // n % 256 == 0: whole waves
+  const float v = in[i];
+  float t = v;
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  xl[i] = xlane_group_sum<LPR>(v);
+  sh[i] = t;
+  (void)n;
+}
+
 }  // namespace sv
 
 using namespace sv;
 
 extern "C" {
+
+int sv_diag_group_sum(const float* in, float* xlane, float* shuffle, int64_t n, int32_t lanes, sv_stream_t stream) {
+  SV_REQUIRE(in && xlane && shuffle && n > 0 && n % 256 == 0, "sv_diag_group_sum: n must be a positive multiple of 256");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = (unsigned)(n / 256);
+  if (lanes == 16) diag_group_sum_kernel<16><<<grid, 256, 0, s>>>(in, xlane, shuffle, n);
+  else if (lanes == 32) diag_group_sum_kernel<32><<<grid, 256, 0, s>>>(in, xlane, shuffle, n);
+  else if (lanes == 64) diag_group_sum_kernel<64><<<grid, 256, 0, s>>>(in, xlane, shuffle, n);
+  else return set_error(SV_ERR_INVALID_ARG, "sv_diag_group_sum: lanes must be 16, 32 or 64");
+  return check_launch("sv_diag_group_sum");
+}
 
 int sv_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
                      int32_t y_dtype, float* mean, float* rstd, int64_t rows, int32_t C, float eps,

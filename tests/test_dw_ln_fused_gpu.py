@@ -87,3 +87,26 @@ def test_dw_ln_unfused_widths_keep_z(dev):
         assert K.value("sv_dwconv7_ln_fused_ok", 1, 8, 8, C, nv.SV_F32, nv.SV_BF16, nv.SV_BF16) == 0
         z, y, _, _ = K.dwconv7_ln_fwd(x, w, b, lw, lb, act_dtype=torch.bfloat16, save_z=False)
         assert z is not None and z.shape == (1, 8, 8, C) and y.shape == (64, C)
+
+
+@pytest.mark.parametrize("lanes", [16, 32, 64])
+def test_xlane_group_sum_is_the_shuffle_butterfly(dev, lanes):
+    """common.h xlane_group_sum (permlane swaps + DPP row rotations, used by the LayerNorm statistics) against the
+    ds_bpermute __shfl_xor butterfly on the same lanes: bitwise, over values of mixed sign and magnitude (so every
+    addition order would show), denormals, zeros and infinities."""
+    g = torch.Generator().manual_seed(lanes)
+    n = 256 * 1024
+    v = torch.randn(n, generator=g) * torch.exp2(torch.randint(-30, 30, (n,), generator=g).float())
+    v[::97] = 0.0
+    v[5::101] = 1e-40
+    v[7::4099] = float("inf")
+    v = v.to(dev)
+    xl, sh = torch.empty_like(v), torch.empty_like(v)
+    K.call("sv_diag_group_sum", K.ptr(v), K.ptr(xl), K.ptr(sh), n, lanes)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(sh)
+    assert torch.equal(xl[fin], sh[fin]) and torch.equal(torch.isfinite(xl), fin)
+    # every lane of a group holds the same sum
+    grp = sh.view(-1, lanes)
+    ok = torch.isfinite(grp).all(1)
+    assert torch.equal(grp[ok], grp[ok][:, :1].expand(-1, lanes))
