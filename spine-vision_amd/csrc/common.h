@@ -165,6 +165,29 @@ __device__ __forceinline__ float xlane_group_sum(float v) {
   return v;
 }
 
+// the value of lane l ^ OFF, from the cross-lane unit: OFF 1 / 2 = quad permutations, 8 = DPP row rotation by 8 (xor 8
+// inside a 16-lane row), 16 / 32 = permlane16 / permlane32 swaps -- each the exact xor partner.  OFF 4 has no single
+// DPP form: xlane_xor<4, true> uses the half-row mirror, whose source lane holds the partner's value only where the
+// quads are uniform (after xor 1 and xor 2 steps of an ascending butterfly).
+template <int OFF, bool QUADS_UNIFORM = false>
+__device__ __forceinline__ float xlane_xor(float v) {
+  const uint32_t u = __float_as_uint(v);
+  if constexpr (OFF == 1) return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0xb1, 0xf, 0xf, false));
+  else if constexpr (OFF == 2) return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0x4e, 0xf, 0xf, false));
+  else if constexpr (OFF == 4) {
+    static_assert(QUADS_UNIFORM, "xor 4 via the half-row mirror needs uniform quads");
+    return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0x141, 0xf, 0xf, false));
+  } else if constexpr (OFF == 8) return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0x128, 0xf, 0xf, false));
+  else if constexpr (OFF == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+  } else {
+    static_assert(OFF == 32, "xor distance 1, 2, 4, 8, 16 or 32");
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+  }
+}
+
 // block-wide sum; `red` must hold >= blockDim.x/64 floats; all threads get the result
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

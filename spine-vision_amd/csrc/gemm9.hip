@@ -438,12 +438,26 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][FN], const EpiAr
 #pragma unroll
       for (int c = 0; c < CH; ++c)
 #pragma unroll
-        for (int w = 0; w < 8; ++w)
+        for (int w = 0; w < 8; ++w) {
+#if SV_STATS_XLANE
+          // the same partners from the cross-lane unit (bitwise the shuffle form): xor 1 / 2 / 8 exact, xor 4 through
+          // the half-row mirror once the quads are uniform
+          st1[c][w] += xlane_xor<1>(st1[c][w]);
+          st2[c][w] += xlane_xor<1>(st2[c][w]);
+          st1[c][w] += xlane_xor<2>(st1[c][w]);
+          st2[c][w] += xlane_xor<2>(st2[c][w]);
+          st1[c][w] += xlane_xor<4, true>(st1[c][w]);
+          st2[c][w] += xlane_xor<4, true>(st2[c][w]);
+          st1[c][w] += xlane_xor<8>(st1[c][w]);
+          st2[c][w] += xlane_xor<8>(st2[c][w]);
+#else
 #pragma unroll
           for (int off = 1; off < 16; off <<= 1) {
             st1[c][w] += __shfl_xor(st1[c][w], off);
             st2[c][w] += __shfl_xor(st2[c][w], off);
           }
+#endif
+        }
       if (ml == 0 && mb < e.M) {
         float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N;
 #pragma unroll

@@ -5,6 +5,12 @@
 
 #include "common.h"
 
+// statistics epilogues' column folds from the cross-lane unit (common.h xlane_xor; bitwise the ds_bpermute shuffles,
+// -DSV_STATS_XLANE=0 keeps those: A/B builds)
+#ifndef SV_STATS_XLANE
+#define SV_STATS_XLANE 1
+#endif
+
 namespace sv {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -362,11 +368,21 @@ __device__ __forceinline__ void wave_group_epilogue(const f32x4 (&acc)[FM][FN], 
     // order, bit-stable), then lanes 0..7 write the group's partial row [mb/64][2][N] (one writer each)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+#if SV_STATS_XLANE
+      // the same partners from the cross-lane unit (exact xor 8 / 16 / 32): bitwise the shuffle form
+      cs1[j] += xlane_xor<8>(cs1[j]);
+      cs2[j] += xlane_xor<8>(cs2[j]);
+      cs1[j] += xlane_xor<16>(cs1[j]);
+      cs2[j] += xlane_xor<16>(cs2[j]);
+      cs1[j] += xlane_xor<32>(cs1[j]);
+      cs2[j] += xlane_xor<32>(cs2[j]);
+#else
 #pragma unroll
       for (int off = 8; off < 64; off <<= 1) {
         cs1[j] += __shfl_xor(cs1[j], off);
         cs2[j] += __shfl_xor(cs2[j], off);
       }
+#endif
     }
     if (l < 8 && okn && mb < e.M) {  // groups wholly past M have no partial row
       float* P = reinterpret_cast<float*>(e.C2) + (size_t)(mb >> 6) * 2 * e.N + n;
