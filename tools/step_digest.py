@@ -51,7 +51,7 @@ def main():
     h = hashlib.sha256()
     for n, p in sorted(model.state_dict().items()):
         h.update(n.encode())
-        h.update(p.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes() if p.numel() else b"")
+        h.update(p.detach().contiguous().cpu().reshape(-1).view(torch.uint8).numpy().tobytes() if p.numel() else b"")
     print(json.dumps({"lib": os.environ.get("SV_LIB_PATH", "default"), "workload": a.workload, "losses": losses,
                       "digest": h.hexdigest()}))
 
