@@ -134,12 +134,6 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x, q.dens, q.phi);
 }
 
-// ---- wave / block reductions (wave64) -------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // xor-butterfly sum over groups of LPR lanes (16, 32 or 64) in __shfl_xor order (partner distance LPR/2 first, then
 // halving), the partners taken from the cross-lane unit instead of ds_bpermute round trips: permlane32 / permlane16
@@ -186,6 +180,22 @@ __device__ __forceinline__ float xlane_xor(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
     return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
   }
+}
+
+// ---- wave / block reductions (wave64) -------------------------------------------------
+// the xor butterflies take their partners from the cross-lane unit (above) instead of ds_bpermute; bitwise the same
+// sums.  -DSV_XLANE=0 builds the shuffle forms everywhere (A/B builds)
+#ifndef SV_XLANE
+#define SV_XLANE 1
+#endif
+__device__ __forceinline__ float wave_sum(float v) {
+#if SV_XLANE
+  return xlane_group_sum<64>(v);
+#else
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+#endif
 }
 
 // block-wide sum; `red` must hold >= blockDim.x/64 floats; all threads get the result

@@ -8,7 +8,7 @@
 // statistics epilogues' column folds from the cross-lane unit (common.h xlane_xor; bitwise the ds_bpermute shuffles,
 // -DSV_STATS_XLANE=0 keeps those: A/B builds)
 #ifndef SV_STATS_XLANE
-#define SV_STATS_XLANE 1
+#define SV_STATS_XLANE SV_XLANE
 #endif
 
 namespace sv {

@@ -163,7 +163,7 @@ __device__ __forceinline__ void st8v(T* __restrict__ p, const float (&v)[8]) {
 // the row statistics' butterfly over LPR lanes: from the cross-lane unit for groups of >= 16 lanes (common.h
 // xlane_group_sum, bitwise the shuffle form; -DSV_LN_XLANE=0 keeps ds_bpermute shuffles, A/B builds)
 #ifndef SV_LN_XLANE
-#define SV_LN_XLANE 1
+#define SV_LN_XLANE SV_XLANE
 #endif
 template <int LPR>
 __device__ __forceinline__ float group_sum(float v) {
