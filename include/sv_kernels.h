@@ -186,7 +186,8 @@ int sv_gemm_slab_finish_bn_bwd(const float* slab, int32_t split, int32_t M, int3
  * y [M, C] bf16, w1 [4C, C] bf16 (torch Linear layout), b1 [4C] f32, w2 [C, 4C] bf16, b2 / gamma [C] f32,
  * x / x_out [M, C] f32 (must not alias).  gelu_grad / gelu_out [M, 4C] bf16, both or neither: the
  * training forward stores GELU'(h) and GELU(h) for the backward (bit for bit the dual epilogue's), the
- * eval forward passes NULL.  C in {128, 192, 256}; every pointer 16-byte aligned; M * 4C * 2 < 2^31.
+ * eval forward passes NULL.  C in {128, 192, 256, 512} (512: the opt-in S3 kernel, measured slower than the two
+ * GEMMs and not taken by default); every pointer 16-byte aligned; M * 4C * 2 < 2^31.
  * x_out is bit for bit the unfused pair's.                                                           */
 int sv_mlp_fwd(const uint16_t* y, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                const float* gamma, const float* x, float* x_out, uint16_t* gelu_grad, uint16_t* gelu_out, int64_t M,

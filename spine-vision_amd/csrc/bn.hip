@@ -299,7 +299,9 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, in
     st_sc1(slot + k * 64 + lane, v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acq_rel: the add releases this workgroup's chunk sums and acquires the others' for the last adder, so
+    // the hand-off is ordered by the memory model, not only by the sc1 encoding and the wait above
+    if (lane == 0) old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (__shfl(old, 0) != S - 1) return false;
     tot = ld_sc1(slot + lane);
     for (int q = 1; q < S; ++q) tot += ld_sc1(slot + q * 64 + lane);
@@ -1242,7 +1244,7 @@ __device__ __forceinline__ void fold_phase(const FoldCtl& f) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int old = 0;
         if (lane == 0)
-          old = __hip_atomic_fetch_add(ctl + kFoldSlot + job * f.ncg + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          old = __hip_atomic_fetch_add(ctl + kFoldSlot + job * f.ncg + cg, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         fin = __shfl(old, 0) == f.S - 1;
         if (fin) {  // every chunk of this channel group has landed: their sums in chunk order
           float tot = ld_sc1(slot + lane);

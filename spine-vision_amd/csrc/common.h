@@ -12,6 +12,19 @@
 
 #include "../../include/sv_kernels.h"
 
+// ---- ISA-checked counted waits (tools/check_vmcnt.py, tests/test_vmcnt_isa.py) ----------------------------------
+// A counted s_waitcnt vmcnt(N) retires a DMA only if at least N vector-memory instructions were issued after it, in
+// the instruction stream the COMPILER emitted, on every path.  These markers let the checker verify that on the
+// device assembly instead of trusting the source order:
+//   SV_VMTAG("name")       after the last vector-memory instruction of a group a later counted wait must retire;
+//   SV_VMWAIT(N, "name:k") s_waitcnt vmcnt(N) that must retire the k-th most recent instance of each listed group
+//                          (k = 1: the latest; several "name:k" separated by spaces);
+//   SV_VMCHECK("name:k")   asserts the same at that point without waiting.
+// The asm statements clobber memory, so the compiler cannot move vector-memory instructions across them.
+#define SV_VMTAG(t) asm volatile("; svtag " t ::: "memory")
+#define SV_VMWAIT(n, t) asm volatile("s_waitcnt vmcnt(%0) ; svwait " t ::"n"(n) : "memory")
+#define SV_VMCHECK(t) asm volatile("; svcheck " t ::: "memory")
+
 namespace sv {
 
 // ---- error plumbing (defined in abi.cpp) ---------------------------------------------

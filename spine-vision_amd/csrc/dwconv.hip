@@ -415,9 +415,10 @@ __global__ void __launch_bounds__(64 * NWV) dwconv7_ln_ring_kernel(const TIN* __
   dw_tile(g, xcd_block(blockIdx.x, gridDim.x, g.xcd), b, h0, w0);
   const int c0 = wv * 64, c = c0 + lane;
   char* ring = dw_smem + wv * PF * ROWB;
-  // [TW][C]: the output row as stored; after the statistics pass, pixel p's mean / rstd in its first two slots (read
-  // only by the lane that writes them: lane l = 0 of the pixel's group), so the whole LDS is 80 KiB at C = 512 (two
-  // workgroups per CU)
+  // [TW][C]: the output row as stored; after the statistics pass, pixel p's mean / rstd in its first two slots, so the
+  // whole LDS is 80 KiB at C = 512 (two workgroups per CU; a separate statistics array would push it past 160 KiB per
+  // two).  Every wave reads those slots after the second barrier of the row and wave 0 overwrites them with its next
+  // row's channel-0/1 values: a third barrier after the reads orders the reuse
   float* zt = reinterpret_cast<float*>(dw_smem + NWV * PF * ROWB);
   const TIN* xg = x + c0;
   float wk[49];
@@ -509,6 +510,7 @@ __global__ void __launch_bounds__(64 * NWV) dwconv7_ln_ring_kernel(const TIN* __
           const float2 m = lds_ld2_f32(zt + o * C);
           if (okh && w0 + o < g.W) st(y + (rbase + w0 + o) * C + c0, lane, (zq[o] - m.x) * m.y * lw + lb);
         }
+        wg_bar_lds();  // every wave has read the statistics slots before any wave stores the next row into zt
       }
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -589,17 +589,21 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         dma<EPI == SV_EPI_SLAB ? SV_G9_SLAB_B_CPOL : 0>(rb, vb, so + j * step, bb + (wid + 8 * j) * 1024);
+      SV_VMTAG("p2");
     } else if constexpr (AK) {
       char* ab = smem + a_off<AK>(l_g);
       const int h = part == 1 ? 0 : 1;  // pieces h*8 + wid (rows 64h + ..) and h*8 + 16 + wid (+128 rows)
       const uint32_t so = (uint32_t)k0 * 2 + (uint32_t)(64 * h * lda * 2);
       dma(ra, va, so, ab + (h * 8 + wid) * 1024);
       dma(ra, va, so + (uint32_t)(128 * lda * 2), ab + (h * 8 + 16 + wid) * 1024);
+      if (part == 1) SV_VMTAG("p1");
+      else SV_VMTAG("p3");
     } else if (part == 1) {
       char* ab = smem + a_off<AK>(l_g);
       const uint32_t so = (uint32_t)((int64_t)k0 * lda * 2), step = (uint32_t)(16 * lda * 2);
 #pragma unroll
       for (int j = 0; j < 4; ++j) dma(ra, va, so + j * step, ab + (wid + 8 * j) * 1024);
+      SV_VMTAG("p1");
     }
   };
   auto advance = [&]() {
@@ -724,6 +728,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
           if (src && (wid == 0 || EPI == SV_EPI_BIAS_GAMMA_RES))
             dma(rsrc(src, (uint32_t)e.N * 4), (uint32_t)(cg.n0 + (threadIdx.x & 63) * 4) * 4, 0,
                 smem + lds_bytes<AK>() + (it & 1) * 2048 + wid * 1024);
+          SV_VMTAG("bias");
         }
       }
       lgkm0();
@@ -737,8 +742,9 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       issue_part(1);
       if (do_cs) colsum_frag(af, cs[0]);
       if (AK) {
-        if (it > 0 && kt <= 1) vm_wait<W2E>();
-        else vm_wait<W2>();
+        // the A quadrant-1 rows of THIS K-tile: the part-3 DMA two K-tiles back
+        if (it > 0 && kt <= 1) SV_VMWAIT(W2E, "p3:2@epi");  // the previous tile's epilogue lies between
+        else SV_VMWAIT(W2, "p3:2");
       }
       lgkm0();
       bar();
@@ -757,8 +763,9 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
       if constexpr (AK) issue_part(3);
       advance();
       if (do_cs) colsum_frag(af, cs[1]);
-      if (it > 0 && kt == 0) vm_wait<W1E>();
-      else vm_wait<W1>();
+      // parts 1 and 2 of K-tile g+1: issued one K-tile back (this K-tile's phases 1-2 issued K-tile g+2's)
+      if (it > 0 && kt == 0) SV_VMWAIT(W1E, "p1:2@epi p2:2@epi");
+      else SV_VMWAIT(W1, "p1:2 p2:2");
       lgkm0();
       bar();
       quad(1, 0);
@@ -783,6 +790,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     }
     epilogue<EPI, P8, AK, FOLD>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
                       LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
+    SV_VMTAG("epi");  // after the epilogue's fixed EpiCount memory instructions (the E in W1E / W2E)
     if constexpr (FOLD) {
       // arrival: every wave's slab stores complete (this also drains the next tile's first DMAs: the K loop's
       // counted waits then find fewer in flight, which they allow), one ticket per workgroup

@@ -9,6 +9,8 @@
 //   CE (label smoothing e, C classes, targets int64, ignore_index -100): per row with a valid target
 //       loss_i = -sum_c q_c log p_c,  q = (1 - e) onehot(y) + e / C,  dl_c = (p_c - q_c) / N_valid
 //   BCE (targets f32, ncls columns): per element  max(x, 0) - x t + log1p(exp(-|x|)),  dl = (sigmoid(x) - t) / (B ncls)
+// A CE target outside [0, C) that is not -100 makes the loss and that row's d(loss)/d(logits) NaN (torch stops with a
+// device-side assert; a silently dropped one-hot term would train on a wrong loss).
 // Sums run in a fixed order (each thread its rows in ascending order, a butterfly per wave, the 4 waves in order):
 // deterministic.
 #include <math.h>
@@ -68,6 +70,7 @@ __global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __rest
   __syncthreads();
   // pass 2: per-row losses and the gradient, the latter already divided by the count and weighted
   float part[kMaxTasks];
+  float nbad = 0.f;  // CE targets outside [0, ncls) that are not ignore_index
 #pragma unroll
   for (int k = 0; k < kMaxTasks; ++k) part[k] = 0.f;
   for (int i = tid; i < B; i += kThreads) {
@@ -82,6 +85,11 @@ __global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __rest
         const int64_t y = reinterpret_cast<const int64_t*>(t.target)[i];
         if (y == -100) {
           for (int c = 0; c < t.ncls; ++c) dx[t.offset + c] = 0.f;
+          continue;
+        }
+        if (y < 0 || y >= t.ncls) {  // torch raises a device-side assert here: poison the row and the loss instead
+          for (int c = 0; c < t.ncls; ++c) dx[t.offset + c] = NAN;
+          nbad += 1.f;
           continue;
         }
         float mx = -INFINITY;
@@ -118,7 +126,8 @@ __global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __rest
     for (int q = 0; q < kMaxTasks; ++q) pk = q == k ? part[q] : pk;  // constant-indexed: part stays in registers
     total += ts.t[k].weight * (block_sum(pk, wsum) * scale[k]);
   }
-  if (tid == 0) loss[0] = total;
+  nbad = block_sum(nbad, wsum);
+  if (tid == 0) loss[0] = nbad > 0.f ? NAN : total;
 }
 
 }  // namespace loss

@@ -171,6 +171,7 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         dma(rw1, v1, (uint32_t)(((j0 + 32 * h) * C + 64 * kb) * 2), st + kb * (HC * 128) + (wa + 4 * h) * 1024);
+    SV_VMTAG("w1");
   };
   auto issue_w2 = [&](int q) {
     const int j0 = (q % K::NCH) * HC;
@@ -180,6 +181,7 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         dma(rw2, v2, (uint32_t)(((64 * j + 32 * h) * K::H + j0) * 2), st + (8 * j + wa + 4 * h) * 1024);
+    SV_VMTAG("w2");
   };
   // vector-memory instructions of group A younger than the DMA each wait retires: the dual epilogue's S stores per
   // chunk, the other ring's N1 pieces (the counts allow them to stay in flight)
@@ -221,10 +223,14 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
 
     for (int ch = 0; ch < K::NCH; ++ch, ++q) {
       // X_q: W1(q) landed (A: issued after X_{q-1}; younger: chunk q-1's stores, W2(q)'s pieces)
-      if (grp == 0) vm_wait<S + N1>();
+      if (grp == 0) SV_VMWAIT(S + N1, "w1:1");
       lgkm0();
       if (!(SV_MLP_DIAG & 4)) bar();
-      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
+      // unconditional (past the end: a harmless re-load of chunk 0 into the free slot): every chunk issues the same
+      // vector-memory instructions, which the counted waits assume.  Round 5 skipped it for q + 1 == total, which left
+      // the last chunk's Y wait with fewer younger instructions than its count: W2 of a workgroup's last chunk was not
+      // covered (tools/check_vmcnt.py found it)
+      if (grp == 0 && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
       const char* st = w1r + (q & 1) * K::W1B;
       const int j0 = ch * HC;
       // this lane's fc1 bias: hidden units j0 + 32 qq + 8 gq .. +7
@@ -288,10 +294,10 @@ mlp_fwd_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, 
         }
       }
       // Y_q: W2(q) landed (A: issued after Y_{q-1}; younger: W1(q+1)'s pieces, this chunk's stores)
-      if (grp == 0) vm_wait<N1 + S>();
+      if (grp == 0) SV_VMWAIT(N1 + S, "w2:1");
       lgkm0();
       if (!(SV_MLP_DIAG & 4)) bar();
-      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
+      if (grp == 0 && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
       // fc2: acc2 += W2[:, chunk] . P^T, k (hidden) ascending
       const char* img2 = w2r + (q & 1) * K::W2B;
 #pragma unroll
@@ -400,12 +406,14 @@ mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
     char* st = smem + OFF_W1 + (q & 1) * W1B;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+    SV_VMTAG("w1");
   };
   auto issue_w2 = [&](int q) {
     const int j0 = (q % NCH) * HC;
     char* st = smem + OFF_W2 + (q & 1) * W2B;
 #pragma unroll
     for (int h = 0; h < 2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wid + 4 * h) * 1024);
+    SV_VMTAG("w2");
   };
   // this wave's y fragments of tile t into its own region (rows past M, and tiles past the end, read as zeros)
   char* ybuf = smem + OFF_Y + wid * YB;
@@ -418,6 +426,7 @@ mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) dma(ry, vy, (uint32_t)(64 * ks), ybuf + (rf * KS + ks) * 1024);
     }
+    SV_VMTAG("y");
   };
   constexpr int S = TRAIN ? RF * 2 : 0;  // the dual epilogue's stores per chunk
 
@@ -431,7 +440,7 @@ mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
     const int row0 = ((int)blockIdx.x + it * (int)gridDim.x) * R + wid * 16 * RF;
     // y of this tile landed (issued at the previous tile's start: a whole tile of vector-memory instructions -- at
     // least 16 chunks x (N1 + N2) -- is younger)
-    vm_wait<32>();
+    SV_VMWAIT(32, "y:1");
     bf16x8 yf[RF][KS];
 #pragma unroll
     for (int rf = 0; rf < RF; ++rf)
@@ -449,8 +458,8 @@ mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
     for (int ch = 0; ch < NCH; ++ch, ++q) {
       // X_q: W1(q) landed.  Younger than it (issued after the previous X barrier): that chunk's stores and W2(q);
       // across a tile boundary also the x loads, the x_out stores and this tile's y prefetch
-      if (ch == 0) vm_wait<XL + S + N2 + XO + YP>();
-      else vm_wait<S + N2>();
+      if (ch == 0) SV_VMWAIT(XL + S + N2 + XO + YP, "w1:1");
+      else SV_VMWAIT(S + N2, "w1:1");
       lgkm0();
       bar();
       issue_w1(q + 1);  // past the end: a harmless re-load of chunk 0 into the free slot (uniform counts)
@@ -520,9 +529,9 @@ mlp128_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
       }
       // Y_q: W2(q) landed.  Younger (issued after the previous Y barrier): W1(q+1) and this chunk's stores; in a
       // tile's first chunk also the x_out stores and the y prefetch, in its last the x loads
-      if (ch == 0) vm_wait<XO + YP + N1 + S>();
-      else if (ch == NCH - 1) vm_wait<N1 + XL + S>();
-      else vm_wait<N1 + S>();
+      if (ch == 0) SV_VMWAIT(XO + YP + N1 + S, "w2:1");
+      else if (ch == NCH - 1) SV_VMWAIT(N1 + XL + S, "w2:1");
+      else SV_VMWAIT(N1 + S, "w2:1");
       lgkm0();
       bar();
       issue_w2(q + 1);
@@ -580,6 +589,11 @@ static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const 
 // (w2t = (W2 gamma)^T [512][128] in W1's layout, w1t = W1^T [128][512] in W2's), GELU'(h) is loaded a chunk ahead,
 // z / mean / rstd a chunk ahead of the epilogue.  dh and bf16(dy) are bit for bit the unfused GEMMs' (same MFMA,
 // operands and k order); dz and the partial sums differ from sv_layernorm_bwd only by f32 summation order.
+// SV_MLPB_XLANE=1: the LayerNorm epilogue's butterflies from the cross-lane unit (common.h xlane_xor) instead of
+// ds_bpermute -- opt-in A/B build; round 5 measured that form non-deterministic run to run (DESIGN "Round 6")
+#ifndef SV_MLPB_XLANE
+#define SV_MLPB_XLANE 0
+#endif
 constexpr int MAX_BWD_WG = 512;  // the grid: min(tiles, 512) workgroups (two per CU), 4 partial rows each
 
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -614,12 +628,14 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
     char* st = smem + OFF_W1 + (q & 1) * W1B;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wid * 1024);
+    SV_VMTAG("w1");
   };
   auto issue_w2 = [&](int q) {
     const int j0 = (q % NCH) * HC;
     char* st = smem + OFF_W2 + (q & 1) * W2B;
 #pragma unroll
     for (int h = 0; h < 2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wid + 4 * h) * 1024);
+    SV_VMTAG("w2");
   };
   char* ybuf = smem + OFF_Y + wid * YB;
   auto tile_row = [&](int it) { return ((int)blockIdx.x + it * (int)gridDim.x) * R + wid * 16 * RF; };
@@ -632,6 +648,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) dma(ry, vy, (uint32_t)(64 * ks), ybuf + (rf * KS + ks) * 1024);
     }
+    SV_VMTAG("y");
   };
   // GELU'(h) of chunk q (tile it = q / NCH): lane -> row, 8 consecutive hidden units, loaded a chunk ahead (two
   // chunks ahead in two alternating register sets measured slower: 444 vs 426 us at base S1)
@@ -658,7 +675,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
   int q = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int row0 = tile_row(it);
-    vm_wait<32>();  // this tile's d fragments (issued a tile ago)
+    SV_VMWAIT(32, "y:1");  // this tile's d fragments (issued a tile ago)
     bf16x8 yf[RF][KS];
 #pragma unroll
     for (int rf = 0; rf < RF; ++rf)
@@ -680,8 +697,8 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
 #endif
       // X_q: W1(q) (here (W2 gamma)^T) landed; younger: the previous chunk's GELU' loads and dh stores, W2(q); across
       // a tile boundary also the z / mean / rstd loads, the dz stores and the d prefetch
-      if (ch == 0) vm_wait<GL + SD + N2 + ZL + ZO + YP>();
-      else vm_wait<GL + SD + N2>();
+      if (ch == 0) SV_VMWAIT(GL + SD + N2 + ZL + ZO + YP, "w1:1");
+      else SV_VMWAIT(GL + SD + N2, "w1:1");
       lgkm0();
       bar();
       issue_w1(q + 1);
@@ -702,6 +719,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
           mu[rf] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmu, mo, 0, 0));
           rs[rf] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, mo, 0, 0));
         }
+        SV_VMTAG("zl");
       }
       const char* st1 = smem + OFF_W1 + (q & 1) * W1B;
       const int j0 = ch * HC;
@@ -742,9 +760,9 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
       }
       // Y_q: W2(q) (here W1^T) landed; younger: W1(q+1), the GELU' loads, this chunk's dh stores; in a tile's first
       // chunk also the dz stores and the d prefetch, in its last the LayerNorm operand loads
-      if (ch == 0) vm_wait<ZO + YP + N1 + GL + SD>();
-      else if (ch == NCH - 1) vm_wait<N1 + GL + ZL + SD>();
-      else vm_wait<N1 + GL + SD>();
+      if (ch == 0) SV_VMWAIT(ZO + YP + N1 + GL + SD, "w2:1");
+      else if (ch == NCH - 1) SV_VMWAIT(N1 + GL + ZL + SD, "w2:1");
+      else SV_VMWAIT(N1 + GL + SD, "w2:1");
       lgkm0();
       bar();
       issue_w2(q + 1);
@@ -763,7 +781,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
 #endif
     // the z / mean / rstd loads (last chunk): younger only that chunk's dh stores and the W2 DMA.  Explicit: the
     // compiler's own wait here was short (tools/mlp_bwd_diag.py: dz / dw differed run to run at M = 524288 without it)
-    vm_wait<SD + N2>();
+    SV_VMWAIT(SD + N2, "zl:1");
     float* la = lacc + wid * 2 * C;
 #pragma unroll
     for (int rf = 0; rf < RF; ++rf) {
@@ -786,10 +804,17 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
           s2 += g * xhat(cf, w);
         }
       }
+#if SV_MLPB_XLANE
+      s1 += xlane_xor<16>(s1);
+      s1 += xlane_xor<32>(s1);
+      s2 += xlane_xor<16>(s2);
+      s2 += xlane_xor<32>(s2);
+#else
       s1 += __shfl_xor(s1, 16);
       s1 += __shfl_xor(s1, 32);
       s2 += __shfl_xor(s2, 16);
       s2 += __shfl_xor(s2, 32);
+#endif
       s1 *= 1.0f / (float)C;
       s2 *= 1.0f / (float)C;
 #pragma unroll
@@ -800,7 +825,12 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
         for (int w = 0; w < 4; ++w) {
           const float dv = dyv(cf, w), xh = xhat(cf, w);
           o[w] = rs[rf] * (dv * lw[w] - s1 - xh * s2);
-          pw[w] = dv * xh;
+          {
+            // the product rounded once, before the butterfly: contracted into its first add (fma), a lane would add its
+            // partner's ROUNDED product to its own exact one -- the two lanes of a pair would differ
+#pragma clang fp contract(off)
+            pw[w] = dv * xh;
+          }
           pb[w] = dv;
         }
         const uint32_t off = m < M ? (uint32_t)(((size_t)m * C + 16 * cf + 4 * gq) * 2) : OOB;
@@ -809,11 +839,24 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
         // lane ml == 0 adds them into the wave's own LDS row (one writer per word: deterministic)
 #pragma unroll
         for (int w = 0; w < 4; ++w)
+#if SV_MLPB_XLANE
+        {
+          pw[w] += xlane_xor<1>(pw[w]);
+          pb[w] += xlane_xor<1>(pb[w]);
+          pw[w] += xlane_xor<2>(pw[w]);
+          pb[w] += xlane_xor<2>(pb[w]);
+          pw[w] += xlane_xor<4, true>(pw[w]);  // quads uniform after xor 1 and 2
+          pb[w] += xlane_xor<4, true>(pb[w]);
+          pw[w] += xlane_xor<8>(pw[w]);
+          pb[w] += xlane_xor<8>(pb[w]);
+        }
+#else
 #pragma unroll
           for (int sh = 1; sh < 16; sh <<= 1) {
             pw[w] += __shfl_xor(pw[w], sh);
             pb[w] += __shfl_xor(pb[w], sh);
           }
+#endif
         if (ml == 0) {
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
@@ -954,6 +997,7 @@ mlp512_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
     char* st = smem + OFF_W1 + (q & 1) * W1B;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) dma(rw1, v1, (uint32_t)((j0 * C + 64 * kb) * 2), st + kb * (HC * 128) + wa * 1024);
+    SV_VMTAG("w1");
   };
   auto issue_w2 = [&](int q) {
     const int ln = lane_id();
@@ -963,6 +1007,7 @@ mlp512_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
     char* st = smem + OFF_W2 + (q & 1) * W2B;
 #pragma unroll
     for (int h = 0; h < N2; ++h) dma(rw2, v2, (uint32_t)((64 * h * H + j0) * 2), st + (wa + 4 * h) * 1024);
+    SV_VMTAG("w2");
   };
   // P slots: this wave's GELU(h) chunk (register image) at OFF_PB + 1 KiB wid; the pair's two at 1 KiB (2 rg + rf)
   constexpr int S = TRAIN ? 2 : 0;  // the dual epilogue's stores per chunk
@@ -998,10 +1043,14 @@ mlp512_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
 
     for (int ch = 0; ch < NCH; ++ch, ++q) {
       // X_q: W1(q) landed (A: issued after X_{q-1}; younger: chunk q-1's stores, W2(q)'s pieces)
-      if (grp == 0 && ch > 0) vm_wait<S + N2>();
+      if (grp == 0 && ch > 0) SV_VMWAIT(S + N2, "w1:1");
       lgkm0();
       if (!(SV_MLP_DIAG & 4)) bar();
-      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
+      // unconditional (past the end: a harmless re-load of chunk 0 into the free slot): every chunk issues the same
+      // vector-memory instructions, which the counted waits assume.  Round 5 skipped it for q + 1 == total, which left
+      // the last chunk's Y wait with fewer younger instructions than its count: W2 of a workgroup's last chunk was not
+      // covered (tools/check_vmcnt.py found it)
+      if (grp == 0 && !(SV_MLP_DIAG & 2)) issue_w1(q + 1);
       const int ln = lane_id();
       const char* st1 = smem + OFF_W1 + (q & 1) * W1B;
       const int j0 = ch * HC;
@@ -1067,10 +1116,10 @@ mlp512_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ w1, c
       __builtin_amdgcn_sched_barrier(0);
       // Y_q: W2(q) landed (A: issued after Y_{q-1}; younger: W1(q+1)'s pieces, this chunk's stores); every wave of the
       // group wrote its P slot
-      if (grp == 0) vm_wait<N1 + S>();
+      if (grp == 0) SV_VMWAIT(N1 + S, "w2:1");
       lgkm0();
       if (!(SV_MLP_DIAG & 4)) bar();
-      if (grp == 0 && q + 1 < total && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
+      if (grp == 0 && !(SV_MLP_DIAG & 2)) issue_w2(q + 1);
       // fc2: acc2 += W2[half, chunk] . P^T over the pair's 32 rows, k (hidden) ascending
       {
         const int ln2 = lane_id();

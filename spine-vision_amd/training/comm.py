@@ -91,29 +91,57 @@ class GradBucketer:
         self.seen: set[int] = set()
         self.works = []
         self.launched = [False] * len(self.buckets)
+        # per bucket: the last readiness event of EVERY stream that reported some of its gradients (stream handle ->
+        # event).  Backbones report from the stream that wrote the gradients (ConvNeXt: block weight gradients on its
+        # side stream, downsample / stem ones on the main stream), so the all-reduce must wait for each of them, not
+        # only for the stream of the last report
+        self.ready_ev: list[dict] = [dict() for _ in self.buckets]
 
     def attach(self, model: torch.nn.Module) -> None:
         """Route readiness from backbones (grad_ready_hook) and autograd-managed params."""
         self._hooks += _attach_ready(model, self.arena, self.mark_ready)
 
     def mark_ready(self, params) -> None:
+        touched: list[int] = []
         for p in params:
             if id(p) in self.seen or id(p) not in self.param_bucket:
                 continue
             self.seen.add(id(p))
             b = self.param_bucket[id(p)]
             self.pending[b] -= 1
+            if b not in touched:
+                touched.append(b)
+        if not touched:
+            return
+        if self.use_streams:
+            # one event on the reporting stream, kept per (bucket, stream): a later report from the same stream
+            # supersedes it (stream order)
+            cur = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            for b in touched:
+                self.ready_ev[b][cur.cuda_stream] = ev
+        for b in touched:
             if self.pending[b] == 0:
                 self._launch(b)
+
+    def _wait_ready(self, b: int) -> None:
+        """The comm stream waits for every stream that wrote bucket b's gradients (and for the launching stream)."""
+        cur = torch.cuda.current_stream()
+        evs = self.ready_ev[b]
+        if cur.cuda_stream not in evs:
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            evs[cur.cuda_stream] = ev
+        for ev in evs.values():
+            self.comm_stream.wait_event(ev)
 
     def _launch(self, b: int) -> None:
         s, e, _ = self.buckets[b]
         view = self.arena.grad_flat[s:e]
         op = dist.ReduceOp.AVG if dist.get_backend(self.group) == "nccl" else dist.ReduceOp.SUM
         if self.use_streams:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            self.comm_stream.wait_event(ev)
+            self._wait_ready(b)
             with torch.cuda.stream(self.comm_stream):
                 e0 = None
                 if self.timing:

@@ -235,7 +235,7 @@ def _bf16_batch():
     return img, coords, torch.ones_like(mask)
 
 
-def _bf16_rank(rank, world, port, out):
+def _bf16_rank(rank, world, port, out, bucket_mb=16.0):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -257,9 +257,11 @@ def _bf16_rank(rank, world, port, out):
     if rank == 1:  # the broadcast must overwrite a diverged replica
         with torch.no_grad():
             m.backbone.stages[2].blocks[5].mlp.fc1.bias.add_(1.0)
-    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=16.0)
+    eng = StepEngine(m, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, distributed=True, bucket_mb=bucket_mb)
     bb = m.backbone
-    setup = (bb.comm_reserve_cus, bb.lean_sync, bb.overlap_wgrad, bb.precision)
+    ds = bb.stages[3].downsample[0].weight
+    first_ends_on_ds = eng.arena.params[eng.bucketer.buckets[0][2][-1]] is ds
+    setup = (bb.comm_reserve_cus, bb.lean_sync, bb.overlap_wgrad, bb.precision, first_ends_on_ds)
     img, coords, mask = _bf16_batch()
     sl = slice(rank * B16, (rank + 1) * B16)
     loss = eng.step_localization(img[sl].to(dev), coords[sl].to(dev), mask[sl].to(dev))
@@ -270,30 +272,23 @@ def _bf16_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(600)
-def test_two_rank_bf16_lean_step_equals_half_batch_average(dev):
-    """Two ranks (gloo, the box's one GPU) run the bf16 ConvNeXt-base step exactly as StepEngine sets it up under
-    data parallelism: the lean side-stream backward with per-block grad-ready events launching the bucketed
-    all-reduce, here with every backward GEMM grid capped by the optional 32-CU comm reserve.  The replicas end bit-identical, and
-    the all-reduced gradient equals, bit for bit, the average of two single-process half-batch gradients
-    ((g0 + g1) / 2 in f32: a 2-rank SUM is order-free and the halving exact).  Reference: accelerate DDP
-    (spine_vision/training/trainers/base.py:253-266), LocalizationTrainer._train_step (localization.py:186-209)."""
-    from spine_vision_amd.training import StepEngine
-
+def _run_bf16_ranks(bucket_mb):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_bf16_rank, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_bf16_rank, args=(r, 2, port, out, bucket_mb)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=500)
         assert p.exitcode == 0, f"rank exited with {p.exitcode}"
-    (l0, g0, p0, nb, setup0), (l1, g1, p1, _, setup1) = out[0], out[1]
-    assert setup0 == setup1 == (32, True, True, "bf16"), setup0
-    assert nb > 1
-    assert torch.equal(g0, g1) and torch.equal(p0, p1)
+    return out[0], out[1]
+
+
+def _half_batch_average(dev, losses):
+    from spine_vision_amd.training import StepEngine
+
     img, coords, mask = _bf16_batch()
     halves = []
     for r in range(2):
@@ -302,10 +297,55 @@ def test_two_rank_bf16_lean_step_equals_half_batch_average(dev):
         sl = slice(r * B16, (r + 1) * B16)
         lr_ = float(eng.step_localization(img[sl].to(dev), coords[sl].to(dev), mask[sl].to(dev)))
         torch.cuda.synchronize()
-        assert lr_ == (l0, l1)[r]  # each rank's loss is its half-batch loss
+        assert lr_ == losses[r]  # each rank's loss is its half-batch loss
         halves.append(eng.arena.grad_flat.cpu().clone())
         del eng, m
-    avg = (halves[0] + halves[1]) / 2
+    return (halves[0] + halves[1]) / 2
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_bf16_lean_step_equals_half_batch_average(dev):
+    """Two ranks (gloo, the box's one GPU) run the bf16 ConvNeXt-base step exactly as StepEngine sets it up under
+    data parallelism: the lean side-stream backward with per-block grad-ready events launching the bucketed
+    all-reduce, here with every backward GEMM grid capped by the optional 32-CU comm reserve.  The replicas end bit-identical, and
+    the all-reduced gradient equals, bit for bit, the average of two single-process half-batch gradients
+    ((g0 + g1) / 2 in f32: a 2-rank SUM is order-free and the halving exact).  Reference: accelerate DDP
+    (spine_vision/training/trainers/base.py:253-266), LocalizationTrainer._train_step (localization.py:186-209)."""
+    (l0, g0, p0, nb, setup0), (l1, g1, p1, _, setup1) = _run_bf16_ranks(16.0)
+    assert setup0[:4] == setup1[:4] == (32, True, True, "bf16"), setup0
+    assert nb > 1
+    assert torch.equal(g0, g1) and torch.equal(p0, p1)
+    avg = _half_batch_average(dev, (l0, l1))
     diff = (g0 - avg).abs().max()
     print(f"[ddp] bf16 world 2: {nb} buckets, max |allreduced - half-batch average| = {float(diff):.3e}")
+    assert torch.equal(g0, avg)
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_bucket_ending_on_downsample_waits_for_every_stream(dev):
+    """a bucket whose last-reported parameter is a downsample's (reported on the main stream)
+    while the same bucket's block weight gradients come from the side stream.  bucket_mb is chosen so the first
+    bucket (from the end of the flat buffer: head + stage-4 blocks) closes exactly on stages[3].downsample's first
+    parameter; GradBucketer must make the comm stream wait on both streams' events, so the all-reduced gradient is
+    still bit for bit the half-batch average."""
+    from spine_vision_amd.training.flat import _align
+
+    m = _model(dev, "bf16")
+    ds = m.backbone.stages[3].downsample[0].weight
+    sizes, seen, i_ds = [], set(), None
+    for p in m.parameters():  # FlatArena's order and 64-B aligned offsets
+        if id(p) in seen:
+            continue
+        seen.add(id(p))
+        if p is ds:
+            i_ds = len(sizes)
+        sizes.append(_align(p.numel()))
+    bucket_mb = sum(sizes[i_ds:]) * 4 / 2**20
+    del m
+    (l0, g0, p0, nb, setup0), (l1, g1, p1, _, setup1) = _run_bf16_ranks(bucket_mb)
+    assert setup0 == setup1 == (32, True, True, "bf16", True), setup0
+    assert torch.equal(g0, g1) and torch.equal(p0, p1)
+    avg = _half_batch_average(dev, (l0, l1))
+    print(f"[ddp] bucket_mb {bucket_mb:.2f}: {nb} buckets, first ends on the stage-4 downsample, "
+          f"max |allreduced - half-batch average| = {float((g0 - avg).abs().max()):.3e}")
     assert torch.equal(g0, avg)

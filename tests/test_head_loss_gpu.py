@@ -116,3 +116,18 @@ def test_task_config_with_focal_loss_falls_back(dev):
     pred = generic._HeadOutputs(zip(["pfirrmann", "modic", "herniation"], logits.split([5, 4, 1], dim=1)))
     pred.logits = logits
     assert m._fused_loss_specs(pred, _targets(8, g, dev)) is None
+
+
+@pytest.mark.parametrize("bad", [5, -3], ids=["past-ncls", "negative"])
+def test_fused_head_loss_out_of_range_target_is_loud(dev, bad):
+    """A CE target outside [0, ncls) that is not ignore_index: torch stops with a device-side assert; the fused loss
+    makes the loss and that row's logits gradient NaN instead of silently dropping the one-hot term."""
+    g = torch.Generator().manual_seed(11)
+    model = generic.Classifier("resnet18", tasks=_tasks(), pretrained=False, dropout=0.0, precision="fp32").to(dev)
+    logits = (torch.randn(8, 10, generator=g) * 3).to(dev)
+    targets = _targets(8, g, dev)
+    targets["pfirrmann"][3] = bad
+    lf, gf = _loss_and_grad(model, logits, targets, True)
+    assert torch.isnan(lf)
+    assert torch.isnan(gf[3, :5]).all()
+    assert torch.isfinite(gf[:3]).all() and torch.isfinite(gf[4:]).all() and torch.isfinite(gf[3, 5:]).all()

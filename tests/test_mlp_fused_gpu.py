@@ -195,12 +195,29 @@ def test_mlp_bwd_fused_matches_three_kernels(dev, M):
     weight / bias gradient partials within f32 summation order."""
     o = _bwd_ops(dev, M, 128, seed=M)
     dh, dz, dw, db = _bwd_fused(o)
-    again = _bwd_fused(o)
+    runs = [_bwd_fused(o) for _ in range(3)]
     rh, rz, rw, rb, rdy = _bwd_unfused(o)
     torch.cuda.synchronize()
-    # run to run bit for bit (a short wait on the LayerNorm operands once showed as dz / dw differing between runs)
-    for a_, b_ in zip((dh, dz, dw, db), again):
-        assert torch.equal(a_, b_)
+    # run to run bit for bit (round 5: the cross-lane epilogue build differed between runs at M = 524288); a mismatch
+    # names the tensor and where it differs (rows -> 128-row tiles -> workgroup and its tile index, the grid being
+    # min(tiles, 512) workgroups striding over the tiles)
+    grid = min((M + 127) // 128, 512)
+    for k, again in enumerate(runs):
+        for name, a_, b_ in zip(("dh", "dz", "dw", "db"), (dh, dz, dw, db), again):
+            if torch.equal(a_, b_):
+                continue
+            bad = (a_ != b_) & ~(torch.isnan(a_) & torch.isnan(b_))
+            msg = f"{name} differs between run 0 and run {k + 1}: {int(bad.sum())} elements"
+            if bad.dim() == 2:
+                rows = bad.any(1).nonzero().flatten().cpu()
+                tiles = torch.unique(rows // 128)
+                cols = bad.any(0).nonzero().flatten().cpu()
+                msg += (f"; rows {rows[:8].tolist()}.. ({rows.numel()} rows, {tiles.numel()} tiles: workgroups "
+                        f"{torch.unique(tiles % grid)[:8].tolist()}.., per-workgroup tile index "
+                        f"{torch.unique(tiles // grid).tolist()}); columns {cols[:16].tolist()}.. ({cols.numel()})")
+            else:
+                msg += f"; channels {bad.nonzero().flatten()[:16].tolist()}"
+            raise AssertionError(msg)
     assert torch.equal(dh, rh)
     dzf, rzf = dz.float(), rz.float()
     assert torch.isfinite(dzf).all()
