@@ -46,13 +46,15 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (guide: ~8 TB/s)
 # vector peak); tools/valu_rate.hip: v_fma_f32 reaches 27.7 and v_pk_fma_f32 29.7 FMA/cycle/SIMD at 8 waves per SIMD
 # (profiles/round3/r5i_valu_rate.txt), so packing does not raise it
 PEAK_VALU_TFMA = 1024 * 32 * 2.4e9 / 1e12
-SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX = 0, 4, 6  # include/sv_kernels.h (checked against native at run time)
+SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX, SV_EPI_LN_BWD = 0, 4, 6, 10  # include/sv_kernels.h (checked at run time)
 # probed GEMM classes: (a_kmajor, b_kmajor[, epilogue])
 PROBE_KEYS = {"wgrad": (False, False, SV_EPI_SLAB), "fc2_dgrad": (True, False, SV_EPI_MUL_AUX),
-              "dgrad": (True, False, SV_EPI_STORE), "fwd": (True, True)}
+              "dgrad": (True, False, SV_EPI_STORE), "dgrad_ln": (True, False, SV_EPI_LN_BWD), "fwd": (True, True)}
 PROBE_NAMES = {"wgrad": "split-K weight gradients dW = dY^T X (fc1, fc2, downsample, stem; side stream)",
                "fc2_dgrad": "fc2 data gradient dh = (dY (W2 gamma)) * GELU'(h) (critical path)",
                "dgrad": "fc1 / downsample data gradients dX = dY W (plain store)",
+               "dgrad_ln": "fc1 data gradient with the block LayerNorm backward in its epilogue (SV_EPI_LN_BWD: "
+                           "dz from dy = dh W1 kept on chip, C = 512 / 1024)",
                "fwd": "forward GEMMs: fc1 (+GELU), fc2 (+gamma, residual), stem, downsample",
                "dw_fwd": "depthwise 7x7 + LayerNorm forward (sv_dwconv7_ln_fwd)",
                "dw_bwd_data": "depthwise 7x7 backward-data (sv_dwconv7_bwd_data, gradient stream += and bf16 copy)",
@@ -550,7 +552,8 @@ def main():
     from spine_vision_amd import native as nv
     from spine_vision_amd.training import Classifier, CoordinateRegressor, StepEngine
 
-    assert (nv.SV_EPI_STORE, nv.SV_EPI_SLAB, nv.SV_EPI_MUL_AUX) == (SV_EPI_STORE, SV_EPI_SLAB, SV_EPI_MUL_AUX)
+    assert (nv.SV_EPI_STORE, nv.SV_EPI_SLAB, nv.SV_EPI_MUL_AUX, nv.SV_EPI_LN_BWD) == (SV_EPI_STORE, SV_EPI_SLAB,
+                                                                                   SV_EPI_MUL_AUX, SV_EPI_LN_BWD)
     torch.manual_seed(42)
     cls = args.workload == "classification"
     if cls:
@@ -649,6 +652,23 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the main queue's busy time: the critical path of the two-stream backward is the stream the
+    # step runs on, not the dominant-by-time side-stream class.  One extra, untimed step with HIP events around every
+    # sv_* launch on that stream (torch's own kernels there -- head, loss -- are not bracketed)
+    main_queue = None
+    if not args.inference and os.environ.get("SV_BENCH_MAINQ", "1") != "0":
+        mstream = engine._stream if getattr(engine, "_stream", None) is not None else torch.cuda.current_stream()
+        nv.STREAM_PROBE = nv.StreamProbe(mstream)
+        try:
+            run_step()
+            torch.cuda.synchronize()
+            sp = nv.STREAM_PROBE
+            main_queue = {"busy_ms_per_step": round(sp.busy_ms(), 3), "launches_per_step": len(sp.events),
+                          "span_ms": round(sp.span_ms(), 3),
+                          "source": "HIP events around every sv_* launch on the step's stream, one extra untimed "
+                                    "step (torch's head / loss kernels excluded)"}
+        finally:
+            nv.STREAM_PROBE = None
     final_loss = float(loss.item())
     # (a diagnostic SV_DIAG_SKIP run skips launches on purpose: its loss is garbage and its line says so)
     assert final_loss == final_loss or K._DIAG_SKIP, "loss is NaN"
@@ -729,6 +749,7 @@ def main():
             "hip_graph": bool(engine.cuda_graph),
         },
         "roofline": roof,
+        "main_queue": main_queue,
         "loss": round(final_loss, 6) if final_loss == final_loss else None,
         **({"diag_skip": sorted(K._DIAG_SKIP)} if K._DIAG_SKIP else {}),
         "hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),

@@ -104,12 +104,26 @@ typedef enum {
                              /* C2 (f32) [ceil(M/64)][2][N] = per 64-row group, column sum and sum */
                              /* of squares of the values as stored (rounded to c_dtype); bf16 only, */
                              /* N % 8 == 0, v3 kernels (a shape they cannot take is an error)      */
-  SV_EPI_STORE_BN_BWD = 9    /* C = acc (bf16: the gradient g0 at a BatchNorm + ReLU output, e.g. a */
+  SV_EPI_STORE_BN_BWD = 9,   /* C = acc (bf16: the gradient g0 at a BatchNorm + ReLU output, e.g. a */
                              /* data gradient) and that BatchNorm's backward statistics: C2 (f32)   */
                              /* [ceil(M/64)][2][N] = per 64-row group, sum g and sum g*xhat, g = C  */
                              /* as stored * (fmaf(gamma*rstd, y-mean, beta) > 0), xhat =            */
                              /* (y-mean)*rstd, y = aux (bf16, the BatchNorm input), the parameters */
                              /* in `bn`; bias NULL, N % 8 == 0, k-major A, m-major B, v3 kernels    */
+  SV_EPI_LN_BWD = 10         /* the LayerNorm backward over C's rows, C never stored (round 6: the  */
+                             /* ConvNeXt fc1 data gradient at C >= 512, ConvNeXtBlock.norm's      */
+                             /* backward in the GEMM's epilogue): dy = bf16(acc) is the gradient at */
+                             /* the LayerNorm output; x^ = (aux - bn->mean[m]) * bn->rstd[m] with   */
+                             /* aux the saved LayerNorm input z (bf16, ld_aux); w = bn->gamma [N];  */
+                             /*   C[m,n]  = bf16( rstd (dy w - mean_n(dy w) - x^ mean_n(dy w x^)) ) */
+                             /*   C2 (f32) [2][ceil(M/128)][N] = per 128-row group, sum dy x^ and    */
+                             /*   sum dy (the weight / bias gradient partials).                     */
+                             /* The row sums span the whole row: the workgroups of a row block's    */
+                             /* N / 256 column tiles exchange theirs through fold_out (f32 work-    */
+                             /* space [ceil(M/256)][N/256][256][2]) and fold_counters (int32        */
+                             /* [2 ceil(M/256)], zero on entry and left zero).  v9 only, bf16, k-   */
+                             /* major A, N % 256 == 0, N <= 1024, one workgroup per tile resident   */
+                             /* (else SV_ERR_UNSUPPORTED: the caller runs the two-pass form).       */
 } sv_epilogue;
 
 /* The BatchNorm whose backward statistics SV_EPI_STORE_BN_BWD / sv_gemm_slab_finish_bn_bwd compute

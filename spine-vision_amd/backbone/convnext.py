@@ -589,10 +589,17 @@ class ConvNeXtHip(nn.Module):
             if w2g is None:
                 w2g = K.scale_rows_bf16(blk.mlp.fc2.weight.detach(), blk.gamma.detach())
             K.linear_dgrad(dsrc, w2g, out=dh, epilogue=nv.SV_EPI_MUL_AUX, aux=gh, compute_bf16=True, policy=pol)
-            dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
-            K.linear_dgrad(dh, w1, out=dy, compute_bf16=True, policy=pol)
-            dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
-                                            db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
+            # fc1 data gradient with the LayerNorm backward in its epilogue (C = 512 / 1024: dy never reaches HBM);
+            # None where the fused form does not apply -> the two passes
+            fused = K.linear_dgrad_ln(dh, w1, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                      db=g(blk.norm.bias), policy=pol)
+            if fused is not None:
+                dz, ln_finish = fused
+            else:
+                dy = torch.empty(M, C, device=d.device, dtype=torch.bfloat16)
+                K.linear_dgrad(dh, w1, out=dy, compute_bf16=True, policy=pol)
+                dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                                db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
         side_cap = pol.grid_cap

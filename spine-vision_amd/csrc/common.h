@@ -148,6 +148,20 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 }
 
 
+// SV_PERMLANE_NOP=n (A/B builds, round 6): n wait states between a v_permlane16/32_swap and the VALU read of its two
+// results (an s_nop the compiler cannot schedule around: the results pass through it).  Tests whether a
+// permlane-swap-write -> VALU-read hazard is left uncovered by the compiler's hazard recognizer.
+#ifndef SV_PERMLANE_NOP
+#define SV_PERMLANE_NOP 0
+#endif
+__device__ __forceinline__ void permlane_guard(uint32_t& a, uint32_t& b) {
+#if SV_PERMLANE_NOP
+  asm volatile("s_nop %2" : "+v"(a), "+v"(b) : "n"(SV_PERMLANE_NOP - 1));
+#else
+  (void)a, (void)b;
+#endif
+}
+
 // xor-butterfly sum over groups of LPR lanes (16, 32 or 64) in __shfl_xor order (partner distance LPR/2 first, then
 // halving), the partners taken from the cross-lane unit instead of ds_bpermute round trips: permlane32 / permlane16
 // swaps for the exact xor-32 / xor-16 partners, DPP row rotation by 8 (xor 8 inside a 16-lane row), rotations by 4 and
@@ -159,11 +173,15 @@ __device__ __forceinline__ float xlane_group_sum(float v) {
   const int lane = threadIdx.x & 63;
   if constexpr (LPR >= 64) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v += __uint_as_float(lane < 32 ? r[1] : r[0]);
+    uint32_t r0 = r[0], r1 = r[1];
+    permlane_guard(r0, r1);
+    v += __uint_as_float(lane < 32 ? r1 : r0);
   }
   if constexpr (LPR >= 32) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v += __uint_as_float((lane & 16) ? r[0] : r[1]);
+    uint32_t r0 = r[0], r1 = r[1];
+    permlane_guard(r0, r1);
+    v += __uint_as_float((lane & 16) ? r0 : r1);
   }
   v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x128, 0xf, 0xf, false));  // row_ror:8
   v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), 0x124, 0xf, 0xf, false));  // row_ror:4
@@ -187,11 +205,15 @@ __device__ __forceinline__ float xlane_xor(float v) {
   } else if constexpr (OFF == 8) return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0x128, 0xf, 0xf, false));
   else if constexpr (OFF == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+    uint32_t r0 = r[0], r1 = r[1];
+    permlane_guard(r0, r1);
+    return __uint_as_float((threadIdx.x & 16) ? r0 : r1);
   } else {
     static_assert(OFF == 32, "xor distance 1, 2, 4, 8, 16 or 32");
     const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+    uint32_t r0 = r[0], r1 = r[1];
+    permlane_guard(r0, r1);
+    return __uint_as_float((threadIdx.x & 32) ? r0 : r1);
   }
 }
 

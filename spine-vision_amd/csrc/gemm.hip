@@ -289,7 +289,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
   SV_REQUIRE(d, "sv_gemm: null descriptor");
   SV_REQUIRE(d->A && d->B && d->C, "sv_gemm: null operand");
   SV_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "sv_gemm: negative size");
-  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_STORE_BN_BWD, "sv_gemm: bad epilogue %d", d->epilogue);
+  SV_REQUIRE(d->epilogue >= SV_EPI_STORE && d->epilogue <= SV_EPI_LN_BWD, "sv_gemm: bad epilogue %d", d->epilogue);
   SV_REQUIRE(d->policy.impl == 0 || d->policy.impl == 2 || d->policy.impl == 3 || d->policy.impl == 8 || d->policy.impl == 9,
              "sv_gemm: policy.impl must be 0, 2, 3, 8 or 9 (got %d)", d->policy.impl);
   SV_REQUIRE(d->policy.grid_cap >= 0 && d->policy.wg_per_cu >= 0 && d->policy.wg_per_cu <= 2 &&
@@ -323,8 +323,12 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     SV_REQUIRE(bf && d->c_dtype == SV_BF16 && d->C2 && d->N % 8 == 0 && d->aux && d->aux_dtype == SV_BF16 && !d->bias &&
                    d->bn && d->bn->mean && d->bn->rstd && d->bn->gamma && d->bn->beta,
                "sv_gemm: STORE_BN_BWD needs bf16 C and aux, C2, N %% 8 == 0, no bias and the bn parameters");
+  if (d->epilogue == SV_EPI_LN_BWD)
+    SV_REQUIRE(bf && d->c_dtype == SV_BF16 && d->C2 && al16(d->C2) && d->aux && d->aux_dtype == SV_BF16 && d->bn &&
+                   d->bn->mean && d->bn->rstd && d->bn->gamma && d->fold_out && d->fold_counters && al16(d->fold_out),
+               "sv_gemm: LN_BWD needs bf16 C and aux (z), C2, the bn mean / rstd / gamma and the exchange workspace");
   if (d->aux) SV_REQUIRE(d->ld_aux % 4 == 0 && al16(d->aux), "sv_gemm: aux must be aligned");
-  if (d->fold_out)
+  if (d->fold_out && d->epilogue != SV_EPI_LN_BWD)
     SV_REQUIRE(d->epilogue == SV_EPI_SLAB && bf && d->fold_counters && d->fold_ld == d->N && al16(d->fold_out),
                "sv_gemm: fold_out needs SV_EPI_SLAB (bf16), fold_counters, fold_ld == N and a 16-byte aligned output");
   if (d->a_scale_k) SV_REQUIRE(al16(d->a_scale_k), "sv_gemm: a_scale_k must be aligned");
@@ -338,6 +342,7 @@ extern "C" int sv_gemm(const sv_gemm_desc* d, sv_stream_t stream) {
     SV_REQUIRE(rc != SV_ERR_UNSUPPORTED, "sv_gemm: STORE_BN_BWD needs K %% 32 == 0, bf16 operands, k-major A, m-major B");
     return rc;
   }
+  if (d->epilogue == SV_EPI_LN_BWD) return launch_gemm9(d, s);  // v9 only; SV_ERR_UNSUPPORTED -> the caller's two passes
   if (d->epilogue == SV_EPI_STORE_STATS) {  // the v3 and v9 kernels carry the statistics epilogue
     const long t9 = (long)ceil_div(d->M, 256) * ceil_div(d->N, 256);
     if ((impl == 0 || impl == 9) && d->N >= 256 && t9 >= 256 && d->a_kmajor) {

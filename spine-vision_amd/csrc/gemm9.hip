@@ -542,6 +542,235 @@ __device__ __forceinline__ void fold_tile(const EpiArgs& e, const Ext& x, const 
   (void)x;
 }
 
+// ---- SV_EPI_LN_BWD (round 6): the LayerNorm backward in the fc1 data gradient's epilogue.  The
+// unfused block stores dy = bf16(dh W1) and sv_layernorm_bwd reads it back with z / mean / rstd; here dy stays in the
+// accumulators.  Its row sums (sum dy w, sum dy w x^) span all N columns while a 256x256 tile holds a quarter / half of
+// a row: every wave sums its 64 columns (lane groups by shuffles), the 4 column waves of the tile through LDS (fixed
+// order), and the tiles of one 256-row block through a global workspace -- each stores its 256 partial row sums
+// write-through (sc1), every storing wave waits for its stores, one lane adds to the block's arrival counter and polls
+// it (sc1 loads) until all N / 256 tiles have arrived (MI355X_MICROARCH.md inter-workgroup table, row 1); every tile
+// then adds the N / 256 partials in tile order, so the tiles of a row use the same sums bit for bit.  The last tile out
+// re-arms both counters.  The host takes this form only when every tile has a workgroup of its own, all resident at
+// once (grid == tiles <= the stream's CUs): a tile waits only for its row-block partners.  A poll that outlasts ~2^26
+// sleeps gives up and poisons its rows (NaN dz) instead of hanging the chip.
+constexpr int kLnRed = 2 * 4 * 128 * 2 * 4;  // LDS: [wm][wn][128 rows][s1, s2] f32 = 8 KiB
+
+__device__ __forceinline__ void ln_bwd_epilogue(const f32x4 (&acc)[FM][FN], const EpiArgs& e, const Ext& x,
+                                                const Fold& f, int m0, int n0, int tilesN, const float* lw_lds,
+                                                float* lred, char* dyl) {
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wm = wid >> 2, wn = wid & 3;
+  const int l = threadIdx.x & 63, ml = l & 15, gq = l >> 4;
+  const int m_w = m0 + 128 * wm, n_w = n0 + 64 * wn;
+  constexpr int CH = 2;  // 32-column chunks of the wave; lane group gq: columns n_w + 32 c + 8 gq .. + 7
+  const float invC = 1.0f / (float)e.N;
+  auto lw_of = [&](int c, float (&lw)[8]) {  // this lane's 8 LayerNorm weights of chunk c (staged in LDS)
+    const float4 a = lds_f4(lw_lds + 64 * wn + 32 * c + 8 * gq), b = lds_f4(lw_lds + 64 * wn + 32 * c + 8 * gq + 4);
+    lw[0] = a.x, lw[1] = a.y, lw[2] = a.z, lw[3] = a.w, lw[4] = b.x, lw[5] = b.y, lw[6] = b.z, lw[7] = b.w;
+  };
+  const auto rz = rsrc(e.aux, x.aux);
+  const auto rmu = rsrc(e.bn_mu, (uint32_t)e.M * 4), rrs = rsrc(e.bn_rs, (uint32_t)e.M * 4);
+  float mu[FM], rs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m_w + 16 * i + ml;
+    const uint32_t o = m < e.M ? (uint32_t)m * 4 : OOB;
+    mu[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmu, o, 0, 0));
+    rs[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, o, 0, 0));
+  }
+  // dy = bf16(acc) (the unfused path's stored dy) parks in the K loop's LDS buffers between the passes, so the 128
+  // accumulators are dead during the exchange: a lane's 16 B per (row fragment, chunk), lane-linear (conflict-free)
+  vm_wait<0>();  // the K loop's DMAs past the end of its stream have landed in those buffers ...
+  bar();         // ... in every wave
+  auto dy_slot = [&](int i, int c) { return dyl + (((wid * FM + i) * 2 + c) * 64 + l) * 16; };
+  auto unpack = [](const u32x4& pk, float (&d)[8]) {
+    const uint32_t wd[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+    for (int w = 0; w < 8; ++w) d[w] = __uint_as_float((w & 1) ? (wd[w >> 1] & 0xffff0000u) : (wd[w >> 1] << 16));
+  };
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][2 * c][r], v[4 + r] = acc[i][2 * c + 1][r];
+      *reinterpret_cast<u32x4*>(dy_slot(i, c)) = pack8(v);
+    }
+  asm volatile("" ::: "memory");  // the accumulators are dead from here on
+  auto dy_back = [&](int i, int c, float (&d)[8]) { unpack(*reinterpret_cast<const u32x4*>(dy_slot(i, c)), d); };
+  auto z_of = [&](const u32x4& raw, int i, float (&xh)[8]) {
+    const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const float zz = __uint_as_float((w & 1) ? (wd[w >> 1] & 0xffff0000u) : (wd[w >> 1] << 16));
+      xh[w] = (zz - mu[i]) * rs[i];
+    }
+  };
+  auto zoff = [&](int i, int c) {
+    const int m = m_w + 16 * i + ml, n = n_w + 32 * c + 8 * gq;
+    return m < e.M ? (uint32_t)(((size_t)m * e.ld_aux + n) * 2) : OOB;
+  };
+  // pass 1, one 32-column chunk at a time (registers: the 128 accumulators stay live throughout): per-row partials
+  // over this lane's columns; per-column partials over the wave's 128 rows (16 lanes ml by shuffles, then lane ml == 0
+  // stores them into [2][ceil(M / 128)][N])
+  const int P = (e.M + 127) / 128, prow = m_w / 128;
+  float s1[FM], s2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) s1[i] = s2[i] = 0.f;
+#pragma nounroll
+  for (int c = 0; c < CH; ++c) {  // a loop, not unrolled: both chunks' state at once would spill
+    float lw[8], pw[8], pb[8];
+    lw_of(c, lw);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) pw[w] = pb[w] = 0.f;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      asm volatile("" ::: "memory");  // one batch of z loads at a time (hoisting them all would spill)
+      u32x4 zr[FM / 2];
+#pragma unroll
+      for (int ii = 0; ii < FM / 2; ++ii) zr[ii] = __builtin_amdgcn_raw_buffer_load_b128(rz, zoff(hb * FM / 2 + ii, c), 0, 0);
+#pragma unroll
+      for (int ii = 0; ii < FM / 2; ++ii) {
+        const int i = hb * FM / 2 + ii;
+        float d[8], xh[8];
+        dy_back(i, c, d);
+        z_of(zr[ii], i, xh);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const float g = d[w] * lw[w];
+          s1[i] += g;
+          s2[i] += g * xh[w];
+          pw[w] += d[w] * xh[w];
+          pb[w] += d[w];
+        }
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+#pragma unroll
+      for (int sh = 1; sh < 16; sh <<= 1) {
+        pw[w] += __shfl_xor(pw[w], sh);
+        pb[w] += __shfl_xor(pb[w], sh);
+      }
+    if (ml == 0 && m_w < e.M) {
+      float* C2 = reinterpret_cast<float*>(e.C2);
+      const int n = n_w + 32 * c + 8 * gq;
+      float4* qw = reinterpret_cast<float4*>(C2 + ((size_t)prow) * e.N + n);
+      float4* qb = reinterpret_cast<float4*>(C2 + ((size_t)P + prow) * e.N + n);
+      qw[0] = make_float4(pw[0], pw[1], pw[2], pw[3]);
+      qw[1] = make_float4(pw[4], pw[5], pw[6], pw[7]);
+      qb[0] = make_float4(pb[0], pb[1], pb[2], pb[3]);
+      qb[1] = make_float4(pb[4], pb[5], pb[6], pb[7]);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // the wave's 64 columns of a row: the 4 lane groups (xor 16, 32)
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    s1[i] += __shfl_xor(s1[i], 16);
+    s1[i] += __shfl_xor(s1[i], 32);
+    s2[i] += __shfl_xor(s2[i], 16);
+    s2[i] += __shfl_xor(s2[i], 32);
+  }
+  // the tile's 4 column waves through LDS (fixed order wn = 0..3)
+  if (gq == 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      float* q = lred + ((wm * 4 + wn) * 128 + 16 * i + ml) * 2;
+      q[0] = s1[i], q[1] = s2[i];
+    }
+  }
+  lgkm0();
+  bar();
+  // the tile's partial row sums -> the workspace, by the wn == 0 wave of each row half (write-through)
+  const int tile_m = m0 / BM, half = n0 / BN;
+  const uint32_t xbytes = (uint32_t)(((size_t)((e.M + BM - 1) / BM) * tilesN * BM * 2) * 4);
+  const auto rx = rsrc(f.out, xbytes);
+  auto xoff = [&](int h, int row) { return (uint32_t)((((size_t)tile_m * tilesN + h) * BM + row) * 8); };
+  if (wn == 0 && gq == 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = 16 * i + ml;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const float* q = lred + ((wm * 4 + w4) * 128 + row) * 2;
+        t1 += q[0];
+        t2 += q[1];
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(t1), __float_as_uint(t2)}, rx,
+                                            xoff(half, 128 * wm + row), 0, kSC1);
+    }
+  }
+  vm_wait<0>();  // every storing wave's stores complete before the workgroup's arrival
+  bar();
+  int* arrive = f.cnt + 2 * tile_m;
+  int* depart = arrive + 1;
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (int spin = 0; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tilesN; ++spin) {
+      if (spin > (1 << 26)) {  // a partner never arrived: give up rather than hang the chip
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_ok = ok;
+  }
+  bar();
+  const bool ok = s_ok != 0;
+  // the row's sums: every tile's partial in tile order (the same additions in every tile of the row block)
+  float S1[FM], S2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) S1[i] = S2[i] = 0.f;
+  for (int h = 0; h < tilesN; ++h) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rx, xoff(h, 128 * wm + 16 * i + ml), 0, kSC1);
+      S1[i] += __uint_as_float(v.x);
+      S2[i] += __uint_as_float(v.y);
+    }
+  }
+  vm_wait<0>();
+  bar();
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tilesN - 1) {
+    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // pass 2: dz = rstd (dy w - s1 / N - x^ s2 / N)  (sv_layernorm_bwd's arithmetic), stored bf16
+  const auto rc = rsrc(e.C, x.c);
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    asm volatile("" ::: "memory");
+    u32x4 zr[FM / 2][CH];
+#pragma unroll
+    for (int ii = 0; ii < FM / 2; ++ii)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) zr[ii][c] = __builtin_amdgcn_raw_buffer_load_b128(rz, zoff(hb * FM / 2 + ii, c), 0, 0);
+#pragma unroll
+    for (int ii = 0; ii < FM / 2; ++ii) {
+      const int i = hb * FM / 2 + ii;
+      const int m = m_w + 16 * i + ml;
+      const float a1 = ok ? S1[i] * invC : __builtin_nanf(""), a2 = S2[i] * invC;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        float d[8], xh[8], o[8], lw[8];
+        lw_of(c, lw);
+        dy_back(i, c, d);
+        z_of(zr[ii][c], i, xh);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) o[w] = rs[i] * (d[w] * lw[w] - a1 - xh[w] * a2);
+        const int n = n_w + 32 * c + 8 * gq;
+        const uint32_t off = m < e.M ? (uint32_t)(((size_t)m * e.ldc + n) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, off, 0, 0);
+      }
+    }
+  }
+  vm_wait<0>();
+}
+
 template <bool AK, bool BKM, int EPI, bool P8, int FOLD = kFoldNone>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int nk, int tilesM,
@@ -624,7 +853,7 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   // forward epilogues read the tile's bias (and gamma) from LDS, staged by DMA: a plain global load
   // in the epilogue would make the compiler drain every DMA in flight (vmcnt(0)) at each tile's end
   constexpr bool LBIAS = AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
-                                EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS);
+                                EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS || EPI == SV_EPI_LN_BWD);
   // DMAs younger than the W1 / W2 targets in steady state (see the phase comments below)
   constexpr int W1 = AK ? 10 : 8, W2 = 10;
   constexpr int W1E = W1 + E > 63 ? 63 : W1 + E, W2E = W2 + E > 63 ? 63 : W2 + E;
@@ -788,8 +1017,17 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     if constexpr (FOLD) {
       if (wm == 0) bar();  // align the two wave halves (waves 4-7 run one barrier behind in the K loop)
     }
-    epilogue<EPI, P8, AK, FOLD>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
-                      LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
+    if constexpr (EPI == SV_EPI_LN_BWD) {
+      // one tile per workgroup (the host's contract): align the staggered wave halves, the epilogue with its
+      // workgroup barriers and the row-block exchange, then re-stagger for the kernel's closing barrier
+      if (wm == 0) bar();
+      ln_bwd_epilogue(acc, e, x, fold, cg.m0, cg.n0, tilesN, reinterpret_cast<const float*>(smem + lds_bytes<AK>()),
+                      reinterpret_cast<float*>(smem + lds_bytes<AK>() + 4096), smem);
+      if (wm == 1) bar();
+    } else {
+      epilogue<EPI, P8, AK, FOLD>(acc, e, x, cg.m0 + wm * 128, cg.n0 + wn * 64, cg.split,
+                        LBIAS ? reinterpret_cast<const float*>(smem + lds_bytes<AK>() + (it & 1) * 2048) : nullptr);
+    }
     SV_VMTAG("epi");  // after the epilogue's fixed EpiCount memory instructions (the E in W1E / W2E)
     if constexpr (FOLD) {
       // arrival: every wave's slab stores complete (this also drains the next tile's first DMAs: the K loop's
@@ -843,7 +1081,9 @@ gemm9_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 template <bool AK, int EPI, int FOLD = kFoldNone>
 constexpr int lds_total() {
   return lds_bytes<AK>() + ((AK && (EPI == SV_EPI_STORE || EPI == SV_EPI_BIAS_GELU_DUAL || EPI == SV_EPI_BIAS_GELU ||
-                                   EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS)) ? 4096 : 0);
+                                   EPI == SV_EPI_BIAS_GAMMA_RES || EPI == SV_EPI_STORE_STATS || EPI == SV_EPI_LN_BWD))
+                                ? 4096 : 0) +
+         (EPI == SV_EPI_LN_BWD ? kLnRed : 0);
 }
 
 template <bool AK, bool BKM, int EPI, bool P8, int FOLD = kFoldNone>
@@ -852,6 +1092,11 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int tilesM = ceil_div(d->M, BM), tilesN = ceil_div(d->N, BN);
   EpiArgs e{d->M, d->N, d->epilogue, d->C, d->c_dtype, d->ldc, d->C2, d->c2_dtype, d->bias, d->gamma,
             d->aux, d->aux_dtype, d->ld_aux};
+  if constexpr (EPI == SV_EPI_LN_BWD) {  // LayerNorm weight staged through the bias slot; mean / rstd per row
+    e.bias = d->bn->gamma;
+    e.bn_mu = d->bn->mean;
+    e.bn_rs = d->bn->rstd;
+  }
   const int cs = d->c_dtype == SV_F32 ? 4 : 2;
   Ext x;
   if (EPI == SV_EPI_SLAB) {
@@ -868,6 +1113,13 @@ static int launch(const sv_gemm_desc* d, int split, hipStream_t s) {
   const int total = tilesM * tilesN * split;
   const int grid = policy_grid(&d->policy, total, 1, s);  // persistent: one workgroup per CU (or the cap)
   const Fold fold{d->fold_out, d->fold_ld, d->fold_accumulate, d->fold_counters};
+  if constexpr (EPI == SV_EPI_LN_BWD) {
+    // the row-block exchange waits for partner tiles: every tile a workgroup of its own, all of them resident at
+    // once on the CUs this stream may use (its CU mask, the policy's cap)
+    int usable = stream_cus(s);
+    if (d->policy.grid_cap > 0 && d->policy.grid_cap < usable) usable = d->policy.grid_cap;
+    if (grid != total || total > usable) return SV_ERR_UNSUPPORTED;
+  }
   if constexpr (FOLD != kFoldNone) {
     // the spread fold waits for a tile's other slices: only when every (tile, slice) unit has a workgroup of its
     // own and the grid is at most half the chip (one workgroup per CU): then two such launches on two streams
@@ -919,6 +1171,15 @@ static int launch_epi(const sv_gemm_desc* d, int split, hipStream_t s) {
     case SV_EPI_STORE_STATS:
       if (!bf_out || !AK || d->N % 8) return SV_ERR_UNSUPPORTED;
       return launch<AK, BKM, SV_EPI_STORE_STATS, true>(d, split, s);
+    case SV_EPI_LN_BWD:
+      if constexpr (!AK) {
+        return SV_ERR_UNSUPPORTED;
+      } else {
+        if (!bf_out || d->aux_dtype != SV_BF16 || d->N % BN || d->N > 4 * BN || split != 1 || !d->bn || !d->C2 ||
+            !d->fold_out || !d->fold_counters)
+          return SV_ERR_UNSUPPORTED;
+        return launch<AK, BKM, SV_EPI_LN_BWD, true>(d, split, s);
+      }
     case SV_EPI_SLAB:
       if (d->C2 && (AK || d->c2_dtype != SV_F32)) return SV_ERR_UNSUPPORTED;  // fused column sum: N/M-major A
       if (d->c_dtype == SV_BF16) {  // bf16 slabs (the weight-gradient layout, folded in a separate pass)

@@ -204,6 +204,8 @@ def gemm(
                 nbytes += M * 4  # its bias gradient (column sums)
         elif epilogue == nv.SV_EPI_BIAS_GELU_DUAL:
             nbytes += M * N * C2.element_size()  # GELU(h) is required; the GELU'(h) store is a design choice
+        elif epilogue == nv.SV_EPI_LN_BWD:
+            nbytes += M * N * C.element_size() + M * 8 + C2.numel() * 4  # dz; mean / rstd; the weight / bias partials
         else:
             nbytes += M * N * C.element_size()
             if C2 is not None:
@@ -222,6 +224,56 @@ def gemm(
     else:
         call("sv_gemm", ctypes.byref(d))
     return C
+
+
+# the LayerNorm backward in the fc1 data gradient's epilogue (SV_EPI_LN_BWD, round 6): dy never reaches HBM.  v9 only,
+# N % 256 == 0 (ConvNeXt C = 512 / 1024), every 256x256 tile resident at once (else the two-pass form runs).
+# SV_FUSED_LN_BWD=0 keeps the two passes (A/B runs)
+FUSED_LN_BWD = os.environ.get("SV_FUSED_LN_BWD", "1") != "0"
+_LN_XCH: dict = {}
+
+
+def linear_dgrad_ln(dh2d, w, z2d, mean, rstd, lnw, *, dw, db, policy=None):
+    """dz = LayerNorm backward of dy = bf16(dh2d @ w) over (z2d, mean, rstd, lnw) in ONE launch (sv_gemm,
+    SV_EPI_LN_BWD); -> (dz bf16 [M, C], finish) as layernorm_bwd(..., defer_reduce=True) returns, or None where the
+    shape or the chip's free CUs do not take the fused form (the caller then runs linear_dgrad + layernorm_bwd)."""
+    if not FUSED_LN_BWD:
+        return None
+    M, K = dh2d.shape
+    C = w.shape[1]
+    if C % 256 or C > 1024 or dh2d.dtype != torch.bfloat16 or z2d.dtype != torch.bfloat16:
+        return None
+    _check(tuple(z2d.shape) == (M, C) and z2d.is_contiguous() and mean.numel() == M and rstd.numel() == M
+           and lnw.numel() == C, "linear_dgrad_ln: z [M, C], mean / rstd [M], lnw [C]")
+    tilesM, tilesN = -(-M // 256), C // 256
+    if tilesM * tilesN > _device_cus(dh2d.device):
+        return None
+    dz = torch.empty(M, C, device=dh2d.device, dtype=torch.bfloat16)
+    P = -(-M // 128)
+    part = torch.empty(2, P, C, device=dh2d.device, dtype=torch.float32)
+    key = (dh2d.device, nv._stream())
+    xch = _LN_XCH.get(key)
+    if xch is None or xch.numel() < tilesM * tilesN * 512:
+        xch = _LN_XCH[key] = torch.empty(max(tilesM * tilesN * 512, 1 << 18), device=dh2d.device, dtype=torch.float32)
+    bn = nv.BnRef(ptr(mean), ptr(rstd), ptr(lnw), None)
+    try:
+        gemm(dh2d, w, M=M, N=C, K=K, a_kmajor=True, b_kmajor=False, lda=K, ldb=C, epilogue=nv.SV_EPI_LN_BWD, C=dz,
+             C2=part, aux=z2d, ld_aux=C, compute_bf16=True, bn=bn, policy=policy,
+             fold=(xch, False, _fold_counters(dh2d.device, tilesM)))
+    except RuntimeError as err:
+        if "(status 2)" in str(err):  # SV_ERR_UNSUPPORTED: not every tile resident at once (CU mask, grid cap)
+            return None
+        raise
+
+    def finish(record: bool = True, defer: list | None = None):
+        if record:
+            part.record_stream(torch.cuda.current_stream())
+        if defer is not None:
+            defer += [(part[0], dw, P, True), (part[1], db, P, True)]
+            return
+        reduce_pair(part[0], dw, part[1], db, P)
+
+    return dz, finish
 
 
 def linear_fwd(x2d, w, *, out, bias=None, epilogue=nv.SV_EPI_STORE, out2=None, gamma=None, residual=None,

@@ -24,7 +24,7 @@ SV_BN_SMALL_MASK, SV_BN_SMALL_RELU, SV_BN_SMALL_DUAL = 0, 1, 2
 SV_HEAD_CE, SV_HEAD_BCE = 0, 1
 SV_BN_FOLD_CTL_INTS, SV_BN_FOLD_WS_FLOATS = 256, 2 * 2 * 2048 + 2 * 64 * 16 * 64  # include/sv_kernels.h
 (SV_EPI_STORE, SV_EPI_BIAS_GELU2, SV_EPI_BIAS_GAMMA_RES, SV_EPI_GELU_GRAD, SV_EPI_SLAB, SV_EPI_BIAS_GELU_DUAL,
- SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS, SV_EPI_STORE_BN_BWD) = range(10)
+ SV_EPI_MUL_AUX, SV_EPI_BIAS_GELU, SV_EPI_STORE_STATS, SV_EPI_STORE_BN_BWD, SV_EPI_LN_BWD) = range(11)
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -267,6 +267,27 @@ def _stream() -> int:
 _FNS: dict = {}  # name -> bound ctypes function (ctypes attribute lookup is a dict miss + a getattr per call)
 
 
+class StreamProbe:
+    """HIP events around every sv_* launch enqueued on one stream (bench.py: the main queue's busy time per step --
+    the critical path of the two-stream backward -- measured live; torch's own kernels on that stream are not
+    bracketed)."""
+
+    def __init__(self, stream: torch.cuda.Stream) -> None:
+        self.handle = stream.cuda_stream
+        self.events: list = []
+
+    def busy_ms(self) -> float:
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+    def span_ms(self) -> float:
+        torch.cuda.synchronize()
+        return self.events[0][0].elapsed_time(self.events[-1][1]) if self.events else 0.0
+
+
+STREAM_PROBE: StreamProbe | None = None
+
+
 def call(name: str, *args):
     """Invoke an sv_* entry point on the current stream; raise RuntimeError on a non-zero status."""
     fn = _FNS.get(name)
@@ -274,7 +295,19 @@ def call(name: str, *args):
         fn = _FNS[name] = getattr(_lib if _lib is not None else lib(), name)
     if name in _VALUE_FNS:
         return fn(*args)
-    rc = fn(*args) if name in _NOSTREAM_FNS else fn(*args, _stream())
+    if name in _NOSTREAM_FNS:
+        rc = fn(*args)
+    else:
+        s = _stream()
+        pr = STREAM_PROBE
+        if pr is not None and s == pr.handle:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = fn(*args, s)
+            e1.record()
+            pr.events.append((e0, e1))
+        else:
+            rc = fn(*args, s)
     if rc != 0:
         msg = lib().sv_last_error_string().decode()
         raise RuntimeError(f"{name} failed (status {rc}): {msg}")

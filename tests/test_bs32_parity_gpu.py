@@ -98,8 +98,12 @@ def test_convnext_large_512_bs64_bf16_step(dev):
 
 @pytest.mark.timeout(900)
 def test_resnet50_256_bs32_bf16_step(dev):
-    from test_resnet_parity_256_gpu import bf16_vs_emulation, report_floor
+    """configs[3] at its per-GPU batch: the kernels against the bf16 emulation (floor check), and the design against
+    the reference's autocast recipe at B=32, where train-mode BatchNorm is well-conditioned (this
+    replaces the self-calibrated BF16_VS_FP32 bound as the ResNet bf16 design pin)."""
+    from test_resnet_parity_256_gpu import bf16_vs_emulation, design_vs_autocast, report_floor
 
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
-    lerr, table = bf16_vs_emulation(dev, "train", 32, engine=True)
+    lerr, table, kept = bf16_vs_emulation(dev, "train", 32, engine=True, keep=True)
     report_floor("resnet50@256 B32 bf16 train (StepEngine)", lerr, table)
+    design_vs_autocast("resnet50@256 B32 bf16 train (StepEngine)", *kept, dev)

@@ -125,9 +125,10 @@ def test_resnet50_256_fp32(dev, mode):
     assert all(v < 1e-5 for v in buf.values()), buf
 
 
-def bf16_vs_emulation(dev, mode, B, engine=False):
+def bf16_vs_emulation(dev, mode, B, engine=False, keep=False):
     """HIP bf16 (whole model, optionally through StepEngine's flat buffers / bf16 shadow as the bench runs it)
-    against oracle.bf16emu in float64 and float32; -> (logit errors, floor_check table)."""
+    against oracle.bf16emu in float64 and float32; -> (logit errors, floor_check table), plus with ``keep``
+    (HIP logits, HIP gradients, the oracle module, image, targets) for the design check."""
     from oracle import bf16emu as be
     from spine_vision_amd.training import Classifier, StepEngine
     from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
@@ -157,7 +158,53 @@ def bf16_vs_emulation(dev, mode, B, engine=False):
         hb = dict(hip.named_buffers())
         berr = {n: rel(hb[n], b) for n, b in b64.items()}
         assert all(v < 1e-2 for v in berr.values()), berr
+    if keep:
+        hg = {n: p.grad.detach().float().cpu() for n, p in hip.named_parameters()}
+        return lerr, table, ({k: v.detach().float().cpu() for k, v in logits.items()}, hg, ref, img, targets)
     return lerr, table
+
+
+# Design check margin on the GRADIENTS (not the logits): train-mode BatchNorm keeps ResNet-50's gradients badly
+# conditioned even at B=32 on this fixture -- measured on MI355X (r13a): HIP 0.346 median / 0.529 worst and the
+# reference's autocast recipe 0.350 / 0.522 from fp32, the same size as the bf16 noise floor itself (float64 vs float32
+# emulation at the same rounding points: 0.24-0.26 median).  Any two bf16 computations land that far from fp32 and
+# their worst tensors trade places from one fixture to the next; a design that rounds in the wrong place shows up as a
+# SYSTEMATIC excess, which the 10 % margin still catches (the logits keep the strict bound: 1.37e-2 vs 1.52e-2).
+DESIGN_GRAD_MARGIN = 1.10
+
+
+def design_vs_autocast(tag, hip_logits, hip_grads, ref, img, targets, dev):
+    """The design pin (as the ConvNeXt bf16_parity's): the HIP bf16 path no farther from the fp32
+    reference than the reference's own recipe -- the oracle model under torch.autocast at the same bf16 width
+    (trainers/base.py:230-237, trainers/classification.py:269-290: conv / linear in bf16, BatchNorm in the input's
+    width with f32 statistics) -- on the worst head's logits (strictly), the median and the worst gradient (within
+    DESIGN_GRAD_MARGIN, see above).  The fp32 reference is the CPU oracle (train-mode BN over the same batch)."""
+    m32 = copy.deepcopy(ref).train()
+    m32.zero_grad(set_to_none=True)
+    o32 = m32(img)
+    m32.get_loss(o32, targets).backward()
+    g32 = {n: q.grad.detach().float() for n, q in m32.named_parameters()}
+    ma = copy.deepcopy(ref).to(dev).train()
+    ma.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        oa = ma(img.to(dev))
+    oa = {k: v.float() for k, v in oa.items()}
+    ma.get_loss(oa, {k: v.to(dev) for k, v in targets.items()}).backward()
+    torch.cuda.synchronize()
+    ga = {n: q.grad.detach().float().cpu() for n, q in ma.named_parameters()}
+    del ma
+    torch.cuda.empty_cache()
+    lh = max(rel(hip_logits[k], o32[k]) for k in LABELS)
+    la = max(rel(oa[k], o32[k]) for k in LABELS)
+    eh = {n: rel(hip_grads[n], g) for n, g in g32.items()}
+    ea = {n: rel(ga[n], g) for n, g in g32.items()}
+    wh, wa = max(eh, key=eh.get), max(ea, key=ea.get)
+    mh, ma_ = float(np.median(list(eh.values()))), float(np.median(list(ea.values())))
+    print(f"[design] {tag}: vs fp32 -- HIP logits {lh:.3e} grad median {mh:.3e} worst {eh[wh]:.3e} ({wh}); "
+          f"autocast-bf16 logits {la:.3e} grad median {ma_:.3e} worst {ea[wa]:.3e} ({wa})")
+    assert lh <= la, (lh, la)
+    assert mh <= DESIGN_GRAD_MARGIN * ma_ and eh[wh] <= DESIGN_GRAD_MARGIN * ea[wa], (mh, ma_, eh[wh], ea[wa])
+    return lh, la, mh, ma_
 
 
 def _keep(d, out):
