@@ -267,6 +267,17 @@ int sv_dwconv7_bwd_weight(const void* dz, int32_t dz_dtype, const void* x, int32
                           float* db_part, int32_t B, int32_t H, int32_t W, int32_t C,
                           sv_stream_t stream);
 
+/* ---- the depthwise conv on the matrix cores (csrc/dwmfma.hip, round 6) --------------------------------
+ * Per channel a banded-Toeplitz GEMM along the image row on v_mfma_f32_16x16x32_bf16.  Operands are rounded to bf16
+ * (x or dz and the taps: the precision torch.autocast gives conv_dw), products exact, sums in f32.  C % 32 == 0.
+ *   fwd:       z (bf16) = bf16(bdw + sum_tap bf16(w) * bf16(x)),  x f32 or bf16 [B,H,W,C] (x_dtype)
+ *   bwd-data:  dx (f32) = (accumulate ? dx : 0) + sum_tap bf16(w[48 - tap]) * dz,  dz bf16; dx_bf16 (nullable)
+ *              receives bf16(dx).  Same contract as sv_dwconv7_bwd_data with dz_dtype = bf16.                  */
+int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const float* bdw, uint16_t* z, int32_t B,
+                        int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
+                             int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+
 /* ---- ConvNeXt stem: Conv2d(3, C, k=4, s=4) + LayerNorm2d, fused --------------------------------
  * img: NCHW f32 [B,3,H,W] (ImageNet-normalised, = the reference batch["image"]); w [C][3*16]
  * (timm stem.0.weight), b [C]; y: NHWC [B,H/4,W/4,C] (y_dtype); mean/rstd [B*H/4*W/4].            */

@@ -27,6 +27,8 @@ Rounding points restated from spine-vision_amd/backbone/resnet.py (``_forward_im
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -293,6 +295,11 @@ def _slab_wgrad(A, Bm, split: int, bf16_slabs: bool):
     return G
 
 
+# The depthwise conv's operands: the matrix-core kernels (csrc/dwmfma.hip, SV_DW_MFMA=1 in the product) round x / dz's
+# partner and the taps to bf16 -- torch.autocast's precision for conv_dw -- where the VALU kernels take f32 x and taps.
+# Same switch and default as spine_vision_amd/kernels.py DW_MFMA (tests/test_bf16emu_cpu.py checks they agree).
+DW_BF16_OPERANDS = os.environ.get("SV_DW_MFMA", "0") != "0"
+
 # the tape keeps the bf16-rounded tensors as bf16 (exact, a quarter of float64's memory); a check that disables the
 # rounding (bf16_round -> identity, test_oracle_golden) must keep them in the working dtype
 STORE_BF16 = True
@@ -305,8 +312,9 @@ class ConvNeXtBf16Emu:
     the large cases on the GPU's float64 units, the small ones on the CPU -- the same code either way)."""
 
     def __init__(self, model: torch.nn.Module, dtype=torch.float64, wgrad_split=None, block_wgrad_target: int = 256,
-                 device="cpu") -> None:
+                 device="cpu", dw_bf16: bool | None = None) -> None:
         self.model = model
+        self.dw_bf16 = DW_BF16_OPERANDS if dw_bf16 is None else dw_bf16
         self.dtype = dtype
         self.device = torch.device(device)
         self.P = {n: p.detach().to(self.device, dtype).clone() for n, p in model.named_parameters()}
@@ -345,7 +353,8 @@ class ConvNeXtBf16Emu:
             blocks = []
             for bi in range(len(st.blocks)):
                 bp = f"{pre}blocks.{bi}."
-                z = q(_dw(x, P[bp + "conv_dw.weight"], P[bp + "conv_dw.bias"]))
+                wdw = P[bp + "conv_dw.weight"]
+                z = q(_dw(q(x), q(wdw), P[bp + "conv_dw.bias"]) if self.dw_bf16 else _dw(x, wdw, P[bp + "conv_dw.bias"]))
                 yf, mean, rstd = _ln_fwd(z, P[bp + "norm.weight"], P[bp + "norm.bias"], 1e-6)
                 y = q(yf)
                 h = y @ self._lin_w(bp + "mlp.fc1.weight").t() + P[bp + "mlp.fc1.bias"]
@@ -404,7 +413,8 @@ class ConvNeXtBf16Emu:
                 G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), wdw.shape, dzc, padding=3,
                                                                        groups=C)
                 G[bp + "conv_dw.bias"] = dz.reshape(M, C).sum(0)
-                d = d + torch.nn.grad.conv2d_input((B, C, H, W), wdw, dzc, padding=3, groups=C).permute(0, 2, 3, 1)
+                d = d + torch.nn.grad.conv2d_input((B, C, H, W), q(wdw) if self.dw_bf16 else wdw, dzc, padding=3,
+                                                   groups=C).permute(0, 2, 3, 1)
             if ds is not None:
                 x_prev, pd, dm, dr = ds
                 pd = pd.to(dt)

@@ -471,13 +471,20 @@ class ConvNeXtHip(nn.Module):
                 with torch.cuda.stream(side) if side is not None else _nullctx():
                     K.linear_wgrad(dh, y, out=g(blk.mlp.fc1.weight), accumulate=True,
                                    bias_out=g(blk.mlp.fc1.bias), compute_bf16=bf, defer=folds, policy=pol)
-                dy = torch.empty(M, C, device=d.device, dtype=act)
-                K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf, policy=pol)
-                # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
-                # the LN weight/bias partials are folded on the side stream (off the data-gradient chain)
-                dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight,
-                                                dw=g(blk.norm.weight), db=g(blk.norm.bias), out_dtype=act,
-                                                defer_reduce=True)
+                # bf16: the LayerNorm backward in the fc1 data gradient's epilogue where it applies (as the lean
+                # schedule does, so both schedules give the same bits)
+                fused = K.linear_dgrad_ln(dh, w1, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
+                                          db=g(blk.norm.bias), policy=pol) if bf else None
+                if fused is not None:
+                    dz, ln_finish = fused
+                else:
+                    dy = torch.empty(M, C, device=d.device, dtype=act)
+                    K.linear_dgrad(dh, w1, out=dy, compute_bf16=bf, policy=pol)
+                    # LayerNorm + depthwise conv; d += dwconv^T(dz) in place, bf16 copy refreshed (old copy dead)
+                    # the LN weight/bias partials are folded on the side stream (off the data-gradient chain)
+                    dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight,
+                                                    dw=g(blk.norm.weight), db=g(blk.norm.bias), out_dtype=act,
+                                                    defer_reduce=True)
                 dz4 = dz.view(B, H, W, C)
                 blk_params = [blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
                               blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.gamma]

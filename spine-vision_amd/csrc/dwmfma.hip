@@ -1,0 +1,293 @@
+// Depthwise 7x7 convolution (pad 3, stride 1, NHWC) on the matrix cores -- ConvNeXtBlock.conv_dw forward and its
+// backward-data (timm convnext.py via spine_vision/training/models/backbone.py:50; round 6).
+//
+// A depthwise conv has no GEMM across channels: every channel has its own 7x7 filter.  What a channel does have is a
+// GEMM along the image ROW: for kernel row kr, the 16 outputs (row m, columns n0 .. n0+15) take
+//     out[m][n] += sum_k T_kr[n][k] * x[m + kr - 3][n0 - 3 + k],   T_kr[n][k] = w[kr][k - n]  (0 <= k - n <= 6)
+// -- a banded Toeplitz matrix T_kr (16 x 32, 7 diagonals) times 16 input rows x 32 input columns.  One
+// v_mfma_f32_16x16x32_bf16 per kernel row computes 256 outputs of one channel; seven of them (kr = 0..6, each reading
+// its input rows one lower) finish a 16 x 16 output block.  The k >= 24 quarter of every K window multiplies zero
+// taps (its A operand reads a zero region), so the matrix cores do 32/7 x the depthwise FLOPs -- still ~3 us of MFMA
+// per ConvNeXt-base S3 layer at bs32, against the VALU kernel's 49 v_fma_f32 per output (dwconv.hip).
+//
+// Operands are bf16 (the precision torch.autocast gives conv_dw), products exact, sums in f32 by the MFMA.
+//
+// Workgroup = 4 waves = one image tile of 16 output rows x 16 NB output columns x 32 channels (8 per wave):
+//   1. the 22 x (16 NB + 6) input pixels x 32 channels are read from HBM (16 B per lane, full 128-B / 64-B channel
+//      segments), rounded to bf16 and TRANSPOSED into channel planes [c][row][col] in LDS (the MFMA operand wants 8
+//      consecutive columns of one channel per lane; NHWC holds 8 consecutive channels of one column);
+//   2. the 32 x 7 Toeplitz rows are built once per workgroup as zero-padded tap windows [c][kr][2 parities][24 bf16]:
+//      lane (n, q) of the T operand needs taps 8q - n .. 8q - n + 7, a 4-byte-aligned 16-byte read of one parity copy;
+//   3. per channel: 7 T operands (28 VGPRs), then per 16-column block 7 MFMAs over LDS reads of the data operand;
+//   4. the accumulators (lane: 4 consecutive output columns of one output row, one channel) are staged through LDS as
+//      [pixel][channel] and stored 16 B per lane (bf16 z with the bias; or f32 dx accumulated + its bf16 copy).
+// Barriers: after the fill, before the staging (the input region is reused), before the read-back.
+#include "common.h"
+#include "gemm_common.h"
+
+namespace sv {
+namespace dwm {
+
+constexpr int CG = 32;           // channels per workgroup (8 per wave)
+constexpr int TH = 16;           // output rows per tile = the MFMA's 16 rows
+constexpr int IR = TH + 6;       // input rows per tile
+constexpr int kThreads = 256;
+constexpr int kTabB = 96;        // bytes per (channel, kernel row) Toeplitz window pair: 2 x 24 bf16
+constexpr int kZeroB = 640;      // zero region read by the k >= 24 lanes (<= 6 RS + 32 + 16 bytes)
+
+template <int NB>
+struct Geo {
+  static constexpr int TW = 16 * NB;                // output columns per tile
+  static constexpr int IC = (TW + 6 + 7) / 8 * 8;   // input columns kept per row (K windows reach column TW + 7)
+  static constexpr int RS = IC * 2;                 // bytes per input row of one channel plane
+  static constexpr int PS = IR * RS + 16;           // bytes per channel plane (+16: the fill's write banks)
+  static constexpr int IN_BYTES = CG * PS;
+  static constexpr int TAB = CG * 7 * kTabB;
+  static constexpr int OP16 = TW * 64 + 16;         // bf16 staging: bytes per output row ([TW pixels][32 ch] + 16)
+  static constexpr int OP32 = 16 * 128 + 16;        // f32 staging (one 16-column block at a time)
+  static constexpr int LDS = IN_BYTES + TAB + kZeroB;
+  static_assert(TH * OP16 <= IN_BYTES && TH * OP32 <= IN_BYTES, "staging reuses the input planes");
+  static_assert(6 * RS + 32 * (NB - 1) + 16 <= kZeroB, "zero region");
+};
+
+struct DwmGeo {
+  int B, H, W, C, tilesW, tilesH, ntiles;
+};
+
+// XCD-contiguous order (dwconv.hip xcd_block): each XCD walks a contiguous range of (tile, channel group) pairs, so the
+// channel groups of one pixel and the halo rows / columns of neighbouring tiles meet in one L2
+__device__ __forceinline__ int xcd_order(int b, int G) { return (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b; }
+
+template <typename T>
+__device__ __forceinline__ void to_bf16(const uint4& raw, uint16_t (&o)[16 / sizeof(T)]) {
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t a = pack2bf(__uint_as_float(raw.x), __uint_as_float(raw.y));
+    const uint32_t b = pack2bf(__uint_as_float(raw.z), __uint_as_float(raw.w));
+    o[0] = (uint16_t)a, o[1] = (uint16_t)(a >> 16), o[2] = (uint16_t)b, o[3] = (uint16_t)(b >> 16);
+  } else {
+    const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (uint16_t)(w[i >> 1] >> (16 * (i & 1)));
+  }
+}
+
+// MODE 0: z (bf16) = bias + conv(x).  MODE 1: dx (f32) = conv_flipped(dz) [+ bf16 copy].  MODE 2: dx += ...
+template <typename TIN, bool FLIP, int MODE, int NB>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const float* __restrict__ bdw,
+                void* __restrict__ out, uint16_t* __restrict__ out_bf16, DwmGeo g) {
+  using G = Geo<NB>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* tin = smem;
+  char* tab = smem + G::IN_BYTES;
+  char* zreg = tab + G::TAB;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ncg = g.C / CG;
+  const int lb = xcd_order(blockIdx.x, gridDim.x);
+  const int cgi = lb % ncg, tile = lb / ncg;
+  const int twi = tile % g.tilesW, t2 = tile / g.tilesW, thi = t2 % g.tilesH, b = t2 / g.tilesH;
+  const int h0 = thi * TH, w0 = twi * G::TW, c0 = cgi * CG;
+
+  // ---- 1. input tile -> bf16 channel planes (every load first, then every LDS write) ----
+  constexpr int EPC = 16 / (int)sizeof(TIN);  // channels per 16-B chunk
+  constexpr int QPP = CG / EPC;               // chunks per pixel
+  constexpr int PPI = 64 / QPP;               // pixels per wave instruction
+  constexpr int TOTAL = IR * G::IC * QPP;
+  static_assert(TOTAL % 64 == 0 && (IR * G::IC) % PPI == 0, "fill geometry");
+  constexpr int NIT = (TOTAL + kThreads - 1) / kThreads;
+  uint4 raw[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int it = tid + k * kThreads;
+    const int l6 = it & 63, pix = (it >> 6) * PPI + l6 % PPI, quad = l6 / PPI;
+    const int row = pix / G::IC, col = pix - row * G::IC;
+    const int hh = h0 - 3 + row, ww = w0 - 3 + col;
+    const bool ok = (TOTAL % kThreads == 0 || it < TOTAL) && col < G::TW + 6 && hh >= 0 && hh < g.H && ww >= 0 &&
+                    ww < g.W;
+    raw[k] = ok ? *reinterpret_cast<const uint4*>(x + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + quad * EPC)
+                : make_uint4(0u, 0u, 0u, 0u);
+  }
+  // ---- 2. Toeplitz windows: thread (c, kr) packs its 7 taps into the two parity copies of the zero-padded row
+  //      Zt[t] = w[kr][t - 8] (t = 8..14), copy 0 = Zt[0..23], copy 1 = Zt[1..24] ----
+  if (tid < CG * 7) {
+    const int c = tid / 7, kr = tid - 7 * c;
+    const float* wp = wdw + (size_t)(c0 + c) * 49 + (FLIP ? 6 - kr : kr) * 7;
+    float w7[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) w7[j] = wp[FLIP ? 6 - j : j];
+    uint4* d = reinterpret_cast<uint4*>(tab + tid * kTabB);
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    d[0] = z4;                                                                                   // copy 0 dwords 0-3
+    d[1] = make_uint4(pack2bf(w7[0], w7[1]), pack2bf(w7[2], w7[3]), pack2bf(w7[4], w7[5]), pack2bf(w7[6], 0.f));
+    d[2] = z4;                                                                                   // dwords 8-11
+    d[3] = make_uint4(0u, 0u, 0u, pack2bf(0.f, w7[0]));                                          // copy 1 dwords 0-3
+    d[4] = make_uint4(pack2bf(w7[1], w7[2]), pack2bf(w7[3], w7[4]), pack2bf(w7[5], w7[6]), 0u);  // 4-7
+    d[5] = z4;
+  }
+  for (int i = tid; i < kZeroB / 16; i += kThreads) reinterpret_cast<uint4*>(zreg)[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int it = tid + k * kThreads;
+    if (TOTAL % kThreads != 0 && it >= TOTAL) break;
+    const int l6 = it & 63, pix = (it >> 6) * PPI + l6 % PPI, quad = l6 / PPI;
+    const int row = pix / G::IC, col = pix - row * G::IC;
+    uint16_t e[EPC];
+    to_bf16<TIN>(raw[k], e);
+    char* p = tin + (quad * EPC) * G::PS + row * G::RS + col * 2;
+#pragma unroll
+    for (int i = 0; i < EPC; ++i) *reinterpret_cast<uint16_t*>(p + i * G::PS) = e[i];
+  }
+  __syncthreads();
+
+  // ---- 3. MFMAs: lane (n = lane & 15, q = lane >> 4) of the T operand takes taps 8q - n .. +7; lane (m, q) of the
+  //      data operand columns 8q .. 8q + 7 of input row m + kr (q = 3: the zero region) ----
+  const int n = lane & 15, q = lane >> 4;
+  int s = 8 * q - n + 8;
+  s = s < 0 ? 0 : (s > 16 ? 16 : s);
+  const int toff = (s & 1) * 48 + (s >> 1) * 4;
+  f32x4 acc[8][NB];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int c = wv * 8 + t;
+    const char* tb = tab + c * 7 * kTabB + toff;
+    bf16x8 tw[7];
+#pragma unroll
+    for (int kr = 0; kr < 7; ++kr) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(tb + kr * kTabB);
+      const uint32_t v4[4] = {p[0], p[1], p[2], p[3]};
+      tw[kr] = __builtin_bit_cast(bf16x8, v4);
+    }
+    const char* ab = q < 3 ? tin + c * G::PS + n * G::RS + 16 * q : zreg;
+    const float bias = MODE == 0 ? bdw[c0 + c] : 0.f;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      f32x4 a = {bias, bias, bias, bias};
+#pragma unroll
+      for (int kr = 0; kr < 7; ++kr) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(ab + kr * G::RS + 32 * nb);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tw[kr], xv, a, 0, 0, 0);
+      }
+      acc[t][nb] = a;
+    }
+  }
+  // lane (m = lane & 15, q) now holds output row h0 + m, columns w0 + 16 nb + 4q + r (r = 0..3), channel 8 wv + t
+  __syncthreads();  // every wave is done with the input planes
+  const int m = lane & 15;
+  if constexpr (MODE == 0) {
+    // ---- 4a. bf16 z: stage [row][pixel][32 ch] (16 B per lane: the wave's 8 channels), read back 16 B per lane ----
+    uint16_t* z = reinterpret_cast<uint16_t*>(out);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint4 v;
+        v.x = pack2bf(acc[0][nb][r], acc[1][nb][r]);
+        v.y = pack2bf(acc[2][nb][r], acc[3][nb][r]);
+        v.z = pack2bf(acc[4][nb][r], acc[5][nb][r]);
+        v.w = pack2bf(acc[6][nb][r], acc[7][nb][r]);
+        *reinterpret_cast<uint4*>(smem + m * G::OP16 + (16 * nb + 4 * q + r) * 64 + wv * 16) = v;
+      }
+    __syncthreads();
+    constexpr int ITEMS = TH * G::TW * 4;
+#pragma unroll
+    for (int k = 0; k < ITEMS / kThreads; ++k) {
+      const int it = tid + k * kThreads;
+      const int ch = it & 3, pix = it >> 2, row = pix / G::TW, col = pix - row * G::TW;
+      const int hh = h0 + row, ww = w0 + col;
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * G::OP16 + col * 64 + ch * 16);
+      if (hh < g.H && ww < g.W)
+        *reinterpret_cast<uint4*>(z + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 8) = v;
+    }
+  } else {
+    // ---- 4b. f32 dx (+= when MODE 2) and its bf16 copy, one 16-column block at a time ----
+    float* dx = reinterpret_cast<float*>(out);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      if (nb > 0) __syncthreads();  // the previous block's read-back is done
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float4* p = reinterpret_cast<float4*>(smem + m * G::OP32 + (4 * q + r) * 128 + wv * 32);
+        p[0] = make_float4(acc[0][nb][r], acc[1][nb][r], acc[2][nb][r], acc[3][nb][r]);
+        p[1] = make_float4(acc[4][nb][r], acc[5][nb][r], acc[6][nb][r], acc[7][nb][r]);
+      }
+      __syncthreads();
+      constexpr int ITEMS = TH * 16 * 8;  // 16 x 16 pixels x 8 chunks of 4 channels
+#pragma unroll
+      for (int k = 0; k < ITEMS / kThreads; ++k) {
+        const int it = tid + k * kThreads;
+        const int ch = it & 7, pix = it >> 3, row = pix >> 4, col = pix & 15;
+        const int hh = h0 + row, ww = w0 + 16 * nb + col;
+        float4 v = *reinterpret_cast<const float4*>(smem + row * G::OP32 + col * 128 + ch * 16);
+        if (hh < g.H && ww < g.W) {
+          const size_t o = ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 4;
+          if constexpr (MODE == 2) {
+            const float4 old = *reinterpret_cast<const float4*>(dx + o);
+            v = make_float4(old.x + v.x, old.y + v.y, old.z + v.z, old.w + v.w);
+          }
+          *reinterpret_cast<float4*>(dx + o) = v;
+          if (out_bf16) *reinterpret_cast<uint2*>(out_bf16 + o) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+        }
+      }
+    }
+  }
+}
+
+static DwmGeo geo(int B, int H, int W, int C, int tw) {
+  DwmGeo g{B, H, W, C, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
+  g.ntiles = B * g.tilesW * g.tilesH;
+  return g;
+}
+
+template <typename TIN, bool FLIP, int MODE, int NB>
+static int launch(const void* x, const float* wdw, const float* bdw, void* out, uint16_t* out_bf16, int B, int H,
+                  int W, int C, hipStream_t s) {
+  using G = Geo<NB>;
+  const DwmGeo g = geo(B, H, W, C, G::TW);
+  const long long grid = (long long)g.ntiles * (C / CG);
+  if (grid > 0x7fffffffLL) return set_error(SV_ERR_INVALID_ARG, "dwconv7 mfma: grid too large");
+  auto k = &dw7_mfma_kernel<TIN, FLIP, MODE, NB>;
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(k), G::LDS, s)) return rc;
+  k<<<(int)grid, kThreads, G::LDS, s>>>((const TIN*)x, wdw, bdw, out, out_bf16, g);
+  return check_launch("sv_dwconv7 (mfma)");
+}
+
+}  // namespace dwm
+}  // namespace sv
+
+using namespace sv;
+
+extern "C" {
+
+int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const float* bdw, uint16_t* z, int32_t B,
+                        int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(x && wdw && bdw && z, "sv_dwconv7_fwd_mfma: null pointer");
+  SV_REQUIRE(C % dwm::CG == 0 && C > 0, "sv_dwconv7_fwd_mfma: C=%d must be a multiple of 32", C);
+  SV_REQUIRE(x_dtype == SV_F32 || x_dtype == SV_BF16, "sv_dwconv7_fwd_mfma: bad x dtype");
+  SV_REQUIRE(x != (const void*)z, "sv_dwconv7_fwd_mfma: x and z must not alias");
+  if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool nb2 = W > 16;
+  if (x_dtype == SV_F32)
+    return nb2 ? dwm::launch<float, false, 0, 2>(x, wdw, bdw, z, nullptr, B, H, W, C, s)
+               : dwm::launch<float, false, 0, 1>(x, wdw, bdw, z, nullptr, B, H, W, C, s);
+  return nb2 ? dwm::launch<uint16_t, false, 0, 2>(x, wdw, bdw, z, nullptr, B, H, W, C, s)
+             : dwm::launch<uint16_t, false, 0, 1>(x, wdw, bdw, z, nullptr, B, H, W, C, s);
+}
+
+int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
+                             int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(dz && wdw && dx, "sv_dwconv7_bwd_data_mfma: null pointer");
+  SV_REQUIRE(C % dwm::CG == 0 && C > 0, "sv_dwconv7_bwd_data_mfma: C=%d must be a multiple of 32", C);
+  SV_REQUIRE((const void*)dz != (const void*)dx && (const void*)dz != (const void*)dx_bf16,
+             "sv_dwconv7_bwd_data_mfma: dz must not alias dx / dx_bf16");
+  if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool nb2 = W > 16;
+  if (accumulate)
+    return nb2 ? dwm::launch<uint16_t, true, 2, 2>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s)
+               : dwm::launch<uint16_t, true, 2, 1>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s);
+  return nb2 ? dwm::launch<uint16_t, true, 1, 2>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s)
+             : dwm::launch<uint16_t, true, 1, 1>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s);
+}
+
+}  // extern "C"

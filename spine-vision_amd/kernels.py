@@ -643,12 +643,36 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
 
 # ----------------------------------------------------------------------------------------------
 # depthwise 7x7 + LN
+# The depthwise conv on the matrix cores (csrc/dwmfma.hip, round 6): per channel a banded-Toeplitz GEMM along the image
+# row on v_mfma_f32_16x16x32_bf16, with bf16 operands (the precision torch.autocast gives conv_dw).  SV_DW_MFMA=1 routes
+# the bf16 training forward (z kept) and the bf16-dz backward-data through it; 0 keeps the f32 VALU kernels (dwconv.hip).
+DW_MFMA = os.environ.get("SV_DW_MFMA", "0") != "0"
+
+
+def dwconv7_fwd_mfma(x4d, wdw, bdw):
+    """z (bf16) = bf16(bdw + sum_tap bf16(w) bf16(x)) (sv_dwconv7_fwd_mfma)."""
+    B, H, W, C = x4d.shape
+    _check(C % 32 == 0 and x4d.is_contiguous() and x4d.dtype in (torch.float32, torch.bfloat16),
+           "dwconv7_fwd_mfma: contiguous f32 / bf16 [B,H,W,C], C % 32 == 0")
+    _check(wdw.dtype == torch.float32 and wdw.is_contiguous() and wdw.numel() == 49 * C and bdw.numel() == C,
+           "dwconv7_fwd_mfma: f32 weight [C,1,7,7], bias [C]")
+    z = torch.empty(B, H, W, C, device=x4d.device, dtype=torch.bfloat16)
+    n = B * H * W * C
+    _timed_call("dw_fwd", n * (x4d.element_size() + 2), "sv_dwconv7_fwd_mfma", ptr(x4d), dt(x4d), ptr(wdw), ptr(bdw),
+                ptr(z), B, H, W, C, flops=98.0 * n)
+    return z
+
+
 def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN, save_z=True):
     """-> z (the conv output, saved for the LayerNorm backward; None when ``save_z`` is False and the one-pass form
     runs), y = LN(z), mean, rstd.  C = 128 / 256 / 512 over an f32 input run as ONE kernel (sv_dwconv7_ln_fused_ok),
     bitwise the two-launch result."""
     B, H, W, C = x4d.shape
     _check(C % 64 == 0, "dwconv7: C must be a multiple of 64")
+    if DW_MFMA and save_z and act_dtype == torch.bfloat16:
+        z = dwconv7_fwd_mfma(x4d, wdw, bdw)
+        y, mean, rstd = layernorm_fwd(z.view(-1, C), lnw, lnb, out_dtype=act_dtype, eps=eps)
+        return z, y, mean, rstd
     act_code = SV_BF16 if act_dtype == torch.bfloat16 else SV_F32
     if not save_z and value("sv_dwconv7_ln_fused_ok", B, H, W, C, dt(x4d), act_code, act_code):
         z = None
@@ -673,6 +697,10 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
     n = B * H * W * C
     # algorithmic: dz read; the f32 gradient stream dx written (and read when accumulating); its bf16 copy
     nb = n * (dz4d.element_size() + 4 * (2 if accumulate else 1) + (2 if dx_bf16 is not None else 0))
+    if DW_MFMA and dz4d.dtype == torch.bfloat16 and C % 32 == 0:
+        _timed_call("dw_bwd_data", nb, "sv_dwconv7_bwd_data_mfma", ptr(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16),
+                    int(accumulate), B, H, W, C, flops=98.0 * n)
+        return
     _timed_call("dw_bwd_data", nb, "sv_dwconv7_bwd_data", ptr(dz4d), dt(dz4d), ptr(wdw), ptr(dx4d), ptr(dx_bf16),
                 int(accumulate), B, H, W, C, fma=49.0 * n)
 

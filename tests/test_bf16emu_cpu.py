@@ -80,3 +80,12 @@ def test_slab_wgrad_rounds_each_contiguous_slice():
     want = sum(be.bf16_round(A[s * 128:(s + 1) * 128].t() @ B[s * 128:(s + 1) * 128]) for s in range(4))
     assert torch.equal(be._slab_wgrad(A, B, 4, True), want)
     assert not torch.equal(want, full)
+
+
+def test_emulation_follows_the_depthwise_operand_precision():
+    """The emulation rounds the depthwise conv's operands to bf16 exactly when the product runs the matrix-core kernels
+    (SV_DW_MFMA, same default in both)."""
+    from oracle import bf16emu
+    from spine_vision_amd import kernels as K
+
+    assert bf16emu.DW_BF16_OPERANDS == K.DW_MFMA

@@ -82,6 +82,19 @@ def main():
                       lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
                                       nv.ptr(bias), 1e-6, nv.ptr(z), nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
                                       nv.ptr(rstd), B, S, S, C)))
+        # the matrix-core kernels (csrc/dwmfma.hip, round 6): bf16 operands
+        cases.append(("mfma fwd f32->bf16", 6 * n,
+                      lambda: nv.call("sv_dwconv7_fwd_mfma", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(z),
+                                      B, S, S, C)))
+
+        def mfma_fwd_ln():
+            nv.call("sv_dwconv7_fwd_mfma", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(z), B, S, S, C)
+            nv.call("sv_layernorm_fwd", nv.ptr(z), nv.SV_BF16, nv.ptr(lnw), nv.ptr(bias), nv.ptr(y), nv.SV_BF16,
+                    nv.ptr(mean), nv.ptr(rstd), B * S * S, C, 1e-6)
+        cases.append(("mfma fwd f32->bf16 + LN", 4 * n + 2 * n + 2 * n + 2 * n, mfma_fwd_ln))
+        cases.append(("mfma bwd_data bf16dz acc+bf16", 2 * n + 4 * n + 4 * n + 2 * n,
+                      lambda: nv.call("sv_dwconv7_bwd_data_mfma", nv.ptr(dzb), nv.ptr(w), nv.ptr(dx), nv.ptr(dxb), 1,
+                                      B, S, S, C)))
         for name, nbytes, fn in cases:
             us = timeit(fn, args.iters)
             print(f"{tag} {st} {name:28s} {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s", flush=True)

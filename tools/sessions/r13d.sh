@@ -10,7 +10,7 @@ O=$ROOTDIR/gpurun_out/$N
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_ln_bwd_fused_gpu.py > $O/ln.log 2>&1 || { grep -E "FAIL|Error|assert|ln_bwd fused" $O/ln.log | head -30; tail -30 $O/ln.log; exit 1; }
 grep -E "ln_bwd fused|passed|failed" $O/ln.log
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $O/tests.log 2>&1 || { grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest --maxfail=5 -q --timeout 300 --timeout-method thread -m gpu tests/ > $O/tests.log 2>&1 || { grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for f in 1 0; do
   SV_FUSED_LN_BWD=$f timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$f.json 2> $O/bench_$f.err || { tail -5 $O/bench_$f.err; exit 1; }
