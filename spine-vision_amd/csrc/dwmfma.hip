@@ -88,24 +88,37 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   const int twi = tile % g.tilesW, t2 = tile / g.tilesW, thi = t2 % g.tilesH, b = t2 / g.tilesH;
   const int h0 = thi * TH, w0 = twi * G::TW, c0 = cgi * CG;
 
-  // ---- 1. input tile -> bf16 channel planes (every load first, then every LDS write) ----
+  // ---- 1. input tile -> bf16 channel planes.  Wave wv loads input rows wv, wv + 4, ..: per row NJ instructions of PPI
+  //      consecutive columns x QPP channel chunks (16 B per lane) through a buffer descriptor over the image, so an
+  //      out-of-image column reads zeros without a branch; every load first, then every LDS write ----
   constexpr int EPC = 16 / (int)sizeof(TIN);  // channels per 16-B chunk
   constexpr int QPP = CG / EPC;               // chunks per pixel
   constexpr int PPI = 64 / QPP;               // pixels per wave instruction
-  constexpr int TOTAL = IR * G::IC * QPP;
-  static_assert(TOTAL % 64 == 0 && (IR * G::IC) % PPI == 0, "fill geometry");
-  constexpr int NIT = (TOTAL + kThreads - 1) / kThreads;
-  uint4 raw[NIT];
+  constexpr int NJ = (G::IC + PPI - 1) / PPI;
+  constexpr int NRW = (IR + 3) / 4;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int fc = lane % PPI, fq = lane / PPI;
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<TIN*>(x + (size_t)b * g.H * g.W * g.C), (short)0, (int)((size_t)g.H * g.W * g.C * sizeof(TIN)),
+      0x00020000);
+  uint32_t loff[NJ];
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int it = tid + k * kThreads;
-    const int l6 = it & 63, pix = (it >> 6) * PPI + l6 % PPI, quad = l6 / PPI;
-    const int row = pix / G::IC, col = pix - row * G::IC;
-    const int hh = h0 - 3 + row, ww = w0 - 3 + col;
-    const bool ok = (TOTAL % kThreads == 0 || it < TOTAL) && col < G::TW + 6 && hh >= 0 && hh < g.H && ww >= 0 &&
-                    ww < g.W;
-    raw[k] = ok ? *reinterpret_cast<const uint4*>(x + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + quad * EPC)
-                : make_uint4(0u, 0u, 0u, 0u);
+  for (int j = 0; j < NJ; ++j) {
+    const int col = j * PPI + fc, ww = w0 - 3 + col;
+    loff[j] = (col < G::TW + 6 && ww >= 0 && ww < g.W) ? (uint32_t)((ww * g.C + c0 + fq * EPC) * (int)sizeof(TIN))
+                                                       : 0x80000000u;
+  }
+  uint4 raw[NRW][NJ];
+#pragma unroll
+  for (int i = 0; i < NRW; ++i) {
+    const int row = wvu + 4 * i, hh = h0 - 3 + row;
+    const bool okr = row < IR && hh >= 0 && hh < g.H;  // wave-uniform
+    const uint32_t ro = okr ? (uint32_t)(hh * g.W * g.C * (int)sizeof(TIN)) : 0u;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, loff[j] + ro, 0, 0);
+      raw[i][j] = okr ? make_uint4(v[0], v[1], v[2], v[3]) : make_uint4(0u, 0u, 0u, 0u);
+    }
   }
   // ---- 2. Toeplitz windows: thread (c, kr) packs its 7 taps into the two parity copies of the zero-padded row
   //      Zt[t] = w[kr][t - 8] (t = 8..14), copy 0 = Zt[0..23], copy 1 = Zt[1..24] ----
@@ -125,17 +138,20 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
     d[5] = z4;
   }
   for (int i = tid; i < kZeroB / 16; i += kThreads) reinterpret_cast<uint4*>(zreg)[i] = make_uint4(0u, 0u, 0u, 0u);
+  char* wb = tin + (fq * EPC) * G::PS + fc * 2;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int it = tid + k * kThreads;
-    if (TOTAL % kThreads != 0 && it >= TOTAL) break;
-    const int l6 = it & 63, pix = (it >> 6) * PPI + l6 % PPI, quad = l6 / PPI;
-    const int row = pix / G::IC, col = pix - row * G::IC;
-    uint16_t e[EPC];
-    to_bf16<TIN>(raw[k], e);
-    char* p = tin + (quad * EPC) * G::PS + row * G::RS + col * 2;
+  for (int i = 0; i < NRW; ++i) {
+    const int row = wvu + 4 * i;
+    if (row >= IR) break;
 #pragma unroll
-    for (int i = 0; i < EPC; ++i) *reinterpret_cast<uint16_t*>(p + i * G::PS) = e[i];
+    for (int j = 0; j < NJ; ++j) {
+      if (NJ * PPI != G::IC && j * PPI + fc >= G::IC) continue;
+      uint16_t e[EPC];
+      to_bf16<TIN>(raw[i][j], e);
+      char* p = wb + row * G::RS + j * PPI * 2;
+#pragma unroll
+      for (int t = 0; t < EPC; ++t) *reinterpret_cast<uint16_t*>(p + t * G::PS) = e[t];
+    }
   }
   __syncthreads();
 
