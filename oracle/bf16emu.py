@@ -298,7 +298,7 @@ def _slab_wgrad(A, Bm, split: int, bf16_slabs: bool):
 # The depthwise conv's operands: the matrix-core kernels (csrc/dwmfma.hip, SV_DW_MFMA=1 in the product) round x / dz's
 # partner and the taps to bf16 -- torch.autocast's precision for conv_dw -- where the VALU kernels take f32 x and taps.
 # Same switch and default as spine_vision_amd/kernels.py DW_MFMA (tests/test_bf16emu_cpu.py checks they agree).
-DW_BF16_OPERANDS = os.environ.get("SV_DW_MFMA", "0") != "0"
+DW_BF16_OPERANDS = os.environ.get("SV_DW_MFMA", "1") != "0"
 
 # the tape keeps the bf16-rounded tensors as bf16 (exact, a quarter of float64's memory); a check that disables the
 # rounding (bf16_round -> identity, test_oracle_golden) must keep them in the working dtype

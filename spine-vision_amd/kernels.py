@@ -644,9 +644,11 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
 # ----------------------------------------------------------------------------------------------
 # depthwise 7x7 + LN
 # The depthwise conv on the matrix cores (csrc/dwmfma.hip, round 6): per channel a banded-Toeplitz GEMM along the image
-# row on v_mfma_f32_16x16x32_bf16, with bf16 operands (the precision torch.autocast gives conv_dw).  SV_DW_MFMA=1 routes
-# the bf16 training forward (z kept) and the bf16-dz backward-data through it; 0 keeps the f32 VALU kernels (dwconv.hip).
-DW_MFMA = os.environ.get("SV_DW_MFMA", "0") != "0"
+# row on v_mfma_f32_16x16x32_bf16, with bf16 operands (the precision torch.autocast gives conv_dw).  Default: the bf16
+# training forward (z kept) and the bf16-dz backward-data run on it (+1.3-1.4 % training step over the f32 VALU kernels,
+# profiles/round6/r13g_*); SV_DW_MFMA=0 keeps the VALU kernels (dwconv.hip), which the f32 parity mode, the tape-free
+# eval forward (one pass with the LayerNorm) and the weight gradient always use.
+DW_MFMA = os.environ.get("SV_DW_MFMA", "1") != "0"
 
 
 def dwconv7_fwd_mfma(x4d, wdw, bdw):

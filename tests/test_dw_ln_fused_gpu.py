@@ -52,8 +52,11 @@ def _inputs(i, B, H, W, C):
     return x, w, b, lw, lb
 
 
-def test_dw_ln_fused_matches_two_launches(dev, tmp_path):
+def test_dw_ln_fused_matches_two_launches(dev, tmp_path, monkeypatch):
     assert os.environ.get("SV_DW_LN_FUSED") is None
+    # the one pass is bitwise the VALU kernels' two launches (f32 taps and x); the training forward's matrix-core
+    # depthwise (bf16 operands, K.DW_MFMA) is pinned by tests/test_dw_mfma_gpu.py
+    monkeypatch.setattr(K, "DW_MFMA", False)
     refs = []
     for i, (B, H, W, C, dts) in enumerate(CASES):
         code = nv.SV_BF16 if dts == "bf16" else nv.SV_F32
