@@ -41,7 +41,7 @@ struct Geo {
   static constexpr int IC = (TW + 6 + 7) / 8 * 8;   // input columns kept per row (K windows reach column TW + 7)
   static constexpr int RS = IC * 2;                 // bytes per input row of one channel plane
   static constexpr int PS = IR * RS + 16;           // bytes per channel plane (+16: the fill's write banks)
-  static constexpr int IN_BYTES = CG * PS;
+  static constexpr int IN_BYTES = CG * PS + 256;    // + the planes' bank skew (<= 7 x 32 B)
   static constexpr int TAB = CG * 7 * kTabB;
   static constexpr int OP16 = TW * 64 + 16;         // bf16 staging: bytes per output row ([TW pixels][32 ch] + 16)
   static constexpr int OP32 = 16 * 128 + 16;        // f32 staging (one 16-column block at a time)
@@ -96,6 +96,10 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   constexpr int PPI = 64 / QPP;               // pixels per wave instruction
   constexpr int NJ = (G::IC + PPI - 1) / PPI;
   constexpr int NRW = (IR + 3) / 4;
+  // channel plane c starts at c PS + ((c / EPC) mod 8) SKEW: the fill's lane groups (PPI columns of EPC channels each)
+  // then write 16 / 32 B runs on distinct banks instead of PS apart on the same ones (r13h: 11.4 M bank-conflict cycles
+  // against 9.2 M active LDS cycles at S1 without the skew)
+  constexpr int SKEW = 2 * PPI;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
   const int fc = lane % PPI, fq = lane / PPI;
   const auto rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -120,6 +124,25 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
       raw[i][j] = okr ? make_uint4(v[0], v[1], v[2], v[3]) : make_uint4(0u, 0u, 0u, 0u);
     }
   }
+  // MODE 2: the accumulated gradient's tile is read now, in flight under the fill and the MFMAs, instead of after them
+  // (r13h: the backward's waves waited 72 % of their cycles, the read-back's dx loads exposed at every tile's end)
+  constexpr int NPRE = MODE == 2 ? NB * (TH * 16 * 8 / kThreads) : 1;
+  float4 pre[NPRE];
+  if constexpr (MODE == 2) {
+    const float* dxo = reinterpret_cast<const float*>(out);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int k = 0; k < TH * 16 * 8 / kThreads; ++k) {
+        const int it = tid + k * kThreads;
+        const int ch = it & 7, pix = it >> 3, row = pix >> 4, col = pix & 15;
+        const int hh = h0 + row, ww = w0 + 16 * nb + col;
+        pre[nb * (TH * 16 * 8 / kThreads) + k] =
+            hh < g.H && ww < g.W
+                ? *reinterpret_cast<const float4*>(dxo + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 4)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  }
   // ---- 2. Toeplitz windows: thread (c, kr) packs its 7 taps into the two parity copies of the zero-padded row
   //      Zt[t] = w[kr][t - 8] (t = 8..14), copy 0 = Zt[0..23], copy 1 = Zt[1..24] ----
   if (tid < CG * 7) {
@@ -138,7 +161,7 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
     d[5] = z4;
   }
   for (int i = tid; i < kZeroB / 16; i += kThreads) reinterpret_cast<uint4*>(zreg)[i] = make_uint4(0u, 0u, 0u, 0u);
-  char* wb = tin + (fq * EPC) * G::PS + fc * 2;
+  char* wb = tin + (fq * EPC) * G::PS + (fq & 7) * SKEW + fc * 2;
 #pragma unroll
   for (int i = 0; i < NRW; ++i) {
     const int row = wvu + 4 * i;
@@ -173,7 +196,7 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
       const uint32_t v4[4] = {p[0], p[1], p[2], p[3]};
       tw[kr] = __builtin_bit_cast(bf16x8, v4);
     }
-    const char* ab = q < 3 ? tin + c * G::PS + n * G::RS + 16 * q : zreg;
+    const char* ab = q < 3 ? tin + c * G::PS + ((c / EPC) & 7) * SKEW + n * G::RS + 16 * q : zreg;
     const float bias = MODE == 0 ? bdw[c0 + c] : 0.f;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
@@ -237,7 +260,7 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
         if (hh < g.H && ww < g.W) {
           const size_t o = ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 4;
           if constexpr (MODE == 2) {
-            const float4 old = *reinterpret_cast<const float4*>(dx + o);
+            const float4 old = pre[nb * (ITEMS / kThreads) + k];
             v = make_float4(old.x + v.x, old.y + v.y, old.z + v.z, old.w + v.w);
           }
           *reinterpret_cast<float4*>(dx + o) = v;
