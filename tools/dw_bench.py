@@ -82,6 +82,10 @@ def main():
                       lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
                                       nv.ptr(bias), 1e-6, nv.ptr(z), nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
                                       nv.ptr(rstd), B, S, S, C)))
+        cases.append(("one-pass f32->bf16 y (eval)", 4 * n + 2 * n,
+                      lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
+                                      nv.ptr(bias), 1e-6, None, nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
+                                      nv.ptr(rstd), B, S, S, C)))
         # the matrix-core kernels (csrc/dwmfma.hip, round 6): bf16 operands
         cases.append(("mfma fwd f32->bf16", 6 * n,
                       lambda: nv.call("sv_dwconv7_fwd_mfma", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(z),
