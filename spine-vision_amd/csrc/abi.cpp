@@ -121,7 +121,7 @@ int policy_grid(const sv_gemm_policy* pol, int total, int per_cu_default, hipStr
 
 extern "C" {
 
-int sv_version(void) { return 8; }
+int sv_version(void) { return 9; }
 
 int sv_ctx_create(int32_t device, sv_ctx** out) {
   SV_REQUIRE(out, "sv_ctx_create: null out");

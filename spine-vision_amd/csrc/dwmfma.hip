@@ -25,26 +25,28 @@
 #include "common.h"
 #include "gemm_common.h"
 
+#include <stdlib.h>
+
 namespace sv {
 namespace dwm {
 
-constexpr int CG = 32;           // channels per workgroup (8 per wave)
+constexpr int kCGMin = 16;       // channels per workgroup: CG = 32 (8 per wave) or 16 (4 per wave; less LDS)
 constexpr int TH = 16;           // output rows per tile = the MFMA's 16 rows
 constexpr int IR = TH + 6;       // input rows per tile
 constexpr int kThreads = 256;
 constexpr int kTabB = 96;        // bytes per (channel, kernel row) Toeplitz window pair: 2 x 24 bf16
 constexpr int kZeroB = 640;      // zero region read by the k >= 24 lanes (<= 6 RS + 32 + 16 bytes)
 
-template <int NB>
+template <int NB, int CG>
 struct Geo {
   static constexpr int TW = 16 * NB;                // output columns per tile
   static constexpr int IC = (TW + 6 + 7) / 8 * 8;   // input columns kept per row (K windows reach column TW + 7)
   static constexpr int RS = IC * 2;                 // bytes per input row of one channel plane
   static constexpr int PS = IR * RS + 16;           // bytes per channel plane (+16: the fill's write banks)
-  static constexpr int IN_BYTES = CG * PS + 256;    // + the planes' bank skew (<= 7 x 32 B)
+  static constexpr int IN_BYTES = CG * PS + 448;    // + the planes' bank skew (<= 7 x 64 B)
   static constexpr int TAB = CG * 7 * kTabB;
-  static constexpr int OP16 = TW * 64 + 16;         // bf16 staging: bytes per output row ([TW pixels][32 ch] + 16)
-  static constexpr int OP32 = 16 * 128 + 16;        // f32 staging (one 16-column block at a time)
+  static constexpr int OP16 = TW * CG * 2 + 16;     // bf16 staging: bytes per output row ([TW pixels][CG ch] + 16)
+  static constexpr int OP32 = 16 * CG * 4 + 16;     // f32 staging (one 16-column block at a time)
   static constexpr int LDS = IN_BYTES + TAB + kZeroB;
   static_assert(TH * OP16 <= IN_BYTES && TH * OP32 <= IN_BYTES, "staging reuses the input planes");
   static_assert(6 * RS + 32 * (NB - 1) + 16 <= kZeroB, "zero region");
@@ -72,11 +74,12 @@ __device__ __forceinline__ void to_bf16(const uint4& raw, uint16_t (&o)[16 / siz
 }
 
 // MODE 0: z (bf16) = bias + conv(x).  MODE 1: dx (f32) = conv_flipped(dz) [+ bf16 copy].  MODE 2: dx += ...
-template <typename TIN, bool FLIP, int MODE, int NB>
+template <typename TIN, bool FLIP, int MODE, int NB, int CG>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
 dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const float* __restrict__ bdw,
                 void* __restrict__ out, uint16_t* __restrict__ out_bf16, DwmGeo g) {
-  using G = Geo<NB>;
+  using G = Geo<NB, CG>;
+  constexpr int CPW = CG / 4;  // channels per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* tin = smem;
   char* tab = smem + G::IN_BYTES;
@@ -126,18 +129,19 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   }
   // MODE 2: the accumulated gradient's tile is read now, in flight under the fill and the MFMAs, instead of after them
   // (r13h: the backward's waves waited 72 % of their cycles, the read-back's dx loads exposed at every tile's end)
-  constexpr int NPRE = MODE == 2 ? NB * (TH * 16 * 8 / kThreads) : 1;
+  constexpr int CH32 = CG / 4;  // 16-B chunks of an f32 pixel
+  constexpr int NPRE = MODE == 2 ? NB * (TH * 16 * CH32 / kThreads) : 1;
   float4 pre[NPRE];
   if constexpr (MODE == 2) {
     const float* dxo = reinterpret_cast<const float*>(out);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-      for (int k = 0; k < TH * 16 * 8 / kThreads; ++k) {
+      for (int k = 0; k < TH * 16 * CH32 / kThreads; ++k) {
         const int it = tid + k * kThreads;
-        const int ch = it & 7, pix = it >> 3, row = pix >> 4, col = pix & 15;
+        const int ch = it % CH32, pix = it / CH32, row = pix >> 4, col = pix & 15;
         const int hh = h0 + row, ww = w0 + 16 * nb + col;
-        pre[nb * (TH * 16 * 8 / kThreads) + k] =
+        pre[nb * (TH * 16 * CH32 / kThreads) + k] =
             hh < g.H && ww < g.W
                 ? *reinterpret_cast<const float4*>(dxo + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 4)
                 : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -184,10 +188,10 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   int s = 8 * q - n + 8;
   s = s < 0 ? 0 : (s > 16 ? 16 : s);
   const int toff = (s & 1) * 48 + (s >> 1) * 4;
-  f32x4 acc[8][NB];
+  f32x4 acc[CPW][NB];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int c = wv * 8 + t;
+  for (int t = 0; t < CPW; ++t) {
+    const int c = wv * CPW + t;
     const char* tb = tab + c * 7 * kTabB + toff;
     bf16x8 tw[7];
 #pragma unroll
@@ -209,7 +213,7 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
       acc[t][nb] = a;
     }
   }
-  // lane (m = lane & 15, q) now holds output row h0 + m, columns w0 + 16 nb + 4q + r (r = 0..3), channel 8 wv + t
+  // lane (m = lane & 15, q) now holds output row h0 + m, columns w0 + 16 nb + 4q + r (r = 0..3), channel CPW wv + t
   __syncthreads();  // every wave is done with the input planes
   const int m = lane & 15;
   if constexpr (MODE == 0) {
@@ -219,21 +223,23 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        uint4 v;
-        v.x = pack2bf(acc[0][nb][r], acc[1][nb][r]);
-        v.y = pack2bf(acc[2][nb][r], acc[3][nb][r]);
-        v.z = pack2bf(acc[4][nb][r], acc[5][nb][r]);
-        v.w = pack2bf(acc[6][nb][r], acc[7][nb][r]);
-        *reinterpret_cast<uint4*>(smem + m * G::OP16 + (16 * nb + 4 * q + r) * 64 + wv * 16) = v;
+        char* p = smem + m * G::OP16 + (16 * nb + 4 * q + r) * (CG * 2) + wv * (CPW * 2);
+        if constexpr (CPW == 8) {
+          *reinterpret_cast<uint4*>(p) = make_uint4(pack2bf(acc[0][nb][r], acc[1][nb][r]), pack2bf(acc[2][nb][r], acc[3][nb][r]),
+                                                    pack2bf(acc[4][nb][r], acc[5][nb][r]), pack2bf(acc[6][nb][r], acc[7][nb][r]));
+        } else {
+          *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(acc[0][nb][r], acc[1][nb][r]), pack2bf(acc[2][nb][r], acc[3][nb][r]));
+        }
       }
     __syncthreads();
-    constexpr int ITEMS = TH * G::TW * 4;
+    constexpr int CH16 = CG / 8;  // 16-B chunks of a bf16 pixel
+    constexpr int ITEMS = TH * G::TW * CH16;
 #pragma unroll
     for (int k = 0; k < ITEMS / kThreads; ++k) {
       const int it = tid + k * kThreads;
-      const int ch = it & 3, pix = it >> 2, row = pix / G::TW, col = pix - row * G::TW;
+      const int ch = it % CH16, pix = it / CH16, row = pix / G::TW, col = pix - row * G::TW;
       const int hh = h0 + row, ww = w0 + col;
-      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * G::OP16 + col * 64 + ch * 16);
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * G::OP16 + col * (CG * 2) + ch * 16);
       if (hh < g.H && ww < g.W)
         *reinterpret_cast<uint4*>(z + ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 8) = v;
     }
@@ -245,18 +251,18 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
       if (nb > 0) __syncthreads();  // the previous block's read-back is done
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float4* p = reinterpret_cast<float4*>(smem + m * G::OP32 + (4 * q + r) * 128 + wv * 32);
+        float4* p = reinterpret_cast<float4*>(smem + m * G::OP32 + (4 * q + r) * (CG * 4) + wv * (CPW * 4));
         p[0] = make_float4(acc[0][nb][r], acc[1][nb][r], acc[2][nb][r], acc[3][nb][r]);
-        p[1] = make_float4(acc[4][nb][r], acc[5][nb][r], acc[6][nb][r], acc[7][nb][r]);
+        if constexpr (CPW == 8) p[1] = make_float4(acc[4][nb][r], acc[5][nb][r], acc[6][nb][r], acc[7][nb][r]);
       }
       __syncthreads();
-      constexpr int ITEMS = TH * 16 * 8;  // 16 x 16 pixels x 8 chunks of 4 channels
+      constexpr int ITEMS = TH * 16 * CH32;  // 16 x 16 pixels x chunks of 4 channels
 #pragma unroll
       for (int k = 0; k < ITEMS / kThreads; ++k) {
         const int it = tid + k * kThreads;
-        const int ch = it & 7, pix = it >> 3, row = pix >> 4, col = pix & 15;
+        const int ch = it % CH32, pix = it / CH32, row = pix >> 4, col = pix & 15;
         const int hh = h0 + row, ww = w0 + 16 * nb + col;
-        float4 v = *reinterpret_cast<const float4*>(smem + row * G::OP32 + col * 128 + ch * 16);
+        float4 v = *reinterpret_cast<const float4*>(smem + row * G::OP32 + col * (CG * 4) + ch * 16);
         if (hh < g.H && ww < g.W) {
           const size_t o = ((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + ch * 4;
           if constexpr (MODE == 2) {
@@ -277,17 +283,31 @@ static DwmGeo geo(int B, int H, int W, int C, int tw) {
   return g;
 }
 
-template <typename TIN, bool FLIP, int MODE, int NB>
-static int launch(const void* x, const float* wdw, const float* bdw, void* out, uint16_t* out_bf16, int B, int H,
-                  int W, int C, hipStream_t s) {
-  using G = Geo<NB>;
+template <typename TIN, bool FLIP, int MODE, int NB, int CG>
+static int launch1(const void* x, const float* wdw, const float* bdw, void* out, uint16_t* out_bf16, int B, int H,
+                   int W, int C, hipStream_t s) {
+  using G = Geo<NB, CG>;
   const DwmGeo g = geo(B, H, W, C, G::TW);
   const long long grid = (long long)g.ntiles * (C / CG);
   if (grid > 0x7fffffffLL) return set_error(SV_ERR_INVALID_ARG, "dwconv7 mfma: grid too large");
-  auto k = &dw7_mfma_kernel<TIN, FLIP, MODE, NB>;
+  auto k = &dw7_mfma_kernel<TIN, FLIP, MODE, NB, CG>;
   if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(k), G::LDS, s)) return rc;
   k<<<(int)grid, kThreads, G::LDS, s>>>((const TIN*)x, wdw, bdw, out, out_bf16, g);
   return check_launch("sv_dwconv7 (mfma)");
+}
+
+// SV_DW_MFMA_CG=16: 16 channels per workgroup (half the LDS, 4 workgroups per CU) instead of 32 (A/B)
+static int cg_choice() {
+  static const int v = getenv("SV_DW_MFMA_CG") ? atoi(getenv("SV_DW_MFMA_CG")) : 32;
+  return v == 16 ? 16 : 32;
+}
+
+template <typename TIN, bool FLIP, int MODE, int NB>
+static int launch(const void* x, const float* wdw, const float* bdw, void* out, uint16_t* out_bf16, int B, int H,
+                  int W, int C, hipStream_t s) {
+  if (cg_choice() == 16 || C % 32 != 0)
+    return launch1<TIN, FLIP, MODE, NB, 16>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
+  return launch1<TIN, FLIP, MODE, NB, 32>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
 }
 
 }  // namespace dwm
@@ -300,7 +320,7 @@ extern "C" {
 int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const float* bdw, uint16_t* z, int32_t B,
                         int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(x && wdw && bdw && z, "sv_dwconv7_fwd_mfma: null pointer");
-  SV_REQUIRE(C % dwm::CG == 0 && C > 0, "sv_dwconv7_fwd_mfma: C=%d must be a multiple of 32", C);
+  SV_REQUIRE(C % dwm::kCGMin == 0 && C > 0, "sv_dwconv7_fwd_mfma: C=%d must be a multiple of 16", C);
   SV_REQUIRE(x_dtype == SV_F32 || x_dtype == SV_BF16, "sv_dwconv7_fwd_mfma: bad x dtype");
   SV_REQUIRE(x != (const void*)z, "sv_dwconv7_fwd_mfma: x and z must not alias");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
@@ -316,7 +336,7 @@ int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const 
 int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
                              int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
   SV_REQUIRE(dz && wdw && dx, "sv_dwconv7_bwd_data_mfma: null pointer");
-  SV_REQUIRE(C % dwm::CG == 0 && C > 0, "sv_dwconv7_bwd_data_mfma: C=%d must be a multiple of 32", C);
+  SV_REQUIRE(C % dwm::kCGMin == 0 && C > 0, "sv_dwconv7_bwd_data_mfma: C=%d must be a multiple of 16", C);
   SV_REQUIRE((const void*)dz != (const void*)dx && (const void*)dz != (const void*)dx_bf16,
              "sv_dwconv7_bwd_data_mfma: dz must not alias dx / dx_bf16");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
