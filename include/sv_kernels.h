@@ -277,6 +277,13 @@ int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const 
                         int32_t H, int32_t W, int32_t C, sv_stream_t stream);
 int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, uint16_t* dx_bf16, int32_t accumulate,
                              int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
+/* backward-weight on the matrix cores: the 7 x 7 taps of a channel are one 16 x 16 MFMA accumulator summed over the
+ * tile's pixels (D[kr][j] = sum_(m,n') x[m + kr][n'] dz[m][n' - j]); dz bf16, x f32 or bf16 rounded to bf16.
+ * Per-workgroup partials dw_part [nparts][C*49], db_part [nparts][C] as sv_dwconv7_bwd_weight's, nparts =
+ * sv_dwconv7_bwd_weight_mfma_nparts(...).  C % 16 == 0.                                                           */
+int sv_dwconv7_bwd_weight_mfma_nparts(int32_t B, int32_t H, int32_t W, int32_t C);
+int sv_dwconv7_bwd_weight_mfma(const uint16_t* dz, const void* x, int32_t x_dtype, float* dw_part, float* db_part,
+                               int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream);
 
 /* ---- ConvNeXt stem: Conv2d(3, C, k=4, s=4) + LayerNorm2d, fused --------------------------------
  * img: NCHW f32 [B,3,H,W] (ImageNet-normalised, = the reference batch["image"]); w [C][3*16]

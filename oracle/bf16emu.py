@@ -410,8 +410,8 @@ class ConvNeXtBf16Emu:
                 G[bp + "mlp.fc1.bias"] = dh.sum(0)
                 wdw = P[bp + "conv_dw.weight"]
                 dzc = dz.permute(0, 3, 1, 2)
-                G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), wdw.shape, dzc, padding=3,
-                                                                       groups=C)
+                G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight((q(x) if self.dw_bf16 else x).permute(0, 3, 1, 2),
+                                                                       wdw.shape, dzc, padding=3, groups=C)
                 G[bp + "conv_dw.bias"] = dz.reshape(M, C).sum(0)
                 d = d + torch.nn.grad.conv2d_input((B, C, H, W), q(wdw) if self.dw_bf16 else wdw, dzc, padding=3,
                                                    groups=C).permute(0, 2, 3, 1)

@@ -73,6 +73,67 @@ __device__ __forceinline__ void to_bf16(const uint4& raw, uint16_t (&o)[16 / siz
   }
 }
 
+// The input tile -> bf16 channel planes [c][row][col] in LDS (plane c at c PS + ((c / EPC) mod 8) SKEW).  Wave wv loads
+// input rows wv, wv + 4, ..: per row NJ instructions of PPI consecutive columns x QPP channel chunks (16 B per lane)
+// through a buffer descriptor over the image, so an out-of-image column reads zeros without a branch.  load() issues
+// every load, store() converts and writes them (the transpose: EPC 2-byte writes per chunk).  The skew puts the fill's
+// lane groups (PPI columns of EPC channels each) on distinct banks instead of PS apart on the same ones (r13h: 11.4 M
+// bank-conflict cycles against 9.2 M active LDS cycles at S1 without it).
+template <typename TIN, int NB, int CG>
+struct XPlanes {
+  using G = Geo<NB, CG>;
+  static constexpr int EPC = 16 / (int)sizeof(TIN);  // channels per 16-B chunk
+  static constexpr int QPP = CG / EPC;               // chunks per pixel
+  static constexpr int PPI = 64 / QPP;               // pixels per wave instruction
+  static constexpr int NJ = (G::IC + PPI - 1) / PPI;
+  static constexpr int NRW = (IR + 3) / 4;
+  static constexpr int SKEW = 2 * PPI;
+  __device__ __forceinline__ static int plane(int c) { return c * G::PS + ((c / EPC) & 7) * SKEW; }
+  uint4 raw[NRW][NJ];
+  __device__ __forceinline__ void load(const TIN* x, const DwmGeo& g, int b, int h0, int w0, int c0, int wvu,
+                                       int lane) {
+    const int fc = lane % PPI, fq = lane / PPI;
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<TIN*>(x + (size_t)b * g.H * g.W * g.C), (short)0,
+                                                      (int)((size_t)g.H * g.W * g.C * sizeof(TIN)), 0x00020000);
+    uint32_t loff[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = j * PPI + fc, ww = w0 - 3 + col;
+      loff[j] = (col < G::TW + 6 && ww >= 0 && ww < g.W) ? (uint32_t)((ww * g.C + c0 + fq * EPC) * (int)sizeof(TIN))
+                                                         : 0x80000000u;
+    }
+#pragma unroll
+    for (int i = 0; i < NRW; ++i) {
+      const int row = wvu + 4 * i, hh = h0 - 3 + row;
+      const bool okr = row < IR && hh >= 0 && hh < g.H;  // wave-uniform
+      const uint32_t ro = okr ? (uint32_t)(hh * g.W * g.C * (int)sizeof(TIN)) : 0u;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, loff[j] + ro, 0, 0);
+        raw[i][j] = okr ? make_uint4(v[0], v[1], v[2], v[3]) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* tin, int wvu, int lane) const {
+    const int fc = lane % PPI, fq = lane / PPI;
+    char* wb = tin + (fq * EPC) * G::PS + (fq & 7) * SKEW + fc * 2;
+#pragma unroll
+    for (int i = 0; i < NRW; ++i) {
+      const int row = wvu + 4 * i;
+      if (row >= IR) break;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (NJ * PPI != G::IC && j * PPI + fc >= G::IC) continue;
+        uint16_t e[EPC];
+        to_bf16<TIN>(raw[i][j], e);
+        char* p = wb + row * G::RS + j * PPI * 2;
+#pragma unroll
+        for (int t = 0; t < EPC; ++t) *reinterpret_cast<uint16_t*>(p + t * G::PS) = e[t];
+      }
+    }
+  }
+};
+
 // MODE 0: z (bf16) = bias + conv(x).  MODE 1: dx (f32) = conv_flipped(dz) [+ bf16 copy].  MODE 2: dx += ...
 template <typename TIN, bool FLIP, int MODE, int NB, int CG>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -91,42 +152,12 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   const int twi = tile % g.tilesW, t2 = tile / g.tilesW, thi = t2 % g.tilesH, b = t2 / g.tilesH;
   const int h0 = thi * TH, w0 = twi * G::TW, c0 = cgi * CG;
 
-  // ---- 1. input tile -> bf16 channel planes.  Wave wv loads input rows wv, wv + 4, ..: per row NJ instructions of PPI
-  //      consecutive columns x QPP channel chunks (16 B per lane) through a buffer descriptor over the image, so an
-  //      out-of-image column reads zeros without a branch; every load first, then every LDS write ----
-  constexpr int EPC = 16 / (int)sizeof(TIN);  // channels per 16-B chunk
-  constexpr int QPP = CG / EPC;               // chunks per pixel
-  constexpr int PPI = 64 / QPP;               // pixels per wave instruction
-  constexpr int NJ = (G::IC + PPI - 1) / PPI;
-  constexpr int NRW = (IR + 3) / 4;
-  // channel plane c starts at c PS + ((c / EPC) mod 8) SKEW: the fill's lane groups (PPI columns of EPC channels each)
-  // then write 16 / 32 B runs on distinct banks instead of PS apart on the same ones (r13h: 11.4 M bank-conflict cycles
-  // against 9.2 M active LDS cycles at S1 without the skew)
-  constexpr int SKEW = 2 * PPI;
+  // ---- 1. input tile -> bf16 channel planes (XPlanes): every load now, the LDS writes after the Toeplitz build ----
+  using XP = XPlanes<TIN, NB, CG>;
+  constexpr int EPC = XP::EPC, SKEW = XP::SKEW;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
-  const int fc = lane % PPI, fq = lane / PPI;
-  const auto rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<TIN*>(x + (size_t)b * g.H * g.W * g.C), (short)0, (int)((size_t)g.H * g.W * g.C * sizeof(TIN)),
-      0x00020000);
-  uint32_t loff[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = j * PPI + fc, ww = w0 - 3 + col;
-    loff[j] = (col < G::TW + 6 && ww >= 0 && ww < g.W) ? (uint32_t)((ww * g.C + c0 + fq * EPC) * (int)sizeof(TIN))
-                                                       : 0x80000000u;
-  }
-  uint4 raw[NRW][NJ];
-#pragma unroll
-  for (int i = 0; i < NRW; ++i) {
-    const int row = wvu + 4 * i, hh = h0 - 3 + row;
-    const bool okr = row < IR && hh >= 0 && hh < g.H;  // wave-uniform
-    const uint32_t ro = okr ? (uint32_t)(hh * g.W * g.C * (int)sizeof(TIN)) : 0u;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, loff[j] + ro, 0, 0);
-      raw[i][j] = okr ? make_uint4(v[0], v[1], v[2], v[3]) : make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
+  XP xp;
+  xp.load(x, g, b, h0, w0, c0, wvu, lane);
   // MODE 2: the accumulated gradient's tile is read now, in flight under the fill and the MFMAs, instead of after them
   // (r13h: the backward's waves waited 72 % of their cycles, the read-back's dx loads exposed at every tile's end)
   constexpr int CH32 = CG / 4;  // 16-B chunks of an f32 pixel
@@ -165,21 +196,7 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
     d[5] = z4;
   }
   for (int i = tid; i < kZeroB / 16; i += kThreads) reinterpret_cast<uint4*>(zreg)[i] = make_uint4(0u, 0u, 0u, 0u);
-  char* wb = tin + (fq * EPC) * G::PS + (fq & 7) * SKEW + fc * 2;
-#pragma unroll
-  for (int i = 0; i < NRW; ++i) {
-    const int row = wvu + 4 * i;
-    if (row >= IR) break;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      if (NJ * PPI != G::IC && j * PPI + fc >= G::IC) continue;
-      uint16_t e[EPC];
-      to_bf16<TIN>(raw[i][j], e);
-      char* p = wb + row * G::RS + j * PPI * 2;
-#pragma unroll
-      for (int t = 0; t < EPC; ++t) *reinterpret_cast<uint16_t*>(p + t * G::PS) = e[t];
-    }
-  }
+  xp.store(tin, wvu, lane);
   __syncthreads();
 
   // ---- 3. MFMAs: lane (n = lane & 15, q = lane >> 4) of the T operand takes taps 8q - n .. +7; lane (m, q) of the
@@ -277,6 +294,163 @@ dw7_mfma_kernel(const TIN* __restrict__ x, const float* __restrict__ wdw, const 
   }
 }
 
+// ---- weight gradient --------------------------------------------------------------------------------------------
+// dW[c][kr][j] = sum_{m,n} dz[m][n] x[m + kr - 3][n + j - 3].  With n' = n + j (the x column, tile-relative) it is a GEMM
+// over the tile's pixels K = (m, n'):
+//     D[kr][j] = sum_K P[kr][K] Q[K][j],   P[kr][(m, n')] = x[m + kr][n'],   Q[(m, n')][j] = dz[m][n' - j]
+// -- the 7 x 7 taps of one channel are one 16 x 16 MFMA accumulator (rows kr, columns j; 49 of 256 used), summed over
+// every pixel of every tile a workgroup visits, so nothing is extracted per tile.  K runs in octs of 8 consecutive
+// columns n' of one row m (one 16-B LDS read of the x plane for P); Q's oct starts j columns earlier in the dz row, a
+// 4-byte-aligned read of one of two parity copies of the zero-padded row (as the forward's Toeplitz windows).  The bias
+// gradient is the tile's plain dz sum, accumulated by the dz fill's threads.  Per workgroup: CG channels, tiles
+// part, part + nparts, .. (16 rows x 16 NB columns each), the next tile's loads in flight under this tile's MFMAs.
+template <int NB, int CG>
+struct WGeo {
+  using G = Geo<NB, CG>;
+  static constexpr int NO = G::IC / 8;              // 8-column octs per x row (n' in [0, IC))
+  static constexpr int NCH = TH * NO / 4;           // K chunks of 32 (4 octs) per tile
+  static constexpr int DZC = G::IC + 8;             // dz row: 8 zero columns, the data, zeros to n' - j <= IC
+  static constexpr int DZR = 2 * DZC * 2;           // bytes per dz row (two parity copies)
+  static constexpr int DZPS = TH * DZR;             // bytes per dz plane
+  static constexpr int DZ_BYTES = CG * DZPS;
+  static constexpr int LDS = G::IN_BYTES + DZ_BYTES;
+  static_assert((TH * NO) % 4 == 0, "whole K chunks");
+};
+
+template <typename TIN, int NB, int CG>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+dw7_wgrad_mfma_kernel(const uint16_t* __restrict__ dz, const TIN* __restrict__ x, float* __restrict__ dw_part,
+                      float* __restrict__ db_part, int nparts, DwmGeo g) {
+  using G = Geo<NB, CG>;
+  using WG = WGeo<NB, CG>;
+  using XP = XPlanes<TIN, NB, CG>;
+  constexpr int CPW = CG / 4, EPC = XP::EPC, SKEW = XP::SKEW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* tin = smem;
+  char* tdz = smem + G::IN_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int ncg = g.C / CG;
+  const int lb = xcd_order(blockIdx.x, gridDim.x);
+  const int cgi = lb % ncg, part = lb / ncg, c0 = cgi * CG;
+  // the dz planes' padding columns stay zero: every tile rewrites only the data columns
+  for (int i = tid; i < WG::DZ_BYTES / 16; i += kThreads) reinterpret_cast<uint4*>(tdz)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  // dz fill: item = (pixel, 8-channel chunk), 16 B per lane; thread tid always holds chunk tid % (CG / 8)
+  constexpr int C8 = CG / 8;
+  constexpr int DZN = TH * G::TW * C8 / kThreads;
+  static_assert((TH * G::TW * C8) % kThreads == 0, "dz fill");
+  const int my_ch = tid % C8;
+  float dbs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const auto rdz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(dz), (short)0, 0x7fffffff, 0x00020000);
+  auto tile_of = [&](int t, int& b, int& h0, int& w0) {
+    const int twi = t % g.tilesW, t2 = t / g.tilesW;
+    b = t2 / g.tilesH;
+    h0 = (t2 % g.tilesH) * TH;
+    w0 = twi * G::TW;
+  };
+  uint4 dzr[DZN];
+  XP xp;
+  auto load_tile = [&](int t) {
+    int b, h0, w0;
+    tile_of(t, b, h0, w0);
+    xp.load(x, g, b, h0, w0, c0, wvu, lane);
+#pragma unroll
+    for (int k = 0; k < DZN; ++k) {
+      const int it = tid + k * kThreads, pix = it / C8, row = pix / G::TW, col = pix - row * G::TW;
+      const int hh = h0 + row, ww = w0 + col;
+      const uint32_t off = hh < g.H && ww < g.W
+                               ? (uint32_t)((((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + my_ch * 8) * 2)
+                               : 0x80000000u;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rdz, off, 0, 0);
+      dzr[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_dz = [&]() {
+#pragma unroll
+    for (int k = 0; k < DZN; ++k) {
+      const int it = tid + k * kThreads, pix = it / C8, row = pix / G::TW, col = pix - row * G::TW;
+      const uint32_t w4[4] = {dzr[k].x, dzr[k].y, dzr[k].z, dzr[k].w};
+      // copy 0 holds padded column col + 8, copy 1 (shifted by one element) col + 7
+      char* p = tdz + (my_ch * 8) * WG::DZPS + row * WG::DZR + (col + 8) * 2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint16_t v = (uint16_t)(w4[e >> 1] >> (16 * (e & 1)));
+        *reinterpret_cast<uint16_t*>(p + e * WG::DZPS) = v;
+        *reinterpret_cast<uint16_t*>(p + e * WG::DZPS + 2 * WG::DZC - 2) = v;
+        dbs[e] += __uint_as_float((uint32_t)v << 16);
+      }
+    }
+  };
+
+  // per-lane operand offsets of every K chunk (the same for every channel and tile): lane (i = lane & 15, q) takes oct
+  // o = 4 chunk + q = (row m, column oct co).  P rows i >= 7 repeat kr = 6 (their D rows are discarded); Q columns
+  // j >= 7 repeat j = 6
+  const int li = lane & 15, q = lane >> 4;
+  const int kr = li < 6 ? li : 6, jj = li < 6 ? li : 6;
+  uint32_t poff[WG::NCH], qoff[WG::NCH];
+  typedef const __attribute__((address_space(3))) char* lds_cptr;
+  const uint32_t pbase = (uint32_t)(size_t)(lds_cptr)(tin + XP::plane(wvu * CPW));
+  const uint32_t qbase = (uint32_t)(size_t)(lds_cptr)(tdz + (wvu * CPW) * WG::DZPS);
+#pragma unroll
+  for (int ch = 0; ch < WG::NCH; ++ch) {
+    const int o = 4 * ch + q, m = o / WG::NO, co = o - m * WG::NO;
+    poff[ch] = pbase + (m + kr) * G::RS + 16 * co;
+    const int sc = 8 * co + 8 - jj;  // padded dz column of the oct's first element
+    qoff[ch] = qbase + m * WG::DZR + (sc & 1) * (2 * WG::DZC) + (sc >> 1) * 4;
+  }
+  f32x4 acc[CPW];
+#pragma unroll
+  for (int t = 0; t < CPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int t = part;
+  if (t < g.ntiles) load_tile(t);
+  for (; t < g.ntiles; t += nparts) {
+    __syncthreads();  // the previous tile's MFMAs are done with the planes
+    xp.store(tin, wvu, lane);
+    store_dz();
+    __syncthreads();
+    if (t + nparts < g.ntiles) load_tile(t + nparts);  // in flight under this tile's MFMAs
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      // the wave's plane offsets are in poff / qoff; channel c of the wave adds c planes (immediate offsets: a wave's
+      // channels start on a skew-group boundary or share one group, so the skew step is c / EPC)
+      static_assert(CPW % EPC == 0 || EPC % CPW == 0, "skew groups");
+      const uint32_t pc = (uint32_t)(c * G::PS + (CPW % EPC == 0 ? (c / EPC) : 0) * SKEW);
+      const uint32_t qc = (uint32_t)(c * WG::DZPS);
+#pragma unroll
+      for (int ch = 0; ch < WG::NCH; ++ch) {
+        typedef const __attribute__((address_space(3))) bf16x8* lds_v8;
+        const bf16x8 pv = *(lds_v8)(size_t)(poff[ch] + pc);
+        const __attribute__((address_space(3))) uint32_t* qp =
+            (const __attribute__((address_space(3))) uint32_t*)(size_t)(qoff[ch] + qc);
+        const uint32_t q4[4] = {qp[0], qp[1], qp[2], qp[3]};
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pv, __builtin_bit_cast(bf16x8, q4), acc[c], 0, 0, 0);
+      }
+    }
+  }
+  // lane (j = lane & 15, q) holds D[4q + r][j] = dW[kr = 4q + r][j] of channel CPW wv + c
+#pragma unroll
+  for (int c = 0; c < CPW; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int krr = 4 * q + r;
+      if (krr < 7 && li < 7) dw_part[(size_t)part * g.C * 49 + (size_t)(c0 + wvu * CPW + c) * 49 + krr * 7 + li] = acc[c][r];
+    }
+  // bias gradient: the dz sums of the threads holding each 8-channel chunk, in thread order through LDS
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [kThreads][8]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = dbs[e];
+  __syncthreads();
+  if (tid < CG) {
+    const int chk = tid / 8, e = tid % 8;
+    float sum = 0.f;
+    for (int u = chk; u < kThreads; u += C8) sum += red[u * 8 + e];
+    db_part[(size_t)part * g.C + c0 + tid] = sum;
+  }
+}
+
 static DwmGeo geo(int B, int H, int W, int C, int tw) {
   DwmGeo g{B, H, W, C, (W + tw - 1) / tw, (H + TH - 1) / TH, 0};
   g.ntiles = B * g.tilesW * g.tilesH;
@@ -308,6 +482,30 @@ static int launch(const void* x, const float* wdw, const float* bdw, void* out, 
   if (cg_choice() == 16 || C % 32 != 0)
     return launch1<TIN, FLIP, MODE, NB, 16>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
   return launch1<TIN, FLIP, MODE, NB, 32>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
+}
+
+constexpr int kWgradCG = 16;  // the weight gradient's channels per workgroup (its dz planes double the LDS)
+
+static int wgrad_nparts(int B, int H, int W, int C) {
+  const int nb = W > 16 ? 2 : 1;
+  const DwmGeo g = geo(B, H, W, C, 16 * nb);
+  const int ncg = C / kWgradCG;
+  int np = 512 / (ncg > 0 ? ncg : 1);  // ~two workgroups per CU over all channel groups
+  if (np > g.ntiles) np = g.ntiles;
+  return np < 1 ? 1 : np;
+}
+
+template <typename TIN, int NB>
+static int launch_wgrad(const uint16_t* dz, const void* x, float* dw_part, float* db_part, int B, int H, int W, int C,
+                        hipStream_t s) {
+  using WG = WGeo<NB, kWgradCG>;
+  const DwmGeo g = geo(B, H, W, C, 16 * NB);
+  const int np = wgrad_nparts(B, H, W, C);
+  const int grid = np * (C / kWgradCG);
+  auto k = &dw7_wgrad_mfma_kernel<TIN, NB, kWgradCG>;
+  if (const int rc = ensure_lds_attr(reinterpret_cast<const void*>(k), WG::LDS, s)) return rc;
+  k<<<grid, kThreads, WG::LDS, s>>>(dz, (const TIN*)x, dw_part, db_part, np, g);
+  return check_launch("sv_dwconv7_bwd_weight_mfma");
 }
 
 }  // namespace dwm
@@ -347,6 +545,26 @@ int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, ui
                : dwm::launch<uint16_t, true, 2, 1>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s);
   return nb2 ? dwm::launch<uint16_t, true, 1, 2>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s)
              : dwm::launch<uint16_t, true, 1, 1>(dz, wdw, nullptr, dx, dx_bf16, B, H, W, C, s);
+}
+
+int sv_dwconv7_bwd_weight_mfma_nparts(int32_t B, int32_t H, int32_t W, int32_t C) {
+  return dwm::wgrad_nparts(B, H, W, C);
+}
+
+int sv_dwconv7_bwd_weight_mfma(const uint16_t* dz, const void* x, int32_t x_dtype, float* dw_part, float* db_part,
+                               int32_t B, int32_t H, int32_t W, int32_t C, sv_stream_t stream) {
+  SV_REQUIRE(dz && x && dw_part && db_part, "sv_dwconv7_bwd_weight_mfma: null pointer");
+  SV_REQUIRE(C % dwm::kWgradCG == 0 && C > 0, "sv_dwconv7_bwd_weight_mfma: C=%d must be a multiple of 16", C);
+  SV_REQUIRE(x_dtype == SV_F32 || x_dtype == SV_BF16, "sv_dwconv7_bwd_weight_mfma: bad x dtype");
+  SV_REQUIRE((size_t)B * H * W * C * 2 < 0x7fffffffull, "sv_dwconv7_bwd_weight_mfma: dz over 2 GiB");
+  if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool nb2 = W > 16;
+  if (x_dtype == SV_F32)
+    return nb2 ? dwm::launch_wgrad<float, 2>(dz, x, dw_part, db_part, B, H, W, C, s)
+               : dwm::launch_wgrad<float, 1>(dz, x, dw_part, db_part, B, H, W, C, s);
+  return nb2 ? dwm::launch_wgrad<uint16_t, 2>(dz, x, dw_part, db_part, B, H, W, C, s)
+             : dwm::launch_wgrad<uint16_t, 1>(dz, x, dw_part, db_part, B, H, W, C, s);
 }
 
 }  // extern "C"

@@ -646,8 +646,8 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
 # The depthwise conv on the matrix cores (csrc/dwmfma.hip, round 6): per channel a banded-Toeplitz GEMM along the image
 # row on v_mfma_f32_16x16x32_bf16, with bf16 operands (the precision torch.autocast gives conv_dw).  Default: the bf16
 # training forward (z kept) and the bf16-dz backward-data run on it (+1.3-1.4 % training step over the f32 VALU kernels,
-# profiles/round6/r13g_*); SV_DW_MFMA=0 keeps the VALU kernels (dwconv.hip), which the f32 parity mode, the tape-free
-# eval forward (one pass with the LayerNorm) and the weight gradient always use.
+# profiles/round6/r13g_*), and the bf16-dz weight gradient; SV_DW_MFMA=0 keeps the VALU kernels (dwconv.hip), which the
+# f32 parity mode and the tape-free eval forward (one pass with the LayerNorm) always use.
 DW_MFMA = os.environ.get("SV_DW_MFMA", "1") != "0"
 
 
@@ -709,13 +709,18 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db, defer: list | None = None):
     B, H, W, C = dz4d.shape
-    P = value("sv_dwconv7_bwd_weight_nparts", B, H, W, C)
+    mfma = DW_MFMA and dz4d.dtype == torch.bfloat16 and C % 16 == 0
+    P = value("sv_dwconv7_bwd_weight_mfma_nparts" if mfma else "sv_dwconv7_bwd_weight_nparts", B, H, W, C)
     pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
     pb = torch.empty(P * C, device=dz4d.device, dtype=torch.float32)
     # algorithmic: dz and x read once, the [C,49] + [C] gradient written (the partials are a design choice)
     nb = B * H * W * C * (dz4d.element_size() + x4d.element_size()) + C * 50 * 4
-    _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
-                B, H, W, C, fma=49.0 * B * H * W * C)
+    if mfma:
+        _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight_mfma", ptr(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
+                    B, H, W, C, flops=98.0 * B * H * W * C)
+    else:
+        _timed_call("dw_wgrad", nb, "sv_dwconv7_bwd_weight", ptr(dz4d), dt(dz4d), ptr(x4d), dt(x4d), ptr(pw), ptr(pb),
+                    B, H, W, C, fma=49.0 * B * H * W * C)
     if defer is not None:
         defer += [(pw, dw, P, True), (pb, db, P, True)]
         return

@@ -130,6 +130,8 @@ _SIGS = {
     "sv_dwconv7_bwd_data": [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_fwd_mfma": [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_data_mfma": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p],
+    "sv_dwconv7_bwd_weight_mfma_nparts": [_i32, _i32, _i32, _i32],
+    "sv_dwconv7_bwd_weight_mfma": [_p, _p, _i32, _p, _p, _i32, _i32, _i32, _i32, _p],
     "sv_dwconv7_bwd_weight_nparts": [_i32, _i32, _i32, _i32],
     "sv_dwconv7_ln_fused_ok": [_i32, _i32, _i32, _i32, _i32, _i32, _i32],
     "sv_diag_group_sum": [_p, _p, _p, _i64, _i32, _p],

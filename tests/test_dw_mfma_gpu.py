@@ -75,3 +75,35 @@ def test_dw_mfma_rejects_bad_channels(dev):
     x, w, b = _operands(dev, (1, 8, 8, 48), seed=1)
     with pytest.raises(Exception):
         K.dwconv7_fwd_mfma(x, w, b)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=IDS)
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16], ids=["xf32", "xbf16"])
+def test_dw_mfma_weight_gradient(dev, shape, xdtype, monkeypatch):
+    """sv_dwconv7_bwd_weight_mfma (through K.dwconv7_bwd_weight, partials folded): the 49 taps and the bias of every
+    channel against a float64 conv2d_weight over bf16(x) and the bf16 dz; bitwise run to run."""
+    monkeypatch.setattr(K, "DW_MFMA", True)
+    B, H, W, C = shape
+    x, _, _ = _operands(dev, shape, seed=11 + sum(shape), xdtype=xdtype)
+    g = torch.Generator().manual_seed(5)
+    dz = (torch.randn(B, H, W, C, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    outs = []
+    for _ in range(2):
+        dw = torch.zeros(C, 49, device=dev)
+        db = torch.zeros(C, device=dev)
+        K.dwconv7_bwd_weight(dz, x, dw=dw, db=db)
+        outs.append((dw, db))
+    ref = torch.nn.grad.conv2d_weight(_q(x).permute(0, 3, 1, 2), (C, 1, 7, 7), dz.double().permute(0, 3, 1, 2),
+                                      padding=3, groups=C).view(C, 49)
+    refb = dz.double().sum((0, 1, 2))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "run to run"
+    dw, db = outs[0]
+    # f32 sums of B H W products (exact bf16 x bf16 products): relative to the sum of |terms| of each tap
+    absref = torch.nn.grad.conv2d_weight(_q(x).abs().permute(0, 3, 1, 2), (C, 1, 7, 7),
+                                         dz.double().abs().permute(0, 3, 1, 2), padding=3, groups=C).view(C, 49)
+    err = (dw.double() - ref).abs()
+    assert not (err > 1e-5 * absref + 1e-12).any(), (float((err / (absref + 1e-30)).max()))
+    errb = (db.double() - refb).abs()
+    assert not (errb > 1e-5 * dz.double().abs().sum((0, 1, 2)) + 1e-12).any()
+    print(f"[dw mfma wgrad] {shape} x {xdtype}: max err / sum|terms| {float((err / (absref + 1e-30)).max()):.2e}")

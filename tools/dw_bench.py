@@ -82,10 +82,11 @@ def main():
                       lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
                                       nv.ptr(bias), 1e-6, nv.ptr(z), nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
                                       nv.ptr(rstd), B, S, S, C)))
-        cases.append(("one-pass f32->bf16 y (eval)", 4 * n + 2 * n,
-                      lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
-                                      nv.ptr(bias), 1e-6, None, nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
-                                      nv.ptr(rstd), B, S, S, C)))
+        if nv.value("sv_dwconv7_ln_fused_ok", B, S, S, C, nv.SV_F32, nv.SV_BF16, nv.SV_BF16):
+            cases.append(("one-pass f32->bf16 y (eval)", 4 * n + 2 * n,
+                          lambda: nv.call("sv_dwconv7_ln_fwd", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(lnw),
+                                          nv.ptr(bias), 1e-6, None, nv.SV_BF16, nv.ptr(y), nv.SV_BF16, nv.ptr(mean),
+                                          nv.ptr(rstd), B, S, S, C)))
         # the matrix-core kernels (csrc/dwmfma.hip, round 6): bf16 operands
         cases.append(("mfma fwd f32->bf16", 6 * n,
                       lambda: nv.call("sv_dwconv7_fwd_mfma", nv.ptr(x), nv.SV_F32, nv.ptr(w), nv.ptr(bias), nv.ptr(z),
@@ -99,6 +100,12 @@ def main():
         cases.append(("mfma bwd_data bf16dz acc+bf16", 2 * n + 4 * n + 4 * n + 2 * n,
                       lambda: nv.call("sv_dwconv7_bwd_data_mfma", nv.ptr(dzb), nv.ptr(w), nv.ptr(dx), nv.ptr(dxb), 1,
                                       B, S, S, C)))
+        Pm = nv.value("sv_dwconv7_bwd_weight_mfma_nparts", B, S, S, C)
+        pwm = torch.empty(Pm * C * 49, device=dev)
+        pbm = torch.empty(Pm * C, device=dev)
+        cases.append(("mfma wgrad bf16dz (kernel only)", 6 * n,
+                      lambda: nv.call("sv_dwconv7_bwd_weight_mfma", nv.ptr(dzb), nv.ptr(x), nv.SV_F32, nv.ptr(pwm),
+                                      nv.ptr(pbm), B, S, S, C)))
         for name, nbytes, fn in cases:
             us = timeit(fn, args.iters)
             print(f"{tag} {st} {name:28s} {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s", flush=True)
