@@ -299,6 +299,8 @@ def _slab_wgrad(A, Bm, split: int, bf16_slabs: bool):
 # partner and the taps to bf16 -- torch.autocast's precision for conv_dw -- where the VALU kernels take f32 x and taps.
 # Same switch and default as spine_vision_amd/kernels.py DW_MFMA (tests/test_bf16emu_cpu.py checks they agree).
 DW_BF16_OPERANDS = os.environ.get("SV_DW_MFMA", "1") != "0"
+# ... and the weight gradient's x, when the product's matrix-core weight gradient is on (SV_DW_MFMA_WGRAD, opt-in)
+DW_BF16_WGRAD = DW_BF16_OPERANDS and os.environ.get("SV_DW_MFMA_WGRAD", "0") != "0"
 
 # the tape keeps the bf16-rounded tensors as bf16 (exact, a quarter of float64's memory); a check that disables the
 # rounding (bf16_round -> identity, test_oracle_golden) must keep them in the working dtype
@@ -315,6 +317,7 @@ class ConvNeXtBf16Emu:
                  device="cpu", dw_bf16: bool | None = None) -> None:
         self.model = model
         self.dw_bf16 = DW_BF16_OPERANDS if dw_bf16 is None else dw_bf16
+        self.dw_bf16_wgrad = self.dw_bf16 and DW_BF16_WGRAD
         self.dtype = dtype
         self.device = torch.device(device)
         self.P = {n: p.detach().to(self.device, dtype).clone() for n, p in model.named_parameters()}
@@ -410,7 +413,7 @@ class ConvNeXtBf16Emu:
                 G[bp + "mlp.fc1.bias"] = dh.sum(0)
                 wdw = P[bp + "conv_dw.weight"]
                 dzc = dz.permute(0, 3, 1, 2)
-                G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight((q(x) if self.dw_bf16 else x).permute(0, 3, 1, 2),
+                G[bp + "conv_dw.weight"] = torch.nn.grad.conv2d_weight((q(x) if self.dw_bf16_wgrad else x).permute(0, 3, 1, 2),
                                                                        wdw.shape, dzc, padding=3, groups=C)
                 G[bp + "conv_dw.bias"] = dz.reshape(M, C).sum(0)
                 d = d + torch.nn.grad.conv2d_input((B, C, H, W), q(wdw) if self.dw_bf16 else wdw, dzc, padding=3,

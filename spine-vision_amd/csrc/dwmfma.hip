@@ -470,16 +470,20 @@ static int launch1(const void* x, const float* wdw, const float* bdw, void* out,
   return check_launch("sv_dwconv7 (mfma)");
 }
 
-// SV_DW_MFMA_CG=16: 16 channels per workgroup (half the LDS, 4 workgroups per CU) instead of 32 (A/B)
-static int cg_choice() {
-  static const int v = getenv("SV_DW_MFMA_CG") ? atoi(getenv("SV_DW_MFMA_CG")) : 32;
-  return v == 16 ? 16 : 32;
+// Channels per workgroup: 16 (40 KiB of LDS, 4 workgroups per CU) or 32 (79 KiB, 2).  Measured (r13l, ConvNeXt-base
+// bs32 standalone): the forward is faster with 16 at every stage (S3 + LayerNorm 35.3 vs 40.9 us, S1 160 vs 168); the
+// backward-data with 16 at C >= 512 (S3 33.3 vs 36.5, S4 19.3 vs 23.8) and with 32 at C = 128 (S1 190 vs 211).
+// SV_DW_MFMA_CG=16 / 32 forces one (A/B).
+static int cg_choice(int mode, int C) {
+  static const int v = getenv("SV_DW_MFMA_CG") ? atoi(getenv("SV_DW_MFMA_CG")) : 0;
+  if (v == 16 || v == 32) return v;
+  return (mode != 0 && C <= 256) ? 32 : 16;
 }
 
 template <typename TIN, bool FLIP, int MODE, int NB>
 static int launch(const void* x, const float* wdw, const float* bdw, void* out, uint16_t* out_bf16, int B, int H,
                   int W, int C, hipStream_t s) {
-  if (cg_choice() == 16 || C % 32 != 0)
+  if (cg_choice(MODE, C) == 16 || C % 32 != 0)
     return launch1<TIN, FLIP, MODE, NB, 16>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
   return launch1<TIN, FLIP, MODE, NB, 32>(x, wdw, bdw, out, out_bf16, B, H, W, C, s);
 }

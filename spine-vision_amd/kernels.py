@@ -646,9 +646,12 @@ def layernorm_bwd(dy2d, x2d, mean, rstd, w, *, dw, db, dx=None, accumulate_dx=Fa
 # The depthwise conv on the matrix cores (csrc/dwmfma.hip, round 6): per channel a banded-Toeplitz GEMM along the image
 # row on v_mfma_f32_16x16x32_bf16, with bf16 operands (the precision torch.autocast gives conv_dw).  Default: the bf16
 # training forward (z kept) and the bf16-dz backward-data run on it (+1.3-1.4 % training step over the f32 VALU kernels,
-# profiles/round6/r13g_*), and the bf16-dz weight gradient; SV_DW_MFMA=0 keeps the VALU kernels (dwconv.hip), which the
-# f32 parity mode and the tape-free eval forward (one pass with the LayerNorm) always use.
+# profiles/round6/r13g_*), and the tape-free eval forward (MFMA + LayerNorm beat the VALU one pass: S3 35.3 vs 44.5 us,
+# r13l); SV_DW_MFMA=0 keeps the VALU kernels (dwconv.hip), which the f32 parity mode always uses.
 DW_MFMA = os.environ.get("SV_DW_MFMA", "1") != "0"
+# the weight gradient on the matrix cores (sv_dwconv7_bwd_weight_mfma): opt-in -- correct, but 20 % slower than the VALU
+# ring kernel standalone and in the step (r13l: S3 39.0 vs 31.9 us; dw_wgrad 3.4-3.8 vs 2.9 ms/step)
+DW_MFMA_WGRAD = DW_MFMA and os.environ.get("SV_DW_MFMA_WGRAD", "0") != "0"
 
 
 def dwconv7_fwd_mfma(x4d, wdw, bdw):
@@ -671,10 +674,10 @@ def dwconv7_ln_fwd(x4d, wdw, bdw, lnw, lnb, *, act_dtype, eps=EPS_LN, save_z=Tru
     bitwise the two-launch result."""
     B, H, W, C = x4d.shape
     _check(C % 64 == 0, "dwconv7: C must be a multiple of 64")
-    if DW_MFMA and save_z and act_dtype == torch.bfloat16:
+    if DW_MFMA and act_dtype == torch.bfloat16:
         z = dwconv7_fwd_mfma(x4d, wdw, bdw)
         y, mean, rstd = layernorm_fwd(z.view(-1, C), lnw, lnb, out_dtype=act_dtype, eps=eps)
-        return z, y, mean, rstd
+        return (z if save_z else None), y, mean, rstd
     act_code = SV_BF16 if act_dtype == torch.bfloat16 else SV_F32
     if not save_z and value("sv_dwconv7_ln_fused_ok", B, H, W, C, dt(x4d), act_code, act_code):
         z = None
@@ -709,7 +712,7 @@ def dwconv7_bwd_data(dz4d, wdw, dx4d, accumulate=True, dx_bf16=None):
 
 def dwconv7_bwd_weight(dz4d, x4d, *, dw, db, defer: list | None = None):
     B, H, W, C = dz4d.shape
-    mfma = DW_MFMA and dz4d.dtype == torch.bfloat16 and C % 16 == 0
+    mfma = DW_MFMA_WGRAD and dz4d.dtype == torch.bfloat16 and C % 16 == 0
     P = value("sv_dwconv7_bwd_weight_mfma_nparts" if mfma else "sv_dwconv7_bwd_weight_nparts", B, H, W, C)
     pw = torch.empty(P * C * 49, device=dz4d.device, dtype=torch.float32)
     pb = torch.empty(P * C, device=dz4d.device, dtype=torch.float32)

@@ -88,4 +88,4 @@ def test_emulation_follows_the_depthwise_operand_precision():
     from oracle import bf16emu
     from spine_vision_amd import kernels as K
 
-    assert bf16emu.DW_BF16_OPERANDS == K.DW_MFMA
+    assert bf16emu.DW_BF16_OPERANDS == K.DW_MFMA and bf16emu.DW_BF16_WGRAD == K.DW_MFMA_WGRAD

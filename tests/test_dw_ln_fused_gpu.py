@@ -72,7 +72,7 @@ def test_dw_ln_fused_matches_two_launches(dev, tmp_path, monkeypatch):
         refs.append([t.cpu() for t in (z, y, m, rs, y, m, rs)])
     # the one pass with z kept (forced), in a child process
     out_file = tmp_path / "one_pass.pt"
-    env = dict(os.environ, SV_DW_LN_FUSED="1")
+    env = dict(os.environ, SV_DW_LN_FUSED="1", SV_DW_MFMA="0")
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, repr(CASES), str(out_file)], env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -83,8 +83,9 @@ def test_dw_ln_fused_matches_two_launches(dev, tmp_path, monkeypatch):
                                                          float((a.float().reshape(e.shape) - e.float()).abs().max()))
 
 
-def test_dw_ln_unfused_widths_keep_z(dev):
-    """C = 64 / 1024 (not the one-pass form) still write z even when the caller keeps none."""
+def test_dw_ln_unfused_widths_keep_z(dev, monkeypatch):
+    """VALU kernels: C = 64 / 1024 (not the one-pass form) still write z even when the caller keeps none."""
+    monkeypatch.setattr(K, "DW_MFMA", False)
     for C in (64, 1024):
         x, w, b, lw, lb = _inputs(7, 1, 8, 8, C)
         assert K.value("sv_dwconv7_ln_fused_ok", 1, 8, 8, C, nv.SV_F32, nv.SV_BF16, nv.SV_BF16) == 0
