@@ -82,7 +82,7 @@ def test_dw_mfma_rejects_bad_channels(dev):
 def test_dw_mfma_weight_gradient(dev, shape, xdtype, monkeypatch):
     """sv_dwconv7_bwd_weight_mfma (through K.dwconv7_bwd_weight, partials folded): the 49 taps and the bias of every
     channel against a float64 conv2d_weight over bf16(x) and the bf16 dz; bitwise run to run."""
-    monkeypatch.setattr(K, "DW_MFMA", True)
+    monkeypatch.setattr(K, "DW_MFMA_WGRAD", True)  # opt-in in the product (slower than the VALU kernel, DESIGN)
     B, H, W, C = shape
     x, _, _ = _operands(dev, shape, seed=11 + sum(shape), xdtype=xdtype)
     g = torch.Generator().manual_seed(5)
