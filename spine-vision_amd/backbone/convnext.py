@@ -609,6 +609,11 @@ class ConvNeXtHip(nn.Module):
                                                 db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
         side.wait_event(main.record_event())
+        # the main stream's next launch is enqueued first: the depthwise backward-data needs only dz, and the host's
+        # side-stream enqueues below left the main queue idle ~18 us per block before it (r13n trace, queue_gaps.py).
+        # The side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
+        db = torch.empty_like(db)
+        K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
         side_cap = pol.grid_cap
         if self.side_grid_cap is not None:
             side_cap = min(self.side_grid_cap, side_cap) if side_cap > 0 else self.side_grid_cap
@@ -643,9 +648,6 @@ class ConvNeXtHip(nn.Module):
                 self._ready([blk.conv_dw.weight, blk.conv_dw.bias, blk.norm.weight, blk.norm.bias,
                              blk.mlp.fc1.weight, blk.mlp.fc1.bias])
             tail.append(job)
-        # the side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer
-        db = torch.empty_like(db)
-        K.dwconv7_bwd_data(dz4, blk.conv_dw.weight, d, accumulate=True, dx_bf16=db)
         return d, db
 
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 6: the depthwise backward-data enqueued before the block's side-stream work (host order only): the schedule
+# and parity tests that pin the lean backward bitwise, the training line twice, the trace's main-queue gaps again
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+ROOTDIR=$(pwd)
+N=${1:-r13o}
+O=$ROOTDIR/gpurun_out/$N
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_parity_geometry_gpu.py tests/test_ddp_gpu.py > $O/tests.log 2>&1 || { grep -E "FAIL|Error|assert" $O/tests.log | head -20; tail -20 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$i.json 2> $O/bench_$i.err || { tail -5 $O/bench_$i.err; exit 1; }
+  python -c "import json; d=json.loads(open('$O/bench_$i.json').read().strip().splitlines()[-1]); print('train', d['value'], d['ms_per_step'], d['main_queue'])"
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/prof" -o run -- python3 "$ROOTDIR/bench.py" --steps 3 --warmup 2 --no-cpu-baseline > "$O/prof_bench.json" 2> "$O/prof.err" || { tail -20 "$O/prof.err"; exit 1; }
+cd "$ROOTDIR"
+KT=$(find $O/prof -name "*kernel_trace.csv" | head -1)
+python tools/queue_gaps.py $KT 15 > $O/gaps.txt; tail -16 $O/gaps.txt
+gzip -f $KT
