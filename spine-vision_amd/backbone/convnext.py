@@ -608,7 +608,7 @@ class ConvNeXtHip(nn.Module):
                 dz, ln_finish = K.layernorm_bwd(dy, z.view(M, C), mean, rstd, blk.norm.weight, dw=g(blk.norm.weight),
                                                 db=g(blk.norm.bias), out_dtype=torch.bfloat16, defer_reduce=True)
         dz4 = dz.view(B, H, W, C)
-        side.wait_event(main.record_event())
+        nv.handoff(main, side)
         # the main stream's next launch is enqueued first: the depthwise backward-data needs only dz, and the host's
         # side-stream enqueues below left the main queue idle ~18 us per block before it (r13n trace, queue_gaps.py).
         # The side stream still reads dsrc (this block's bf16 gradient copy): the next copy gets a fresh buffer

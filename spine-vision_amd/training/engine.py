@@ -141,6 +141,10 @@ class StepEngine:
                 if hasattr(m, "comm_reserve_cus"):
                     m.comm_reserve_cus = self.comm_reserve_cus
                     m.comm_cu_mask = mask
+        # SV_MAIN_STREAM_PRIO=1 (A/B): the step on a high-priority stream, so that when CUs free up the critical path's
+        # next kernel is dispatched before the weight-gradient side stream's queued workgroups
+        if self._stream is None and self.device.type == "cuda" and os.environ.get("SV_MAIN_STREAM_PRIO", "0") != "0":
+            self._stream = torch.cuda.Stream(self.device, priority=-1)
         if distributed:
             broadcast_parameters(self.arena, model)
             self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb)
