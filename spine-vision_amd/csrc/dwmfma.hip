@@ -525,6 +525,8 @@ int sv_dwconv7_fwd_mfma(const void* x, int32_t x_dtype, const float* wdw, const 
   SV_REQUIRE(C % dwm::kCGMin == 0 && C > 0, "sv_dwconv7_fwd_mfma: C=%d must be a multiple of 16", C);
   SV_REQUIRE(x_dtype == SV_F32 || x_dtype == SV_BF16, "sv_dwconv7_fwd_mfma: bad x dtype");
   SV_REQUIRE(x != (const void*)z, "sv_dwconv7_fwd_mfma: x and z must not alias");
+  SV_REQUIRE((size_t)H * W * C * (x_dtype == SV_F32 ? 4 : 2) < 0x7fffffffull,
+             "sv_dwconv7_fwd_mfma: one image of x over 2 GiB (buffer-descriptor range)");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const bool nb2 = W > 16;
@@ -541,6 +543,7 @@ int sv_dwconv7_bwd_data_mfma(const uint16_t* dz, const float* wdw, float* dx, ui
   SV_REQUIRE(C % dwm::kCGMin == 0 && C > 0, "sv_dwconv7_bwd_data_mfma: C=%d must be a multiple of 16", C);
   SV_REQUIRE((const void*)dz != (const void*)dx && (const void*)dz != (const void*)dx_bf16,
              "sv_dwconv7_bwd_data_mfma: dz must not alias dx / dx_bf16");
+  SV_REQUIRE((size_t)H * W * C * 2 < 0x7fffffffull, "sv_dwconv7_bwd_data_mfma: one image of dz over 2 GiB");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const bool nb2 = W > 16;
@@ -560,7 +563,8 @@ int sv_dwconv7_bwd_weight_mfma(const uint16_t* dz, const void* x, int32_t x_dtyp
   SV_REQUIRE(dz && x && dw_part && db_part, "sv_dwconv7_bwd_weight_mfma: null pointer");
   SV_REQUIRE(C % dwm::kWgradCG == 0 && C > 0, "sv_dwconv7_bwd_weight_mfma: C=%d must be a multiple of 16", C);
   SV_REQUIRE(x_dtype == SV_F32 || x_dtype == SV_BF16, "sv_dwconv7_bwd_weight_mfma: bad x dtype");
-  SV_REQUIRE((size_t)B * H * W * C * 2 < 0x7fffffffull, "sv_dwconv7_bwd_weight_mfma: dz over 2 GiB");
+  SV_REQUIRE((size_t)B * H * W * C * 2 < 0x7fffffffull && (size_t)H * W * C * 4 < 0x7fffffffull,
+             "sv_dwconv7_bwd_weight_mfma: dz over 2 GiB / one image of x over 2 GiB");
   if (B <= 0 || H <= 0 || W <= 0) return SV_OK;
   hipStream_t s = (hipStream_t)stream;
   const bool nb2 = W > 16;
