@@ -336,14 +336,11 @@ dw7_wgrad_mfma_kernel(const uint16_t* __restrict__ dz, const TIN* __restrict__ x
   // the dz planes' padding columns stay zero: every tile rewrites only the data columns
   for (int i = tid; i < WG::DZ_BYTES / 16; i += kThreads) reinterpret_cast<uint4*>(tdz)[i] = make_uint4(0u, 0u, 0u, 0u);
 
-  // dz fill: item = (pixel, 8-channel chunk), 16 B per lane.  A 32-lane half takes 32 consecutive pixels of one chunk
-  // (its 2-byte LDS writes land in 16 consecutive dwords: no bank conflict across the chunk planes, r13r); thread tid
-  // always holds chunk (tid / 32) % C8
+  // dz fill: item = (pixel, 8-channel chunk), 16 B per lane; thread tid always holds chunk tid % (CG / 8)
   constexpr int C8 = CG / 8;
   constexpr int DZN = TH * G::TW * C8 / kThreads;
   static_assert((TH * G::TW * C8) % kThreads == 0, "dz fill");
-  const int my_ch = (tid >> 5) % C8;
-  auto dz_pix = [&](int it) { return (it / (32 * C8)) * 32 + (it & 31); };
+  const int my_ch = tid % C8;
   float dbs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const auto rdz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(dz), (short)0, 0x7fffffff, 0x00020000);
   auto tile_of = [&](int t, int& b, int& h0, int& w0) {
@@ -360,7 +357,7 @@ dw7_wgrad_mfma_kernel(const uint16_t* __restrict__ dz, const TIN* __restrict__ x
     xp.load(x, g, b, h0, w0, c0, wvu, lane);
 #pragma unroll
     for (int k = 0; k < DZN; ++k) {
-      const int it = tid + k * kThreads, pix = dz_pix(it), row = pix / G::TW, col = pix - row * G::TW;
+      const int it = tid + k * kThreads, pix = it / C8, row = pix / G::TW, col = pix - row * G::TW;
       const int hh = h0 + row, ww = w0 + col;
       const uint32_t off = hh < g.H && ww < g.W
                                ? (uint32_t)((((size_t)(b * g.H + hh) * g.W + ww) * g.C + c0 + my_ch * 8) * 2)
@@ -372,7 +369,7 @@ dw7_wgrad_mfma_kernel(const uint16_t* __restrict__ dz, const TIN* __restrict__ x
   auto store_dz = [&]() {
 #pragma unroll
     for (int k = 0; k < DZN; ++k) {
-      const int it = tid + k * kThreads, pix = dz_pix(it), row = pix / G::TW, col = pix - row * G::TW;
+      const int it = tid + k * kThreads, pix = it / C8, row = pix / G::TW, col = pix - row * G::TW;
       const uint32_t w4[4] = {dzr[k].x, dzr[k].y, dzr[k].z, dzr[k].w};
       // copy 0 holds padded column col + 8, copy 1 (shifted by one element) col + 7
       char* p = tdz + (my_ch * 8) * WG::DZPS + row * WG::DZR + (col + 8) * 2;
@@ -449,8 +446,7 @@ dw7_wgrad_mfma_kernel(const uint16_t* __restrict__ dz, const TIN* __restrict__ x
   if (tid < CG) {
     const int chk = tid / 8, e = tid % 8;
     float sum = 0.f;
-    for (int u = 0; u < kThreads; ++u)
-      if (((u >> 5) % C8) == chk) sum += red[u * 8 + e];
+    for (int u = chk; u < kThreads; u += C8) sum += red[u * 8 + e];
     db_part[(size_t)part * g.C + c0 + tid] = sum;
   }
 }
