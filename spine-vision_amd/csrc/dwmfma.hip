@@ -1,5 +1,6 @@
-// Depthwise 7x7 convolution (pad 3, stride 1, NHWC) on the matrix cores -- ConvNeXtBlock.conv_dw forward and its
-// backward-data (timm convnext.py via spine_vision/training/models/backbone.py:50; round 6).
+// Depthwise 7x7 convolution (pad 3, stride 1, NHWC) on the matrix cores -- ConvNeXtBlock.conv_dw forward, its
+// backward-data and (opt-in) its weight gradient (timm convnext.py via spine_vision/training/models/backbone.py:50;
+// round 6).
 //
 // A depthwise conv has no GEMM across channels: every channel has its own 7x7 filter.  What a channel does have is a
 // GEMM along the image ROW: for kernel row kr, the 16 outputs (row m, columns n0 .. n0+15) take
@@ -12,11 +13,12 @@
 //
 // Operands are bf16 (the precision torch.autocast gives conv_dw), products exact, sums in f32 by the MFMA.
 //
-// Workgroup = 4 waves = one image tile of 16 output rows x 16 NB output columns x 32 channels (8 per wave):
-//   1. the 22 x (16 NB + 6) input pixels x 32 channels are read from HBM (16 B per lane, full 128-B / 64-B channel
-//      segments), rounded to bf16 and TRANSPOSED into channel planes [c][row][col] in LDS (the MFMA operand wants 8
-//      consecutive columns of one channel per lane; NHWC holds 8 consecutive channels of one column);
-//   2. the 32 x 7 Toeplitz rows are built once per workgroup as zero-padded tap windows [c][kr][2 parities][24 bf16]:
+// Workgroup = 4 waves = one image tile of 16 output rows x 16 NB output columns x CG channels (CG = 16 or 32, CG / 4
+// per wave; the host picks per pass, launch() below):
+//   1. the 22 x (16 NB + 6) input pixels x CG channels are read from HBM (16 B per lane, 32-128-B channel segments),
+//      rounded to bf16 and TRANSPOSED into channel planes [c][row][col] in LDS (the MFMA operand wants 8 consecutive
+//      columns of one channel per lane; NHWC holds 8 consecutive channels of one column);
+//   2. the CG x 7 Toeplitz rows are built once per workgroup as zero-padded tap windows [c][kr][2 parities][24 bf16]:
 //      lane (n, q) of the T operand needs taps 8q - n .. 8q - n + 7, a 4-byte-aligned 16-byte read of one parity copy;
 //   3. per channel: 7 T operands (28 VGPRs), then per 16-column block 7 MFMAs over LDS reads of the data operand;
 //   4. the accumulators (lane: 4 consecutive output columns of one output row, one channel) are staged through LDS as
