@@ -116,39 +116,21 @@ struct XPlanes {
       }
     }
   }
-  // Column pairs: lanes 2i, 2i + 1 hold columns 2i, 2i + 1 (same channels).  They swap half their channels (one DPP
-  // quad permutation per dword), then the even lane writes channels [0, EPC/2) and the odd lane [EPC/2, EPC) as one
-  // dword per channel holding both columns: half the LDS writes of one 2-byte write per element, and no two lanes
-  // writing halves of one dword.
   __device__ __forceinline__ void store(char* tin, int wvu, int lane) const {
-    static_assert(PPI % 2 == 0 && G::IC % 2 == 0, "column pairs");
-    constexpr int HC = EPC / 2;
     const int fc = lane % PPI, fq = lane / PPI;
-    const bool odd = fc & 1;
-    char* wb = tin + (fq * EPC + (odd ? HC : 0)) * G::PS + (fq & 7) * SKEW + (fc & ~1) * 2;
+    char* wb = tin + (fq * EPC) * G::PS + (fq & 7) * SKEW + fc * 2;
 #pragma unroll
     for (int i = 0; i < NRW; ++i) {
       const int row = wvu + 4 * i;
       if (row >= IR) break;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
+        if (NJ * PPI != G::IC && j * PPI + fc >= G::IC) continue;
         uint16_t e[EPC];
         to_bf16<TIN>(raw[i][j], e);
-        uint32_t rcv[HC / 2];
-#pragma unroll
-        for (int k = 0; k < HC / 2; ++k) {
-          const int t0 = (odd ? 0 : HC) + 2 * k;  // the channels the partner keeps
-          const uint32_t snd = (uint32_t)e[t0] | ((uint32_t)e[t0 + 1] << 16);
-          rcv[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd, 0xb1, 0xf, 0xf, false);  // lane ^ 1
-        }
-        if (NJ * PPI != G::IC && j * PPI + fc >= G::IC) continue;  // both lanes of a pair (IC even)
         char* p = wb + row * G::RS + j * PPI * 2;
 #pragma unroll
-        for (int t = 0; t < HC; ++t) {
-          const uint32_t mine = e[(odd ? HC : 0) + t];
-          const uint32_t other = (rcv[t >> 1] >> (16 * (t & 1))) & 0xffffu;
-          *reinterpret_cast<uint32_t*>(p + t * G::PS) = odd ? (other | (mine << 16)) : (mine | (other << 16));
-        }
+        for (int t = 0; t < EPC; ++t) *reinterpret_cast<uint16_t*>(p + t * G::PS) = e[t];
       }
     }
   }
