@@ -182,7 +182,14 @@ class ConvNeXtHip(nn.Module):
         # (x GELU'), the fc1 data gradient and the LayerNorm backward as ONE kernel (sv_mlp_bwd): dh is not read back and
         # dy never reaches HBM (SV_FUSED_MLP_BWD=0: the three kernels, A/B runs)
         self.fused_mlp_bwd = os.environ.get("SV_FUSED_MLP_BWD", "1") != "0"
+        # StepEngine(overlap_optimizer=True) installs a training.engine.ParamGate: the forward then waits for each
+        # stage's chunk of the previous step's AdamW just before the stage instead of for the whole update
+        self.param_gate = None
         self._init_weights()
+
+    def param_gate_groups(self) -> list[nn.Module]:
+        """The parameter groups in forward (and arena) order, one optimizer chunk each (training.engine.ParamGate)."""
+        return [self.stem, *self.stages, self.head]
 
     # -- timm-style init (ConvNeXt._init_weights): trunc_normal(.02) for conv/linear, zero bias
     def _init_weights(self) -> None:
@@ -252,6 +259,9 @@ class ConvNeXtHip(nn.Module):
         tape = _Tape(img=img) if save else None
         cache: dict = tape.wcache if save else {}
         stem_conv, stem_ln = self.stem[0], self.stem[1]
+        gate = self.param_gate
+        if gate is not None:
+            gate.wait(self.stem)
         if save and bf and self.overlap_wgrad:
             # the fc2 dgrad operand bf16(W2 * gamma) of every block, made on the (otherwise idle during
             # the forward) side stream beside the forward; the backward waits on one event
@@ -269,6 +279,8 @@ class ConvNeXtHip(nn.Module):
                 else:
                     tape.w2g[id(blk)] = torch.empty(blk.mlp.fc2.weight.shape, device=img.device, dtype=torch.bfloat16)
             side.wait_event(main.record_event())
+            if gate is not None:  # every block's weights: the whole update
+                gate.wait_all(side)
             with torch.cuda.stream(side):
                 for blk in blocks:
                     if id(blk) in fused_b:
@@ -295,6 +307,8 @@ class ConvNeXtHip(nn.Module):
             if save:
                 tape.stem = (s_mean, s_rstd)
         for st in self.stages:
+            if gate is not None:
+                gate.wait(st)
             ds_saved = None
             if not isinstance(st.downsample, nn.Identity):
                 ln, conv = st.downsample[0], st.downsample[1]
@@ -346,6 +360,8 @@ class ConvNeXtHip(nn.Module):
                 x = xo
             if save:
                 tape.stages.append((ds_saved, blocks_saved))
+        if gate is not None:  # the head norm here, the model's heads after the return
+            gate.wait_all()
         feat, pooled, p_mean, p_rstd = K.pool_ln_fwd(x, self.head.norm.weight, self.head.norm.bias)
         if save:
             tape.pool = (pooled, p_mean, p_rstd)

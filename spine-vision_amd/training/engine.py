@@ -52,6 +52,46 @@ class InflightLimiter:
             self._events.popleft().synchronize()
 
 
+class ParamGate:
+    """Where a forward may start while the previous step's AdamW still runs (StepEngine(overlap_optimizer=True)).
+
+    The optimizer updates the flat arena in chunks on its own stream -- one chunk per group of the backbone's
+    ``param_gate_groups()`` (stem, stages, in forward order and arena order), the rest (the model's heads) last -- and
+    records an event after each.  The backbone calls ``wait(module)`` before it reads a group's parameters (or their
+    bf16 shadow) and ``wait_all()`` before returning, so the heads' reads follow every chunk.  With no optimizer in
+    flight both are no-ops."""
+
+    def __init__(self, arena: FlatArena, groups: list) -> None:
+        end = {id(p): o + p.numel() for p, o in zip(arena.params, arena.offsets)}
+        self.bounds: list[int] = []
+        self._chunk: dict[int, int] = {}
+        for g in groups:
+            ends = [end[id(p)] for p in g.parameters() if id(p) in end]
+            if not ends:
+                continue
+            b = max(ends)
+            if self.bounds and b <= self.bounds[-1]:
+                raise ValueError("ParamGate: groups out of arena order")
+            self.bounds.append(b)
+        if not self.bounds or self.bounds[-1] < arena.numel:
+            self.bounds.append(arena.numel)
+        for g in groups:
+            ends = [end[id(p)] for p in g.parameters() if id(p) in end]
+            if ends:
+                self._chunk[id(g)] = next(i for i, b in enumerate(self.bounds) if b >= max(ends))
+        self.events: list | None = None
+
+    def wait(self, module: torch.nn.Module, stream: torch.cuda.Stream | None = None) -> None:
+        if self.events is None:
+            return
+        k = self._chunk.get(id(module), len(self.events) - 1)
+        (stream or torch.cuda.current_stream()).wait_event(self.events[k])
+
+    def wait_all(self, stream: torch.cuda.Stream | None = None) -> None:
+        if self.events is not None:
+            (stream or torch.cuda.current_stream()).wait_event(self.events[-1])
+
+
 class _Graphed:
     """One captured training step: static inputs, the HIP graph, its loss output and the device AdamW
     scalars [runs][4] refilled before each replay from a small ring of pinned host buffers."""
@@ -99,7 +139,8 @@ class StepEngine:
     def __init__(self, model: torch.nn.Module, device: torch.device | str, *, lr: float = 1e-4,
                  weight_decay: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  grad_clip: float | None = 1.0, distributed: bool | None = None, bucket_mb: float = 64.0,
-                 cuda_graph: bool = False, comm_reserve_cus: int | None = None) -> None:
+                 cuda_graph: bool = False, comm_reserve_cus: int | None = None,
+                 overlap_optimizer: bool | None = None) -> None:
         # a backbone whose backward queries events (ConvNeXt's lean side-stream release) declares
         # graph_safe = False and cannot be captured: asking for it is an error, not a silent fallback.
         if cuda_graph:
@@ -159,6 +200,26 @@ class StepEngine:
         self.cuda_graph = bool(cuda_graph) and not distributed and self.device.type == "cuda"
         self._graphs: dict = {}
         self._warm: set = set()
+        # overlap_optimizer: AdamW runs on its own stream in backbone-stage chunks, and the next step's forward starts
+        # each stage once that stage's chunk is done (ParamGate) instead of after the whole update; the next step's
+        # gradient zeroing follows the update on that stream and the backward waits for it.  Same arithmetic, same
+        # bits.  Parameters read between steps outside the backbone's forward need sync_params() first.  Only for a
+        # model whose one gate-aware backbone (param_gate_groups) leads the arena; SV_OPT_OVERLAP=1 turns it on.
+        if overlap_optimizer is None:
+            overlap_optimizer = os.environ.get("SV_OPT_OVERLAP", "0") != "0"
+        self.gate: ParamGate | None = None
+        self._opt_stream = None
+        self._opt_pending = False
+        self._opt_keep = None
+        if overlap_optimizer and self.device.type == "cuda" and not self.cuda_graph:
+            gated = [m for m in model.modules() if hasattr(m, "param_gate_groups")]
+            if len(gated) == 1:
+                bb = gated[0]
+                first = next((p for p in bb.parameters()), None)
+                if first is not None and self.arena.offsets[self.arena.index_of(first)] == 0:
+                    self.gate = ParamGate(self.arena, bb.param_gate_groups())
+                    bb.param_gate = self.gate
+                    self._opt_stream = torch.cuda.Stream(self.device)
 
     def step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
         """Run one optimisation step; returns the (device) loss tensor."""
@@ -172,22 +233,46 @@ class StepEngine:
         cur.wait_stream(self._stream)
         return loss
 
+    def sync_params(self, stream: torch.cuda.Stream | None = None) -> None:
+        """Order ``stream`` (default: the current one) after an optimizer update still running on the overlap
+        stream -- before reading parameters, their gradients or the AdamW state outside the backbone's forward."""
+        if self._opt_pending:
+            (stream or torch.cuda.current_stream(self.device)).wait_stream(self._opt_stream)
+
     def _step(self, loss_fn: Callable[[torch.nn.Module], torch.Tensor]) -> torch.Tensor:
-        self.optimizer.zero_grad()
+        zero_ev = None
+        if self._opt_pending:
+            # the previous update still reads the gradients: zero them after it, on its stream
+            with torch.cuda.stream(self._opt_stream):
+                self.optimizer.zero_grad()
+            zero_ev = self._opt_stream.record_event()
+        else:
+            self.optimizer.zero_grad()
         if self.buffer_sync is not None:
             self.buffer_sync.sync()
-        loss = loss_fn(self.model)
+        loss = loss_fn(self.model)  # the backbone waits for each stage's chunk of the previous update (ParamGate)
+        if zero_ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(zero_ev)
+            self._opt_pending = False
+            self.gate.events = None
         loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
         if self.after_backward is not None:
             self.after_backward()
         scale = None
+        nc = None
         if self.grad_clip:
             nc = K.grad_clip_coef(self.arena.grad_flat, self.grad_clip)
             self.last_grad_norm = nc[0:1]
             scale = nc[1:2]
-        self.optimizer.step(grad_scale=scale)
+        if self.gate is not None:
+            self._opt_stream.wait_stream(torch.cuda.current_stream(self.device))
+            self.gate.events = self.optimizer.step_chunked(self.gate.bounds, self._opt_stream, grad_scale=scale)
+            self._opt_keep = nc  # read on the overlap stream: alive until the next step has waited for it
+            self._opt_pending = True
+        else:
+            self.optimizer.step(grad_scale=scale)
         if self.limiter is not None:
             self.limiter.step_done()
         return loss.detach()

@@ -51,6 +51,32 @@ class FlatAdamW(torch.optim.Optimizer):
                          step=st, grad_scale=grad_scale)
         return loss
 
+    @torch.no_grad()
+    def step_chunked(self, bounds: list[int], stream: torch.cuda.Stream,
+                     grad_scale: torch.Tensor | None = None) -> list[torch.cuda.Event]:
+        """step() on ``stream`` in arena chunks [0, bounds[0]), [bounds[0], bounds[1]), ... (bounds ascending, the
+        last = arena.numel): the same per-element update (bitwise step()'s), one event recorded after each chunk, so
+        that a forward can start on a stage as soon as that stage's chunk is done (StepEngine(overlap_optimizer))."""
+        group = self.param_groups[0]
+        a = self.arena
+        shadow = a.shadow_flat
+        runs = self._runs()
+        events = []
+        lo = 0
+        with torch.cuda.stream(stream):
+            for hi in bounds:
+                for s, e, st in runs:
+                    s_, e_ = max(s, lo), min(e, hi)
+                    if s_ >= e_:
+                        continue
+                    K.adamw_flat(a.param_flat[s_:e_], a.grad_flat[s_:e_], self.exp_avg[s_:e_], self.exp_avg_sq[s_:e_],
+                                 shadow[s_:e_] if shadow is not None else None, lr=group["lr"],
+                                 beta1=group["betas"][0], beta2=group["betas"][1], eps=group["eps"],
+                                 weight_decay=group["weight_decay"], step=st, grad_scale=grad_scale)
+                events.append(stream.record_event())
+                lo = hi
+        return events
+
     def _runs(self) -> list[tuple[int, int, int]]:
         """Advance the step count of every trainable parameter and return the maximal contiguous
         [start, end) ranges of trainable parameters that share a (new) step count."""
