@@ -279,6 +279,31 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def classification_line(args) -> dict:
+    """BASELINE configs[3] per GPU (ResNet-50 3-head classification 256x256, bs32) beside the headline line, so the
+    driver's own N=1 run times it too (VERDICT r5 missing 5).  A child process of this script (never an exec), run
+    after the headline's timed region; its JSON line is condensed here.  SV_BENCH_CLS=0 skips it."""
+    steps, warmup = max(args.steps, 20), max(args.warmup, 5)
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "classification", "--steps", str(steps),
+           "--warmup", str(warmup), "--no-cpu-baseline", "--precision", args.precision]
+    env = dict(os.environ, SV_BENCH_CLS="0")
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s"}
+    wall = time.perf_counter() - t0
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-800:]}
+    d = json.loads(lines[-1])
+    return {"metric": d["metric"], "value": d["value"], "unit": d["unit"], "n_gpus": 1, "steps": d["steps"],
+            "warmup": d["warmup"], "ms_per_step": d["ms_per_step"], "dtype": d["dtype"], "config": d["config"],
+            "step_mfma_frac": d["roofline"].get("step_mfma_frac"), "main_queue": d.get("main_queue"),
+            "loss": d.get("loss"), "child_wall_s": round(wall, 1),
+            "baseline_config": "BASELINE.json configs[3] (ResNet50 multi-task classification 256x256), per GPU"}
+
+
 def selftest(args, world: int, rank: int) -> None:
     """--selftest: the multi-rank plumbing of this script on CPU (gloo) -- launcher, rank env, the flat
     bucketed all-reduce and the max-over-ranks timing -- on a small torch model.  Not a measurement."""
@@ -800,6 +825,9 @@ def main():
                                  latency_samples_ms=samples[0], hbm_gbs=HBM_SUSTAINED_GBS) for bw in (200.0, 300.0, 400.0)]
     if world > 1:
         result["config"]["comm_reserve_cus"] = engine.comm_reserve_cus
+    if (rank == 0 and world == 1 and not cls and not args.inference and args.backbone == "convnext_base"
+            and os.environ.get("SV_BENCH_CLS", "1") != "0"):
+        result["configs3_classification"] = classification_line(args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
         if not cls and not args.inference:

@@ -589,10 +589,15 @@ static int launch(const uint16_t* y, const uint16_t* w1, const float* b1, const 
 // (w2t = (W2 gamma)^T [512][128] in W1's layout, w1t = W1^T [128][512] in W2's), GELU'(h) is loaded a chunk ahead,
 // z / mean / rstd a chunk ahead of the epilogue.  dh and bf16(dy) are bit for bit the unfused GEMMs' (same MFMA,
 // operands and k order); dz and the partial sums differ from sv_layernorm_bwd only by f32 summation order.
-// SV_MLPB_XLANE=1: the LayerNorm epilogue's butterflies from the cross-lane unit (common.h xlane_xor) instead of
-// ds_bpermute -- opt-in A/B build; round 5 measured that form non-deterministic run to run (DESIGN "Round 6")
+// SV_MLPB_XLANE=3: the LayerNorm epilogue's butterflies from the cross-lane unit (common.h xlane_xor) instead of
+// ds_bpermute -- opt-in A/B build; round 5 measured that form non-deterministic run to run (DESIGN "Round 6").
+// Bit 1: the row sums' permlane16 / permlane32 swaps; bit 2: the weight / bias partials' DPP steps (bisection builds)
 #ifndef SV_MLPB_XLANE
 #define SV_MLPB_XLANE 0
+#endif
+// SV_MLPB_PIN=1 (default): the z / mean / rstd registers are consumed only below the epilogue's counted wait
+#ifndef SV_MLPB_PIN
+#define SV_MLPB_PIN 1
 #endif
 constexpr int MAX_BWD_WG = 512;  // the grid: min(tiles, 512) workgroups (two per CU), 4 partial rows each
 
@@ -782,6 +787,17 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
     // the z / mean / rstd loads (last chunk): younger only that chunk's dh stores and the W2 DMA.  Explicit: the
     // compiler's own wait here was short (tools/mlp_bwd_diag.py: dz / dw differed run to run at M = 524288 without it)
     SV_VMWAIT(SD + N2, "zl:1");
+#if SV_MLPB_PIN
+    // the operands pass through the wait: no consumer can be scheduled above it under a vmcnt of the compiler's own
+    // (DESIGN "Round 6": the compiler's waits for these loads count on in-order retirement behind younger stores and
+    // LDS-DMA; with the consumers hoisted that way the cross-lane build's dz / dw differed run to run)
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf) {
+#pragma unroll
+      for (int cf = 0; cf < CF; ++cf) asm volatile("" : "+v"(zr[rf][cf]));
+      asm volatile("" : "+v"(mu[rf]), "+v"(rs[rf]));
+    }
+#endif
     float* la = lacc + wid * 2 * C;
 #pragma unroll
     for (int rf = 0; rf < RF; ++rf) {
@@ -804,7 +820,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
           s2 += g * xhat(cf, w);
         }
       }
-#if SV_MLPB_XLANE
+#if SV_MLPB_XLANE & 1
       s1 += xlane_xor<16>(s1);
       s1 += xlane_xor<32>(s1);
       s2 += xlane_xor<16>(s2);
@@ -839,7 +855,7 @@ mlpb128_kernel(const uint16_t* __restrict__ d, const uint16_t* __restrict__ w2t,
         // lane ml == 0 adds them into the wave's own LDS row (one writer per word: deterministic)
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-#if SV_MLPB_XLANE
+#if SV_MLPB_XLANE & 2
         {
           pw[w] += xlane_xor<1>(pw[w]);
           pb[w] += xlane_xor<1>(pb[w]);
