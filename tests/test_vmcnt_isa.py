@@ -115,3 +115,36 @@ def test_checker_path_condition():
 \ts_waitcnt vmcnt(2) ; svwait w:1@e
 """)
     assert rows and rows[0]["ok"], rows
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc absent")
+def test_fused_mlp_bwd_ln_operands_consumed_below_their_wait():
+    """The fused S1 MLP backward's LayerNorm operands (z / mean / rstd, group "zl") are read only below their own
+    counted wait.  The unpinned cross-lane build (SV_MLPB_XLANE=3 SV_MLPB_PIN=0) -- the one measured to differ run to
+    run in dz / dw (profiles/round6/r15_xlane_bisect) -- has its consumers hoisted above that wait, and the check
+    must see it; the shipped build and the pinned cross-lane build must not."""
+    shipped = cv.check_early_use_text(cv.build_asm(("mlp.hip",))["mlp.hip"])
+    rows = [r for k, rs in shipped.items() if "mlpb128" in k for r in rs]
+    assert rows and all(r["loads"] == 20 and r["wait"] is not None for r in rows), rows
+    assert not any(r["uses"] for r in rows), [u for r in rows for u in r["uses"][:4]]
+    pinned = cv.check_early_use_text(cv.build_asm(("mlp.hip",), ("-DSV_MLPB_XLANE=3",))["mlp.hip"])
+    assert not any(r["uses"] for k, rs in pinned.items() if "mlpb128" in k for r in rs)
+    bad = cv.check_early_use_text(cv.build_asm(("mlp.hip",), ("-DSV_MLPB_XLANE=3", "-DSV_MLPB_PIN=0"))["mlp.hip"])
+    assert any(r["uses"] for k, rs in bad.items() if "mlpb128" in k for r in rs)
+
+
+def test_early_use_check_on_a_synthetic_kernel():
+    body = """\tbuffer_load_dwordx4 v[10:13], v1, s[0:3], 0 offen
+\tbuffer_load_dwordx2 v[20:21], v2, s[4:7], 0 offen
+\ts_nop 0
+\tbuffer_load_dword v22, v3, s[8:11], 0 offen
+\t; svtag zl
+\tv_add_f32_e32 v30, v10, v31
+{use}\ts_waitcnt vmcnt(0) ; svwait zl:1
+\tv_mul_f32_e32 v32, v20, v22
+"""
+    clean = cv.check_early_use((_HEAD + body.format(use="") + _TAIL).splitlines())
+    assert clean[0]["loads"] == 2 and not clean[0]["uses"]
+    hoisted = cv.check_early_use((_HEAD + body.format(use="\tv_sub_f32_e32 v33, v21, v31\n") + _TAIL).splitlines())
+    assert [ins for _, ins in hoisted[0]["uses"]] == ["v_sub_f32_e32 v33, v21, v31"]

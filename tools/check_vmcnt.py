@@ -675,8 +675,71 @@ def check_text(text: str, witness: bool = False, only: str | None = None, jobs: 
     return {n: r for n, r in res if r}
 
 
-def build_asm(srcs=CHECKED_SOURCES) -> dict[str, str]:
-    """Device assembly of the checked sources with build_native()'s flags (hipcc -S --cuda-device-only)."""
+# Groups whose LOADED REGISTERS must not be touched above the group's own counted wait (``svwait g:1``): the
+# compiler waits for such a consumer with a vmcnt of its own, counted on in-order retirement behind the younger
+# stores and LDS-DMA, and the fused MLP backward's dz / dw then differed run to run (DESIGN "Round 6", r15a-c).
+# group -> the load opcodes that make it up (the contiguous run of those loads just before ``svtag g``).
+EARLY_USE_GROUPS = {"zl": ("buffer_load_dword", "buffer_load_dwordx2")}
+_VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+
+
+def _vregs(text: str) -> set[int]:
+    out: set[int] = set()
+    for m in _VREG.finditer(text):
+        if m.group(1) is not None:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.add(int(m.group(3)))
+    return out
+
+
+def check_early_use(lines: list[str], groups=EARLY_USE_GROUPS) -> list[dict]:
+    """Per group tag found in the kernel: the instructions between the group's loads and its ``svwait g:1`` (text
+    order) that read or write a register those loads fill.  A row with ``uses`` non-empty fails."""
+    body = [ln.split(";")[0].strip() if not re.search(r";\s*sv(tag|wait)", ln) else ln.strip() for ln in lines]
+    rows = []
+    for g, ops in groups.items():
+        for ti, ln in enumerate(body):
+            if not re.search(rf";\s*svtag\s+{re.escape(g)}\b", ln):
+                continue
+            loads, regs, j = [], set(), ti - 1
+            while j >= 0:
+                op = body[j].split()[0] if body[j] else ""
+                if VMEM.match(op) or body[j].startswith(";") and "svtag" in body[j]:
+                    if op not in ops:
+                        break
+                    loads.append(j)
+                    regs |= _vregs(body[j].split(None, 1)[1].split(",")[0])
+                j -= 1
+            if not loads:
+                rows.append({"group": g, "line": ti, "loads": 0, "uses": [], "wait": None})
+                continue
+            wait = next((k for k in range(ti + 1, len(body)) if re.search(rf"svwait\b.*\b{re.escape(g)}:1\b", body[k])),
+                        None)
+            end = wait if wait is not None else len(body)
+            uses = []
+            for k in range(min(loads) + 1, end):
+                if k in loads or not body[k] or body[k].startswith((";", ".")) or body[k].endswith(":"):
+                    continue
+                parts = body[k].split(None, 1)
+                if len(parts) > 1 and _vregs(parts[1]) & regs:
+                    uses.append((k, body[k]))
+            rows.append({"group": g, "line": ti, "loads": len(loads), "uses": uses, "wait": wait})
+    return rows
+
+
+def check_early_use_text(text: str) -> dict[str, list[dict]]:
+    """Kernel symbol -> check_early_use rows, for every kernel carrying a tag of an EARLY_USE_GROUPS group."""
+    out = {}
+    for n, ln in split_kernels(text).items():
+        if any(re.search(rf";\s*svtag\s+{re.escape(g)}\b", x) for x in ln for g in EARLY_USE_GROUPS):
+            out[n] = check_early_use(ln)
+    return out
+
+
+def build_asm(srcs=CHECKED_SOURCES, defines=()) -> dict[str, str]:
+    """Device assembly of the checked sources with build_native()'s flags (hipcc -S --cuda-device-only), plus
+    ``defines`` (e.g. ``("-DSV_MLPB_PIN=0",)`` for an A/B build)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     import __graft_entry__ as ge
@@ -688,7 +751,7 @@ def build_asm(srcs=CHECKED_SOURCES) -> dict[str, str]:
         def one(src):
             path = os.path.join(ge.CSRC, src)
             s_out = os.path.join(td, src + ".s")
-            cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + ge.compile_flags(src) + [
+            cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + ge.compile_flags(src) + list(defines) + [
                 "--cuda-device-only", "-S", path, "-o", s_out]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
@@ -731,6 +794,14 @@ def main() -> int:
                               f"{'' if r['known'] else '  [unknown group]'}{'' if r['ok'] else '  <-- OUTSTANDING'}")
                         if r.get("witness"):
                             print("        witness (block labels):", " ".join(r["witness"][-40:]))
+        for kern, rows in check_early_use_text(text).items():
+            for r in rows:
+                ok = r["loads"] and r["wait"] is not None and not r["uses"]
+                bad += not ok
+                print(f"{'ok  ' if ok else 'FAIL'} {f}: {kern[:90]}  group {r['group']}: {r['loads']} loads, "
+                      f"{len(r['uses'])} uses above their svwait")
+                for k, ins in r["uses"][:8]:
+                    print(f"      line {k}: {ins}")
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(full, fh, indent=1)
