@@ -39,6 +39,10 @@ _MULTI_PACK = os.environ.get("SV_MULTI_PACK", "1") != "0"
 _POOLED_STEM_BWD = os.environ.get("SV_POOLED_STEM_BWD", "1") != "0"
 # SV_FIRST_BLOCK_SIDE=0: the first block's weight gradients on the main stream (A/B runs)
 _FIRST_BLOCK_SIDE = os.environ.get("SV_FIRST_BLOCK_SIDE", "1") != "0"
+# SV_DEFER_WGRAD_FLUSH=1: a block's side-stream weight gradients are enqueued after the NEXT block's first BatchNorm
+# backward pass, so the main queue has work while the host enqueues them (the traced step's largest main-queue idle
+# sits before each block's first BatchNorm pass, r16b); same kernels and operands, so the same bits
+_DEFER_FLUSH = os.environ.get("SV_DEFER_WGRAD_FLUSH", "0") == "1"
 # SV_BN_BWD_EPI: the inner BatchNorms' backward statistics from the split-K finish of their data gradient
 # (split, default: +2.2 %), also from the unsplit GEMMs' epilogue (1: no faster than a separate pass, the
 # layer1/2 epilogues absorb what the pass saved), or from their own pass everywhere (0) -- r6e A/B
@@ -482,7 +486,8 @@ class ResNetHip(nn.Module):
 
     @torch.no_grad()
     def _block_backward(self, blk, saved_block, d: torch.Tensor, side=None, keep=None, deferred=None,
-                        batch_stats: bool = True, pol: "nv.GemmPolicy | None" = None) -> torch.Tensor:
+                        batch_stats: bool = True, pol: "nv.GemmPolicy | None" = None,
+                        pending: list | None = None) -> torch.Tensor:
         """Backward of one residual block given d = dL/d(block output) (``grad_dtype``, NHWC, contiguous);
         accumulates the block's parameter gradients and returns dL/d(block input) (``grad_dtype``).
 
@@ -516,6 +521,7 @@ class ResNetHip(nn.Module):
             dy = K.bn_bwd(gm, y.view(rows, Cq), mean, rstd, bn.weight, act=out.view(rows, Cq),
                           dgamma=g(bn.weight), dbeta=g(bn.bias), dx_dtype=act, mask_inplace=True,
                           batch_stats=batch_stats)
+        self._flush_pending(pending)  # the previous block's weight gradients, now that the main queue has work
         params = [bn.weight, bn.bias]
         for ci in range(len(convs) - 1, -1, -1):
             conv, bn, _, _, _, _ = convs[ci]
@@ -559,8 +565,15 @@ class ResNetHip(nn.Module):
         else:
             dx = gm.view(x_in.shape)  # identity shortcut: the masked gradient flows straight through
             K.conv_bwd_data(dy.view(saved[0][1].shape), wp1, s1, dx=dx, accumulate=True, policy=pol)
-        self._flush_wgrads(jobs, params, side, keep, deferred, pol)
+        if pending is not None and side is not None:
+            pending.append((jobs, params, side, keep, deferred, pol))
+        else:
+            self._flush_wgrads(jobs, params, side, keep, deferred, pol)
         return dx
+
+    def _flush_pending(self, pending: list | None) -> None:
+        while pending:
+            self._flush_wgrads(*pending.pop(0))
 
     @torch.no_grad()
     def _backward_impl(self, tape: _Tape, dfeat: torch.Tensor) -> None:
@@ -574,6 +587,7 @@ class ResNetHip(nn.Module):
         pol = nv.policy(grid_cap=main_cap)  # the main stream's GEMM policy, passed with each call
         keep: list = []
         deferred: list | None = [] if side is not None else None
+        pending: list | None = [] if (_DEFER_FLUSH and side is not None) else None
         d = K.avgpool_bwd(dfeat, tape.out_shape, dx_dtype=self.grad_dtype)  # gradient of the last block output
         blocks = list(self.blocks())
         for i, (blk, saved_block) in zip(range(len(blocks) - 1, -1, -1), zip(reversed(blocks), reversed(tape.blocks))):
@@ -582,7 +596,7 @@ class ResNetHip(nn.Module):
             # weight gradient, which stays on the main stream as the last producer); the side queue is
             # empty by then (r4k trace), so they no longer wait behind a backlog: +0.5 % (r4s A/B)
             d = self._block_backward(blk, saved_block, d, side if (i > 0 or _FIRST_BLOCK_SIDE) else None, keep,
-                                     deferred, batch_stats=tape.batch_stats, pol=pol)
+                                     deferred, batch_stats=tape.batch_stats, pol=pol, pending=pending)
         # stem: maxpool -> BN + ReLU -> conv7x7 (weight gradient only)
         x0, y0, m0, r0, a0, idx, wp0, s0 = tape.stem
         B, H, W, C = a0.shape
@@ -595,6 +609,7 @@ class ResNetHip(nn.Module):
             dy0 = K.bn_bwd(da0.view(-1, C), y0.view(-1, C), m0, r0, self.bn1.weight, relu_beta=self.bn1.bias.detach(),
                            dgamma=g(self.bn1.weight), dbeta=g(self.bn1.bias), dx_dtype=act,
                            batch_stats=tape.batch_stats)
+        self._flush_pending(pending)
         self._flush_wgrads([(dy0.view(y0.shape), x0, s0, g(self.conv1.weight))],
                            [self.conv1.weight, self.bn1.weight, self.bn1.bias], None, keep, deferred, pol)
         if side is not None:

@@ -357,3 +357,39 @@ def test_resnet_graph_forward_two_forwards_one_backward(dev):
     assert len(a._fgraphs) == 1
     for ga, gb in zip(*grads):
         assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("backbone", ["resnet50", "resnet18"])
+def test_resnet_deferred_wgrad_flush_bitwise(dev, backbone, monkeypatch):
+    """SV_DEFER_WGRAD_FLUSH: each block's side-stream weight gradients enqueued after the next block's first
+    BatchNorm backward pass instead of at the block's end.  Same kernels and operands: losses, gradients, parameters
+    and BN running statistics equal the in-order enqueue bit for bit over 4 steps (side stream on)."""
+    from spine_vision_amd.backbone import resnet as rn
+    from spine_vision_amd.training import StepEngine
+    from spine_vision_amd.training.trainers.classification import _create_tasks_for_training
+
+    tasks = _create_tasks_for_training(target_labels=["pfirrmann", "modic", "herniation"], label_smoothing=0.1)
+    runs = []
+    for defer in (False, True):
+        monkeypatch.setattr(rn, "_DEFER_FLUSH", defer)
+        torch.manual_seed(7)
+        model = Classifier(backbone, tasks=tasks, pretrained=False, dropout=0.0, precision="bf16").to(dev).train()
+        assert model.backbone.overlap_wgrad
+        eng = StepEngine(model, dev, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+        g = torch.Generator().manual_seed(3)
+        losses, grads = [], []
+        for _ in range(4):
+            img = torch.rand(8, 3, 128, 128, generator=g).to(dev)
+            tg = {"pfirrmann": torch.randint(0, 5, (8,), generator=g).to(dev),
+                  "modic": torch.randint(0, 4, (8,), generator=g).to(dev),
+                  "herniation": torch.randint(0, 2, (8,), generator=g).float().to(dev)}
+            losses.append(float(eng.step_classification(img, tg)))
+            torch.cuda.synchronize()
+            grads.append([p.grad.detach().cpu().clone() for p in model.parameters()])
+        runs.append((losses, grads, [p.detach().cpu().clone() for p in model.parameters()],
+                     [b.detach().cpu().clone() for b in model.buffers()]))
+    (la, ga, pa, ba), (lb, gb, pb, bb) = runs
+    assert la == lb
+    assert all(torch.equal(x, y) for sa, sb in zip(ga, gb) for x, y in zip(sa, sb))
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert all(torch.equal(x, y) for x, y in zip(ba, bb))
